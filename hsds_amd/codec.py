@@ -1,0 +1,148 @@
+"""Drop-in mirror of the HSDS chunk-codec functions (hsds/util/storUtil.py:48-281).
+
+Same names, argument meaning and error behaviour as the reference:
+  * `_uncompress(data, compressor, shuffle, level, dtype, chunk_shape)` (storUtil.py:182)
+    detects Blosc frames (cbuffer_metainfo typesize > 0, storUtil.py:195-196),
+    decodes them (in-frame unshuffle, the external shuffle is then skipped,
+    storUtil.py:203-204) or inflates a zlib stream (storUtil.py:209-220) and
+    byte-unshuffles it (storUtil.py:225-226).  Any codec failure raises
+    HTTPInternalServerError, an unknown shuffle code raises ValueError.
+  * `_shuffle` / `_unshuffle` codec 1 = numcodecs.Shuffle(itemsize) (storUtil.py:94-143).
+
+All byte work runs on the MI355X through the C ABI (include/hsds_amd.h); there is
+no CPU fallback.  Bitshuffle (codec 2) and Blosc inner codecs other than zlib are
+outside this engine's scope and raise.
+"""
+import numpy as np
+
+from . import _native as nat
+
+try:  # the reference raises aiohttp's HTTP exceptions from the codec layer
+    from aiohttp.web_exceptions import HTTPInternalServerError
+except Exception:  # pragma: no cover - aiohttp is in the image
+    class HTTPInternalServerError(Exception):
+        pass
+
+BYTE_SHUFFLE = 1
+BIT_SHUFFLE = 2
+
+
+def getCompressors():
+    """Compressor names this engine decodes (storUtil.getCompressors naming: zlib is
+    reported as gzip, plus the deflate synonym, storUtil.py:52-66)."""
+    return ["gzip", "deflate"]
+
+
+def getSupportedFilters(include_compressors=True):
+    filters = ["shuffle", "fletcher32", "nbit", "scaleoffset"]
+    if include_compressors:
+        filters.extend(getCompressors())
+    return filters
+
+
+def _compressor_code(compressor):
+    if not compressor or compressor == "scaleoffset":
+        return nat.COMP_NONE
+    if compressor in ("gzip", "deflate", "zlib"):
+        return nat.COMP_ZLIB
+    return nat.COMP_OTHER
+
+
+def _as_bytes(data):
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(data, dtype=np.uint8)
+    return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+
+
+def _itemsize(dtype):
+    return 1 if dtype is None else np.dtype(dtype).itemsize
+
+
+def _shuffle(codec, data, chunk_shape=None, dtype=None):
+    """storUtil._shuffle (storUtil.py:94): codec 1 = byte shuffle."""
+    if codec == BYTE_SHUFFLE:
+        src = _as_bytes(data)
+        out = np.empty(src.size, np.uint8)
+        rc = nat.lib().hsds_shuffle(nat.engine().h, src.ctypes.data, src.size, _itemsize(dtype),
+                                    out.ctypes.data)
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_shuffle")
+        return out.tobytes()
+    if codec == BIT_SHUFFLE:
+        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+    raise ValueError()
+
+
+def _unshuffle(codec, data, dtype=None, chunk_shape=None):
+    """storUtil._unshuffle (storUtil.py:136): codec 1 = byte unshuffle."""
+    if codec == BYTE_SHUFFLE:
+        src = _as_bytes(data)
+        out = np.empty(src.size, np.uint8)
+        rc = nat.lib().hsds_unshuffle(nat.engine().h, src.ctypes.data, src.size, _itemsize(dtype),
+                                      out.ctypes.data)
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_unshuffle")
+        return out.tobytes()
+    if codec == BIT_SHUFFLE:
+        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+    raise ValueError()
+
+
+def _blosc_nbytes(src):
+    """Decoded size recorded in a Blosc1 header, or None when `src` is not a Blosc frame."""
+    if src.size >= 16 and src[0] <= 2 and src[3] > 0:
+        return int(src[4]) | (int(src[5]) << 8) | (int(src[6]) << 16) | (int(src[7]) << 24)
+    return None
+
+
+def _uncompress(data, compressor=None, shuffle=0, level=None, dtype=None, chunk_shape=None):
+    """storUtil._uncompress (storUtil.py:182-235) on the GPU."""
+    if shuffle not in (0, BYTE_SHUFFLE, BIT_SHUFFLE) and shuffle:
+        raise ValueError()
+    comp = _compressor_code(compressor)
+    src = _as_bytes(data)
+    itemsize = _itemsize(dtype)
+    if comp == nat.COMP_NONE and not shuffle:
+        return bytes(src)
+    if shuffle == BIT_SHUFFLE:
+        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+    if comp == nat.COMP_NONE:
+        expected = src.size              # shuffle only: _unshuffle of the bytes as given
+    elif chunk_shape is not None:
+        expected = int(np.prod(chunk_shape)) * itemsize
+    else:
+        nb = _blosc_nbytes(src) if comp != nat.COMP_NONE else None
+        if nb is not None:
+            expected = nb
+        elif comp == nat.COMP_NONE:
+            expected = src.size
+        else:
+            expected = None
+    if expected is None:
+        # size unknown (zlib.decompress semantics): grow the capacity until it fits
+        cap = max(1 << 16, src.size * 8)
+        while True:
+            out = np.empty(cap, np.uint8)
+            n = nat.lib().hsds_uncompress(nat.engine().h, src.ctypes.data, src.size, comp, int(shuffle),
+                                          itemsize, out.ctypes.data, -cap)
+            if n == nat.ERR_SIZE and cap < (1 << 31):
+                cap *= 4
+                continue
+            break
+    else:
+        out = np.empty(max(expected, 1), np.uint8)
+        n = nat.lib().hsds_uncompress(nat.engine().h, src.ctypes.data, src.size, comp, int(shuffle),
+                                      itemsize, out.ctypes.data, expected)
+    if n < 0:
+        if n in (nat.ERR_ARG, nat.ERR_DEVICE):
+            raise nat.NativeError(n, "hsds_uncompress")
+        raise HTTPInternalServerError()
+    return out[:n].tobytes()
+
+
+def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape=None):
+    """storUtil._compress (storUtil.py:238-281).  The GPU deflate encoder is the
+    next SURVEY.md section 8 row for this engine; until it lands this raises."""
+    if not compressor and shuffle != BIT_SHUFFLE:
+        return data
+    raise NotImplementedError("GPU Blosc/zlib encoder not built yet (write path, BASELINE config 5)")

@@ -1,0 +1,614 @@
+// engine.hip -- MI355X (gfx950) chunk codec + hyperslab engine behind include/hsds_amd.h.
+//
+// Kernels (all batched over many chunks, one launch per stage):
+//   frame_walk_kernel   one thread per chunk: Blosc1 / zlib / raw detection
+//                       (storUtil._uncompress, storUtil.py:182-235) and emission of
+//                       one work item per deflate stream / raw split
+//   scan_kernel         exclusive scan of items per chunk (single workgroup)
+//   inflate_kernel      persistent waves pull stream items from a device counter;
+//                       one wavefront decodes one zlib stream (inflate_wave.h)
+//   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
+//   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
+//                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
+// Every launch is asynchronous on the caller's stream; no host synchronisation
+// inside the batched entry points.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/hsds_amd.h"
+#include "inflate_wave.h"
+
+#define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
+
+namespace {
+
+constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
+constexpr int INFLATE_WAVES_PER_CU = 3;
+
+enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_INEXACT = 0x100 };
+
+struct Item {          // 32 bytes
+  uint64_t src;
+  uint64_t dst;
+  uint32_t src_len;
+  uint32_t dst_len;
+  uint32_t chunk;
+  uint32_t kind;
+};
+
+struct ChunkMeta {     // post-decode unshuffle work for one chunk
+  uint64_t tmp;        // staged (shuffled) bytes
+  uint64_t dst;
+  uint32_t mode;       // 0 none, 1 Blosc blocks (ts, bs), 2 whole chunk (itemsize)
+  uint32_t ts;
+  uint32_t bs;
+  uint32_t nbytes;
+};
+
+__device__ __forceinline__ uint32_t rd8(const uint8_t* p) { return p[0]; }
+__device__ __forceinline__ uint32_t rd32le(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// -------------------------------------------------------------------------
+// frame walk: one thread per chunk.  Restates c-blosc 1.21 blosc_decompress
+// frame rules (see oracle/oracle.c orc_blosc_decode) and storUtil._uncompress's
+// dispatch.  Items go to slot range [chunk*KSLOTS, chunk*KSLOTS + count).
+// -------------------------------------------------------------------------
+__global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
+                                  int64_t nchunks, uint8_t* dst_base, uint8_t* tmp_base, Item* __restrict__ slots,
+                                  uint32_t* __restrict__ counts, ChunkMeta* __restrict__ meta,
+                                  uint32_t* __restrict__ meta_list, uint32_t* __restrict__ meta_count,
+                                  int32_t* __restrict__ status, int compressor, int shuffle, int itemsize,
+                                  int inexact) {
+  const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const hsds_chunk_desc c = chunks[ci];
+  const uint8_t* s = src_base + c.src_off;
+  const uint64_t L = c.src_len, n = c.dst_len;
+  uint8_t* out = dst_base + c.dst_off;
+  uint8_t* tmp = tmp_base + c.dst_off;
+  Item* slot = slots + ci * KSLOTS;
+  int st = HSDS_OK;
+  uint32_t cnt = 0;
+  ChunkMeta m = {0, (uint64_t)out, 0, 0, 0, (uint32_t)n};
+  auto emit = [&](uint32_t kind, const uint8_t* sp, uint64_t sl, uint8_t* dp, uint64_t dl) {
+    if (cnt >= (uint32_t)KSLOTS) { st = HSDS_ERR_UNSUPPORTED; return; }
+    Item it;
+    it.src = (uint64_t)sp; it.dst = (uint64_t)dp; it.src_len = (uint32_t)sl; it.dst_len = (uint32_t)dl;
+    it.chunk = (uint32_t)ci; it.kind = kind;
+    slot[cnt++] = it;
+  };
+  if (L >= (1ull << 28) || n >= (1ull << 31)) {
+    st = HSDS_ERR_UNSUPPORTED;
+  } else if (compressor == HSDS_COMP_NONE) {
+    if (L != n) st = HSDS_ERR_SIZE;
+    else if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
+    else if (shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1) {
+      if (n % (uint64_t)itemsize) st = HSDS_ERR_ARG;
+      else { emit(ITEM_RAW, s, L, tmp, n); m.mode = 2; m.tmp = (uint64_t)tmp; m.ts = (uint32_t)itemsize; }
+    } else emit(ITEM_RAW, s, L, out, n);
+  } else if (L >= 4 && rd8(s) <= 2 && rd8(s + 3) > 0) {
+    // ---- Blosc1 frame (shuffle filter handled in-frame: storUtil.py:203-204) ----
+    if (L < 16) st = HSDS_ERR_FRAME;
+    else {
+      const uint32_t ver = rd8(s), verlz = rd8(s + 1), flags = rd8(s + 2), ts = rd8(s + 3);
+      const uint64_t nbytes = rd32le(s + 4), bs = rd32le(s + 8), cbytes = rd32le(s + 12);
+      if (ver != 2 || cbytes > L || cbytes < 16) st = HSDS_ERR_FRAME;
+      else if (nbytes != n) st = HSDS_ERR_SIZE;
+      else if (flags & 0x02) {
+        if (nbytes + 16 > cbytes) st = HSDS_ERR_FRAME;
+        else emit(ITEM_RAW, s + 16, nbytes, out, nbytes);
+      } else if (((flags >> 5) & 7) != 3) st = HSDS_ERR_UNSUPPORTED;
+      else if (verlz != 1) st = HSDS_ERR_FRAME;
+      else if (flags & 0x04) st = HSDS_ERR_UNSUPPORTED;
+      else if (nbytes > 0) {
+        if (bs == 0 || bs > nbytes) st = HSDS_ERR_FRAME;
+        else {
+          const uint64_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
+          const uint64_t hdr = 16 + 4 * nblocks;
+          const int doshuffle = (flags & 0x01) && ts > 1;
+          uint8_t* target = doshuffle ? tmp : out;
+          if (hdr > cbytes) st = HSDS_ERR_FRAME;
+          for (uint64_t b = 0; b < nblocks && st == HSDS_OK; b++) {
+            const int isleft = (b == nblocks - 1) && leftover;
+            const uint64_t bsz = isleft ? leftover : bs;
+            const uint32_t nspl = (!(flags & 0x10) && ts <= 16 && bs / ts >= 128 && !isleft) ? ts : 1;
+            const uint64_t neblock = bsz / nspl;
+            int64_t p = (int32_t)rd32le(s + 16 + 4 * b);
+            if (p < (int64_t)hdr || p >= (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
+            for (uint32_t j = 0; j < nspl; j++) {
+              if (p + 4 > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
+              const int64_t cs = (int32_t)rd32le(s + p);
+              p += 4;
+              if (cs < 0 || p + cs > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
+              emit((uint64_t)cs == neblock ? ITEM_RAW : ITEM_ZLIB, s + p, (uint64_t)cs,
+                   target + b * bs + j * neblock, neblock);
+              if (st != HSDS_OK) break;
+              p += cs;
+            }
+          }
+          if (doshuffle) { m.mode = 1; m.tmp = (uint64_t)tmp; m.ts = ts; m.bs = (uint32_t)bs; }
+        }
+      }
+    }
+  } else if (compressor == HSDS_COMP_ZLIB) {
+    if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
+    else if (shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1) {
+      if (n % (uint64_t)itemsize) st = HSDS_ERR_ARG;
+      else { emit(ITEM_ZLIB, s, L, tmp, n); m.mode = 2; m.tmp = (uint64_t)tmp; m.ts = (uint32_t)itemsize; }
+    } else emit(inexact ? (ITEM_ZLIB | ITEM_INEXACT) : ITEM_ZLIB, s, L, out, n);
+  } else {
+    st = HSDS_ERR_UNSUPPORTED;
+  }
+  if (st != HSDS_OK) { cnt = 0; m.mode = 0; }
+  counts[ci] = cnt;
+  status[ci] = st;
+  meta[ci] = m;
+  if (m.mode) {
+    const uint32_t k = atomicAdd(meta_count, 1u);
+    meta_list[k] = (uint32_t)ci;
+  }
+}
+
+// exclusive scan of counts[0..n) into offs[0..n], single workgroup of 1024 threads
+__global__ void scan_kernel(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offs, int64_t n) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const uint32_t v = i < n ? counts[i] : 0u;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const uint32_t y = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
+      __syncthreads();
+      part[threadIdx.x] += y;
+      __syncthreads();
+    }
+    if (i < n) offs[i] = carry + part[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offs[n] = carry;
+}
+
+// -------------------------------------------------------------------------
+// inflate: persistent 64-thread workgroups; each pulls stream items from a
+// device counter until the batch total (offs[nchunks]) is exhausted.
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
+                                                     int64_t nchunks, uint32_t* __restrict__ counter,
+                                                     int32_t* __restrict__ status, uint32_t* __restrict__ sizes,
+                                                     hz::Tune tune) {
+  __shared__ hz::Shared sh;
+  const uint32_t total = offs[nchunks];
+  const int lane = threadIdx.x;
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(counter, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= total) break;
+    // chunk of this item: largest c with offs[c] <= item
+    int64_t lo = 0, hi = nchunks - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const Item it = slots[lo * KSLOTS + (item - offs[lo])];
+    int st;
+    if ((it.kind & 0xff) == ITEM_RAW) {
+      const uint8_t* sp = (const uint8_t*)it.src;
+      uint8_t* dp = (uint8_t*)it.dst;
+      for (uint32_t i = lane; i < it.dst_len; i += 64) dp[i] = sp[i];
+      st = HSDS_OK;
+    } else {
+      hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
+                           (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr};
+      st = hz::inflate_stream<hz::Stats>(sh, job, tune, (hz::Stats*)nullptr);
+    }
+    if (lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
+    __syncthreads();
+  }
+}
+
+// -------------------------------------------------------------------------
+// unshuffle of staged chunks: work items = (listed chunk, 4 KiB output tile)
+// -------------------------------------------------------------------------
+__device__ __forceinline__ void unshuffle_range(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                uint64_t len, uint32_t n, uint64_t beg, uint64_t end) {
+  const uint64_t count = len / n, body = count * n;
+  for (uint64_t q = beg; q < end; q++) {
+    out[q] = q < body ? in[(q % n) * count + q / n] : in[q];
+  }
+}
+
+__global__ void unshuffle_kernel(const ChunkMeta* __restrict__ meta, const uint32_t* __restrict__ meta_list,
+                                 const uint32_t* __restrict__ meta_count, const int32_t* __restrict__ status) {
+  const uint32_t nlist = *meta_count;
+  for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+    const uint32_t ci = meta_list[li];
+    if (status[ci] != HSDS_OK) continue;
+    const ChunkMeta m = meta[ci];
+    const uint8_t* in = (const uint8_t*)m.tmp;
+    uint8_t* out = (uint8_t*)m.dst;
+    if (m.mode == 2) {
+      const uint32_t n = m.ts;
+      const uint64_t count = m.nbytes / n, body = count * n;
+      for (uint64_t q = threadIdx.x; q < m.nbytes; q += blockDim.x)
+        out[q] = q < body ? in[(q % n) * count + q / n] : in[q];
+    } else {
+      const uint64_t nb = m.nbytes, bs = m.bs;
+      for (uint64_t b0 = 0; b0 < nb; b0 += bs) {
+        const uint64_t bsz = nb - b0 < bs ? nb - b0 : bs;
+        const uint32_t n = m.ts;
+        const uint64_t count = bsz / n, body = count * n;
+        for (uint64_t q = threadIdx.x; q < bsz; q += blockDim.x)
+          out[b0 + q] = q < body ? in[b0 + (q % n) * count + q / n] : in[b0 + q];
+      }
+    }
+  }
+}
+
+// plain device shuffle / unshuffle of one buffer (numcodecs.Shuffle semantics)
+__global__ void shuffle_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t len,
+                               uint32_t n, int inverse) {
+  const uint64_t count = len / n, body = count * n;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x) {
+    if (q >= body) { out[q] = in[q]; continue; }
+    if (inverse) out[q] = in[(q % n) * count + q / n];          // unshuffle: element-major out
+    else out[(q % n) * count + q / n] = in[q];                  // shuffle:   plane-major out
+  }
+}
+
+// -------------------------------------------------------------------------
+// strided region copy / compare (numpy basic slicing)
+// -------------------------------------------------------------------------
+struct RegionIter {
+  int rank;
+  int64_t count[HSDS_MAX_RANK];
+};
+
+__device__ __forceinline__ void region_offsets(const hsds_copy_desc& d, int64_t e, int64_t& so, int64_t& doff) {
+  so = (int64_t)d.src_off;
+  doff = (int64_t)d.dst_off;
+  for (int k = d.rank - 1; k >= 0; k--) {
+    const int64_t c = d.count[k];
+    const int64_t i = e % c;
+    e /= c;
+    so += i * d.src_stride[k];
+    doff += i * d.dst_stride[k];
+  }
+}
+
+__device__ __forceinline__ void copy_elem(const uint8_t* s, uint8_t* d, int itemsize) {
+  if (itemsize == 4 && !(((uintptr_t)s | (uintptr_t)d) & 3)) { *(uint32_t*)d = *(const uint32_t*)s; return; }
+  if (itemsize == 8 && !(((uintptr_t)s | (uintptr_t)d) & 7)) { *(uint64_t*)d = *(const uint64_t*)s; return; }
+  if (itemsize == 2 && !(((uintptr_t)s | (uintptr_t)d) & 1)) { *(uint16_t*)d = *(const uint16_t*)s; return; }
+  for (int b = 0; b < itemsize; b++) d[b] = s[b];
+}
+
+__global__ void copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                            const hsds_copy_desc* __restrict__ descs, int64_t n,
+                            const int32_t* __restrict__ flags) {
+  for (int64_t di = blockIdx.y; di < n; di += gridDim.y) {
+    if (flags && !flags[di]) continue;
+    const hsds_copy_desc d = descs[di];
+    int64_t total = 1;
+    for (int k = 0; k < d.rank; k++) total *= d.count[k];
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+      int64_t so, doff;
+      region_offsets(d, e, so, doff);
+      copy_elem(src + so, dst + doff, d.itemsize);
+    }
+  }
+}
+
+__device__ __forceinline__ int elem_differs(const uint8_t* a, const uint8_t* b, int itemsize, int kind) {
+  switch (kind) {
+    case HSDS_KIND_F32: { float x, y; memcpy(&x, a, 4); memcpy(&y, b, 4); return !(x == y); }
+    case HSDS_KIND_F64: { double x, y; memcpy(&x, a, 8); memcpy(&y, b, 8); return !(x == y); }
+    case HSDS_KIND_F16: { _Float16 x, y; memcpy(&x, a, 2); memcpy(&y, b, 2); return !(x == y); }
+    case HSDS_KIND_C64: { float x[2], y[2]; memcpy(x, a, 8); memcpy(y, b, 8); return !(x[0] == y[0] && x[1] == y[1]); }
+    case HSDS_KIND_C128: { double x[2], y[2]; memcpy(x, a, 16); memcpy(y, b, 16); return !(x[0] == y[0] && x[1] == y[1]); }
+    default: {
+      for (int k = 0; k < itemsize; k++) if (a[k] != b[k]) return 1;
+      return 0;
+    }
+  }
+}
+
+// d_b: new data (desc.src_*), d_a: chunk (desc.dst_*)
+__global__ void compare_kernel(const uint8_t* __restrict__ b, const uint8_t* __restrict__ a,
+                               const hsds_copy_desc* __restrict__ descs, int64_t n, int kind,
+                               int32_t* __restrict__ differs) {
+  for (int64_t di = blockIdx.y; di < n; di += gridDim.y) {
+    const hsds_copy_desc d = descs[di];
+    int64_t total = 1;
+    for (int k = 0; k < d.rank; k++) total *= d.count[k];
+    int found = 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total && !found;
+         e += (int64_t)gridDim.x * blockDim.x) {
+      int64_t so, doff;
+      region_offsets(d, e, so, doff);
+      found = elem_differs(a + doff, b + so, d.itemsize, kind);
+    }
+    if (__any(found) && (threadIdx.x & 63) == 0) atomicOr(&differs[di], 1);
+  }
+}
+
+__global__ void zero_i32_kernel(int32_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
+}
+
+}  // namespace
+
+// =========================================================================
+// engine
+// =========================================================================
+struct hsds_engine {
+  int device;
+  int num_cus;
+  hz::Tune tune;
+  // workspace (grown on demand)
+  uint8_t* ws = nullptr;
+  size_t ws_bytes = 0;
+  uint8_t* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  // host staging for the single-chunk host API
+  uint8_t* h_dev_src = nullptr;
+  size_t h_dev_src_bytes = 0;
+  uint8_t* h_dev_dst = nullptr;
+  size_t h_dev_dst_bytes = 0;
+  hipEvent_t ev0, ev1;
+  int ev_valid = 0;
+};
+
+static int grow(void** p, size_t* have, size_t need) {
+  if (*have >= need) return 0;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  size_t sz = need + need / 4 + 4096;
+  if (hipMalloc(p, sz) != hipSuccess) return HSDS_ERR_DEVICE;
+  *have = sz;
+  return 0;
+}
+
+extern "C" {
+
+const char* hsds_version(void) { return HSDS_VERSION; }
+
+const char* hsds_strerror(int s) {
+  switch (s) {
+    case HSDS_OK: return "ok";
+    case HSDS_ERR_FRAME: return "malformed Blosc frame";
+    case HSDS_ERR_DATA: return "corrupt deflate stream";
+    case HSDS_ERR_TRUNC: return "truncated stream";
+    case HSDS_ERR_SIZE: return "decoded size mismatch";
+    case HSDS_ERR_UNSUPPORTED: return "unsupported codec or layout";
+    case HSDS_ERR_ARG: return "invalid argument";
+    case HSDS_ERR_DEVICE: return "HIP runtime error";
+    default: return "unknown status";
+  }
+}
+
+int hsds_engine_create(int device, hsds_engine** out) {
+  if (!out) return HSDS_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return HSDS_ERR_DEVICE;
+  hsds_engine* e = new hsds_engine();
+  e->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
+  e->num_cus = prop.multiProcessorCount;
+  e->tune.L0 = 384;
+  e->tune.W = 96;
+  e->tune.adapt = 1;
+  e->tune.C = 192;
+  e->tune.max_rounds = 4;
+  if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
+  *out = e;
+  return HSDS_OK;
+}
+
+void hsds_engine_destroy(hsds_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  if (e->ws) hipFree(e->ws);
+  if (e->tmp) hipFree(e->tmp);
+  if (e->h_dev_src) hipFree(e->h_dev_src);
+  if (e->h_dev_dst) hipFree(e->h_dev_dst);
+  hipEventDestroy(e->ev0);
+  hipEventDestroy(e->ev1);
+  delete e;
+}
+
+int hsds_set_tuning(hsds_engine* e, uint32_t seg_bits, uint32_t warmup_bits, uint32_t cont_bits, int32_t rounds) {
+  if (!e) return HSDS_ERR_ARG;
+  if (seg_bits < (uint32_t)hz::LMIN || seg_bits > (uint32_t)hz::LMAX) return HSDS_ERR_ARG;
+  if (warmup_bits > (uint32_t)hz::WMAX || cont_bits > (uint32_t)hz::CMAX || rounds < 0 || rounds > 64) return HSDS_ERR_ARG;
+  e->tune.L0 = seg_bits;
+  e->tune.W = warmup_bits;
+  e->tune.C = cont_bits;
+  e->tune.max_rounds = rounds;
+  return HSDS_OK;
+}
+
+static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                             void* d_dst, uint64_t dst_extent, int32_t* d_status, int compressor, int shuffle,
+                             int itemsize, void* stream, int inexact, uint32_t** inexact_size) {
+  if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_status))) return HSDS_ERR_ARG;
+  if (itemsize < 1) itemsize = 1;
+  if (nchunks == 0) return HSDS_OK;
+  if (nchunks > (int64_t)(1u << 24)) return HSDS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  // workspace layout
+  const size_t sz_slots = (size_t)nchunks * KSLOTS * sizeof(Item);
+  const size_t sz_counts = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
+  const size_t sz_offs = ((size_t)(nchunks + 1) * 4 + 255) & ~(size_t)255;
+  const size_t sz_meta = (size_t)nchunks * sizeof(ChunkMeta);
+  const size_t sz_list = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
+  const size_t need = sz_slots + sz_counts + sz_offs + sz_meta + sz_list + 256;
+  if (grow((void**)&e->ws, &e->ws_bytes, need)) return HSDS_ERR_DEVICE;
+  uint8_t* w = e->ws;
+  Item* slots = (Item*)w; w += sz_slots;
+  uint32_t* counts = (uint32_t*)w; w += sz_counts;
+  uint32_t* offs = (uint32_t*)w; w += sz_offs;
+  ChunkMeta* meta = (ChunkMeta*)w; w += sz_meta;
+  uint32_t* list = (uint32_t*)w; w += sz_list;
+  uint32_t* ctr = (uint32_t*)w;   // [0] inflate item counter, [1] meta list count, [2] inexact size
+  // staging for shuffled outputs (F2 chunks, Blosc typesize > 1): same offsets as
+  // the destination buffer, so it spans the destination extent
+  if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
+  if (hipMemsetAsync(ctr, 0, 16, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  const int tpb = 256;
+  const int nb = (int)((nchunks + tpb - 1) / tpb);
+  hipLaunchKernelGGL(frame_walk_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
+                     (uint8_t*)d_dst, e->tmp, slots, counts, meta, list, ctr + 1, d_status, compressor, shuffle,
+                     itemsize, inexact);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
+  int64_t grid = (int64_t)e->num_cus * INFLATE_WAVES_PER_CU;
+  if (grid > nchunks * 4) grid = nchunks * 4;
+  if (grid < 1) grid = 1;
+  hipEventRecord(e->ev0, st);
+  hipLaunchKernelGGL(inflate_kernel, dim3((unsigned)grid), dim3(64), 0, st, slots, offs, nchunks, ctr, d_status,
+                     ctr + 2, e->tune);
+  hipEventRecord(e->ev1, st);
+  e->ev_valid = 1;
+  hipLaunchKernelGGL(unshuffle_kernel, dim3(2048), dim3(256), 0, st, meta, list, ctr + 1, d_status);
+  if (hipGetLastError() != hipSuccess) return HSDS_ERR_DEVICE;
+  if (inexact_size) *inexact_size = ctr + 2;
+  return HSDS_OK;
+}
+
+int hsds_decode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                      void* d_dst, uint64_t dst_extent, int32_t* d_status, int compressor, int shuffle,
+                      int itemsize, void* stream) {
+  return decode_batch_impl(e, d_src, d_chunks, nchunks, d_dst, dst_extent, d_status, compressor, shuffle, itemsize,
+                           stream, 0, nullptr);
+}
+
+int hsds_last_inflate_ms(hsds_engine* e, float* ms) {
+  if (!e || !ms || !e->ev_valid) return HSDS_ERR_ARG;
+  if (hipEventElapsedTime(ms, e->ev0, e->ev1) != hipSuccess) return HSDS_ERR_DEVICE;
+  return HSDS_OK;
+}
+
+int64_t hsds_uncompress(hsds_engine* e, const void* src, int64_t srclen, int compressor, int shuffle, int itemsize,
+                        void* dst, int64_t expected) {
+  if (!e || srclen < 0 || (srclen && !src) || (expected && !dst)) return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  const int inexact = expected < 0;
+  if (inexact) expected = -expected;
+  // device staging: [src bytes | chunk descriptor] and [dst bytes | status]
+  const size_t desc_off = ((size_t)srclen + 255) & ~(size_t)255;
+  const size_t stat_off = ((size_t)expected + 255) & ~(size_t)255;
+  if (grow((void**)&e->h_dev_src, &e->h_dev_src_bytes, desc_off + sizeof(hsds_chunk_desc))) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->h_dev_dst, &e->h_dev_dst_bytes, stat_off + 64)) return HSDS_ERR_DEVICE;
+  hsds_chunk_desc c = {0, (uint64_t)srclen, 0, (uint64_t)expected};
+  hsds_chunk_desc* dd = (hsds_chunk_desc*)(e->h_dev_src + desc_off);
+  int32_t* dstat = (int32_t*)(e->h_dev_dst + stat_off);
+  if (srclen && hipMemcpy(e->h_dev_src, src, (size_t)srclen, hipMemcpyHostToDevice) != hipSuccess)
+    return HSDS_ERR_DEVICE;
+  if (hipMemcpy(dd, &c, sizeof(c), hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
+  uint32_t* dsize = nullptr;
+  int r = decode_batch_impl(e, e->h_dev_src, dd, 1, e->h_dev_dst, (uint64_t)expected, dstat, compressor, shuffle,
+                            itemsize, nullptr, inexact, &dsize);
+  if (r) return r;
+  int32_t status = 0;
+  if (hipMemcpy(&status, dstat, 4, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (status) return status;
+  if (inexact) {
+    uint32_t got = 0;
+    if (hipMemcpy(&got, dsize, 4, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+    expected = got;
+  }
+  if (expected && hipMemcpy(dst, e->h_dev_dst, (size_t)expected, hipMemcpyDeviceToHost) != hipSuccess)
+    return HSDS_ERR_DEVICE;
+  return expected;
+}
+
+static int launch_shuffle(const void* d_src, int64_t n, int itemsize, void* d_dst, void* stream, int inverse) {
+  if (n < 0 || itemsize < 1 || (n && (!d_src || !d_dst))) return HSDS_ERR_ARG;
+  if (n == 0) return HSDS_OK;
+  if (itemsize == 1) {
+    return hipMemcpyAsync(d_dst, d_src, (size_t)n, hipMemcpyDeviceToDevice, (hipStream_t)stream) == hipSuccess
+               ? HSDS_OK : HSDS_ERR_DEVICE;
+  }
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(shuffle_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)d_src, (uint8_t*)d_dst, (uint64_t)n, (uint32_t)itemsize, inverse);
+  return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+int hsds_shuffle_device(hsds_engine* e, const void* d_src, int64_t n, int itemsize, void* d_dst, void* stream) {
+  if (!e) return HSDS_ERR_ARG;
+  return launch_shuffle(d_src, n, itemsize, d_dst, stream, 0);
+}
+int hsds_unshuffle_device(hsds_engine* e, const void* d_src, int64_t n, int itemsize, void* d_dst, void* stream) {
+  if (!e) return HSDS_ERR_ARG;
+  return launch_shuffle(d_src, n, itemsize, d_dst, stream, 1);
+}
+
+static int host_shuffle(hsds_engine* e, const void* src, int64_t n, int itemsize, void* dst, int inverse) {
+  if (!e || n < 0 || itemsize < 1 || (n && (!src || !dst))) return HSDS_ERR_ARG;
+  if (n == 0) return HSDS_OK;
+  hipSetDevice(e->device);
+  if (grow((void**)&e->h_dev_src, &e->h_dev_src_bytes, (size_t)n)) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->h_dev_dst, &e->h_dev_dst_bytes, (size_t)n)) return HSDS_ERR_DEVICE;
+  if (hipMemcpy(e->h_dev_src, src, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
+  int r = launch_shuffle(e->h_dev_src, n, itemsize, e->h_dev_dst, nullptr, inverse);
+  if (r) return r;
+  if (hipMemcpy(dst, e->h_dev_dst, (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  return HSDS_OK;
+}
+
+int hsds_shuffle(hsds_engine* e, const void* src, int64_t n, int itemsize, void* dst) {
+  return host_shuffle(e, src, n, itemsize, dst, 0);
+}
+int hsds_unshuffle(hsds_engine* e, const void* src, int64_t n, int itemsize, void* dst) {
+  return host_shuffle(e, src, n, itemsize, dst, 1);
+}
+
+static int launch_copy(const void* d_src, void* d_dst, const hsds_copy_desc* d_desc, int64_t n, const int32_t* flags,
+                       void* stream) {
+  if (n < 0 || (n && (!d_src || !d_dst || !d_desc))) return HSDS_ERR_ARG;
+  if (n == 0) return HSDS_OK;
+  const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
+  hipLaunchKernelGGL(copy_kernel, dim3(8, gy), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d_src,
+                     (uint8_t*)d_dst, d_desc, n, flags);
+  return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+int hsds_copy_batch(hsds_engine* e, const void* d_src, void* d_dst, const hsds_copy_desc* d_desc, int64_t n,
+                    void* stream) {
+  if (!e) return HSDS_ERR_ARG;
+  return launch_copy(d_src, d_dst, d_desc, n, nullptr, stream);
+}
+
+int hsds_copy_batch_if(hsds_engine* e, const void* d_src, void* d_dst, const hsds_copy_desc* d_desc, int64_t n,
+                       const int32_t* d_flags, void* stream) {
+  if (!e || (n && !d_flags)) return HSDS_ERR_ARG;
+  return launch_copy(d_src, d_dst, d_desc, n, d_flags, stream);
+}
+
+int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const hsds_copy_desc* d_desc, int64_t n,
+                       int kind, int32_t* d_differs, void* stream) {
+  if (!e || n < 0 || (n && (!d_a || !d_b || !d_desc || !d_differs))) return HSDS_ERR_ARG;
+  if (n == 0) return HSDS_OK;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(zero_i32_kernel, dim3(64), dim3(256), 0, st, d_differs, n);
+  const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
+  hipLaunchKernelGGL(compare_kernel, dim3(8, gy), dim3(256), 0, st, (const uint8_t*)d_b, (const uint8_t*)d_a,
+                     d_desc, n, kind, d_differs);
+  return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+}  // extern "C"

@@ -1,0 +1,1011 @@
+// inflate_wave.h -- one-wavefront-per-stream zlib (RFC 1950/1951) decoder.
+//
+// Replaces, for the HSDS data-node hot path, the zlib inflate that the reference
+// reaches through storUtil._uncompress (hsds/util/storUtil.py:209-220, CPython
+// zlib.decompress) and through c-blosc's zlib_wrap_decompress for every Blosc split
+// (storUtil.py:195-208).  Output must be bit-identical to libz; errors map to the
+// same "500" outcome (corrupt data, truncated stream, adler32 mismatch).
+//
+// Algorithm (see DESIGN.md "Inflate"):
+//   The 64 lanes of a wavefront cooperate on ONE deflate stream.  Inside a Huffman
+//   block the bitstream window [win_start, win_start + 64*L) is cut into 64 segments
+//   of L bits.  Phase A: lane i speculatively decodes tokens starting W bits before
+//   its segment (lane 0 starts exactly at the known token boundary), marking every
+//   token start in an LDS bitmap and storing tokens in LDS.  Phase B: lane i is
+//   "synced" when the exit position of lane i-1 (first token start at or after the
+//   end of segment i-1) is one of lane i's marked token starts; from there on its
+//   decode is the true decode (Huffman self-synchronisation).  The longest synced
+//   prefix of lanes is accepted.  Phase C: output offsets by a wave prefix sum,
+//   literals written, LZ77 matches resolved in rounds against a frontier F (all
+//   output below F is final), adler32 accumulated per lane as position-weighted
+//   sums and combined once per stream.
+//
+// The file is SINGLE SOURCE for two drivers:
+//   * HIP (gfx950):  every lane is a real SIMT lane, LANE_LOOP is one iteration.
+//   * CPU emulation (tests/emu): LANE_LOOP iterates lanes 0..63 in order, so the
+//     same orchestration (including every cross-lane step) is unit-tested on CPU.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define HZ_GPU 1
+#define HZ_HD __device__ __forceinline__
+#define LANE_VAR(T, name) T name
+#define LV(name) name
+#define LANE_LOOP for (int lane = (int)threadIdx.x, _once = 1; _once; _once = 0)
+#define WAVE_SYNC() __syncthreads()
+#define WAVE_SYNC_GLOBAL() \
+  do { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); __syncthreads(); \
+       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); } while (0)
+#else
+#include <string.h>
+#include <stdio.h>
+#define HZ_GPU 0
+#define HZ_HD static inline
+#define LANE_VAR(T, name) T name[64]
+#define LV(name) name[lane]
+#define LANE_LOOP for (int lane = 0; lane < 64; lane++)
+#define WAVE_SYNC() do {} while (0)
+#define WAVE_SYNC_GLOBAL() do {} while (0)
+#endif
+
+namespace hz {
+
+constexpr int WAVE = 64;
+constexpr int LL_ROOT = 10;
+constexpr int D_ROOT = 8;
+constexpr int TMAX = 64;            // tokens stored per lane per window
+constexpr int LMAX = 512;           // max segment length (bits)
+constexpr int LMIN = 64;
+constexpr int SCAP = 6144;           // window output bytes resolved in LDS
+constexpr int CMAX = 256;           // max continuation bits into the next segment
+constexpr int OVR = 64;             // bitmap bits past the last token start
+constexpr int BM_WORDS = (LMAX + CMAX + OVR) / 32 + 1;
+// staged input dwords: window (64 L) + warm-up (<= L) + alignment + overrun/peek
+constexpr int WMAX = 1024;
+constexpr int IN_WORDS = (WAVE * LMAX + WMAX + CMAX + 256) / 32 + 8;
+constexpr uint32_t ADLER_MOD = 65521;
+
+// status codes (include/hsds_amd.h)
+constexpr int ST_OK = 0;
+constexpr int ST_FRAME = -1;
+constexpr int ST_DATA = -2;
+constexpr int ST_TRUNC = -3;
+constexpr int ST_SIZE = -4;
+constexpr int ST_UNSUP = -5;
+
+// decode-table entry: bits 0-3 code length, 4-7 extra bits, 8-10 kind, 16-31 value
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SLOW = 3, K_BAD = 4 };
+HZ_HD uint32_t ent(uint32_t kind, uint32_t nbits, uint32_t extra, uint32_t value) {
+  return nbits | (extra << 4) | (kind << 8) | (value << 16);
+}
+HZ_HD uint32_t e_bits(uint32_t e) { return e & 15u; }
+HZ_HD uint32_t e_extra(uint32_t e) { return (e >> 4) & 15u; }
+HZ_HD uint32_t e_kind(uint32_t e) { return (e >> 8) & 7u; }
+HZ_HD uint32_t e_val(uint32_t e) { return e >> 16; }
+
+// tokens: literal = byte; match = 0x80000000 | len<<16 | (dist-1); EOB / ERR markers
+constexpr uint32_t T_MATCH = 0x80000000u;
+constexpr uint32_t T_EOB = 0x40000000u;
+constexpr uint32_t T_ERR = 0x40000001u;
+
+// stop reasons of a Phase-A lane
+constexpr int S_NONE = 0, S_EOB = 1, S_ERR = 2;
+
+struct Shared {
+  uint32_t lut_ll[1 << LL_ROOT];
+  uint32_t lut_d[1 << D_ROOT];
+  uint32_t tok[TMAX][WAVE];          // token-major: lane-parallel accesses hit 64 banks
+  uint32_t bitmap[WAVE][BM_WORDS];
+  uint32_t in32[IN_WORDS + 4];
+  uint32_t exitpos[WAVE];
+  uint32_t syncpos[WAVE];
+  uint32_t contpos[WAVE];
+  uint32_t flag[WAVE];
+  uint16_t ref[SCAP];
+  uint32_t obase[WAVE + 1];
+  uint32_t done[WAVE];
+  uint32_t flag2[WAVE];
+  uint16_t sorted_ll[288];
+  uint16_t sorted_d[32];
+  uint16_t cnt_ll[16];
+  uint16_t cnt_d[16];
+  uint16_t cnt_cl[16];
+  uint16_t sorted_cl[20];
+  uint8_t lens[320 + 32];
+  // uniform scalars published by lane 0
+  int32_t u_status;
+  uint32_t u_pos;
+  uint32_t u_nlen, u_ndist;
+  uint32_t u_stage_base;
+  uint32_t u_stored_len;
+};
+
+HZ_HD uint32_t bmask(uint32_t n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1u); }
+
+HZ_HD uint32_t popc32(uint32_t x) {
+#if HZ_GPU
+  return __popc(x);
+#else
+  return (uint32_t)__builtin_popcount(x);
+#endif
+}
+
+HZ_HD uint32_t rev_bits(uint32_t v, int n) {
+  uint32_t r = 0;
+  for (int i = 0; i < n; i++) { r = (r << 1) | (v & 1u); v >>= 1; }
+  return r;
+}
+
+// ---- base / extra tables (RFC 1951 3.2.5) ----------------------------------
+HZ_HD uint32_t len_base(uint32_t s) {   // s = 0..28  (symbol 257+s)
+  const uint16_t t[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                          35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+  return t[s];
+}
+HZ_HD uint32_t len_extra(uint32_t s) {
+  return (s < 8 || s == 28) ? 0u : (s - 4) >> 2;
+}
+HZ_HD uint32_t dist_base(uint32_t s) {
+  const uint16_t t[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385,
+                          513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+  return t[s];
+}
+HZ_HD uint32_t dist_extra(uint32_t s) { return s < 4 ? 0u : (s - 2) >> 1; }
+
+HZ_HD uint32_t ll_entry(uint32_t sym, uint32_t len) {
+  if (sym < 256) return ent(K_LIT, len, 0, sym);
+  if (sym == 256) return ent(K_EOB, len, 0, 0);
+  if (sym <= 285) return ent(K_LEN, len, len_extra(sym - 257), len_base(sym - 257));
+  return ent(K_BAD, len ? len : 1, 0, 0);
+}
+HZ_HD uint32_t d_entry(uint32_t sym, uint32_t len) {
+  if (sym < 30) return ent(K_LEN, len, dist_extra(sym), dist_base(sym));
+  return ent(K_BAD, len ? len : 1, 0, 0);
+}
+
+// ---- LDS bit access ---------------------------------------------------------
+// Bit positions are relative to the 4-byte aligned base of the stream, so every
+// staged dword load is aligned.  peek64 returns >= 64 valid bits at `pos`.
+HZ_HD uint64_t peek64(const Shared* sh, uint32_t pos) {
+  uint32_t w = pos - sh->u_stage_base;
+  uint32_t i = w >> 5, s = w & 31u;
+  uint64_t lo = (uint64_t)sh->in32[i] | ((uint64_t)sh->in32[i + 1] << 32);
+  uint64_t hi = sh->in32[i + 2];
+  return s ? ((lo >> s) | (hi << (64 - s))) : lo;
+}
+
+// canonical (slow path) decode for codes longer than the root:
+// returns (sym | len << 16), or 0xffffffff when no code matches.
+HZ_HD uint32_t canon_decode(const uint16_t* cnt, const uint16_t* sorted, uint64_t bits) {
+  int code = 0, first = 0, index = 0;
+  for (int len = 1; len <= 15; len++) {
+    code |= (int)(bits & 1u);
+    bits >>= 1;
+    int count = cnt[len];
+    if (code - count < first) return (uint32_t)sorted[index + (code - first)] | ((uint32_t)len << 16);
+    index += count;
+    first += count;
+    first <<= 1;
+    code <<= 1;
+  }
+  return 0xffffffffu;
+}
+
+HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
+  uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
+  if (e_kind(e) == K_SLOW) {
+    uint32_t r = canon_decode(sh->cnt_ll, sh->sorted_ll, bits);
+    e = (r == 0xffffffffu) ? ent(K_BAD, 1, 0, 0) : ll_entry(r & 0xffff, r >> 16);
+  }
+  return e;
+}
+HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
+  uint32_t e = sh->lut_d[bits & ((1u << D_ROOT) - 1)];
+  if (e_kind(e) == K_SLOW) {
+    uint32_t r = canon_decode(sh->cnt_d, sh->sorted_d, bits);
+    e = (r == 0xffffffffu) ? ent(K_BAD, 1, 0, 0) : d_entry(r & 0xffff, r >> 16);
+  }
+  return e;
+}
+
+
+// decode one token (literal, length+distance, EOB, or invalid) at bit `p`.
+// Invalid codes advance one bit so that a speculative decoder keeps going.
+HZ_HD void decode_token(const Shared* sh, uint32_t p, uint32_t& tokv, uint32_t& adv) {
+  const uint64_t bits = peek64(sh, p);
+  const uint32_t e = lookup_ll(sh, bits);
+  const uint32_t kind = e_kind(e), nb = e_bits(e);
+  if (kind == K_LIT) { tokv = e_val(e); adv = nb; return; }
+  if (kind == K_LEN) {
+    const uint32_t xb = e_extra(e);
+    const uint32_t len = e_val(e) + ((uint32_t)(bits >> nb) & bmask(xb));
+    const uint32_t c = nb + xb;
+    const uint64_t b2 = bits >> c;
+    const uint32_t ed = lookup_d(sh, b2);
+    if (e_kind(ed) != K_LEN) { tokv = T_ERR; adv = 1; return; }
+    const uint32_t nd = e_bits(ed), xd = e_extra(ed);
+    const uint32_t dist = e_val(ed) + ((uint32_t)(b2 >> nd) & bmask(xd));
+    tokv = T_MATCH | (len << 16) | (dist - 1u);
+    adv = c + nd + xd;
+    return;
+  }
+  if (kind == K_EOB) { tokv = T_EOB; adv = nb; return; }
+  tokv = T_ERR; adv = 1;
+}
+
+HZ_HD void mark_bit(Shared* sh, int lane, uint32_t rel) {
+  if (rel < (uint32_t)(BM_WORDS * 32)) sh->bitmap[lane][rel >> 5] |= 1u << (rel & 31u);
+}
+
+// relative bit position of the k-th (0-based) mark of a lane
+HZ_HD uint32_t nth_mark(const Shared* sh, int lane, uint32_t k) {
+  uint32_t c = 0;
+  for (uint32_t w = 0; w < (uint32_t)BM_WORDS; w++) {
+    uint32_t m = sh->bitmap[lane][w];
+    const uint32_t pc = popc32(m);
+    if (c + pc > k) {
+      for (;;) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        if (c == k) return w * 32u + b;
+        c++;
+        m &= m - 1u;
+      }
+    }
+    c += pc;
+  }
+  return 0xffffffffu;
+}
+
+// ---- global memory helpers -------------------------------------------------
+// aligned dword k of the stream's aligned base; bytes outside [lo, hi) are zero.
+HZ_HD uint32_t load_word(const uint8_t* base, uint32_t k, uint32_t lo, uint32_t hi) {
+  uint32_t b0 = k * 4u;
+  if (b0 >= hi || b0 + 4u <= lo) return 0u;
+  uint32_t v = *(const uint32_t*)(base + b0);
+  if (b0 < lo) v &= ~bmask((lo - b0) * 8u);
+  if (b0 + 4u > hi) v &= bmask((hi - b0) * 8u);
+  return v;
+}
+
+}  // namespace hz
+
+// ---- wave-collective helpers (the only places the two drivers differ) -------
+#if HZ_GPU
+#define WAVE_BALLOT(expr) ((uint64_t)__ballot((expr) ? 1 : 0))
+namespace hz {
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) { uint32_t y = __shfl_xor(v, o, 64); v = y < v ? y : v; }
+  return v;
+}
+}  // namespace hz
+#define WAVE_EXCL_SCAN(arr_or_var, out) out = hz::wave_excl_scan(arr_or_var, lane)
+#define WAVE_SUM(v) hz::wave_sum(v)
+#else
+#define WAVE_BALLOT(expr)                                          \
+  ([&]() {                                                         \
+    uint64_t _m = 0;                                               \
+    for (int lane = 0; lane < 64; lane++) if (expr) _m |= 1ull << lane; \
+    return _m;                                                     \
+  }())
+#endif
+
+namespace hz {
+
+// ---------------------------------------------------------------------------
+// Cooperative Huffman table construction (RFC 1951 3.2.2 canonical codes).
+// lens[0..n) -> cnt[16], sorted[], lut (root bits).  Returns ST_OK or ST_DATA
+// following zlib inflate_table's rules: over-subscribed always fails; an
+// incomplete code fails for the code-length code, and for the literal/length and
+// distance codes unless it is a single code of length 1.  n == 0 (no codes,
+// e.g. no distances) is accepted and every lookup then decodes as invalid.
+// kind: 0 = code-length code, 1 = literal/length, 2 = distance.
+// ---------------------------------------------------------------------------
+struct TableArgs {
+  const uint8_t* lens;
+  int n;
+  uint16_t* cnt;
+  uint16_t* sorted;
+  uint32_t* lut;
+  int root;
+  int kind;
+};
+
+}  // namespace hz
+
+// Table build as a macro-free function per driver is awkward because it needs
+// ballots; it is written once in the SIMT style below.
+#define HZ_BUILD_TABLE(sh, A, status_out)                                               \
+  do {                                                                                  \
+    /* counts (lane 0 serial: n <= 320) */                                              \
+    LANE_LOOP {                                                                         \
+      if (lane == 0) {                                                                  \
+        for (int l = 0; l < 16; l++) (A).cnt[l] = 0;                                    \
+        for (int s = 0; s < (A).n; s++) (A).cnt[(A).lens[s]]++;                         \
+        (A).cnt[0] = 0;                                                                 \
+        int left = 1, maxl = 0, bad = 0;                                                \
+        for (int l = 1; l <= 15; l++) {                                                 \
+          left <<= 1; left -= (A).cnt[l];                                               \
+          if ((A).cnt[l]) maxl = l;                                                     \
+          if (left < 0) bad = 1;                                                        \
+        }                                                                               \
+        if (!bad && maxl > 0 && left > 0 && ((A).kind == 0 || maxl != 1)) bad = 1;      \
+        if ((A).kind == 0 && maxl == 0) bad = 1;                                        \
+        /* sorted symbols in canonical order */                                         \
+        int offs[16]; offs[1] = 0;                                                      \
+        for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + (A).cnt[l];                \
+        for (int s = 0; s < (A).n; s++) if ((A).lens[s]) (A).sorted[offs[(A).lens[s]]++] = (uint16_t)s; \
+        (sh).u_status = bad ? hz::ST_DATA : hz::ST_OK;                                  \
+      }                                                                                 \
+    }                                                                                   \
+    WAVE_SYNC();                                                                        \
+    /* LUT fill: every root index decoded canonically (balanced across lanes) */       \
+    LANE_LOOP {                                                                         \
+      for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
+        int code = 0, first = 0, index = 0; uint32_t bits = (uint32_t)idx;              \
+        uint32_t e = hz::ent(hz::K_SLOW, (A).root, 0, 0);                               \
+        for (int len = 1; len <= (A).root; len++) {                                     \
+          code |= (int)(bits & 1u); bits >>= 1;                                         \
+          int count = (A).cnt[len];                                                     \
+          if (code - count < first) {                                                   \
+            uint32_t sym = (A).sorted[index + (code - first)];                          \
+            e = (A).kind == 1 ? hz::ll_entry(sym, len)                                  \
+              : (A).kind == 2 ? hz::d_entry(sym, len) : hz::ent(hz::K_LIT, len, 0, sym); \
+            break;                                                                      \
+          }                                                                             \
+          index += count; first += count; first <<= 1; code <<= 1;                     \
+        }                                                                               \
+        (A).lut[idx] = e;                                                               \
+      }                                                                                 \
+    }                                                                                   \
+    WAVE_SYNC();                                                                        \
+    status_out = (sh).u_status;                                                         \
+  } while (0)
+
+namespace hz {
+
+// Work description for one zlib stream.
+struct StreamJob {
+  const uint8_t* src;   // stream bytes (any alignment)
+  uint32_t src_len;
+  uint8_t* dst;         // output
+  uint32_t dst_len;     // expected size (exact) or capacity (exact == 0)
+  uint32_t exact;       // 1: output must be exactly dst_len bytes
+  uint32_t* out_len;    // optional: decoded length
+};
+
+// Tunables (runtime so that tests can sweep them)
+struct Tune {
+  uint32_t L0;     // initial segment bits
+  uint32_t W;      // warm-up bits
+  uint32_t adapt;  // adapt L to the token density
+  uint32_t C;      // continuation budget (bits)
+  int max_rounds;  // repair rounds per window
+};
+
+// Statistics (emulator / diagnostics only)
+struct Stats {
+  uint64_t windows, lanes_valid, tokens, matches, match_bytes, lit_bytes, rounds, blocks, stored;
+  uint64_t steps_max, steps_sum, repairs, hops, maxhops;
+};
+
+}  // namespace hz
+
+// ===========================================================================
+// The stream decoder.  `sh` is the wave's LDS block.  Returns a status code
+// (uniform).  Written in SIMT style: code outside LANE_LOOP is uniform across the
+// wave and runs redundantly on every lane; LANE_LOOP bodies never break/continue
+// at their top level and never return.
+// ===========================================================================
+#define HZ_STAGE(sh, base_al, lo, hi, first_word, nwords)                          \
+  do {                                                                              \
+    WAVE_SYNC();                                                                    \
+    LANE_LOOP {                                                                     \
+      for (uint32_t _k = (uint32_t)lane; _k < (uint32_t)(nwords) + 4u; _k += 64)    \
+        (sh).in32[_k] = _k < (uint32_t)(nwords)                                     \
+                            ? hz::load_word((base_al), (first_word) + _k, (lo), (hi)) : 0u; \
+    }                                                                               \
+    (sh).u_stage_base = (first_word) * 32u;                                          \
+    WAVE_SYNC();                                                                    \
+  } while (0)
+
+namespace hz {
+
+template <class StatsT>
+#if HZ_GPU
+__device__
+#else
+static
+#endif
+int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* stats) {
+  // aligned base so that every staged dword load is aligned
+  const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 3u);
+  const uint8_t* base = job.src - a;
+  const uint32_t lo = a, hi = a + job.src_len;   // valid byte range of the stream
+  const uint32_t limit_bits = hi * 8u;
+  const uint32_t dst_len = job.dst_len;
+  uint8_t* const dst = job.dst;
+
+  LANE_VAR(uint32_t, s1);   // adler32 partial sums: S1 = sum b, S2 = sum pos*b (mod 65521)
+  LANE_VAR(uint32_t, s2);
+  LANE_LOOP { LV(s1) = 0; LV(s2) = 0; }
+
+  // ---- zlib header (RFC 1950) ----
+  if (job.src_len < 2) return ST_TRUNC;
+  HZ_STAGE(sh, base, lo, hi, 0u, 2u);
+  {
+    uint32_t hdr16 = (uint32_t)(peek64(&sh, lo * 8u) & 0xffffu);
+    uint32_t cmf = hdr16 & 0xff, flg = hdr16 >> 8;
+    if ((cmf & 0x0f) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0) return ST_DATA;
+    if (flg & 0x20) return ST_DATA;  // preset dictionary: Z_NEED_DICT
+  }
+  uint32_t pos = lo * 8u + 16u;
+  uint32_t out = 0;
+  uint32_t L = tune.L0 < (uint32_t)LMIN ? (uint32_t)LMIN : tune.L0 > (uint32_t)LMAX ? (uint32_t)LMAX : tune.L0;
+
+  for (;;) {  // ---- deflate blocks ----
+    HZ_STAGE(sh, base, lo, hi, pos >> 5, 128u);
+    if (pos + 3u > limit_bits) return ST_TRUNC;
+    const uint32_t h3 = (uint32_t)(peek64(&sh, pos) & 7u);
+    pos += 3;
+    const uint32_t bfinal = h3 & 1u, btype = h3 >> 1;
+    if (stats) stats->blocks++;
+    if (btype == 3) return ST_DATA;
+    if (btype == 0) {
+      // ---- stored block ----
+      pos = (pos + 7u) & ~7u;
+      if (pos + 32u > limit_bits) return ST_TRUNC;
+      const uint32_t ln = (uint32_t)(peek64(&sh, pos) & 0xffffffffu);
+      const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
+      if ((len ^ 0xffffu) != nlen) return ST_DATA;
+      pos += 32u;
+      if (pos + len * 8u > limit_bits) return ST_TRUNC;
+      if (out + len > dst_len) return ST_SIZE;
+      const uint32_t sb = pos >> 3;  // byte index relative to the aligned base
+      LANE_LOOP {
+        uint32_t a1 = LV(s1), a2 = LV(s2);
+        for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
+          const uint32_t b = base[sb + i];
+          dst[out + i] = (uint8_t)b;
+          a1 += b;
+          a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
+        }
+        LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
+      }
+      out += len;
+      pos += len * 8u;
+      if (stats) stats->stored++;
+      WAVE_SYNC_GLOBAL();
+      if (bfinal) break;
+      continue;
+    }
+    // ---- Huffman code lengths ----
+    uint32_t nlen = 288, ndist = 32;
+    if (btype == 1) {
+      LANE_LOOP {
+        for (int s = lane; s < 320; s += 64)
+          sh.lens[s] = s >= 288 ? 5 : s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+      }
+      WAVE_SYNC();
+    } else {
+      // dynamic header (RFC 1951 3.2.7): lane 0 decodes it serially from LDS
+      LANE_LOOP {
+        if (lane == 0) {
+          int st = ST_OK;
+          uint32_t p = pos;
+          const uint64_t b = peek64(&sh, p);
+          const uint32_t hlit = (uint32_t)(b & 31u) + 257u, hdist = (uint32_t)((b >> 5) & 31u) + 1u;
+          const uint32_t hclen = (uint32_t)((b >> 10) & 15u) + 4u;
+          p += 14;
+          if (hlit > 286 || hdist > 30) st = ST_DATA;
+          const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+          uint8_t cl[19];
+          for (int i = 0; i < 19; i++) cl[i] = 0;
+          for (uint32_t i = 0; i < hclen; i++) { cl[order[i]] = (uint8_t)(peek64(&sh, p) & 7u); p += 3; }
+          uint16_t* cnt = sh.cnt_cl;
+          uint16_t* srt = sh.sorted_cl;
+          for (int l = 0; l < 16; l++) cnt[l] = 0;
+          for (int i = 0; i < 19; i++) cnt[cl[i]]++;
+          cnt[0] = 0;
+          int left = 1, maxl = 0;
+          for (int l = 1; l <= 15; l++) {
+            left <<= 1; left -= cnt[l];
+            if (cnt[l]) maxl = l;
+            if (left < 0) st = ST_DATA;
+          }
+          if (left > 0 || maxl == 0) st = ST_DATA;  // code-length code must be complete
+          int offs[16];
+          offs[1] = 0;
+          for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
+          for (int i = 0; i < 19; i++) if (cl[i]) srt[offs[cl[i]]++] = (uint16_t)i;
+          const uint32_t total = hlit + hdist;
+          uint32_t n = 0;
+          const uint32_t stage_end = sh.u_stage_base + 128u * 32u;
+          while (st == ST_OK && n < total) {
+            if (p + 96u > stage_end) { st = ST_DATA; break; }
+            uint64_t bits = peek64(&sh, p);
+            const uint32_t r = canon_decode(cnt, srt, bits);
+            if (r == 0xffffffffu) { st = ST_DATA; break; }
+            const uint32_t sym = r & 0xffff, l = r >> 16;
+            p += l;
+            bits >>= l;
+            if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
+            uint32_t rep, val = 0;
+            if (sym == 16) {
+              if (n == 0) { st = ST_DATA; break; }
+              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(bits & 3u); p += 2;
+            } else if (sym == 17) { rep = 3 + (uint32_t)(bits & 7u); p += 3; }
+            else { rep = 11 + (uint32_t)(bits & 127u); p += 7; }
+            if (n + rep > total) { st = ST_DATA; break; }
+            for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
+          }
+          if (st == ST_OK && p > limit_bits) st = ST_TRUNC;
+          if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;  // missing end-of-block code
+          if (st == ST_OK) {
+            for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
+            for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
+            for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
+          }
+          sh.u_status = st;
+          sh.u_pos = p;
+          sh.u_nlen = hlit;
+          sh.u_ndist = hdist;
+        }
+      }
+      WAVE_SYNC();
+      const int hst = sh.u_status;
+      if (hst != ST_OK) return hst;
+      pos = sh.u_pos;
+      nlen = sh.u_nlen;
+      ndist = sh.u_ndist;
+    }
+    {
+      int bst = ST_OK;
+      TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1};
+      HZ_BUILD_TABLE(sh, tll, bst);
+      if (bst != ST_OK) return bst;
+      TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2};
+      HZ_BUILD_TABLE(sh, td, bst);
+      if (bst != ST_OK) return bst;
+    }
+
+    // ---- windows over the Huffman block ----
+    for (;;) {
+      if (stats) stats->windows++;
+      const uint32_t win_start = pos;
+      const uint32_t W = tune.W, C = tune.C;
+      {
+        const uint32_t first_bit = win_start >= W ? win_start - W : 0u;
+        const uint32_t words = (64u * L + W + C + 256u) / 32u + 3u;
+        HZ_STAGE(sh, base, lo, hi, first_bit >> 5, words);
+      }
+
+      // -------- Phase A: speculative decode of 64 segments --------
+      // lane i decodes from (segment start - W); tokens whose start lies inside its
+      // own segment [ss, ss+L) are stored and their start bits marked.
+      LANE_VAR(uint32_t, seg_start);
+      LANE_VAR(uint32_t, ntok);
+      LANE_VAR(int, storing);
+      LANE_VAR(uint32_t, nsteps);
+      LANE_LOOP {
+        const uint32_t ss = win_start + (uint32_t)lane * L;
+        const uint32_t se = ss + L;
+        uint32_t p = (lane > 0 && ss - win_start > W) ? ss - W : win_start;
+        int st = p >= ss;
+        uint32_t nt = 0, steps = 0;
+        for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
+        uint32_t mw_idx = 0, mw = 0;  // bitmap word cached in a register (monotonic positions)
+        for (;;) {
+          if (p >= se) break;
+          if (!st && p >= ss) st = 1;
+          if (st && nt >= (uint32_t)TMAX) break;
+          uint32_t tokv, adv;
+          decode_token(&sh, p, tokv, adv);
+          steps++;
+          if (st) {
+            const uint32_t rel = p - ss, wi = rel >> 5;
+            if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
+            mw |= 1u << (rel & 31u);
+            sh.tok[nt][lane] = tokv;
+            nt++;
+          }
+          p += adv;
+        }
+        if (st) {
+          sh.bitmap[lane][mw_idx] |= mw;
+          mark_bit(&sh, lane, p - ss);   // exit boundary (start of the next token)
+        }
+        LV(seg_start) = ss;
+        LV(ntok) = nt;
+        LV(storing) = st;
+        LV(nsteps) = steps;
+        sh.exitpos[lane] = p;
+        sh.syncpos[lane] = 0xffffffffu;
+      }
+      WAVE_SYNC();
+
+      // -------- Phase A': continuation --------
+      // lane i keeps decoding from its exit until it reaches a token start that
+      // lane i+1 marked (then both decodes coincide from there on), for at most C
+      // bits into segment i+1.  Tokens decoded here belong to lane i.
+      LANE_LOOP {
+        const uint32_t ss = LV(seg_start);
+        uint32_t p = sh.exitpos[lane], nt = LV(ntok), steps = 0;
+        if (lane < 63 && LV(storing)) {
+          const uint32_t ssn = ss + L;
+          for (;;) {
+            const uint32_t reln = p - ssn;
+            if (p >= ssn && reln < (uint32_t)(BM_WORDS * 32) &&
+                ((sh.bitmap[lane + 1][reln >> 5] >> (reln & 31u)) & 1u)) {
+              sh.syncpos[lane + 1] = p;
+              break;
+            }
+            if (p >= ssn + C || nt >= (uint32_t)TMAX) break;
+            uint32_t tokv, adv;
+            decode_token(&sh, p, tokv, adv);
+            steps++;
+            mark_bit(&sh, lane, p - ss);
+            sh.tok[nt][lane] = tokv;
+            nt++;
+            p += adv;
+          }
+          mark_bit(&sh, lane, p - ss);     // final boundary of this lane's decode
+        }
+        LV(ntok) = nt;
+        LV(nsteps) += steps;
+        sh.contpos[lane] = p;
+      }
+      WAVE_SYNC();
+      // -------- repair rounds --------
+      // A lane whose predecessor's continuation never met one of its marks is
+      // "failed": its speculative path had not merged with the true path.  It
+      // re-decodes its segment from the predecessor's final position (a true token
+      // boundary once the predecessor is valid) and continues into its successor.
+      LANE_VAR(int, failed);
+      LANE_LOOP {
+        LV(failed) = lane > 0 && sh.syncpos[lane] == 0xffffffffu;
+        sh.flag[lane] = (uint32_t)LV(failed);
+      }
+      WAVE_SYNC();
+      for (int round = 0; round < tune.max_rounds; round++) {
+        const uint64_t fm = WAVE_BALLOT(LV(failed));
+        if (!fm) break;
+        if (stats) stats->repairs++;
+        LANE_LOOP {
+          const int redo = LV(failed) && !sh.flag[lane - 1 < 0 ? 0 : lane - 1] &&
+                           sh.contpos[lane - 1 < 0 ? 0 : lane - 1] >= LV(seg_start);
+          const int next_failed = lane < 63 ? (int)sh.flag[lane + 1] : 1;
+          uint32_t steps = 0;
+          if (redo) {
+            const uint32_t ss = LV(seg_start), se = ss + L;
+            uint32_t p = sh.contpos[lane - 1];
+            uint32_t nt = 0;
+            for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
+            // segment part (starts at a true boundary, possibly before or after ss)
+            while (p < se && nt < (uint32_t)TMAX) {
+              uint32_t tokv, adv;
+              decode_token(&sh, p, tokv, adv);
+              steps++;
+              mark_bit(&sh, lane, p - ss);
+              sh.tok[nt][lane] = tokv;
+              nt++;
+              p += adv;
+            }
+            if (lane < 63) {
+              const uint32_t ssn = se;
+              if (!next_failed) sh.syncpos[lane + 1] = 0xffffffffu;
+              for (;;) {
+                const uint32_t reln = p - ssn;
+                if (!next_failed && p >= ssn && reln < (uint32_t)(BM_WORDS * 32) &&
+                    ((sh.bitmap[lane + 1][reln >> 5] >> (reln & 31u)) & 1u)) {
+                  sh.syncpos[lane + 1] = p;
+                  break;
+                }
+                if (next_failed || p >= ssn + C || nt >= (uint32_t)TMAX) break;
+                uint32_t tokv, adv;
+                decode_token(&sh, p, tokv, adv);
+                steps++;
+                mark_bit(&sh, lane, p - ss);
+                sh.tok[nt][lane] = tokv;
+                nt++;
+                p += adv;
+              }
+            }
+            mark_bit(&sh, lane, p - ss);
+            sh.contpos[lane] = p;
+            sh.syncpos[lane] = sh.contpos[lane - 1];   // whole token list is valid
+            LV(ntok) = nt;
+          }
+          LV(nsteps) += steps;
+          sh.flag2[lane] = (uint32_t)redo;
+        }
+        WAVE_SYNC();
+        LANE_LOOP {
+          if (sh.flag2[lane]) LV(failed) = 0;
+          else if (lane > 0 && sh.flag2[lane - 1] && sh.syncpos[lane] == 0xffffffffu) LV(failed) = 1;
+        }
+        WAVE_SYNC();
+        LANE_LOOP { sh.flag[lane] = (uint32_t)LV(failed); }
+        WAVE_SYNC();
+      }
+      if (stats) {
+#if !HZ_GPU
+        uint32_t mx = 0; uint64_t sm = 0;
+        for (int lane = 0; lane < 64; lane++) { mx = nsteps[lane] > mx ? nsteps[lane] : mx; sm += nsteps[lane]; }
+        stats->steps_max += mx; stats->steps_sum += sm;
+#endif
+      }
+
+      // -------- Phase B: validity --------
+      LANE_VAR(uint32_t, tok_first);
+      LANE_VAR(uint32_t, tok_end);
+      LANE_VAR(int, endk);       // 0 none, 1 EOB, 2 ERR inside the valid range
+      LANE_LOOP {
+        uint32_t tf = 0;
+        int ok = lane == 0;
+        if (lane > 0 && sh.syncpos[lane] != 0xffffffffu && !LV(failed)) {
+          ok = 1;
+          const uint32_t sp = sh.syncpos[lane];
+          const uint32_t rel = sp >= LV(seg_start) ? sp - LV(seg_start) : 0u;
+          uint32_t c = 0;
+          for (uint32_t w = 0; w < (rel >> 5); w++) c += popc32(sh.bitmap[lane][w]);
+          c += popc32(sh.bitmap[lane][rel >> 5] & bmask(rel & 31u));
+          tf = c;
+        }
+        uint32_t te = LV(ntok);
+        int ek = 0;
+        if (ok) {
+          for (uint32_t t = tf; t < te; t++) {
+            const uint32_t v = sh.tok[t][lane];
+            if (v == T_EOB || v == T_ERR) { ek = v == T_EOB ? 1 : 2; te = t; break; }
+          }
+        }
+        LV(tok_first) = ok ? tf : 0xffffffffu;
+        LV(tok_end) = te;
+        LV(endk) = ek;
+      }
+      const uint64_t smask = WAVE_BALLOT(LV(tok_first) != 0xffffffffu);
+      uint32_t V = 0;
+      while (V < 64u && ((smask >> V) & 1ull)) V++;
+      const uint64_t emask = WAVE_BALLOT(LV(endk) != 0) & (V >= 64 ? ~0ull : ((1ull << V) - 1ull));
+      int end_lane = -1;
+      for (uint32_t k = 0; k < V; k++) if ((emask >> k) & 1ull) { end_lane = (int)k; break; }
+      if (end_lane >= 0) V = (uint32_t)end_lane + 1u;
+      if (stats) stats->lanes_valid += V;
+
+      // -------- Phase C: emit --------
+      LANE_VAR(uint32_t, tcur);
+      LANE_VAR(uint32_t, tend);
+      LANE_VAR(uint32_t, olen);
+      LANE_LOOP {
+        uint32_t tf = LV(tok_first), te = LV(tok_end), ol = 0;
+        if ((uint32_t)lane >= V) { tf = 0; te = 0; }
+        if (lane == end_lane) {
+          sh.u_status = LV(endk);
+          // bit position after the EOB token = the mark following token te
+          sh.u_pos = nth_mark(&sh, lane, te + 1u) + LV(seg_start);
+        }
+        for (uint32_t t = tf; t < te; t++) {
+          const uint32_t v = sh.tok[t][lane];
+          ol += (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+        }
+        LV(tcur) = tf; LV(tend) = te; LV(olen) = ol;
+      }
+      WAVE_SYNC();
+      if (end_lane >= 0 && sh.u_status == 2) {
+        return sh.u_pos + 64u > limit_bits ? ST_TRUNC : ST_DATA;
+      }
+      LANE_VAR(uint32_t, opos);
+      uint32_t wtotal = 0;
+      uint32_t ntok_valid = 0;
+#if HZ_GPU
+      {
+        const uint32_t ob = wave_excl_scan(olen, (int)threadIdx.x);
+        wtotal = wave_sum(olen);
+        ntok_valid = wave_sum(tend - tcur);
+        opos = out + ob;
+      }
+#else
+      for (int lane = 0; lane < 64; lane++) {
+        opos[lane] = out + wtotal; wtotal += olen[lane]; ntok_valid += tend[lane] - tcur[lane];
+      }
+#endif
+      if (stats) stats->tokens += ntok_valid;
+      if (out + wtotal > dst_len) return ST_SIZE;
+      const uint32_t npos = end_lane >= 0 ? sh.u_pos : sh.contpos[V - 1];
+      if (npos > limit_bits) return ST_TRUNC;
+
+      if (wtotal <= (uint32_t)SCAP) {
+        // ---- LDS path: byte-level source map, chased to literals / earlier output ----
+        // ref[r] for window byte r: 0x4000|b literal, r' < 0x4000 internal reference,
+        // 0x8000|(x-1) byte x positions before the window (already final in dst).
+        const uint32_t wbeg = out;
+        LANE_VAR(int, lerr);
+        LANE_LOOP {
+          int err = 0;
+          uint32_t op = LV(opos);
+          for (uint32_t t = LV(tcur); t < LV(tend); t++) {
+            const uint32_t v = sh.tok[t][lane];
+            if (!(v & T_MATCH)) { sh.ref[op - wbeg] = (uint16_t)(0x4000u | v); op++; continue; }
+            const uint32_t len = (v >> 16) & 0x1ffu, d = (v & 0x7fffu) + 1u;
+            if (d > op) { err = 1; break; }          // invalid distance too far back
+            uint32_t jj = 0;
+            for (uint32_t k = 0; k < len; k++) {
+              const uint32_t q = op - d + jj;         // source of byte op+k
+              sh.ref[op + k - wbeg] = q >= wbeg ? (uint16_t)(q - wbeg) : (uint16_t)(0x8000u | (wbeg - q - 1u));
+              jj++; if (jj == d) jj = 0;
+            }
+            op += len;
+          }
+          LV(lerr) = err;
+        }
+        WAVE_SYNC();
+        if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
+        if (stats) stats->rounds++;
+        // chase: references strictly decrease, so every chain ends in a literal or
+        // an external byte; resolved values are written back (benign races: every
+        // stored value is a valid ancestor of the position)
+        LANE_LOOP {
+          for (uint32_t r = (uint32_t)lane; r < wtotal; r += 64) {
+            uint32_t v = sh.ref[r];
+            uint32_t hops = 0;
+            while (v < 0x4000u) { v = sh.ref[v]; hops++; }
+            sh.ref[r] = (uint16_t)v;
+            if (stats) { stats->hops += hops; if (hops > stats->maxhops) stats->maxhops = hops; }
+          }
+        }
+        WAVE_SYNC();
+        // flush: lane-contiguous 4-byte groups, external bytes gathered from dst
+        LANE_LOOP {
+          uint32_t a1 = LV(s1), a2 = LV(s2);
+          const uint32_t head = (uint32_t)((4u - (((uintptr_t)(dst + wbeg)) & 3u)) & 3u);  // bytes before the first aligned dword
+          for (uint32_t r = (uint32_t)lane; r < (head < wtotal ? head : wtotal); r += 64) {
+            const uint32_t v = sh.ref[r];
+            const uint32_t b = (v & 0x8000u) ? dst[wbeg - (v & 0x7fffu) - 1u] : (v & 0xffu);
+            dst[wbeg + r] = (uint8_t)b;
+            a1 += b; a2 = (uint32_t)((a2 + (uint64_t)((wbeg + r) % ADLER_MOD) * b) % ADLER_MOD);
+          }
+          for (uint32_t r = head + 4u * (uint32_t)lane; r < wtotal; r += 256u) {
+            const uint32_t n = wtotal - r < 4u ? wtotal - r : 4u;
+            uint32_t w = 0;
+            for (uint32_t k = 0; k < n; k++) {
+              const uint32_t v = sh.ref[r + k];
+              const uint32_t b = (v & 0x8000u) ? dst[wbeg - (v & 0x7fffu) - 1u] : (v & 0xffu);
+              w |= b << (8u * k);
+              a1 += b; a2 = (uint32_t)((a2 + (uint64_t)((wbeg + r + k) % ADLER_MOD) * b) % ADLER_MOD);
+            }
+            if (n == 4u) *(uint32_t*)(dst + wbeg + r) = w;
+            else for (uint32_t k = 0; k < n; k++) dst[wbeg + r + k] = (uint8_t)(w >> (8u * k));
+          }
+          LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
+        }
+        WAVE_SYNC_GLOBAL();
+        if (stats) { stats->lit_bytes += 0; }
+      } else {
+        // rounds: every lane walks its tokens in order; a match is copied once all
+        // source bytes outside the lane's own (sequentially written) region are final:
+        // earlier windows always are, other lanes' regions of this window are checked
+        // against their progress published at the end of the previous round.
+        LANE_VAR(int, lerr);
+        LANE_VAR(uint32_t, mybase);
+        LANE_LOOP { LV(lerr) = 0; LV(mybase) = LV(opos); sh.obase[lane] = LV(opos); sh.done[lane] = LV(opos); }
+        WAVE_SYNC();
+        const uint32_t wbeg = out;
+        for (;;) {
+          if (stats) stats->rounds++;
+          LANE_LOOP {
+            uint32_t t = LV(tcur), op = LV(opos), a1 = LV(s1), a2 = LV(s2);
+            const uint32_t te = LV(tend), my0 = LV(mybase);
+            while (t < te) {
+              const uint32_t v = sh.tok[t][lane];
+              if (!(v & T_MATCH)) {
+                dst[op] = (uint8_t)v;
+                a1 += v;
+                a2 = (uint32_t)((a2 + (uint64_t)(op % ADLER_MOD) * v) % ADLER_MOD);
+                if (stats) stats->lit_bytes++;
+                op++; t++;
+                continue;
+              }
+              const uint32_t len = (v >> 16) & 0x1ffu, d = (v & 0x7fffu) + 1u;
+              if (d > op) { LV(lerr) = 1; t = te; break; }  // invalid distance too far back
+              const uint32_t src = op - d;
+              const uint32_t e = src + (len < d ? len : d);
+              if (e > wbeg && src < my0) {
+                // bytes of other lanes' regions in [max(src, wbeg), min(e, my0))
+                const uint32_t x = src > wbeg ? src : wbeg;
+                int lo_j = 0, hi_j = lane - 1;       // largest j < lane with obase[j] <= x
+                while (lo_j < hi_j) {
+                  const int mid = (lo_j + hi_j + 1) >> 1;
+                  if (sh.obase[mid] <= x) lo_j = mid; else hi_j = mid - 1;
+                }
+                int ready = 1;
+                for (int j = lo_j; j < lane && sh.obase[j] < e; j++) {
+                  const uint32_t rend = sh.obase[j + 1];
+                  const uint32_t need = e < rend ? e : rend;
+                  if (sh.done[j] < need) { ready = 0; break; }
+                }
+                if (!ready) break;
+              }
+              // out[op + k] = out[src + k % d]; every source byte lies below op
+              uint32_t j = 0;
+              for (uint32_t k0 = 0; k0 < len; k0 += 16) {
+                uint8_t buf[16];
+                const uint32_t m = len - k0 < 16u ? len - k0 : 16u;
+                uint32_t jj = j;
+                for (uint32_t k = 0; k < m; k++) {
+                  buf[k] = dst[src + jj];
+                  jj++; if (jj == d) jj = 0;
+                }
+                for (uint32_t k = 0; k < m; k++) {
+                  const uint32_t q = op + k0 + k;
+                  dst[q] = buf[k];
+                  a1 += buf[k];
+                  a2 = (uint32_t)((a2 + (uint64_t)(q % ADLER_MOD) * buf[k]) % ADLER_MOD);
+                }
+                j = jj;
+              }
+              if (stats) { stats->matches++; stats->match_bytes += len; }
+              op += len; t++;
+            }
+            LV(tcur) = t; LV(opos) = op; LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
+          }
+          WAVE_SYNC_GLOBAL();
+          if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
+          LANE_LOOP { sh.done[lane] = LV(opos); }
+          WAVE_SYNC();
+          if (!WAVE_BALLOT(LV(tcur) < LV(tend))) break;
+        }
+      }
+      out += wtotal;
+      pos = npos;
+      if (end_lane >= 0) break;        // EOB: the next block header follows
+      // next segment length: keep about half of TMAX tokens per segment so the
+      // continuation has room
+      if (tune.adapt) {
+        const uint32_t used = npos - win_start;
+        const uint32_t bpt16 = ntok_valid ? (used * 16u) / ntok_valid : 16u * 8u;  // bits/token x16
+        const uint32_t target = (bpt16 * (uint32_t)TMAX) / (2u * 16u);
+        L = target < (uint32_t)LMIN ? (uint32_t)LMIN : target > (uint32_t)LMAX ? (uint32_t)LMAX : target;
+      }
+    }
+    if (bfinal) break;
+  }
+  // ---- trailer: adler32 (big-endian) after byte alignment ----
+  pos = (pos + 7u) & ~7u;
+  if (pos + 32u > limit_bits) return ST_TRUNC;
+  HZ_STAGE(sh, base, lo, hi, pos >> 5, 4u);
+  const uint32_t t32 = (uint32_t)(peek64(&sh, pos) & 0xffffffffu);
+  const uint32_t want = (t32 >> 24) | ((t32 >> 8) & 0xff00u) | ((t32 << 8) & 0xff0000u) | (t32 << 24);
+  uint64_t S1 = 0, S2 = 0;
+#if HZ_GPU
+  S1 = wave_sum64((uint64_t)s1);
+  S2 = wave_sum64((uint64_t)s2);
+#else
+  for (int lane = 0; lane < 64; lane++) { S1 += s1[lane]; S2 += s2[lane]; }
+#endif
+  const uint32_t A = (uint32_t)((1u + S1) % ADLER_MOD);
+  const uint32_t B = (uint32_t)(((uint64_t)(out % ADLER_MOD) * A + ADLER_MOD - (S2 % ADLER_MOD)) % ADLER_MOD);
+  if (((B << 16) | A) != want) return ST_DATA;
+  if (job.exact && out != dst_len) return ST_SIZE;
+  if (job.out_len) *job.out_len = out;
+  return ST_OK;
+}
+
+}  // namespace hz

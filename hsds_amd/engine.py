@@ -1,0 +1,136 @@
+"""Batched, device-resident chunk decode and hyperslab copies (torch tensors in HBM).
+
+This is the batched form of the DN hot loop: the reference decodes one chunk per
+request (datanode_lib.get_chunk -> get_chunk_bytes -> storUtil._uncompress,
+hsds/datanode_lib.py:796-945, 948-1142) and copies one selection per chunk
+(chunkUtil.chunkReadSelection, chunkUtil.py:882; chunk_crawl.py:418).  Here a whole
+request's chunks go to the GPU in one call.  torch is used only for device memory
+and streams; all byte work happens in the C-ABI kernels.
+"""
+import numpy as np
+import torch
+
+from . import _native as nat
+
+CHUNK_DESC_DTYPE = np.dtype([("src_off", "<u8"), ("src_len", "<u8"), ("dst_off", "<u8"), ("dst_len", "<u8")])
+COPY_DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("src_stride", "<i8", (nat.MAX_RANK,)),
+                            ("dst_stride", "<i8", (nat.MAX_RANK,)), ("count", "<i8", (nat.MAX_RANK,)),
+                            ("rank", "<i4"), ("itemsize", "<i4")])
+assert CHUNK_DESC_DTYPE.itemsize == 32 and COPY_DESC_DTYPE.itemsize == 216
+
+
+def _stream_handle(stream):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("device tensor expected")
+    return t.data_ptr()
+
+
+def to_device_bytes(arr, device):
+    """numpy structured / uint8 array -> uint8 tensor on `device`."""
+    raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+    return torch.from_numpy(raw.copy()).to(device, non_blocking=False)
+
+
+class ChunkEngine:
+    """Batched decode of HSDS chunk objects (F1 Blosc-zlib frames, F2 zlib+shuffle
+    streams, raw chunks) resident in device memory."""
+
+    def __init__(self, device=None):
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.eng = nat.engine(self.device.index)
+
+    def set_tuning(self, **kw):
+        self.eng.set_tuning(**kw)
+
+    def decode(self, src, chunk_descs, dst, status, compressor="zlib", shuffle=1, itemsize=1, stream=None):
+        """Asynchronously decode `chunk_descs` (uint8 device tensor holding
+        CHUNK_DESC_DTYPE records, or a numpy array of them) from `src` into `dst`;
+        per-chunk HSDS_* status codes land in `status` (int32 device tensor)."""
+        if isinstance(chunk_descs, np.ndarray):
+            n = chunk_descs.size
+            chunk_descs = to_device_bytes(chunk_descs, self.device)
+        else:
+            n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
+        comp = {None: 0, "": 0, "scaleoffset": 0, "gzip": 1, "deflate": 1, "zlib": 1}.get(compressor, 2)
+        rc = nat.lib().hsds_decode_batch(self.eng.h, _ptr(src), _ptr(chunk_descs), n, _ptr(dst),
+                                         dst.numel() * dst.element_size(), _ptr(status), comp, int(shuffle),
+                                         int(itemsize), _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_decode_batch")
+        return chunk_descs
+
+    def last_inflate_ms(self):
+        return self.eng.last_inflate_ms()
+
+    def copy(self, src, dst, copy_descs, stream=None, flags=None):
+        """Asynchronous strided region copies (COPY_DESC_DTYPE records)."""
+        if isinstance(copy_descs, np.ndarray):
+            n = copy_descs.size
+            copy_descs = to_device_bytes(copy_descs, self.device)
+        else:
+            n = copy_descs.numel() // COPY_DESC_DTYPE.itemsize
+        if flags is None:
+            rc = nat.lib().hsds_copy_batch(self.eng.h, _ptr(src), _ptr(dst), _ptr(copy_descs), n,
+                                           _stream_handle(stream))
+        else:
+            rc = nat.lib().hsds_copy_batch_if(self.eng.h, _ptr(src), _ptr(dst), _ptr(copy_descs), n,
+                                              _ptr(flags), _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_copy_batch")
+        return copy_descs
+
+    def compare(self, data, chunk, copy_descs, kind, differs, stream=None):
+        if isinstance(copy_descs, np.ndarray):
+            n = copy_descs.size
+            copy_descs = to_device_bytes(copy_descs, self.device)
+        else:
+            n = copy_descs.numel() // COPY_DESC_DTYPE.itemsize
+        rc = nat.lib().hsds_compare_batch(self.eng.h, _ptr(data), _ptr(chunk), _ptr(copy_descs), n, int(kind),
+                                          _ptr(differs), _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_compare_batch")
+        return copy_descs
+
+    def unshuffle(self, src, dst, itemsize, stream=None):
+        rc = nat.lib().hsds_unshuffle_device(self.eng.h, _ptr(src), src.numel(), int(itemsize), _ptr(dst),
+                                             _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_unshuffle_device")
+
+    def shuffle(self, src, dst, itemsize, stream=None):
+        rc = nat.lib().hsds_shuffle_device(self.eng.h, _ptr(src), src.numel(), int(itemsize), _ptr(dst),
+                                           _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_shuffle_device")
+
+
+def pack_chunks(blobs, dst_lens, align=256):
+    """Concatenate stored chunk blobs into one uint8 array and build descriptors.
+    Returns (src uint8 ndarray, descs CHUNK_DESC_DTYPE ndarray, dst_extent)."""
+    n = len(blobs)
+    descs = np.zeros(n, CHUNK_DESC_DTYPE)
+    off = 0
+    for i, b in enumerate(blobs):
+        descs[i]["src_off"] = off
+        descs[i]["src_len"] = len(b)
+        off += (len(b) + align - 1) // align * align
+    src = np.zeros(max(off, 1), np.uint8)
+    for i, b in enumerate(blobs):
+        o = int(descs[i]["src_off"])
+        src[o:o + len(b)] = np.frombuffer(b, np.uint8) if not isinstance(b, np.ndarray) else b
+    doff = 0
+    for i, L in enumerate(dst_lens):
+        descs[i]["dst_off"] = doff
+        descs[i]["dst_len"] = L
+        doff += (L + align - 1) // align * align
+    return src, descs, doff

@@ -1,0 +1,148 @@
+/*
+ * hsds_amd.h -- C ABI of the MI355X chunk codec / hyperslab engine for the HSDS
+ * data-node hot path.  Plain pointers and sizes only; every entry point returns
+ * 0 (or a byte count) on success and a negative HSDS_ERR_* code on failure.
+ *
+ * Reference interfaces replaced (paths relative to the HSDS 0.9.4 source tree):
+ *   hsds_uncompress      <- hsds/util/storUtil.py:182  _uncompress(data, compressor, shuffle, level, dtype, chunk_shape)
+ *   hsds_decode_batch    <- the per-chunk _uncompress loop of getStorBytes (storUtil.py:486-519),
+ *                           getHyperChunks (storUtil.py:557-580) and get_chunk_bytes
+ *                           (hsds/datanode_lib.py:796-945), batched over many chunks
+ *   hsds_shuffle         <- storUtil.py:94   _shuffle(codec=1, ...)   (numcodecs.Shuffle.encode)
+ *   hsds_unshuffle       <- storUtil.py:136  _unshuffle(codec=1, ...) (numcodecs.Shuffle.decode)
+ *   hsds_copy_batch      <- hsds/util/chunkUtil.py:882 chunkReadSelection (chunk_arr[slices]) and
+ *                           hsds/chunk_crawl.py:418 np_arr[data_sel] = chunk_arr (SN slab scatter),
+ *                           chunk_crawl.py:135 arr[data_sel] (SN write gather)
+ *   hsds_compare_batch + hsds_copy_batch_if
+ *                        <- chunkUtil.py:932 chunkWriteSelection (ndarray_compare, then chunk_arr[slices] = data)
+ *
+ * Threading: an engine is bound to one device and may be used from one host thread
+ * at a time (HSDS data nodes are single-threaded asyncio processes).  All *_batch
+ * calls are asynchronous on the given hipStream_t (pass NULL for the default
+ * stream); host-buffer calls are synchronous.
+ */
+#ifndef HSDS_AMD_H
+#define HSDS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (per call and per chunk) ------------------------------- */
+#define HSDS_OK 0
+#define HSDS_ERR_FRAME -1       /* malformed Blosc frame                          */
+#define HSDS_ERR_DATA -2        /* corrupt deflate data, bad adler32, bad header  */
+#define HSDS_ERR_TRUNC -3       /* stream ends before its end-of-stream marker    */
+#define HSDS_ERR_SIZE -4        /* decoded size differs from the expected size    */
+#define HSDS_ERR_UNSUPPORTED -5 /* other Blosc codec, bitshuffle, rank > 8 ...    */
+#define HSDS_ERR_ARG -6         /* invalid argument                               */
+#define HSDS_ERR_DEVICE -7      /* HIP runtime failure                            */
+
+/* compressor codes (storUtil._uncompress compressor argument) */
+#define HSDS_COMP_NONE 0        /* None / "scaleoffset"                           */
+#define HSDS_COMP_ZLIB 1        /* "gzip" / "deflate" / "zlib"                    */
+#define HSDS_COMP_OTHER 2       /* other Blosc codec name: only Blosc frames      */
+
+/* shuffle codes (storUtil.BYTE_SHUFFLE / BIT_SHUFFLE) */
+#define HSDS_SHUFFLE_NONE 0
+#define HSDS_SHUFFLE_BYTE 1
+#define HSDS_SHUFFLE_BIT 2      /* not supported (bitshuffle+LZ4)                 */
+
+#define HSDS_MAX_RANK 8
+
+typedef struct hsds_engine hsds_engine;
+
+/* One stored chunk in a batch: byte ranges in the batch source / destination. */
+typedef struct {
+  uint64_t src_off;  /* offset of the stored (compressed) bytes in the source buffer   */
+  uint64_t src_len;  /* stored length                                                  */
+  uint64_t dst_off;  /* offset of the decoded chunk in the destination buffer          */
+  uint64_t dst_len;  /* expected decoded size = prod(chunk_shape) * itemsize           */
+} hsds_chunk_desc;
+
+/* One strided N-d region copy (numpy basic-slicing semantics):
+ *   for every index tuple i (0 <= i[k] < count[k]):
+ *     dst[dst_off + sum i[k]*dst_stride[k]] <- src[src_off + sum i[k]*src_stride[k]]
+ * moving `itemsize` bytes per element.  Strides are in bytes and already include
+ * the slice step. */
+typedef struct {
+  uint64_t src_off;
+  uint64_t dst_off;
+  int64_t src_stride[HSDS_MAX_RANK];
+  int64_t dst_stride[HSDS_MAX_RANK];
+  int64_t count[HSDS_MAX_RANK];
+  int32_t rank;
+  int32_t itemsize;
+} hsds_copy_desc;
+
+/* element kinds for hsds_compare_batch (numpy array_equal semantics) */
+#define HSDS_KIND_BYTES 0       /* integers, bool, fixed strings: bytewise         */
+#define HSDS_KIND_F16 1
+#define HSDS_KIND_F32 2
+#define HSDS_KIND_F64 3
+#define HSDS_KIND_C64 4
+#define HSDS_KIND_C128 5
+
+/* ---- engine lifecycle ------------------------------------------------------ */
+int hsds_engine_create(int device, hsds_engine** out);
+void hsds_engine_destroy(hsds_engine* e);
+const char* hsds_version(void);
+const char* hsds_strerror(int status);
+
+/* Tuning of the inflate kernel (segment bits, warm-up bits, continuation bits,
+ * repair rounds).  Defaults are set by hsds_engine_create. */
+int hsds_set_tuning(hsds_engine* e, uint32_t seg_bits, uint32_t warmup_bits, uint32_t cont_bits,
+                    int32_t repair_rounds);
+
+/* ---- decode -------------------------------------------------------------- */
+/* Batched, device-resident decode.  d_src, d_chunks, d_dst, d_status are device
+ * pointers; decoded chunk k is written to d_dst + d_chunks[k].dst_off and its
+ * status (HSDS_OK or HSDS_ERR_*) to d_status[k].  compressor / shuffle / itemsize
+ * follow storUtil._uncompress: Blosc frames are detected per chunk
+ * (cbuffer_metainfo typesize > 0) and unshuffle themselves; otherwise a zlib
+ * stream is inflated (compressor == HSDS_COMP_ZLIB) and then byte-unshuffled
+ * with `itemsize` when shuffle == HSDS_SHUFFLE_BYTE.  dst_extent = bytes spanned by
+ * d_dst (max dst_off + dst_len); the engine keeps a staging buffer of that size
+ * for chunks that must be unshuffled after inflate. */
+int hsds_decode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks,
+                      int64_t nchunks, void* d_dst, uint64_t dst_extent, int32_t* d_status,
+                      int compressor, int shuffle, int itemsize, void* stream);
+
+/* Host-buffer single chunk: mirrors storUtil._uncompress.  Returns the decoded
+ * length (== expected) or a negative HSDS_ERR_* code.  expected < 0 means the
+ * size is unknown (zlib.decompress without a chunk shape): capacity is -expected
+ * and the actual decoded length is returned. */
+int64_t hsds_uncompress(hsds_engine* e, const void* src, int64_t srclen, int compressor, int shuffle,
+                        int itemsize, void* dst, int64_t expected);
+
+/* Device time (ms) of the inflate kernel of the most recent hsds_decode_batch,
+ * measured with HIP events on that call's stream (valid after the stream syncs). */
+int hsds_last_inflate_ms(hsds_engine* e, float* ms);
+
+/* ---- shuffle ------------------------------------------------------------- */
+int hsds_shuffle_device(hsds_engine* e, const void* d_src, int64_t n, int itemsize, void* d_dst,
+                        void* stream);
+int hsds_unshuffle_device(hsds_engine* e, const void* d_src, int64_t n, int itemsize, void* d_dst,
+                          void* stream);
+int hsds_shuffle(hsds_engine* e, const void* src, int64_t n, int itemsize, void* dst);
+int hsds_unshuffle(hsds_engine* e, const void* src, int64_t n, int itemsize, void* dst);
+
+/* ---- hyperslab selection ---------------------------------------------------- */
+int hsds_copy_batch(hsds_engine* e, const void* d_src, void* d_dst, const hsds_copy_desc* d_desc,
+                    int64_t n, void* stream);
+/* d_differs[k] = 1 if region k of d_a (chunk) differs from region k of d_b (data)
+ * under numpy array_equal semantics for `kind`, else 0.  The region geometry is
+ * desc.src_* for d_b and desc.dst_* for d_a (the write direction). */
+int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const hsds_copy_desc* d_desc,
+                       int64_t n, int kind, int32_t* d_differs, void* stream);
+/* copy only the descriptors whose d_flags[k] != 0 */
+int hsds_copy_batch_if(hsds_engine* e, const void* d_src, void* d_dst, const hsds_copy_desc* d_desc,
+                       int64_t n, const int32_t* d_flags, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HSDS_AMD_H */

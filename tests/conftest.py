@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    import numpy as np
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "codec_cases.json")))
+    arrs = np.load(os.path.join(ROOT, "tests", "golden", "codec_cases.npz"))
+    return d, arrs
+
+
+@pytest.fixture(scope="session")
+def selection_golden():
+    import json
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "selection_cases.json")))
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    from oracle import oracle as orc
+    orc.lib()
+    return orc
