@@ -189,6 +189,15 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
   __shared__ hz::Shared sh;
   const uint32_t total = offs[nchunks];
   const int lane = threadIdx.x;
+#ifdef HZ_PROFILE
+  HzProf prof_;
+  for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
+  prof_.last = __builtin_amdgcn_s_memtime();
+  prof_.cur = 0;
+  HzProf* prof = &prof_;
+#else
+  HzProf* prof = nullptr;
+#endif
   for (;;) {
     uint32_t item = 0;
     if (lane == 0) item = atomicAdd(counter, 1u);
@@ -210,11 +219,19 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
     } else {
       hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
                            (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr};
-      st = hz::inflate_stream<hz::Stats>(sh, job, tune, (hz::Stats*)nullptr);
+      st = hz::inflate_stream<hz::Stats>(sh, job, tune, (hz::Stats*)nullptr, prof);
     }
     if (lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
     __syncthreads();
   }
+#ifdef HZ_PROFILE
+  {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    prof_.acc[prof_.cur] += now - prof_.last;
+    if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&hz_prof[i], (unsigned long long)prof_.acc[i]);
+  }
+#endif
+  (void)prof;
 }
 
 // -------------------------------------------------------------------------
@@ -492,6 +509,20 @@ int hsds_decode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
                       int itemsize, void* stream) {
   return decode_batch_impl(e, d_src, d_chunks, nchunks, d_dst, dst_extent, d_status, compressor, shuffle, itemsize,
                            stream, 0, nullptr);
+}
+
+int hsds_debug_profile(unsigned long long* out16, int reset) {
+#ifdef HZ_PROFILE
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(hz_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hz_prof), z, sizeof(z)) != hipSuccess) return HSDS_ERR_DEVICE;
+  }
+  return HSDS_OK;
+#else
+  (void)out16; (void)reset;
+  return HSDS_ERR_UNSUPPORTED;
+#endif
 }
 
 int hsds_last_inflate_ms(hsds_engine* e, float* ms) {

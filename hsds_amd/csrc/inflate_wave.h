@@ -50,11 +50,24 @@
 #define WAVE_SYNC_GLOBAL() do {} while (0)
 #endif
 
+#if HZ_GPU && defined(HZ_PROFILE)
+__device__ unsigned long long hz_prof[16];
+struct HzProf { uint64_t acc[16]; uint64_t last; int cur; };
+#define HZ_T(slot)                                                                          \
+  do { if (prof) { const uint64_t _now = __builtin_amdgcn_s_memtime();                      \
+       prof->acc[prof->cur] += _now - prof->last; prof->last = _now; prof->cur = (slot); } } while (0)
+#else
+struct HzProf { int unused; };
+#define HZ_T(slot) do {} while (0)
+#endif
+
 namespace hz {
 
 constexpr int WAVE = 64;
 constexpr int LL_ROOT = 10;
 constexpr int D_ROOT = 8;
+constexpr int LL_SUB = 512;         // second-level entries (codes longer than the root)
+constexpr int D_SUB = 256;
 constexpr int TMAX = 64;            // tokens stored per lane per window
 constexpr int LMAX = 512;           // max segment length (bits)
 constexpr int LMIN = 64;
@@ -76,7 +89,7 @@ constexpr int ST_SIZE = -4;
 constexpr int ST_UNSUP = -5;
 
 // decode-table entry: bits 0-3 code length, 4-7 extra bits, 8-10 kind, 16-31 value
-enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SLOW = 3, K_BAD = 4 };
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SLOW = 3, K_BAD = 4, K_SUB = 5 };
 HZ_HD uint32_t ent(uint32_t kind, uint32_t nbits, uint32_t extra, uint32_t value) {
   return nbits | (extra << 4) | (kind << 8) | (value << 16);
 }
@@ -94,8 +107,10 @@ constexpr uint32_t T_ERR = 0x40000001u;
 constexpr int S_NONE = 0, S_EOB = 1, S_ERR = 2;
 
 struct Shared {
-  uint32_t lut_ll[1 << LL_ROOT];
-  uint32_t lut_d[1 << D_ROOT];
+  uint32_t lut_ll[(1 << LL_ROOT) + LL_SUB];
+  uint32_t lut_d[(1 << D_ROOT) + D_SUB];
+  uint16_t tb_first[16];
+  uint16_t tb_offs[17];
   uint32_t tok[TMAX][WAVE];          // token-major: lane-parallel accesses hit 64 banks
   uint32_t bitmap[WAVE][BM_WORDS];
   uint32_t in32[IN_WORDS + 4];
@@ -195,6 +210,7 @@ HZ_HD uint32_t canon_decode(const uint16_t* cnt, const uint16_t* sorted, uint64_
 
 HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
+  if (e_kind(e) == K_SUB) e = sh->lut_ll[e_val(e) + ((uint32_t)(bits >> LL_ROOT) & bmask(e_extra(e)))];
   if (e_kind(e) == K_SLOW) {
     uint32_t r = canon_decode(sh->cnt_ll, sh->sorted_ll, bits);
     e = (r == 0xffffffffu) ? ent(K_BAD, 1, 0, 0) : ll_entry(r & 0xffff, r >> 16);
@@ -203,6 +219,7 @@ HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
 }
 HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_d[bits & ((1u << D_ROOT) - 1)];
+  if (e_kind(e) == K_SUB) e = sh->lut_d[e_val(e) + ((uint32_t)(bits >> D_ROOT) & bmask(e_extra(e)))];
   if (e_kind(e) == K_SLOW) {
     uint32_t r = canon_decode(sh->cnt_d, sh->sorted_d, bits);
     e = (r == 0xffffffffu) ? ent(K_BAD, 1, 0, 0) : d_entry(r & 0xffff, r >> 16);
@@ -233,6 +250,63 @@ HZ_HD void decode_token(const Shared* sh, uint32_t p, uint32_t& tokv, uint32_t& 
   }
   if (kind == K_EOB) { tokv = T_EOB; adv = nb; return; }
   tokv = T_ERR; adv = 1;
+}
+
+
+// ---- register bit reader over the staged window ------------------------------
+// bb holds `avail` (>= 32 after fill) bits starting at bit position `pos`; the next
+// staged dword is prefetched into `nxt` so a refill never waits on LDS.
+struct BitRd {
+  uint64_t bb;
+  uint32_t avail;
+  uint32_t widx;
+  uint32_t nxt;
+  uint32_t pos;
+};
+
+HZ_HD void br_init(const Shared* sh, BitRd& r, uint32_t p, uint32_t stage_base) {
+  const uint32_t w = p - stage_base, i = w >> 5, s = w & 31u;
+  const uint64_t lo = (uint64_t)sh->in32[i] | ((uint64_t)sh->in32[i + 1] << 32);
+  r.bb = lo >> s;
+  r.avail = 64u - s;
+  r.widx = i + 2u;
+  r.nxt = sh->in32[i + 2];
+  r.pos = p;
+}
+
+HZ_HD void br_fill(const Shared* sh, BitRd& r) {
+  if (r.avail < 32u) {
+    r.bb |= (uint64_t)r.nxt << r.avail;
+    r.avail += 32u;
+    r.widx++;
+    r.nxt = sh->in32[r.widx];
+  }
+}
+
+HZ_HD void br_drop(BitRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n; }
+
+// decode one token at r.pos and advance past it.  Invalid codes advance by their
+// table length (any deterministic advance keeps speculative decoders consistent;
+// a real error stops the stream at the ERR token's start).
+HZ_HD uint32_t next_token(const Shared* sh, BitRd& r) {
+  br_fill(sh, r);
+  const uint32_t e = lookup_ll(sh, r.bb);
+  const uint32_t kind = e_kind(e), nb = e_bits(e);
+  if (kind == K_LIT) { br_drop(r, nb); return e_val(e); }
+  if (kind == K_LEN) {
+    const uint32_t xb = e_extra(e);
+    const uint32_t len = e_val(e) + ((uint32_t)(r.bb >> nb) & bmask(xb));
+    br_drop(r, nb + xb);
+    br_fill(sh, r);
+    const uint32_t ed = lookup_d(sh, r.bb);
+    if (e_kind(ed) != K_LEN) { br_drop(r, e_bits(ed)); return T_ERR; }
+    const uint32_t nd = e_bits(ed), xd = e_extra(ed);
+    const uint32_t dist = e_val(ed) + ((uint32_t)(r.bb >> nd) & bmask(xd));
+    br_drop(r, nd + xd);
+    return T_MATCH | (len << 16) | (dist - 1u);
+  }
+  br_drop(r, nb ? nb : 1u);
+  return kind == K_EOB ? T_EOB : T_ERR;
 }
 
 HZ_HD void mark_bit(Shared* sh, int lane, uint32_t rel) {
@@ -273,7 +347,8 @@ HZ_HD uint32_t load_word(const uint8_t* base, uint32_t k, uint32_t lo, uint32_t 
 
 // ---- wave-collective helpers (the only places the two drivers differ) -------
 #if HZ_GPU
-#define WAVE_BALLOT(expr) ((uint64_t)__ballot((expr) ? 1 : 0))
+#define WAVE_BALLOT(expr) \
+  ([&]() { const int lane = (int)threadIdx.x; (void)lane; return (uint64_t)__ballot((expr) ? 1 : 0); }())
 namespace hz {
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
   uint32_t x = v;
@@ -326,6 +401,7 @@ struct TableArgs {
   uint32_t* lut;
   int root;
   int kind;
+  int nsub;     // second-level capacity after the 2^root root entries
 };
 
 }  // namespace hz
@@ -348,9 +424,18 @@ struct TableArgs {
         }                                                                               \
         if (!bad && maxl > 0 && left > 0 && ((A).kind == 0 || maxl != 1)) bad = 1;      \
         if ((A).kind == 0 && maxl == 0) bad = 1;                                        \
-        /* sorted symbols in canonical order */                                         \
+        /* sorted symbols in canonical order; first code / offset per length */         \
         int offs[16]; offs[1] = 0;                                                      \
         for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + (A).cnt[l];                \
+        {                                                                               \
+          int code = 0;                                                                 \
+          for (int l = 1; l <= 15; l++) {                                               \
+            code = (code + (l > 1 ? (A).cnt[l - 1] : 0)) << 1;                          \
+            (sh).tb_first[l] = (uint16_t)code;                                          \
+            (sh).tb_offs[l] = (uint16_t)offs[l];                                        \
+          }                                                                             \
+          (sh).tb_offs[16] = (uint16_t)(offs[15] + (A).cnt[15]);                        \
+        }                                                                               \
         for (int s = 0; s < (A).n; s++) if ((A).lens[s]) (A).sorted[offs[(A).lens[s]]++] = (uint16_t)s; \
         (sh).u_status = bad ? hz::ST_DATA : hz::ST_OK;                                  \
       }                                                                                 \
@@ -376,6 +461,52 @@ struct TableArgs {
       }                                                                                 \
     }                                                                                   \
     WAVE_SYNC();                                                                        \
+    /* second level: lane 0 allocates one subtable per root prefix of longer codes */  \
+    const int _R = (A).root;                                                            \
+    const int _k0 = (sh).tb_offs[_R + 1], _k1 = (sh).tb_offs[16];                       \
+    if (_k1 > _k0) {                                                                    \
+      LANE_LOOP {                                                                       \
+        if (lane == 0) {                                                                \
+          int used = 0, k = _k0;                                                        \
+          while (k < _k1) {                                                             \
+            /* codes with the same root prefix are contiguous in canonical order */     \
+            const int l0 = (A).lens[(A).sorted[k]];                                     \
+            const int p = ((int)(sh).tb_first[l0] + (k - (int)(sh).tb_offs[l0])) >> (l0 - _R); \
+            int k2 = k, lmax = l0;                                                      \
+            while (k2 < _k1) {                                                          \
+              const int l2 = (A).lens[(A).sorted[k2]];                                  \
+              const int p2 = ((int)(sh).tb_first[l2] + (k2 - (int)(sh).tb_offs[l2])) >> (l2 - _R); \
+              if (p2 != p) break;                                                       \
+              lmax = l2; k2++;                                                          \
+            }                                                                           \
+            const int sb = lmax - _R;                                                   \
+            if (used + (1 << sb) <= (A).nsub)                                           \
+              (A).lut[hz::rev_bits((uint32_t)p, _R)] =                                  \
+                  hz::ent(hz::K_SUB, _R, sb, (uint32_t)((1 << _R) + used));             \
+            used += 1 << sb;                                                            \
+            k = k2;                                                                     \
+          }                                                                             \
+        }                                                                               \
+      }                                                                                 \
+      WAVE_SYNC();                                                                      \
+      /* fill subtables by symbol (zlib-style replication) */                           \
+      LANE_LOOP {                                                                       \
+        for (int k = _k0 + lane; k < _k1; k += 64) {                                    \
+          const uint32_t sym = (A).sorted[k];                                           \
+          const int len = (A).lens[sym];                                                \
+          const int c = (int)(sh).tb_first[len] + (k - (int)(sh).tb_offs[len]);         \
+          const int p = c >> (len - _R);                                                \
+          const uint32_t re = (A).lut[hz::rev_bits((uint32_t)p, _R)];                   \
+          if (hz::e_kind(re) != hz::K_SUB) continue;                                    \
+          const int sb = (int)hz::e_extra(re), off = (int)hz::e_val(re);                \
+          const int tl = len - _R;                                                      \
+          const uint32_t j0 = hz::rev_bits((uint32_t)(c & ((1 << tl) - 1)), tl);        \
+          const uint32_t e = (A).kind == 1 ? hz::ll_entry(sym, len) : hz::d_entry(sym, len); \
+          for (int m = 0; m < (1 << (sb - tl)); m++) (A).lut[off + (j0 | (m << tl))] = e; \
+        }                                                                               \
+      }                                                                                 \
+      WAVE_SYNC();                                                                      \
+    }                                                                                   \
     status_out = (sh).u_status;                                                         \
   } while (0)
 
@@ -434,7 +565,8 @@ __device__
 #else
 static
 #endif
-int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* stats) {
+int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* stats, HzProf* prof = nullptr) {
+  (void)prof;
   // aligned base so that every staged dword load is aligned
   const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 3u);
   const uint8_t* base = job.src - a;
@@ -461,6 +593,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
   uint32_t L = tune.L0 < (uint32_t)LMIN ? (uint32_t)LMIN : tune.L0 > (uint32_t)LMAX ? (uint32_t)LMAX : tune.L0;
 
   for (;;) {  // ---- deflate blocks ----
+    HZ_T(1);
     HZ_STAGE(sh, base, lo, hi, pos >> 5, 128u);
     if (pos + 3u > limit_bits) return ST_TRUNC;
     const uint32_t h3 = (uint32_t)(peek64(&sh, pos) & 7u);
@@ -497,6 +630,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       continue;
     }
     // ---- Huffman code lengths ----
+    HZ_T(2);
     uint32_t nlen = 288, ndist = 32;
     if (btype == 1) {
       LANE_LOOP {
@@ -578,10 +712,11 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
     }
     {
       int bst = ST_OK;
-      TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1};
+      TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB};
+      HZ_T(3);
       HZ_BUILD_TABLE(sh, tll, bst);
       if (bst != ST_OK) return bst;
-      TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2};
+      TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB};
       HZ_BUILD_TABLE(sh, td, bst);
       if (bst != ST_OK) return bst;
     }
@@ -589,6 +724,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
     // ---- windows over the Huffman block ----
     for (;;) {
       if (stats) stats->windows++;
+      HZ_T(4);
       const uint32_t win_start = pos;
       const uint32_t W = tune.W, C = tune.C;
       {
@@ -597,9 +733,11 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
         HZ_STAGE(sh, base, lo, hi, first_bit >> 5, words);
       }
 
+      HZ_T(5);
       // -------- Phase A: speculative decode of 64 segments --------
       // lane i decodes from (segment start - W); tokens whose start lies inside its
       // own segment [ss, ss+L) are stored and their start bits marked.
+      const uint32_t stage_base = ((win_start >= W ? win_start - W : 0u) >> 5) * 32u;
       LANE_VAR(uint32_t, seg_start);
       LANE_VAR(uint32_t, ntok);
       LANE_VAR(int, storing);
@@ -607,72 +745,80 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       LANE_LOOP {
         const uint32_t ss = win_start + (uint32_t)lane * L;
         const uint32_t se = ss + L;
-        uint32_t p = (lane > 0 && ss - win_start > W) ? ss - W : win_start;
-        int st = p >= ss;
+        const uint32_t p0 = (lane > 0 && ss - win_start > W) ? ss - W : win_start;
+        int st = p0 >= ss;
         uint32_t nt = 0, steps = 0;
         for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
         uint32_t mw_idx = 0, mw = 0;  // bitmap word cached in a register (monotonic positions)
-        for (;;) {
-          if (p >= se) break;
-          if (!st && p >= ss) st = 1;
+        BitRd r;
+        br_init(&sh, r, p0, stage_base);
+        while (r.pos < se) {
+          if (!st && r.pos >= ss) st = 1;
           if (st && nt >= (uint32_t)TMAX) break;
-          uint32_t tokv, adv;
-          decode_token(&sh, p, tokv, adv);
+          const uint32_t tp = r.pos;
+          const uint32_t tokv = next_token(&sh, r);
           steps++;
           if (st) {
-            const uint32_t rel = p - ss, wi = rel >> 5;
+            const uint32_t rel = tp - ss, wi = rel >> 5;
             if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
             mw |= 1u << (rel & 31u);
             sh.tok[nt][lane] = tokv;
             nt++;
           }
-          p += adv;
         }
         if (st) {
           sh.bitmap[lane][mw_idx] |= mw;
-          mark_bit(&sh, lane, p - ss);   // exit boundary (start of the next token)
+          mark_bit(&sh, lane, r.pos - ss);   // exit boundary (start of the next token)
         }
         LV(seg_start) = ss;
         LV(ntok) = nt;
         LV(storing) = st;
         LV(nsteps) = steps;
-        sh.exitpos[lane] = p;
+        sh.exitpos[lane] = r.pos;
         sh.syncpos[lane] = 0xffffffffu;
       }
       WAVE_SYNC();
 
+      HZ_T(6);
       // -------- Phase A': continuation --------
       // lane i keeps decoding from its exit until it reaches a token start that
       // lane i+1 marked (then both decodes coincide from there on), for at most C
       // bits into segment i+1.  Tokens decoded here belong to lane i.
       LANE_LOOP {
         const uint32_t ss = LV(seg_start);
-        uint32_t p = sh.exitpos[lane], nt = LV(ntok), steps = 0;
+        uint32_t nt = LV(ntok), steps = 0;
+        uint32_t pend = sh.exitpos[lane];
         if (lane < 63 && LV(storing)) {
           const uint32_t ssn = ss + L;
+          BitRd r;
+          br_init(&sh, r, pend, stage_base);
+          uint32_t nw_idx = 0xffffffffu, nw = 0;     // cached word of lane+1's bitmap
+          uint32_t mw_idx = (r.pos - ss) >> 5, mw = 0;
           for (;;) {
-            const uint32_t reln = p - ssn;
-            if (p >= ssn && reln < (uint32_t)(BM_WORDS * 32) &&
-                ((sh.bitmap[lane + 1][reln >> 5] >> (reln & 31u)) & 1u)) {
-              sh.syncpos[lane + 1] = p;
-              break;
+            const uint32_t reln = r.pos - ssn;
+            if (r.pos >= ssn && reln < (uint32_t)(BM_WORDS * 32)) {
+              if ((reln >> 5) != nw_idx) { nw_idx = reln >> 5; nw = sh.bitmap[lane + 1][nw_idx]; }
+              if ((nw >> (reln & 31u)) & 1u) { sh.syncpos[lane + 1] = r.pos; break; }
             }
-            if (p >= ssn + C || nt >= (uint32_t)TMAX) break;
-            uint32_t tokv, adv;
-            decode_token(&sh, p, tokv, adv);
+            if (r.pos >= ssn + C || nt >= (uint32_t)TMAX) break;
+            const uint32_t rel = r.pos - ss, wi = rel >> 5;
+            const uint32_t tokv = next_token(&sh, r);
             steps++;
-            mark_bit(&sh, lane, p - ss);
+            if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
+            mw |= 1u << (rel & 31u);
             sh.tok[nt][lane] = tokv;
             nt++;
-            p += adv;
           }
-          mark_bit(&sh, lane, p - ss);     // final boundary of this lane's decode
+          if (mw_idx < (uint32_t)BM_WORDS) sh.bitmap[lane][mw_idx] |= mw;
+          pend = r.pos;
+          mark_bit(&sh, lane, pend - ss);     // final boundary of this lane's decode
         }
         LV(ntok) = nt;
         LV(nsteps) += steps;
-        sh.contpos[lane] = p;
+        sh.contpos[lane] = pend;
       }
       WAVE_SYNC();
+      HZ_T(7);
       // -------- repair rounds --------
       // A lane whose predecessor's continuation never met one of its marks is
       // "failed": its speculative path had not merged with the true path.  It
@@ -695,41 +841,44 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
           uint32_t steps = 0;
           if (redo) {
             const uint32_t ss = LV(seg_start), se = ss + L;
-            uint32_t p = sh.contpos[lane - 1];
             uint32_t nt = 0;
             for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
-            // segment part (starts at a true boundary, possibly before or after ss)
-            while (p < se && nt < (uint32_t)TMAX) {
-              uint32_t tokv, adv;
-              decode_token(&sh, p, tokv, adv);
+            BitRd r;
+            br_init(&sh, r, sh.contpos[lane - 1], stage_base);
+            uint32_t mw_idx = (r.pos - ss) >> 5, mw = 0;
+            // segment part (starts at a true boundary at or after ss)
+            while (r.pos < se && nt < (uint32_t)TMAX) {
+              const uint32_t rel = r.pos - ss, wi = rel >> 5;
+              const uint32_t tokv = next_token(&sh, r);
               steps++;
-              mark_bit(&sh, lane, p - ss);
+              if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
+              mw |= 1u << (rel & 31u);
               sh.tok[nt][lane] = tokv;
               nt++;
-              p += adv;
             }
             if (lane < 63) {
               const uint32_t ssn = se;
               if (!next_failed) sh.syncpos[lane + 1] = 0xffffffffu;
+              uint32_t nw_idx = 0xffffffffu, nw = 0;
               for (;;) {
-                const uint32_t reln = p - ssn;
-                if (!next_failed && p >= ssn && reln < (uint32_t)(BM_WORDS * 32) &&
-                    ((sh.bitmap[lane + 1][reln >> 5] >> (reln & 31u)) & 1u)) {
-                  sh.syncpos[lane + 1] = p;
-                  break;
+                const uint32_t reln = r.pos - ssn;
+                if (!next_failed && r.pos >= ssn && reln < (uint32_t)(BM_WORDS * 32)) {
+                  if ((reln >> 5) != nw_idx) { nw_idx = reln >> 5; nw = sh.bitmap[lane + 1][nw_idx]; }
+                  if ((nw >> (reln & 31u)) & 1u) { sh.syncpos[lane + 1] = r.pos; break; }
                 }
-                if (next_failed || p >= ssn + C || nt >= (uint32_t)TMAX) break;
-                uint32_t tokv, adv;
-                decode_token(&sh, p, tokv, adv);
+                if (next_failed || r.pos >= ssn + C || nt >= (uint32_t)TMAX) break;
+                const uint32_t rel = r.pos - ss, wi = rel >> 5;
+                const uint32_t tokv = next_token(&sh, r);
                 steps++;
-                mark_bit(&sh, lane, p - ss);
+                if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
+                mw |= 1u << (rel & 31u);
                 sh.tok[nt][lane] = tokv;
                 nt++;
-                p += adv;
               }
             }
-            mark_bit(&sh, lane, p - ss);
-            sh.contpos[lane] = p;
+            if (mw_idx < (uint32_t)BM_WORDS) sh.bitmap[lane][mw_idx] |= mw;
+            mark_bit(&sh, lane, r.pos - ss);
+            sh.contpos[lane] = r.pos;
             sh.syncpos[lane] = sh.contpos[lane - 1];   // whole token list is valid
             LV(ntok) = nt;
           }
@@ -753,6 +902,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
 #endif
       }
 
+      HZ_T(8);
       // -------- Phase B: validity --------
       LANE_VAR(uint32_t, tok_first);
       LANE_VAR(uint32_t, tok_end);
@@ -790,6 +940,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       if (end_lane >= 0) V = (uint32_t)end_lane + 1u;
       if (stats) stats->lanes_valid += V;
 
+      HZ_T(9);
       // -------- Phase C: emit --------
       LANE_VAR(uint32_t, tcur);
       LANE_VAR(uint32_t, tend);
@@ -812,182 +963,164 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       if (end_lane >= 0 && sh.u_status == 2) {
         return sh.u_pos + 64u > limit_bits ? ST_TRUNC : ST_DATA;
       }
-      LANE_VAR(uint32_t, opos);
-      uint32_t wtotal = 0;
-      uint32_t ntok_valid = 0;
+      HZ_T(10);
+      // output offsets; the window keeps only what fits the LDS reference map
+      LANE_VAR(uint32_t, obase);
 #if HZ_GPU
-      {
-        const uint32_t ob = wave_excl_scan(olen, (int)threadIdx.x);
-        wtotal = wave_sum(olen);
-        ntok_valid = wave_sum(tend - tcur);
-        opos = out + ob;
-      }
+      obase = wave_excl_scan(olen, (int)threadIdx.x);
 #else
-      for (int lane = 0; lane < 64; lane++) {
-        opos[lane] = out + wtotal; wtotal += olen[lane]; ntok_valid += tend[lane] - tcur[lane];
+      { uint32_t acc = 0; for (int lane = 0; lane < 64; lane++) { obase[lane] = acc; acc += olen[lane]; } }
+#endif
+      uint32_t npos;
+      {
+        const uint64_t over = WAVE_BALLOT((uint32_t)lane < V && LV(obase) + LV(olen) > (uint32_t)SCAP);
+        uint32_t k = 0;
+        while (k < V && !((over >> k) & 1ull)) k++;
+        if (k < V) {
+          if (k == 0) {
+            // lane 0 alone overflows: keep its first tokens that fit (>= 1 token)
+            LANE_LOOP {
+              if (lane == 0) {
+                uint32_t t = LV(tcur), acc = 0;
+                while (t < LV(tend)) {
+                  const uint32_t v = sh.tok[t][lane];
+                  const uint32_t n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+                  if (acc + n > (uint32_t)SCAP) break;
+                  acc += n; t++;
+                }
+                LV(tend) = t; LV(olen) = acc;
+                sh.u_pos = win_start + nth_mark(&sh, lane, t);
+              }
+            }
+            WAVE_SYNC();
+            npos = sh.u_pos;
+            V = 1;
+          } else {
+            V = k;
+            npos = sh.contpos[k - 1];
+          }
+          end_lane = -1;                 // an EOB beyond the cut is met again next window
+          LANE_LOOP { if ((uint32_t)lane >= V) { LV(tcur) = 0; LV(tend) = 0; LV(olen) = 0; } }
+        } else {
+          npos = end_lane >= 0 ? sh.u_pos : sh.contpos[V - 1];
+        }
       }
+      uint32_t wtotal = 0, ntok_valid = 0;
+#if HZ_GPU
+      wtotal = wave_sum(olen);
+      ntok_valid = wave_sum(tend - tcur);
+#else
+      for (int lane = 0; lane < 64; lane++) { wtotal += olen[lane]; ntok_valid += tend[lane] - tcur[lane]; }
 #endif
       if (stats) stats->tokens += ntok_valid;
       if (out + wtotal > dst_len) return ST_SIZE;
-      const uint32_t npos = end_lane >= 0 ? sh.u_pos : sh.contpos[V - 1];
       if (npos > limit_bits) return ST_TRUNC;
 
-      if (wtotal <= (uint32_t)SCAP) {
-        // ---- LDS path: byte-level source map, chased to literals / earlier output ----
-        // ref[r] for window byte r: 0x4000|b literal, r' < 0x4000 internal reference,
-        // 0x8000|(x-1) byte x positions before the window (already final in dst).
-        const uint32_t wbeg = out;
-        LANE_VAR(int, lerr);
-        LANE_LOOP {
-          int err = 0;
-          uint32_t op = LV(opos);
-          for (uint32_t t = LV(tcur); t < LV(tend); t++) {
-            const uint32_t v = sh.tok[t][lane];
-            if (!(v & T_MATCH)) { sh.ref[op - wbeg] = (uint16_t)(0x4000u | v); op++; continue; }
-            const uint32_t len = (v >> 16) & 0x1ffu, d = (v & 0x7fffu) + 1u;
-            if (d > op) { err = 1; break; }          // invalid distance too far back
+      // ---- byte-level source map in LDS ----
+      // ref[r] for window byte r: 0x4000|b literal, r' < 0x4000 internal reference,
+      // 0x8000|(x-1) the byte x positions before the window (final in dst).
+      const uint32_t wbeg = out;
+      LANE_VAR(int, lerr);
+      LANE_LOOP {
+        int err = 0;
+        uint32_t op = LV(obase);                  // window-relative
+        for (uint32_t t = LV(tcur); t < LV(tend); t++) {
+          const uint32_t v = sh.tok[t][lane];
+          if (!(v & T_MATCH)) { sh.ref[op] = (uint16_t)(0x4000u | v); op++; continue; }
+          const uint32_t len = (v >> 16) & 0x1ffu, d = (v & 0x7fffu) + 1u;
+          if (d > wbeg + op) { err = 1; break; }  // invalid distance too far back
+          if (stats) { stats->matches++; stats->match_bytes += len; }
+          if (d <= op) {                          // source inside the window
             uint32_t jj = 0;
             for (uint32_t k = 0; k < len; k++) {
-              const uint32_t q = op - d + jj;         // source of byte op+k
-              sh.ref[op + k - wbeg] = q >= wbeg ? (uint16_t)(q - wbeg) : (uint16_t)(0x8000u | (wbeg - q - 1u));
+              sh.ref[op + k] = (uint16_t)(op - d + jj);
               jj++; if (jj == d) jj = 0;
             }
-            op += len;
-          }
-          LV(lerr) = err;
-        }
-        WAVE_SYNC();
-        if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
-        if (stats) stats->rounds++;
-        // chase: references strictly decrease, so every chain ends in a literal or
-        // an external byte; resolved values are written back (benign races: every
-        // stored value is a valid ancestor of the position)
-        LANE_LOOP {
-          for (uint32_t r = (uint32_t)lane; r < wtotal; r += 64) {
-            uint32_t v = sh.ref[r];
-            uint32_t hops = 0;
-            while (v < 0x4000u) { v = sh.ref[v]; hops++; }
-            sh.ref[r] = (uint16_t)v;
-            if (stats) { stats->hops += hops; if (hops > stats->maxhops) stats->maxhops = hops; }
-          }
-        }
-        WAVE_SYNC();
-        // flush: lane-contiguous 4-byte groups, external bytes gathered from dst
-        LANE_LOOP {
-          uint32_t a1 = LV(s1), a2 = LV(s2);
-          const uint32_t head = (uint32_t)((4u - (((uintptr_t)(dst + wbeg)) & 3u)) & 3u);  // bytes before the first aligned dword
-          for (uint32_t r = (uint32_t)lane; r < (head < wtotal ? head : wtotal); r += 64) {
-            const uint32_t v = sh.ref[r];
-            const uint32_t b = (v & 0x8000u) ? dst[wbeg - (v & 0x7fffu) - 1u] : (v & 0xffu);
-            dst[wbeg + r] = (uint8_t)b;
-            a1 += b; a2 = (uint32_t)((a2 + (uint64_t)((wbeg + r) % ADLER_MOD) * b) % ADLER_MOD);
-          }
-          for (uint32_t r = head + 4u * (uint32_t)lane; r < wtotal; r += 256u) {
-            const uint32_t n = wtotal - r < 4u ? wtotal - r : 4u;
-            uint32_t w = 0;
-            for (uint32_t k = 0; k < n; k++) {
-              const uint32_t v = sh.ref[r + k];
-              const uint32_t b = (v & 0x8000u) ? dst[wbeg - (v & 0x7fffu) - 1u] : (v & 0xffu);
-              w |= b << (8u * k);
-              a1 += b; a2 = (uint32_t)((a2 + (uint64_t)((wbeg + r + k) % ADLER_MOD) * b) % ADLER_MOD);
+          } else {
+            uint32_t jj = 0;
+            for (uint32_t k = 0; k < len; k++) {
+              const uint32_t back = d - jj;       // source = window start - (back - op)
+              sh.ref[op + k] = back > op ? (uint16_t)(0x8000u | (back - op - 1u)) : (uint16_t)(op - back);
+              jj++; if (jj == d) jj = 0;
             }
-            if (n == 4u) *(uint32_t*)(dst + wbeg + r) = w;
-            else for (uint32_t k = 0; k < n; k++) dst[wbeg + r + k] = (uint8_t)(w >> (8u * k));
           }
-          LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
+          op += len;
         }
-        WAVE_SYNC_GLOBAL();
-        if (stats) { stats->lit_bytes += 0; }
-      } else {
-        // rounds: every lane walks its tokens in order; a match is copied once all
-        // source bytes outside the lane's own (sequentially written) region are final:
-        // earlier windows always are, other lanes' regions of this window are checked
-        // against their progress published at the end of the previous round.
-        LANE_VAR(int, lerr);
-        LANE_VAR(uint32_t, mybase);
-        LANE_LOOP { LV(lerr) = 0; LV(mybase) = LV(opos); sh.obase[lane] = LV(opos); sh.done[lane] = LV(opos); }
-        WAVE_SYNC();
-        const uint32_t wbeg = out;
-        for (;;) {
-          if (stats) stats->rounds++;
-          LANE_LOOP {
-            uint32_t t = LV(tcur), op = LV(opos), a1 = LV(s1), a2 = LV(s2);
-            const uint32_t te = LV(tend), my0 = LV(mybase);
-            while (t < te) {
-              const uint32_t v = sh.tok[t][lane];
-              if (!(v & T_MATCH)) {
-                dst[op] = (uint8_t)v;
-                a1 += v;
-                a2 = (uint32_t)((a2 + (uint64_t)(op % ADLER_MOD) * v) % ADLER_MOD);
-                if (stats) stats->lit_bytes++;
-                op++; t++;
-                continue;
-              }
-              const uint32_t len = (v >> 16) & 0x1ffu, d = (v & 0x7fffu) + 1u;
-              if (d > op) { LV(lerr) = 1; t = te; break; }  // invalid distance too far back
-              const uint32_t src = op - d;
-              const uint32_t e = src + (len < d ? len : d);
-              if (e > wbeg && src < my0) {
-                // bytes of other lanes' regions in [max(src, wbeg), min(e, my0))
-                const uint32_t x = src > wbeg ? src : wbeg;
-                int lo_j = 0, hi_j = lane - 1;       // largest j < lane with obase[j] <= x
-                while (lo_j < hi_j) {
-                  const int mid = (lo_j + hi_j + 1) >> 1;
-                  if (sh.obase[mid] <= x) lo_j = mid; else hi_j = mid - 1;
-                }
-                int ready = 1;
-                for (int j = lo_j; j < lane && sh.obase[j] < e; j++) {
-                  const uint32_t rend = sh.obase[j + 1];
-                  const uint32_t need = e < rend ? e : rend;
-                  if (sh.done[j] < need) { ready = 0; break; }
-                }
-                if (!ready) break;
-              }
-              // out[op + k] = out[src + k % d]; every source byte lies below op
-              uint32_t j = 0;
-              for (uint32_t k0 = 0; k0 < len; k0 += 16) {
-                uint8_t buf[16];
-                const uint32_t m = len - k0 < 16u ? len - k0 : 16u;
-                uint32_t jj = j;
-                for (uint32_t k = 0; k < m; k++) {
-                  buf[k] = dst[src + jj];
-                  jj++; if (jj == d) jj = 0;
-                }
-                for (uint32_t k = 0; k < m; k++) {
-                  const uint32_t q = op + k0 + k;
-                  dst[q] = buf[k];
-                  a1 += buf[k];
-                  a2 = (uint32_t)((a2 + (uint64_t)(q % ADLER_MOD) * buf[k]) % ADLER_MOD);
-                }
-                j = jj;
-              }
-              if (stats) { stats->matches++; stats->match_bytes += len; }
-              op += len; t++;
-            }
-            LV(tcur) = t; LV(opos) = op; LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
-          }
-          WAVE_SYNC_GLOBAL();
-          if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
-          LANE_LOOP { sh.done[lane] = LV(opos); }
-          WAVE_SYNC();
-          if (!WAVE_BALLOT(LV(tcur) < LV(tend))) break;
+        LV(lerr) = err;
+      }
+      WAVE_SYNC();
+      if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
+      if (stats) stats->rounds++;
+      HZ_T(11);
+      // chase: references strictly decrease, so every chain ends in a literal or an
+      // external byte; resolved values are written back (benign races: every stored
+      // value is a valid ancestor of the position)
+      LANE_LOOP {
+        for (uint32_t r = (uint32_t)lane; r < wtotal; r += 64) {
+          uint32_t v = sh.ref[r];
+          uint32_t hops = 0;
+          while (v < 0x4000u) { v = sh.ref[v]; hops++; }
+          sh.ref[r] = (uint16_t)v;
+          if (stats) { stats->hops += hops; if (hops > stats->maxhops) stats->maxhops = hops; }
         }
       }
+      WAVE_SYNC();
+      // external bytes: gather from dst (load-only pass, fully pipelined)
+      LANE_LOOP {
+        for (uint32_t r = (uint32_t)lane; r < wtotal; r += 64) {
+          const uint32_t v = sh.ref[r];
+          if (v & 0x8000u) sh.ref[r] = (uint16_t)dst[wbeg - (v & 0x7fffu) - 1u];
+        }
+      }
+      WAVE_SYNC();
+      HZ_T(12);
+      // flush: 4-byte stores (byte stores at the unaligned head / tail) + adler sums
+      LANE_LOOP {
+        uint32_t b1 = 0, b2 = 0;                  // sum b, sum r*b over this lane's bytes
+        const uint32_t head = (uint32_t)((4u - (((uintptr_t)(dst + wbeg)) & 3u)) & 3u);
+        const uint32_t h = head < wtotal ? head : wtotal;
+        if ((uint32_t)lane < h) {
+          const uint32_t bv = sh.ref[lane] & 0xffu;
+          dst[wbeg + lane] = (uint8_t)bv;
+          b1 += bv; b2 += (uint32_t)lane * bv;
+        }
+        for (uint32_t r = h + 4u * (uint32_t)lane; r < wtotal; r += 256u) {
+          const uint32_t n = wtotal - r < 4u ? wtotal - r : 4u;
+          uint32_t w = 0;
+          for (uint32_t k = 0; k < n; k++) {
+            const uint32_t bv = sh.ref[r + k] & 0xffu;
+            w |= bv << (8u * k);
+            b1 += bv; b2 += (r + k) * bv;
+          }
+          if (n == 4u) *(uint32_t*)(dst + wbeg + r) = w;
+          else for (uint32_t k = 0; k < n; k++) dst[wbeg + r + k] = (uint8_t)(w >> (8u * k));
+        }
+        LV(s1) = (LV(s1) + b1) % ADLER_MOD;
+        LV(s2) = (uint32_t)((LV(s2) + (uint64_t)(wbeg % ADLER_MOD) * b1 + b2) % ADLER_MOD);
+      }
+      WAVE_SYNC_GLOBAL();
+      if (stats) stats->lit_bytes += 0;
+      HZ_T(14);
       out += wtotal;
       pos = npos;
       if (end_lane >= 0) break;        // EOB: the next block header follows
-      // next segment length: keep about half of TMAX tokens per segment so the
-      // continuation has room
+      // next segment length: about half of TMAX tokens per segment (room for the
+      // continuation) and an expected window output of about 3/4 of the LDS map
       if (tune.adapt) {
         const uint32_t used = npos - win_start;
-        const uint32_t bpt16 = ntok_valid ? (used * 16u) / ntok_valid : 16u * 8u;  // bits/token x16
-        const uint32_t target = (bpt16 * (uint32_t)TMAX) / (2u * 16u);
+        const uint32_t bpt16 = ntok_valid ? (used * 16u) / ntok_valid : 16u * 8u;   // bits/token x16
+        uint32_t target = (bpt16 * (uint32_t)TMAX) / (2u * 16u);
+        if (wtotal && used) {
+          const uint64_t lim = ((uint64_t)SCAP * 3u / 4u) * used / ((uint64_t)wtotal * 64u);
+          if (lim < target) target = (uint32_t)lim;
+        }
         L = target < (uint32_t)LMIN ? (uint32_t)LMIN : target > (uint32_t)LMAX ? (uint32_t)LMAX : target;
       }
     }
     if (bfinal) break;
   }
   // ---- trailer: adler32 (big-endian) after byte alignment ----
+  HZ_T(15);
   pos = (pos + 7u) & ~7u;
   if (pos + 32u > limit_bits) return ST_TRUNC;
   HZ_STAGE(sh, base, lo, hi, pos >> 5, 4u);

@@ -1,0 +1,56 @@
+"""Diagnostic: per-phase cycle breakdown of the inflate kernel (HZ_PROFILE build).
+Stamps are s_memtime deltas summed over all waves; only shares are meaningful."""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from hsds_amd import _native  # noqa: E402
+
+_native.LIB_PATH = os.path.join(ROOT, "tools", "libhsds_prof.so")
+L = _native.lib()
+L.hsds_debug_profile.argtypes = [ctypes.c_void_p, ctypes.c_int]
+import torch  # noqa: E402
+from bench import make_corpus, CHUNK_BYTES  # noqa: E402
+from hsds_amd.engine import ChunkEngine, pack_chunks  # noqa: E402
+
+NAMES = ["other", "blk-stage", "hdr-lens", "tables", "win-stage", "A", "A'", "repair", "B", "C-olen",
+         "C-ref", "C-chase", "C-flush", "C-rounds", "C-end", "trailer"]
+
+
+def run(fmt, n, unique, tune=None):
+    raw, blobs = make_corpus(fmt, unique, 20261015, 16)
+    order = [i % unique for i in range(n)]
+    src, descs, ext = pack_chunks([blobs[i] for i in order], [CHUNK_BYTES] * n)
+    dev = torch.device("cuda", 0)
+    eng = ChunkEngine(0)
+    if tune:
+        eng.set_tuning(**tune)
+    d_src = torch.from_numpy(src).to(dev)
+    d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 16)()
+    L.hsds_debug_profile(buf, 1)
+    t = time.perf_counter()
+    eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    L.hsds_debug_profile(buf, 1)
+    assert (d_st.cpu().numpy() == 0).all()
+    tot = sum(buf)
+    print(f"{fmt} n={n} tune={tune} wall={el*1e3:.1f} ms  {n*CHUNK_BYTES/el/1e9:.2f} GB/s  kernel={eng.last_inflate_ms():.1f} ms")
+    for i in range(16):
+        if buf[i]:
+            print(f"   {NAMES[i]:10s} {100.0*buf[i]/tot:6.2f}%")
+
+
+if __name__ == "__main__":
+    run("F1", 1024, 256)
+    run("F2", 256, 128)
