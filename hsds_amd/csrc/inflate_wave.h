@@ -31,6 +31,14 @@
 #include <hip/hip_runtime.h>
 #define HZ_GPU 1
 #define HZ_HD __device__ __forceinline__
+// global (address space 1) pointers: plain global_load/global_store that only
+// count on vmcnt, instead of flat accesses that also hold up every LDS wait
+typedef __attribute__((address_space(1))) uint8_t hz_gu8;
+typedef __attribute__((address_space(1))) const uint8_t hz_gcu8;
+typedef __attribute__((address_space(1))) uint32_t hz_gu32;
+typedef __attribute__((address_space(1))) const uint32_t hz_gcu32;
+#define HZ_GLOBAL(T, p) ((T)(uintptr_t)(p))
+#define HZ_UNROLL _Pragma("unroll")
 #define LANE_VAR(T, name) T name
 #define LV(name) name
 #define LANE_LOOP for (int lane = (int)threadIdx.x, _once = 1; _once; _once = 0)
@@ -43,6 +51,12 @@
 #include <stdio.h>
 #define HZ_GPU 0
 #define HZ_HD static inline
+typedef uint8_t hz_gu8;
+typedef const uint8_t hz_gcu8;
+typedef uint32_t hz_gu32;
+typedef const uint32_t hz_gcu32;
+#define HZ_GLOBAL(T, p) ((T)(p))
+#define HZ_UNROLL
 #define LANE_VAR(T, name) T name[64]
 #define LV(name) name[lane]
 #define LANE_LOOP for (int lane = 0; lane < 64; lane++)
@@ -66,8 +80,11 @@ namespace hz {
 constexpr int WAVE = 64;
 constexpr int LL_ROOT = 10;
 constexpr int D_ROOT = 8;
-constexpr int LL_SUB = 512;         // second-level entries (codes longer than the root)
-constexpr int D_SUB = 256;
+// second-level entries (codes longer than the root).  Sized above zlib's exact
+// worst cases (ENOUGH: 286 symbols / root 10 -> 308 extra entries; 30 symbols /
+// root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
+constexpr int LL_SUB = 512;
+constexpr int D_SUB = 384;
 constexpr int TMAX = 64;            // tokens stored per lane per window
 constexpr int LMAX = 512;           // max segment length (bits)
 constexpr int LMIN = 64;
@@ -111,6 +128,7 @@ struct Shared {
   uint32_t lut_d[(1 << D_ROOT) + D_SUB];
   uint16_t tb_first[16];
   uint16_t tb_offs[17];
+  uint16_t tb_next[16];
   uint32_t tok[TMAX][WAVE];          // token-major: lane-parallel accesses hit 64 banks
   uint32_t bitmap[WAVE][BM_WORDS];
   uint32_t in32[IN_WORDS + 4];
@@ -120,6 +138,8 @@ struct Shared {
   uint32_t flag[WAVE];
   uint16_t ref[SCAP];
   uint32_t obase[WAVE + 1];
+  uint16_t tcur_l[WAVE];
+  uint16_t tend_l[WAVE];
   uint32_t done[WAVE];
   uint32_t flag2[WAVE];
   uint16_t sorted_ll[288];
@@ -144,6 +164,33 @@ HZ_HD uint32_t popc32(uint32_t x) {
   return __popc(x);
 #else
   return (uint32_t)__builtin_popcount(x);
+#endif
+}
+
+// RFC 1951 order of the code-length code lengths, packed 5 bits per entry
+HZ_HD uint32_t cl_order(uint32_t i) {
+  // 16,17,18,0,8,7,9,6,10,5,11,4 | 12,3,13,2,14,1,15
+  const uint64_t lo = 16ull | 17ull << 5 | 18ull << 10 | 0ull << 15 | 8ull << 20 | 7ull << 25 | 9ull << 30 |
+                      6ull << 35 | 10ull << 40 | 5ull << 45 | 11ull << 50 | 4ull << 55;
+  const uint64_t hi = 12ull | 3ull << 5 | 13ull << 10 | 2ull << 15 | 14ull << 20 | 1ull << 25 | 15ull << 30;
+  return (uint32_t)((i < 12 ? lo >> (5 * i) : hi >> (5 * (i - 12))) & 31u);
+}
+
+HZ_HD uint32_t popc64(uint64_t x) {
+#if HZ_GPU
+  return (uint32_t)__popcll(x);
+#else
+  return (uint32_t)__builtin_popcountll(x);
+#endif
+}
+
+HZ_HD void atomicAdd_lds(uint16_t* p, int v) {
+#if HZ_GPU
+  // 16-bit counters live in LDS: add to the containing aligned dword
+  uint32_t* w = (uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+  atomicAdd(w, (uint32_t)v << (((uintptr_t)p & 2) * 8));
+#else
+  *p = (uint16_t)(*p + v);
 #endif
 }
 
@@ -211,22 +258,13 @@ HZ_HD uint32_t canon_decode(const uint16_t* cnt, const uint16_t* sorted, uint64_
 HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
   if (e_kind(e) == K_SUB) e = sh->lut_ll[e_val(e) + ((uint32_t)(bits >> LL_ROOT) & bmask(e_extra(e)))];
-  if (e_kind(e) == K_SLOW) {
-    uint32_t r = canon_decode(sh->cnt_ll, sh->sorted_ll, bits);
-    e = (r == 0xffffffffu) ? ent(K_BAD, 1, 0, 0) : ll_entry(r & 0xffff, r >> 16);
-  }
   return e;
 }
 HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_d[bits & ((1u << D_ROOT) - 1)];
   if (e_kind(e) == K_SUB) e = sh->lut_d[e_val(e) + ((uint32_t)(bits >> D_ROOT) & bmask(e_extra(e)))];
-  if (e_kind(e) == K_SLOW) {
-    uint32_t r = canon_decode(sh->cnt_d, sh->sorted_d, bits);
-    e = (r == 0xffffffffu) ? ent(K_BAD, 1, 0, 0) : d_entry(r & 0xffff, r >> 16);
-  }
   return e;
 }
-
 
 // decode one token (literal, length+distance, EOB, or invalid) at bit `p`.
 // Invalid codes advance one bit so that a speculative decoder keeps going.
@@ -275,12 +313,14 @@ HZ_HD void br_init(const Shared* sh, BitRd& r, uint32_t p, uint32_t stage_base) 
 }
 
 HZ_HD void br_fill(const Shared* sh, BitRd& r) {
-  if (r.avail < 32u) {
-    r.bb |= (uint64_t)r.nxt << r.avail;
-    r.avail += 32u;
-    r.widx++;
-    r.nxt = sh->in32[r.widx];
-  }
+  // branch-free: always read the next staged word, keep it only when used
+  const uint32_t need = r.avail < 32u;
+  const uint64_t add = (uint64_t)r.nxt << (r.avail & 31u);
+  r.bb |= need ? add : 0ull;
+  r.avail += need ? 32u : 0u;
+  r.widx += need;
+  const uint32_t nn = sh->in32[r.widx];
+  r.nxt = need ? nn : r.nxt;
 }
 
 HZ_HD void br_drop(BitRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n; }
@@ -291,22 +331,20 @@ HZ_HD void br_drop(BitRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n;
 HZ_HD uint32_t next_token(const Shared* sh, BitRd& r) {
   br_fill(sh, r);
   const uint32_t e = lookup_ll(sh, r.bb);
-  const uint32_t kind = e_kind(e), nb = e_bits(e);
-  if (kind == K_LIT) { br_drop(r, nb); return e_val(e); }
+  const uint32_t kind = e_kind(e), nb = e_bits(e), xb = e_extra(e), val = e_val(e);
+  const uint32_t len = val + ((uint32_t)(r.bb >> nb) & bmask(xb));
+  br_drop(r, nb + xb);
+  uint32_t tok = kind == K_LIT ? val : kind == K_EOB ? T_EOB : T_ERR;
   if (kind == K_LEN) {
-    const uint32_t xb = e_extra(e);
-    const uint32_t len = e_val(e) + ((uint32_t)(r.bb >> nb) & bmask(xb));
-    br_drop(r, nb + xb);
     br_fill(sh, r);
     const uint32_t ed = lookup_d(sh, r.bb);
-    if (e_kind(ed) != K_LEN) { br_drop(r, e_bits(ed)); return T_ERR; }
     const uint32_t nd = e_bits(ed), xd = e_extra(ed);
     const uint32_t dist = e_val(ed) + ((uint32_t)(r.bb >> nd) & bmask(xd));
-    br_drop(r, nd + xd);
-    return T_MATCH | (len << 16) | (dist - 1u);
+    const int ok = e_kind(ed) == K_LEN;
+    br_drop(r, ok ? nd + xd : nd);
+    tok = ok ? (T_MATCH | (len << 16) | (dist - 1u)) : T_ERR;
   }
-  br_drop(r, nb ? nb : 1u);
-  return kind == K_EOB ? T_EOB : T_ERR;
+  return tok;
 }
 
 HZ_HD void mark_bit(Shared* sh, int lane, uint32_t rel) {
@@ -334,10 +372,10 @@ HZ_HD uint32_t nth_mark(const Shared* sh, int lane, uint32_t k) {
 
 // ---- global memory helpers -------------------------------------------------
 // aligned dword k of the stream's aligned base; bytes outside [lo, hi) are zero.
-HZ_HD uint32_t load_word(const uint8_t* base, uint32_t k, uint32_t lo, uint32_t hi) {
+HZ_HD uint32_t load_word(hz_gcu8* base, uint32_t k, uint32_t lo, uint32_t hi) {
   uint32_t b0 = k * 4u;
   if (b0 >= hi || b0 + 4u <= lo) return 0u;
-  uint32_t v = *(const uint32_t*)(base + b0);
+  uint32_t v = *(hz_gcu32*)(base + b0);
   if (b0 < lo) v &= ~bmask((lo - b0) * 8u);
   if (b0 + 4u > hi) v &= bmask((hi - b0) * 8u);
   return v;
@@ -410,12 +448,19 @@ struct TableArgs {
 // ballots; it is written once in the SIMT style below.
 #define HZ_BUILD_TABLE(sh, A, status_out)                                               \
   do {                                                                                  \
-    /* counts (lane 0 serial: n <= 320) */                                              \
+    /* counts: LDS atomics over all lanes */                                          \
+    LANE_LOOP { if (lane < 16) (A).cnt[lane] = 0; }                                     \
+    WAVE_SYNC();                                                                        \
+    LANE_LOOP {                                                                         \
+      for (int s = lane; s < (A).n; s += 64) {                                          \
+        const int l = (A).lens[s];                                                      \
+        if (l) hz::atomicAdd_lds(&(A).cnt[l], 1);                                       \
+      }                                                                                 \
+    }                                                                                   \
+    WAVE_SYNC();                                                                        \
+    /* validity (zlib inflate_table rules), first code and offset per length */        \
     LANE_LOOP {                                                                         \
       if (lane == 0) {                                                                  \
-        for (int l = 0; l < 16; l++) (A).cnt[l] = 0;                                    \
-        for (int s = 0; s < (A).n; s++) (A).cnt[(A).lens[s]]++;                         \
-        (A).cnt[0] = 0;                                                                 \
         int left = 1, maxl = 0, bad = 0;                                                \
         for (int l = 1; l <= 15; l++) {                                                 \
           left <<= 1; left -= (A).cnt[l];                                               \
@@ -424,28 +469,43 @@ struct TableArgs {
         }                                                                               \
         if (!bad && maxl > 0 && left > 0 && ((A).kind == 0 || maxl != 1)) bad = 1;      \
         if ((A).kind == 0 && maxl == 0) bad = 1;                                        \
-        /* sorted symbols in canonical order; first code / offset per length */         \
-        int offs[16]; offs[1] = 0;                                                      \
-        for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + (A).cnt[l];                \
-        {                                                                               \
-          int code = 0;                                                                 \
-          for (int l = 1; l <= 15; l++) {                                               \
-            code = (code + (l > 1 ? (A).cnt[l - 1] : 0)) << 1;                          \
-            (sh).tb_first[l] = (uint16_t)code;                                          \
-            (sh).tb_offs[l] = (uint16_t)offs[l];                                        \
-          }                                                                             \
-          (sh).tb_offs[16] = (uint16_t)(offs[15] + (A).cnt[15]);                        \
+        int code = 0, off = 0;                                                          \
+        for (int l = 1; l <= 15; l++) {                                                 \
+          code = (code + (l > 1 ? (A).cnt[l - 1] : 0)) << 1;                            \
+          (sh).tb_first[l] = (uint16_t)code;                                            \
+          (sh).tb_offs[l] = (uint16_t)off;                                              \
+          (sh).tb_next[l] = (uint16_t)off;                                              \
+          off += (A).cnt[l];                                                            \
         }                                                                               \
-        for (int s = 0; s < (A).n; s++) if ((A).lens[s]) (A).sorted[offs[(A).lens[s]]++] = (uint16_t)s; \
+        (sh).tb_offs[16] = (uint16_t)off;                                               \
         (sh).u_status = bad ? hz::ST_DATA : hz::ST_OK;                                  \
       }                                                                                 \
     }                                                                                   \
     WAVE_SYNC();                                                                        \
+    /* canonical order: ranks within a length via ballots, 64 symbols at a time */     \
+    for (int _c = 0; _c < (A).n; _c += 64) {                                            \
+      LANE_VAR(int, _l);                                                                \
+      LANE_LOOP { LV(_l) = _c + lane < (A).n ? (A).lens[_c + lane] : 0; }               \
+      for (int L = 1; L <= 15; L++) {                                                   \
+        if (!(A).cnt[L]) continue;                                                      \
+        const uint64_t m = WAVE_BALLOT(LV(_l) == L);                                    \
+        if (!m) continue;                                                               \
+        LANE_LOOP {                                                                     \
+          if (LV(_l) == L) {                                                            \
+            const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;        \
+            (A).sorted[(sh).tb_next[L] + hz::popc64(below)] = (uint16_t)(_c + lane);    \
+          }                                                                             \
+        }                                                                               \
+        WAVE_SYNC();                                                                    \
+        LANE_LOOP { if (lane == 0) (sh).tb_next[L] = (uint16_t)((sh).tb_next[L] + hz::popc64(m)); } \
+        WAVE_SYNC();                                                                    \
+      }                                                                                 \
+    }                                                                                   \
     /* LUT fill: every root index decoded canonically (balanced across lanes) */       \
     LANE_LOOP {                                                                         \
       for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
         int code = 0, first = 0, index = 0; uint32_t bits = (uint32_t)idx;              \
-        uint32_t e = hz::ent(hz::K_SLOW, (A).root, 0, 0);                               \
+        uint32_t e = hz::ent(hz::K_BAD, 1, 0, 0);                                       \
         for (int len = 1; len <= (A).root; len++) {                                     \
           code |= (int)(bits & 1u); bits >>= 1;                                         \
           int count = (A).cnt[len];                                                     \
@@ -480,10 +540,9 @@ struct TableArgs {
               lmax = l2; k2++;                                                          \
             }                                                                           \
             const int sb = lmax - _R;                                                   \
-            if (used + (1 << sb) <= (A).nsub)                                           \
-              (A).lut[hz::rev_bits((uint32_t)p, _R)] =                                  \
-                  hz::ent(hz::K_SUB, _R, sb, (uint32_t)((1 << _R) + used));             \
-            used += 1 << sb;                                                            \
+            (A).lut[hz::rev_bits((uint32_t)p, _R)] =                                    \
+                hz::ent(hz::K_SUB, _R, sb, (uint32_t)((1 << _R) + used));               \
+            used += 1 << sb;  /* <= nsub for every complete code (see LL_SUB/D_SUB) */  \
             k = k2;                                                                     \
           }                                                                             \
         }                                                                               \
@@ -569,11 +628,11 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
   (void)prof;
   // aligned base so that every staged dword load is aligned
   const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 3u);
-  const uint8_t* base = job.src - a;
+  hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, job.src - a);
   const uint32_t lo = a, hi = a + job.src_len;   // valid byte range of the stream
   const uint32_t limit_bits = hi * 8u;
   const uint32_t dst_len = job.dst_len;
-  uint8_t* const dst = job.dst;
+  hz_gu8* const dst = HZ_GLOBAL(hz_gu8*, job.dst);
 
   LANE_VAR(uint32_t, s1);   // adler32 partial sums: S1 = sum b, S2 = sum pos*b (mod 65521)
   LANE_VAR(uint32_t, s2);
@@ -639,66 +698,81 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       }
       WAVE_SYNC();
     } else {
-      // dynamic header (RFC 1951 3.2.7): lane 0 decodes it serially from LDS
+      // dynamic header (RFC 1951 3.2.7): lane 0 decodes it serially from the staged
+      // input with a register bit reader and a 7-bit code-length lookup table
       LANE_LOOP {
         if (lane == 0) {
           int st = ST_OK;
-          uint32_t p = pos;
-          const uint64_t b = peek64(&sh, p);
-          const uint32_t hlit = (uint32_t)(b & 31u) + 257u, hdist = (uint32_t)((b >> 5) & 31u) + 1u;
-          const uint32_t hclen = (uint32_t)((b >> 10) & 15u) + 4u;
-          p += 14;
+          BitRd r;
+          br_init(&sh, r, pos, sh.u_stage_base);
+          br_fill(&sh, r);
+          const uint32_t hlit = (uint32_t)(r.bb & 31u) + 257u, hdist = (uint32_t)((r.bb >> 5) & 31u) + 1u;
+          const uint32_t hclen = (uint32_t)((r.bb >> 10) & 15u) + 4u;
+          br_drop(r, 14);
           if (hlit > 286 || hdist > 30) st = ST_DATA;
-          const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-          uint8_t cl[19];
+          uint16_t* cl = sh.sorted_cl;               // code-length code lengths (19)
           for (int i = 0; i < 19; i++) cl[i] = 0;
-          for (uint32_t i = 0; i < hclen; i++) { cl[order[i]] = (uint8_t)(peek64(&sh, p) & 7u); p += 3; }
+          for (uint32_t i = 0; i < hclen; i++) {
+            br_fill(&sh, r);
+            cl[cl_order(i)] = (uint16_t)(r.bb & 7u);
+            br_drop(r, 3);
+          }
           uint16_t* cnt = sh.cnt_cl;
-          uint16_t* srt = sh.sorted_cl;
           for (int l = 0; l < 16; l++) cnt[l] = 0;
           for (int i = 0; i < 19; i++) cnt[cl[i]]++;
           cnt[0] = 0;
           int left = 1, maxl = 0;
-          for (int l = 1; l <= 15; l++) {
+          for (int l = 1; l <= 7; l++) {
             left <<= 1; left -= cnt[l];
             if (cnt[l]) maxl = l;
             if (left < 0) st = ST_DATA;
           }
           if (left > 0 || maxl == 0) st = ST_DATA;  // code-length code must be complete
-          int offs[16];
-          offs[1] = 0;
-          for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
-          for (int i = 0; i < 19; i++) if (cl[i]) srt[offs[cl[i]]++] = (uint16_t)i;
+          // 7-bit LUT (sym | len << 8) in the distance table's space (rebuilt below)
+          uint32_t* clut = sh.lut_d;
+          if (st == ST_OK) {
+            uint32_t next[8];
+            uint32_t code = 0;
+            for (int l = 1; l <= 7; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; next[l] = code; }
+            for (int i = 0; i < 19; i++) {
+              const uint32_t l = cl[i];
+              if (!l) continue;
+              const uint32_t rc = rev_bits(next[l]++, (int)l);
+              for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint32_t)i | (l << 8);
+            }
+          }
           const uint32_t total = hlit + hdist;
           uint32_t n = 0;
           const uint32_t stage_end = sh.u_stage_base + 128u * 32u;
           while (st == ST_OK && n < total) {
-            if (p + 96u > stage_end) { st = ST_DATA; break; }
-            uint64_t bits = peek64(&sh, p);
-            const uint32_t r = canon_decode(cnt, srt, bits);
-            if (r == 0xffffffffu) { st = ST_DATA; break; }
-            const uint32_t sym = r & 0xffff, l = r >> 16;
-            p += l;
-            bits >>= l;
+            if (r.pos + 64u > stage_end) { st = ST_DATA; break; }   // header longer than any valid one
+            br_fill(&sh, r);
+            const uint32_t e = clut[r.bb & 127u];
+            const uint32_t sym = e & 0xffu, l = e >> 8;
+            br_drop(r, l);
             if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
             uint32_t rep, val = 0;
             if (sym == 16) {
               if (n == 0) { st = ST_DATA; break; }
-              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(bits & 3u); p += 2;
-            } else if (sym == 17) { rep = 3 + (uint32_t)(bits & 7u); p += 3; }
-            else { rep = 11 + (uint32_t)(bits & 127u); p += 7; }
+              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(r.bb & 3u); br_drop(r, 2);
+            } else if (sym == 17) { rep = 3 + (uint32_t)(r.bb & 7u); br_drop(r, 3); }
+            else { rep = 11 + (uint32_t)(r.bb & 127u); br_drop(r, 7); }
             if (n + rep > total) { st = ST_DATA; break; }
             for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
           }
-          if (st == ST_OK && p > limit_bits) st = ST_TRUNC;
+          if (st == ST_OK && r.pos > limit_bits) st = ST_TRUNC;
           if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;  // missing end-of-block code
           if (st == ST_OK) {
             for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
             for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
             for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
           }
+#if !HZ_GPU && defined(HZ_DEBUG)
+          { unsigned long long hsh = 0; for (uint32_t i = 0; i < 320; i++) hsh = hsh * 31 + sh.lens[i];
+            printf("HDR pos=%u end=%u hlit=%u hdist=%u st=%d hash=%llu\n", pos, r.pos, hlit, hdist, st, hsh); }
+#endif
           sh.u_status = st;
-          sh.u_pos = p;
+          sh.u_pos = r.pos;
           sh.u_nlen = hlit;
           sh.u_ndist = hdist;
         }
@@ -1020,31 +1094,60 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       // ref[r] for window byte r: 0x4000|b literal, r' < 0x4000 internal reference,
       // 0x8000|(x-1) the byte x positions before the window (final in dst).
       const uint32_t wbeg = out;
+      // publish per-lane token ranges so that any lane can walk any lane's tokens
+      LANE_LOOP {
+        sh.obase[lane] = LV(obase);
+        sh.tcur_l[lane] = (uint16_t)LV(tcur);
+        sh.tend_l[lane] = (uint16_t)LV(tend);
+        if (lane == 63) sh.obase[64] = wtotal;
+      }
+      WAVE_SYNC();
       LANE_VAR(int, lerr);
       LANE_LOOP {
+        // lane w produces the references of output bytes [w*B, (w+1)*B): balanced
+        // whatever the token / output distribution across the owning lanes
         int err = 0;
-        uint32_t op = LV(obase);                  // window-relative
-        for (uint32_t t = LV(tcur); t < LV(tend); t++) {
-          const uint32_t v = sh.tok[t][lane];
-          if (!(v & T_MATCH)) { sh.ref[op] = (uint16_t)(0x4000u | v); op++; continue; }
-          const uint32_t len = (v >> 16) & 0x1ffu, d = (v & 0x7fffu) + 1u;
-          if (d > wbeg + op) { err = 1; break; }  // invalid distance too far back
-          if (stats) { stats->matches++; stats->match_bytes += len; }
-          if (d <= op) {                          // source inside the window
-            uint32_t jj = 0;
-            for (uint32_t k = 0; k < len; k++) {
-              sh.ref[op + k] = (uint16_t)(op - d + jj);
-              jj++; if (jj == d) jj = 0;
-            }
-          } else {
-            uint32_t jj = 0;
-            for (uint32_t k = 0; k < len; k++) {
-              const uint32_t back = d - jj;       // source = window start - (back - op)
-              sh.ref[op + k] = back > op ? (uint16_t)(0x8000u | (back - op - 1u)) : (uint16_t)(op - back);
-              jj++; if (jj == d) jj = 0;
-            }
+        const uint32_t B = (wtotal + 63u) >> 6;
+        const uint32_t x0 = (uint32_t)lane * B;
+        const uint32_t x1 = x0 + B < wtotal ? x0 + B : wtotal;
+        if (x0 < x1) {
+          int lo_j = 0, hi_j = 63;                 // owner: largest j with obase[j] <= x0
+          while (lo_j < hi_j) {
+            const int mid = (lo_j + hi_j + 1) >> 1;
+            if (sh.obase[mid] <= x0) lo_j = mid; else hi_j = mid - 1;
           }
-          op += len;
+          int j = lo_j;
+          uint32_t t = sh.tcur_l[j], q = sh.obase[j];
+          uint32_t v = sh.tok[t][j];
+          uint32_t n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+          while (q + n <= x0) {                    // token of lane j containing x0
+            q += n; t++;
+            v = sh.tok[t][j];
+            n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+          }
+          uint32_t d = (v & 0x7fffu) + 1u;
+          uint32_t jj = (v & T_MATCH) ? (x0 - q) % d : 0u;
+          int32_t base = (int32_t)q - (int32_t)d;
+          uint32_t tend_j = sh.tend_l[j];
+          if ((v & T_MATCH) && d > wbeg + q) err = 1;
+          for (uint32_t x = x0; x < x1 && !err; x++) {
+            if (x == q + n) {                      // next token (possibly of the next lane)
+              q = x; t++;
+              while (t >= tend_j) { j++; t = sh.tcur_l[j]; tend_j = sh.tend_l[j]; }
+              v = sh.tok[t][j];
+              n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+              d = (v & 0x7fffu) + 1u;
+              base = (int32_t)q - (int32_t)d;
+              jj = 0;
+              if ((v & T_MATCH) && d > wbeg + q) { err = 1; break; }
+            }
+            const int32_t srcq = base + (int32_t)jj;
+            const uint32_t rv = !(v & T_MATCH) ? (0x4000u | v)
+                              : srcq >= 0 ? (uint32_t)srcq : (0x8000u | (uint32_t)(-srcq - 1));
+            sh.ref[x] = (uint16_t)rv;
+            jj++;
+            jj = jj == d ? 0u : jj;
+          }
         }
         LV(lerr) = err;
       }
@@ -1065,11 +1168,22 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
         }
       }
       WAVE_SYNC();
-      // external bytes: gather from dst (load-only pass, fully pipelined)
+      // external bytes: gather from dst, 8 independent loads in flight per lane
       LANE_LOOP {
-        for (uint32_t r = (uint32_t)lane; r < wtotal; r += 64) {
-          const uint32_t v = sh.ref[r];
-          if (v & 0x8000u) sh.ref[r] = (uint16_t)dst[wbeg - (v & 0x7fffu) - 1u];
+        for (uint32_t r0 = (uint32_t)lane; r0 < wtotal; r0 += 64u * 8u) {
+          uint32_t v[8], b[8];
+HZ_UNROLL
+          for (int k = 0; k < 8; k++) {
+            const uint32_t r = r0 + 64u * (uint32_t)k;
+            v[k] = r < wtotal ? sh.ref[r] : 0x4000u;
+          }
+HZ_UNROLL
+          for (int k = 0; k < 8; k++) b[k] = (v[k] & 0x8000u) ? (uint32_t)dst[wbeg - (v[k] & 0x7fffu) - 1u] : v[k];
+HZ_UNROLL
+          for (int k = 0; k < 8; k++) {
+            const uint32_t r = r0 + 64u * (uint32_t)k;
+            if (r < wtotal && (v[k] & 0x8000u)) sh.ref[r] = (uint16_t)b[k];
+          }
         }
       }
       WAVE_SYNC();
@@ -1092,7 +1206,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             w |= bv << (8u * k);
             b1 += bv; b2 += (r + k) * bv;
           }
-          if (n == 4u) *(uint32_t*)(dst + wbeg + r) = w;
+          if (n == 4u) *(hz_gu32*)(dst + wbeg + r) = w;
           else for (uint32_t k = 0; k < n; k++) dst[wbeg + r + k] = (uint8_t)(w >> (8u * k));
         }
         LV(s1) = (LV(s1) + b1) % ADLER_MOD;
