@@ -110,6 +110,147 @@ def run_format(fmt, args, dev, rank, world):
     return res
 
 
+def run_e2e(r, args, dev, nsub=8):
+    """PCIe-inclusive rate: stored objects in pinned host memory
+    -> hipMemcpyAsync H2D -> decode -> D2H into a pinned host buffer, pipelined over
+    `nsub` sub-batches on three streams (copy-in / decode / copy-out)."""
+    import torch
+    from hsds_amd.engine import ChunkEngine, pack_chunks, to_device_bytes, CHUNK_DESC_DTYPE
+    blobs, order = r["blobs"], r["order"]
+    n = len(order)
+    src, descs, ext = pack_chunks([blobs[i] for i in order], [CHUNK_BYTES] * n)
+    h_src = torch.from_numpy(src).pin_memory()
+    h_out = torch.empty(ext, dtype=torch.uint8).pin_memory()
+    d_src = torch.empty(src.size, dtype=torch.uint8, device=dev)
+    d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_desc = to_device_bytes(descs, dev)
+    eng = ChunkEngine(dev.index)
+    s_in, s_dec, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    bounds = [n * k // nsub for k in range(nsub + 1)]
+    D = CHUNK_DESC_DTYPE.itemsize
+
+    def rng_src(a, b):
+        return int(descs[a]["src_off"]), int(descs[b - 1]["src_off"] + descs[b - 1]["src_len"])
+
+    def rng_dst(a, b):
+        return int(descs[a]["dst_off"]), int(descs[b - 1]["dst_off"] + descs[b - 1]["dst_len"])
+
+    def step():
+        for k in range(nsub):
+            a, b = bounds[k], bounds[k + 1]
+            s0, s1 = rng_src(a, b)
+            o0, o1 = rng_dst(a, b)
+            with torch.cuda.stream(s_in):
+                d_src[s0:s1].copy_(h_src[s0:s1], non_blocking=True)
+                e_in = torch.cuda.Event()
+                e_in.record(s_in)
+            s_dec.wait_event(e_in)
+            eng.decode(d_src, d_desc[a * D:b * D], d_dst, d_st[a:b], compressor="zlib", shuffle=1,
+                       itemsize=4 if r["fmt"] == "F2" else 1, stream=s_dec)
+            e_dec = torch.cuda.Event()
+            e_dec.record(s_dec)
+            s_out.wait_event(e_dec)
+            with torch.cuda.stream(s_out):
+                h_out[o0:o1].copy_(d_dst[o0:o1], non_blocking=True)
+
+    step()
+    torch.cuda.synchronize()
+    assert int(d_st.abs().sum()) == 0
+    o = int(descs[n - 1]["dst_off"])
+    assert np.array_equal(h_out[o:o + CHUNK_BYTES].numpy(), r["raw"][order[n - 1]])
+    steps = max(1, min(args.steps, 3))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # raw link rates for context (one direction at a time)
+    t1 = time.perf_counter()
+    d_src.copy_(h_src, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = src.size / (time.perf_counter() - t1) / 1e9
+    t1 = time.perf_counter()
+    h_out.copy_(d_dst, non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = ext / (time.perf_counter() - t1) / 1e9
+    out = {"value": round(n * CHUNK_BYTES * steps / el / 1e9, 2), "unit": "GB/s",
+           "what": f"pinned host stored objects -> H2D -> decode -> D2H pinned, {nsub} pipelined sub-batches",
+           "h2d_GBps": round(h2d, 1), "d2h_GBps": round(d2h, 1), "steps": steps}
+    del d_src, d_dst, h_src, h_out
+    torch.cuda.empty_cache()
+    return out
+
+
+CFG3_DIMS, CFG3_LAYOUT = (512, 2048, 2048), (16, 64, 128)
+CFG3_SEL = (slice(0, 512, 2), slice(3, 2048, 5), slice(1, 2048, 3))
+
+
+def run_cfg3(args, dev):
+    """configs[2]: 3D int16 dataset, shuffle+deflate 256 KiB chunks, strided selection
+    [0:512:2, 3:2048:5, 1:2048:3] across all 16 384 chunks; one step = batch decode +
+    fused strided gather of every chunk's selection + placement into the result slab."""
+    import torch
+    from hsds_amd import crawl
+    from oracle import oracle as orc
+    from concurrent.futures import ThreadPoolExecutor
+    threads = min(16, os.cpu_count() or 1)
+    plan = crawl.SelectionPlan("d-5a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", CFG3_DIMS, CFG3_LAYOUT, CFG3_SEL,
+                               np.int16, 1)
+    ids = plan.chunk_ids(0)
+    nuniq = min(args.unique, len(ids))
+    csz = int(np.prod(CFG3_LAYOUT))
+
+    def mk(i):
+        g = np.random.default_rng(20261015 + i)
+        return (np.cumsum(g.normal(size=csz)) * 100).astype("<i2").view(np.uint8)
+    with ThreadPoolExecutor(threads) as ex:
+        raw = list(ex.map(mk, range(nuniq)))
+    enc = orc.encode_batch(raw, op="blosc", typesize=1, clevel=4, shuffle=1, nthreads=threads)
+    blobs = {cid: enc[k % nuniq] for k, cid in enumerate(ids)}
+    rd = crawl.ShardedReader(plan, 0, dev)
+    st = rd.upload(blobs)
+    gathered = torch.empty(plan.gathered_nbytes, dtype=torch.uint8, device=dev)
+    slab = torch.zeros(plan.slab_nbytes, dtype=torch.uint8, device=dev)
+    for _ in range(max(1, args.warmup)):
+        rd.read(st, slab=slab, gathered=gathered, check=False)
+    torch.cuda.synchronize()
+    assert int(st["d_status"].abs().sum()) == 0
+    host = slab.cpu().numpy().view(np.int16).reshape(plan.slab_shape)
+    for k in (0, len(ids) // 3, len(ids) - 1):
+        p = plan.pieces[plan.by_rank[0][k]]
+        c = raw[k % nuniq].view(np.int16).reshape(CFG3_LAYOUT)
+        assert np.array_equal(host[p.data_slices], c[p.chunk_slices]), f"cfg3 piece {k}"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rd.read(st, slab=slab, gathered=gathered, check=False)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.steps
+    comp = sum(len(blobs[c]) for c in ids)
+    out = {"value": round(plan.slab_nbytes / el / 1e9, 3), "unit": "GB/s selected",
+           "decoded_GBps": round(len(ids) * csz * 2 / el / 1e9, 2), "ms_per_step": round(el * 1e3, 3),
+           "chunks": len(ids), "selected_bytes": plan.slab_nbytes, "compressed_bytes": comp,
+           "algorithmic_GBps": round((comp + plan.slab_nbytes) / el / 1e9, 2),
+           "workload": "configs[2]: int16 512x2048x2048, 16x64x128 chunks (F1 L4), "
+                       "select [0:512:2,3:2048:5,1:2048:3], decode+gather+place"}
+    del gathered, slab, st
+    torch.cuda.empty_cache()
+    return out
+
+
+def load_traffic(args, world):
+    """HBM bytes per inflate launch from the committed PMC passes (tools/pmc_traffic.sh):
+    2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
+    p = os.path.join(ROOT, "profiles", "r1_traffic.json")
+    if not os.path.exists(p):
+        return None
+    t = json.load(open(p))
+    if t.get("chunks") != args.chunks or t.get("unique") != args.unique:
+        return None
+    return t
+
+
 def cpu_baseline(blobs, seconds, threads):
     """Oracle decode (c-blosc frame walk + libz, same as the reference path) on the
     box's host cores, bounded to about `seconds` of wall time."""
@@ -136,6 +277,8 @@ def main():
     ap.add_argument("--f2", type=int, default=1, help="also measure F2 (HDF5 zlib+shuffle) chunks")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-timing", type=int, default=0)
+    ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
+    ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -178,10 +321,18 @@ def main():
                      "kernel": "inflate_kernel", "kernel_ms": round(r1["kernel_ms"], 3),
                      "bytes_per_launch": launch_bytes},
     }
+    tr = load_traffic(args, world)
+    if tr is not None:
+        out["roofline"]["traffic"] = tr["bytes_per_launch"]
+        out["roofline"]["traffic_source"] = tr["source"]
     if r2 is not None:
         v2 = r2["dec_bytes"] * world * args.steps / r2["elapsed_s"] / 1e9
         out["f2"] = {"value": round(v2, 2), "unit": "GB/s", "format": "HDF5 chunk: zlib L4 of byte-shuffled f32",
                      "compressed_bytes_per_gpu": r2["comp_bytes"], "inflate_kernel_ms": round(r2["kernel_ms"], 3)}
+    if world == 1 and args.e2e:
+        out["e2e_pcie"] = run_e2e(r1, args, dev)
+    if world == 1 and args.cfg3:
+        out["cfg3"] = run_cfg3(args, dev)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = min(16, os.cpu_count() or 1)
         sample = r1["blobs"][:256]
