@@ -25,7 +25,8 @@
 namespace {
 
 constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
-constexpr int INFLATE_WAVES_PER_CU = 3;
+constexpr int INFLATE_WAVES_PER_CU = 5;   // LDS-bound: sizeof(hz::Shared) <= 32 KiB
+static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
 
 enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_INEXACT = 0x100 };
 
@@ -371,6 +372,7 @@ __global__ void zero_i32_kernel(int32_t* p, int64_t n) {
 struct hsds_engine {
   int device;
   int num_cus;
+  int inflate_blocks_per_cu;   // occupancy of inflate_kernel (LDS-bound)
   hz::Tune tune;
   // workspace (grown on demand)
   uint8_t* ws = nullptr;
@@ -423,6 +425,10 @@ int hsds_engine_create(int device, hsds_engine** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
   e->num_cus = prop.multiProcessorCount;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, inflate_kernel, 64, 0) != hipSuccess || occ < 1)
+    occ = INFLATE_WAVES_PER_CU;
+  e->inflate_blocks_per_cu = occ;
   e->tune.L0 = 384;
   e->tune.W = 96;
   e->tune.adapt = 1;
@@ -490,7 +496,7 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
                      (uint8_t*)d_dst, e->tmp, slots, counts, meta, list, ctr + 1, d_status, compressor, shuffle,
                      itemsize, inexact);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
-  int64_t grid = (int64_t)e->num_cus * INFLATE_WAVES_PER_CU;
+  int64_t grid = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
   if (grid > nchunks * 4) grid = nchunks * 4;
   if (grid < 1) grid = 1;
   hipEventRecord(e->ev0, st);

@@ -85,9 +85,10 @@ constexpr int D_ROOT = 8;
 // root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
 constexpr int LL_SUB = 512;
 constexpr int D_SUB = 384;
-constexpr int TMAX = 64;            // tokens stored per lane per window
+constexpr int TMAX = 48;            // tokens stored per lane per window
 constexpr int LMAX = 512;           // max segment length (bits)
 constexpr int LMIN = 64;
+constexpr uint32_t ADAPT_FILL16 = 10; // adaptive L aims at this many 16ths of TMAX tokens per segment
 constexpr int SCAP = 6144;           // window output bytes resolved in LDS
 constexpr int CMAX = 256;           // max continuation bits into the next segment
 constexpr int OVR = 64;             // bitmap bits past the last token start
@@ -105,15 +106,14 @@ constexpr int ST_TRUNC = -3;
 constexpr int ST_SIZE = -4;
 constexpr int ST_UNSUP = -5;
 
-// decode-table entry: bits 0-3 code length, 4-7 extra bits, 8-10 kind, 16-31 value
-enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SLOW = 3, K_BAD = 4, K_SUB = 5 };
-HZ_HD uint32_t ent(uint32_t kind, uint32_t nbits, uint32_t extra, uint32_t value) {
-  return nbits | (extra << 4) | (kind << 8) | (value << 16);
-}
-HZ_HD uint32_t e_bits(uint32_t e) { return e & 15u; }
-HZ_HD uint32_t e_extra(uint32_t e) { return (e >> 4) & 15u; }
-HZ_HD uint32_t e_kind(uint32_t e) { return (e >> 8) & 7u; }
-HZ_HD uint32_t e_val(uint32_t e) { return e >> 16; }
+// 16-bit decode-table entry: bits 0-3 code length, bits 4-15 symbol (literal/length
+// table: 0-255 literal, 256 end of block, 257-285 length, anything else invalid;
+// distance table: 0-29, anything else invalid).  Code length 0 marks a pointer to a
+// second-level table: bits 4-12 its offset after the root entries, 13-15 its index
+// bits.  Length / distance bases and extra-bit counts are computed from the symbol.
+constexpr uint32_t SYM_BAD = 0xfffu;
+HZ_HD uint16_t ent_sym(uint32_t len, uint32_t sym) { return (uint16_t)(len | (sym << 4)); }
+HZ_HD uint16_t ent_sub(uint32_t off, uint32_t sb) { return (uint16_t)((off << 4) | (sb << 13)); }
 
 // tokens: literal = byte; match = 0x80000000 | len<<16 | (dist-1); EOB / ERR markers
 constexpr uint32_t T_MATCH = 0x80000000u;
@@ -124,24 +124,30 @@ constexpr uint32_t T_ERR = 0x40000001u;
 constexpr int S_NONE = 0, S_EOB = 1, S_ERR = 2;
 
 struct Shared {
-  uint32_t lut_ll[(1 << LL_ROOT) + LL_SUB];
-  uint32_t lut_d[(1 << D_ROOT) + D_SUB];
+  uint16_t lut_ll[(1 << LL_ROOT) + LL_SUB];
+  uint16_t lut_d[(1 << D_ROOT) + D_SUB];
   uint16_t tb_first[16];
   uint16_t tb_offs[17];
   uint16_t tb_next[16];
   uint32_t tok[TMAX][WAVE];          // token-major: lane-parallel accesses hit 64 banks
-  uint32_t bitmap[WAVE][BM_WORDS];
-  uint32_t in32[IN_WORDS + 4];
-  uint32_t exitpos[WAVE];
-  uint32_t syncpos[WAVE];
+  // The window's decode state (input staging, token-start bitmaps, per-lane exit /
+  // sync / repair flags) is dead once phase C starts building the byte reference
+  // map, and is rebuilt by the next window's staging / phase A: the two share LDS.
+  union {
+    struct {
+      uint32_t bitmap[WAVE][BM_WORDS];
+      uint32_t in32[IN_WORDS + 4];
+      uint32_t exitpos[WAVE];
+      uint32_t syncpos[WAVE];
+      uint32_t flag[WAVE];
+      uint32_t flag2[WAVE];
+    };
+    uint16_t ref[SCAP];
+  };
   uint32_t contpos[WAVE];
-  uint32_t flag[WAVE];
-  uint16_t ref[SCAP];
   uint32_t obase[WAVE + 1];
   uint16_t tcur_l[WAVE];
   uint16_t tend_l[WAVE];
-  uint32_t done[WAVE];
-  uint32_t flag2[WAVE];
   uint16_t sorted_ll[288];
   uint16_t sorted_d[32];
   uint16_t cnt_ll[16];
@@ -200,33 +206,6 @@ HZ_HD uint32_t rev_bits(uint32_t v, int n) {
   return r;
 }
 
-// ---- base / extra tables (RFC 1951 3.2.5) ----------------------------------
-HZ_HD uint32_t len_base(uint32_t s) {   // s = 0..28  (symbol 257+s)
-  const uint16_t t[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                          35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-  return t[s];
-}
-HZ_HD uint32_t len_extra(uint32_t s) {
-  return (s < 8 || s == 28) ? 0u : (s - 4) >> 2;
-}
-HZ_HD uint32_t dist_base(uint32_t s) {
-  const uint16_t t[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385,
-                          513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-  return t[s];
-}
-HZ_HD uint32_t dist_extra(uint32_t s) { return s < 4 ? 0u : (s - 2) >> 1; }
-
-HZ_HD uint32_t ll_entry(uint32_t sym, uint32_t len) {
-  if (sym < 256) return ent(K_LIT, len, 0, sym);
-  if (sym == 256) return ent(K_EOB, len, 0, 0);
-  if (sym <= 285) return ent(K_LEN, len, len_extra(sym - 257), len_base(sym - 257));
-  return ent(K_BAD, len ? len : 1, 0, 0);
-}
-HZ_HD uint32_t d_entry(uint32_t sym, uint32_t len) {
-  if (sym < 30) return ent(K_LEN, len, dist_extra(sym), dist_base(sym));
-  return ent(K_BAD, len ? len : 1, 0, 0);
-}
-
 // ---- LDS bit access ---------------------------------------------------------
 // Bit positions are relative to the 4-byte aligned base of the stream, so every
 // staged dword load is aligned.  peek64 returns >= 64 valid bits at `pos`.
@@ -238,58 +217,16 @@ HZ_HD uint64_t peek64(const Shared* sh, uint32_t pos) {
   return s ? ((lo >> s) | (hi << (64 - s))) : lo;
 }
 
-// canonical (slow path) decode for codes longer than the root:
-// returns (sym | len << 16), or 0xffffffff when no code matches.
-HZ_HD uint32_t canon_decode(const uint16_t* cnt, const uint16_t* sorted, uint64_t bits) {
-  int code = 0, first = 0, index = 0;
-  for (int len = 1; len <= 15; len++) {
-    code |= (int)(bits & 1u);
-    bits >>= 1;
-    int count = cnt[len];
-    if (code - count < first) return (uint32_t)sorted[index + (code - first)] | ((uint32_t)len << 16);
-    index += count;
-    first += count;
-    first <<= 1;
-    code <<= 1;
-  }
-  return 0xffffffffu;
-}
-
 HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
-  if (e_kind(e) == K_SUB) e = sh->lut_ll[e_val(e) + ((uint32_t)(bits >> LL_ROOT) & bmask(e_extra(e)))];
+  if (!(e & 15u)) e = sh->lut_ll[(1u << LL_ROOT) + ((e >> 4) & 511u) + ((uint32_t)(bits >> LL_ROOT) & bmask(e >> 13))];
   return e;
 }
 HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_d[bits & ((1u << D_ROOT) - 1)];
-  if (e_kind(e) == K_SUB) e = sh->lut_d[e_val(e) + ((uint32_t)(bits >> D_ROOT) & bmask(e_extra(e)))];
+  if (!(e & 15u)) e = sh->lut_d[(1u << D_ROOT) + ((e >> 4) & 511u) + ((uint32_t)(bits >> D_ROOT) & bmask(e >> 13))];
   return e;
 }
-
-// decode one token (literal, length+distance, EOB, or invalid) at bit `p`.
-// Invalid codes advance one bit so that a speculative decoder keeps going.
-HZ_HD void decode_token(const Shared* sh, uint32_t p, uint32_t& tokv, uint32_t& adv) {
-  const uint64_t bits = peek64(sh, p);
-  const uint32_t e = lookup_ll(sh, bits);
-  const uint32_t kind = e_kind(e), nb = e_bits(e);
-  if (kind == K_LIT) { tokv = e_val(e); adv = nb; return; }
-  if (kind == K_LEN) {
-    const uint32_t xb = e_extra(e);
-    const uint32_t len = e_val(e) + ((uint32_t)(bits >> nb) & bmask(xb));
-    const uint32_t c = nb + xb;
-    const uint64_t b2 = bits >> c;
-    const uint32_t ed = lookup_d(sh, b2);
-    if (e_kind(ed) != K_LEN) { tokv = T_ERR; adv = 1; return; }
-    const uint32_t nd = e_bits(ed), xd = e_extra(ed);
-    const uint32_t dist = e_val(ed) + ((uint32_t)(b2 >> nd) & bmask(xd));
-    tokv = T_MATCH | (len << 16) | (dist - 1u);
-    adv = c + nd + xd;
-    return;
-  }
-  if (kind == K_EOB) { tokv = T_EOB; adv = nb; return; }
-  tokv = T_ERR; adv = 1;
-}
-
 
 // ---- register bit reader over the staged window ------------------------------
 // bb holds `avail` (>= 32 after fill) bits starting at bit position `pos`; the next
@@ -331,16 +268,24 @@ HZ_HD void br_drop(BitRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n;
 HZ_HD uint32_t next_token(const Shared* sh, BitRd& r) {
   br_fill(sh, r);
   const uint32_t e = lookup_ll(sh, r.bb);
-  const uint32_t kind = e_kind(e), nb = e_bits(e), xb = e_extra(e), val = e_val(e);
-  const uint32_t len = val + ((uint32_t)(r.bb >> nb) & bmask(xb));
+  const uint32_t nb = e & 15u, p = e >> 4;
+  // RFC 1951 3.2.5 length codes: symbol 257+s, s < 8 -> 3+s, s == 28 -> 258,
+  // otherwise ((4 | s&3) << x) + 3 with x = (s-4)/4 extra bits
+  const uint32_t s = p - 257u;
+  const int islen = s < 29u;
+  const uint32_t xb = (islen && s >= 8u && s < 28u) ? (s - 4u) >> 2 : 0u;
+  const uint32_t base = s < 8u ? s + 3u : s == 28u ? 258u : ((4u | (s & 3u)) << xb) + 3u;
+  const uint32_t len = base + ((uint32_t)(r.bb >> nb) & bmask(xb));
   br_drop(r, nb + xb);
-  uint32_t tok = kind == K_LIT ? val : kind == K_EOB ? T_EOB : T_ERR;
-  if (kind == K_LEN) {
+  uint32_t tok = p < 256u ? p : p == 256u ? T_EOB : T_ERR;
+  if (islen) {
     br_fill(sh, r);
     const uint32_t ed = lookup_d(sh, r.bb);
-    const uint32_t nd = e_bits(ed), xd = e_extra(ed);
-    const uint32_t dist = e_val(ed) + ((uint32_t)(r.bb >> nd) & bmask(xd));
-    const int ok = e_kind(ed) == K_LEN;
+    const uint32_t nd = ed & 15u, d = ed >> 4;
+    // distance codes: d < 4 -> d+1, otherwise ((2 | d&1) << x) + 1 with x = d/2-1
+    const int ok = d < 30u;
+    const uint32_t xd = (ok && d >= 2u) ? (d - 2u) >> 1 : 0u;
+    const uint32_t dist = (d < 4u ? d + 1u : ((2u | (d & 1u)) << xd) + 1u) + ((uint32_t)(r.bb >> nd) & bmask(xd));
     br_drop(r, ok ? nd + xd : nd);
     tok = ok ? (T_MATCH | (len << 16) | (dist - 1u)) : T_ERR;
   }
@@ -436,7 +381,7 @@ struct TableArgs {
   int n;
   uint16_t* cnt;
   uint16_t* sorted;
-  uint32_t* lut;
+  uint16_t* lut;
   int root;
   int kind;
   int nsub;     // second-level capacity after the 2^root root entries
@@ -505,19 +450,18 @@ struct TableArgs {
     LANE_LOOP {                                                                         \
       for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
         int code = 0, first = 0, index = 0; uint32_t bits = (uint32_t)idx;              \
-        uint32_t e = hz::ent(hz::K_BAD, 1, 0, 0);                                       \
+        uint32_t e = hz::ent_sym(1, hz::SYM_BAD);                                       \
         for (int len = 1; len <= (A).root; len++) {                                     \
           code |= (int)(bits & 1u); bits >>= 1;                                         \
           int count = (A).cnt[len];                                                     \
           if (code - count < first) {                                                   \
             uint32_t sym = (A).sorted[index + (code - first)];                          \
-            e = (A).kind == 1 ? hz::ll_entry(sym, len)                                  \
-              : (A).kind == 2 ? hz::d_entry(sym, len) : hz::ent(hz::K_LIT, len, 0, sym); \
+            e = hz::ent_sym((uint32_t)len, sym);                                        \
             break;                                                                      \
           }                                                                             \
           index += count; first += count; first <<= 1; code <<= 1;                     \
         }                                                                               \
-        (A).lut[idx] = e;                                                               \
+        (A).lut[idx] = (uint16_t)e;                                                     \
       }                                                                                 \
     }                                                                                   \
     WAVE_SYNC();                                                                        \
@@ -540,8 +484,7 @@ struct TableArgs {
               lmax = l2; k2++;                                                          \
             }                                                                           \
             const int sb = lmax - _R;                                                   \
-            (A).lut[hz::rev_bits((uint32_t)p, _R)] =                                    \
-                hz::ent(hz::K_SUB, _R, sb, (uint32_t)((1 << _R) + used));               \
+            (A).lut[hz::rev_bits((uint32_t)p, _R)] = hz::ent_sub((uint32_t)used, (uint32_t)sb); \
             used += 1 << sb;  /* <= nsub for every complete code (see LL_SUB/D_SUB) */  \
             k = k2;                                                                     \
           }                                                                             \
@@ -556,11 +499,11 @@ struct TableArgs {
           const int c = (int)(sh).tb_first[len] + (k - (int)(sh).tb_offs[len]);         \
           const int p = c >> (len - _R);                                                \
           const uint32_t re = (A).lut[hz::rev_bits((uint32_t)p, _R)];                   \
-          if (hz::e_kind(re) != hz::K_SUB) continue;                                    \
-          const int sb = (int)hz::e_extra(re), off = (int)hz::e_val(re);                \
+          if (re & 15u) continue;                                                       \
+          const int sb = (int)(re >> 13), off = (1 << _R) + (int)((re >> 4) & 511u);    \
           const int tl = len - _R;                                                      \
           const uint32_t j0 = hz::rev_bits((uint32_t)(c & ((1 << tl) - 1)), tl);        \
-          const uint32_t e = (A).kind == 1 ? hz::ll_entry(sym, len) : hz::d_entry(sym, len); \
+          const uint16_t e = hz::ent_sym((uint32_t)len, sym);                           \
           for (int m = 0; m < (1 << (sb - tl)); m++) (A).lut[off + (j0 | (m << tl))] = e; \
         }                                                                               \
       }                                                                                 \
@@ -585,7 +528,7 @@ struct StreamJob {
 struct Tune {
   uint32_t L0;     // initial segment bits
   uint32_t W;      // warm-up bits
-  uint32_t adapt;  // adapt L to the token density
+  uint32_t adapt;  // 0: fixed L; 1: adapt L to the token density; n > 1: same, aiming at n/16 of TMAX tokens
   uint32_t C;      // continuation budget (bits)
   int max_rounds;  // repair rounds per window
 };
@@ -729,7 +672,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
           }
           if (left > 0 || maxl == 0) st = ST_DATA;  // code-length code must be complete
           // 7-bit LUT (sym | len << 8) in the distance table's space (rebuilt below)
-          uint32_t* clut = sh.lut_d;
+          uint16_t* clut = sh.lut_d;
           if (st == ST_OK) {
             uint32_t next[8];
             uint32_t code = 0;
@@ -738,7 +681,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
               const uint32_t l = cl[i];
               if (!l) continue;
               const uint32_t rc = rev_bits(next[l]++, (int)l);
-              for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint32_t)i | (l << 8);
+              for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint16_t)(i | (l << 8));
             }
           }
           const uint32_t total = hlit + hdist;
@@ -1223,7 +1166,8 @@ HZ_UNROLL
       if (tune.adapt) {
         const uint32_t used = npos - win_start;
         const uint32_t bpt16 = ntok_valid ? (used * 16u) / ntok_valid : 16u * 8u;   // bits/token x16
-        uint32_t target = (bpt16 * (uint32_t)TMAX) / (2u * 16u);
+        const uint32_t fill16 = tune.adapt > 1u ? tune.adapt : ADAPT_FILL16;   // of TMAX, /16
+        uint32_t target = (bpt16 * (uint32_t)TMAX * fill16) / (16u * 16u);
         if (wtotal && used) {
           const uint64_t lim = ((uint64_t)SCAP * 3u / 4u) * used / ((uint64_t)wtotal * 64u);
           if (lim < target) target = (uint32_t)lim;
