@@ -85,11 +85,11 @@ constexpr int D_ROOT = 8;
 // root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
 constexpr int LL_SUB = 512;
 constexpr int D_SUB = 384;
-constexpr int TMAX = 48;            // tokens stored per lane per window
-constexpr int LMAX = 512;           // max segment length (bits)
+constexpr int TMAX = 40;            // tokens stored per lane per window
+constexpr int LMAX = 384;           // max segment length (bits)
 constexpr int LMIN = 64;
 constexpr uint32_t ADAPT_FILL16 = 10; // adaptive L aims at this many 16ths of TMAX tokens per segment
-constexpr int SCAP = 6144;           // window output bytes resolved in LDS
+constexpr int SCAP = 5120;           // window output bytes resolved in LDS
 constexpr int CMAX = 256;           // max continuation bits into the next segment
 constexpr int OVR = 64;             // bitmap bits past the last token start
 constexpr int BM_WORDS = (LMAX + CMAX + OVR) / 32 + 1;
@@ -847,6 +847,9 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
         sh.flag[lane] = (uint32_t)LV(failed);
       }
       WAVE_SYNC();
+#if !HZ_GPU
+      uint32_t rsteps[64] = {0};
+#endif
       for (int round = 0; round < tune.max_rounds; round++) {
         const uint64_t fm = WAVE_BALLOT(LV(failed));
         if (!fm) break;
@@ -857,52 +860,93 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
           const int next_failed = lane < 63 ? (int)sh.flag[lane + 1] : 1;
           uint32_t steps = 0;
           if (redo) {
+            // re-decode from the predecessor's true exit; as soon as the true path
+            // lands on a token start of this lane's own speculative path, the rest
+            // of that path (tokens, continuation, successor sync) is already right:
+            // splice it in instead of decoding it again
             const uint32_t ss = LV(seg_start), se = ss + L;
-            uint32_t nt = 0;
-            for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
-            BitRd r;
-            br_init(&sh, r, sh.contpos[lane - 1], stage_base);
-            uint32_t mw_idx = (r.pos - ss) >> 5, mw = 0;
-            // segment part (starts at a true boundary at or after ss)
-            while (r.pos < se && nt < (uint32_t)TMAX) {
-              const uint32_t rel = r.pos - ss, wi = rel >> 5;
-              const uint32_t tokv = next_token(&sh, r);
-              steps++;
-              if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
-              mw |= 1u << (rel & 31u);
-              sh.tok[nt][lane] = tokv;
-              nt++;
+            const uint32_t old_nt = LV(ntok);
+            const uint32_t start = sh.contpos[lane - 1];
+            const uint32_t old_sync_next = lane < 63 ? sh.syncpos[lane + 1] : 0xffffffffu;
+            if (lane < 63 && !next_failed) sh.syncpos[lane + 1] = 0xffffffffu;
+            uint32_t cw = (start - ss) >> 5;          // bitmap word being rewritten
+            uint32_t oldc = 0;                        // old marks below word cw
+            for (uint32_t w = 0; w < cw && w < (uint32_t)BM_WORDS; w++) {
+              oldc += popc32(sh.bitmap[lane][w]);
+              sh.bitmap[lane][w] = 0;
             }
-            if (lane < 63) {
-              const uint32_t ssn = se;
-              if (!next_failed) sh.syncpos[lane + 1] = 0xffffffffu;
-              uint32_t nw_idx = 0xffffffffu, nw = 0;
-              for (;;) {
-                const uint32_t reln = r.pos - ssn;
-                if (!next_failed && r.pos >= ssn && reln < (uint32_t)(BM_WORDS * 32)) {
+            uint32_t ow = cw < (uint32_t)BM_WORDS ? sh.bitmap[lane][cw] : 0u;   // its old marks
+            uint32_t mw = 0;                          // its new marks
+            uint32_t nt = 0;
+            int merged = 0, nomerge = 0;
+            BitRd r;
+            br_init(&sh, r, start, stage_base);
+            uint32_t nw_idx = 0xffffffffu, nw = 0;
+            for (;;) {
+              const uint32_t rel = r.pos - ss, wi = rel >> 5;
+              if (wi != cw) {
+                oldc += popc32(ow);
+                if (cw < (uint32_t)BM_WORDS) sh.bitmap[lane][cw] = mw;
+                for (uint32_t w = cw + 1; w < wi && w < (uint32_t)BM_WORDS; w++) {
+                  oldc += popc32(sh.bitmap[lane][w]);
+                  sh.bitmap[lane][w] = 0;
+                }
+                cw = wi; mw = 0;
+                ow = wi < (uint32_t)BM_WORDS ? sh.bitmap[lane][wi] : 0u;
+              }
+              const uint32_t jcur = oldc + popc32(ow & bmask(rel & 31u));   // old tokens before here
+              if (((ow >> (rel & 31u)) & 1u) && !nomerge && jcur <= old_nt) {
+                // nt <= jcur: new tokens only ever overwrote old slots below jcur
+                sh.bitmap[lane][cw] = mw | (ow & ~bmask(rel & 31u));
+                if (nt < jcur) { for (uint32_t t = jcur; t < old_nt; t++) sh.tok[nt + t - jcur][lane] = sh.tok[t][lane]; }
+                nt += old_nt - jcur;
+                merged = 1;
+                break;
+              }
+              if (r.pos >= se) {                      // continuation into the successor
+                if (lane == 63 || next_failed) break;
+                const uint32_t reln = r.pos - se;
+                if (reln < (uint32_t)(BM_WORDS * 32)) {
                   if ((reln >> 5) != nw_idx) { nw_idx = reln >> 5; nw = sh.bitmap[lane + 1][nw_idx]; }
                   if ((nw >> (reln & 31u)) & 1u) { sh.syncpos[lane + 1] = r.pos; break; }
                 }
-                if (next_failed || r.pos >= ssn + C || nt >= (uint32_t)TMAX) break;
-                const uint32_t rel = r.pos - ss, wi = rel >> 5;
-                const uint32_t tokv = next_token(&sh, r);
-                steps++;
-                if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
-                mw |= 1u << (rel & 31u);
-                sh.tok[nt][lane] = tokv;
-                nt++;
+                if (r.pos >= se + C) break;
               }
+              if (nt >= (uint32_t)TMAX) break;
+              const uint32_t tokv = next_token(&sh, r);
+              steps++;
+              mw |= 1u << (rel & 31u);
+              if (nt >= jcur) nomerge = 1;            // slot nt may still hold a needed old token
+              sh.tok[nt][lane] = tokv;
+              nt++;
             }
-            if (mw_idx < (uint32_t)BM_WORDS) sh.bitmap[lane][mw_idx] |= mw;
-            mark_bit(&sh, lane, r.pos - ss);
-            sh.contpos[lane] = r.pos;
-            sh.syncpos[lane] = sh.contpos[lane - 1];   // whole token list is valid
+#if !HZ_GPU && defined(HZ_DEBUG)
+            if (!merged) printf("NOMERGE lane=%d L=%u start=%u end=%u old_nt=%u nt=%u nomerge=%d next_failed=%d oldc=%u se=%u\n", lane, L, start - ss, r.pos - ss, old_nt, nt, nomerge, next_failed, oldc, se - ss);
+#endif
+            if (merged) {
+              if (lane < 63) sh.syncpos[lane + 1] = old_sync_next;   // the old continuation stands
+            } else {
+              // final boundary mark; old marks at or after it are stale
+              const uint32_t rel = r.pos - ss;
+              if (cw < (uint32_t)BM_WORDS) sh.bitmap[lane][cw] = mw;
+              for (uint32_t w = cw + 1; w < (uint32_t)BM_WORDS; w++) sh.bitmap[lane][w] = 0;
+              mark_bit(&sh, lane, rel);
+              sh.contpos[lane] = r.pos;
+            }
+            sh.syncpos[lane] = start;                 // whole token list is valid
             LV(ntok) = nt;
+            if (stats) { stats->matches++; stats->match_bytes += (uint64_t)merged; stats->stored += (uint64_t)(!merged && nomerge); stats->blocks += (uint64_t)(!merged && old_nt < (uint32_t)TMAX && LV(storing) && sh.exitpos[lane] < se ); }
           }
           LV(nsteps) += steps;
+#if !HZ_GPU
+          rsteps[lane] = steps;
+#endif
           sh.flag2[lane] = (uint32_t)redo;
         }
         WAVE_SYNC();
+#if !HZ_GPU
+        if (stats) { uint32_t mx = 0; for (int l = 0; l < 64; l++) mx = rsteps[l] > mx ? rsteps[l] : mx; stats->lit_bytes += mx; }
+#endif
         LANE_LOOP {
           if (sh.flag2[lane]) LV(failed) = 0;
           else if (lane > 0 && sh.flag2[lane - 1] && sh.syncpos[lane] == 0xffffffffu) LV(failed) = 1;
