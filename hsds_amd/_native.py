@@ -8,7 +8,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhsds_amd.so")
+# HSDS_AMD_LIB: development override (A/B timing of two builds); the default is the in-tree build
+LIB_PATH = os.environ.get("HSDS_AMD_LIB") or os.path.join(_HERE, "libhsds_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hsds_amd.h")
 
 OK = 0

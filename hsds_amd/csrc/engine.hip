@@ -25,7 +25,7 @@
 namespace {
 
 constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
-constexpr int INFLATE_WAVES_PER_CU = 6;   // LDS-bound: sizeof(hz::Shared) <= 26.6 KiB
+constexpr int INFLATE_WAVES_PER_CU = 7;   // LDS-bound: sizeof(hz::Shared) <= 22.8 KiB
 static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
 
 enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_INEXACT = 0x100 };
@@ -428,6 +428,11 @@ int hsds_engine_create(int device, hsds_engine** out) {
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, inflate_kernel, 64, 0) != hipSuccess || occ < 1)
     occ = INFLATE_WAVES_PER_CU;
+  // development override (A/B experiments): fewer resident inflate wavefronts per CU
+  if (const char* ev = getenv("HSDS_INFLATE_WAVES")) {
+    const int v = atoi(ev);
+    if (v >= 1 && v < occ) occ = v;
+  }
   e->inflate_blocks_per_cu = occ;
   e->tune.L0 = 384;
   e->tune.W = 96;

@@ -85,10 +85,10 @@ constexpr int D_ROOT = 8;
 // root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
 constexpr int LL_SUB = 512;
 constexpr int D_SUB = 384;
-constexpr int TMAX = 40;            // tokens stored per lane per window
+constexpr int SLOTS = 58;           // 16-bit token slots per lane per window (a match takes two)
 constexpr int LMAX = 384;           // max segment length (bits)
 constexpr int LMIN = 64;
-constexpr uint32_t ADAPT_FILL16 = 10; // adaptive L aims at this many 16ths of TMAX tokens per segment
+constexpr uint32_t ADAPT_FILL16 = 11; // adaptive L aims at this many 16ths of SLOTS token slots per segment
 constexpr int SCAP = 5120;           // window output bytes resolved in LDS
 constexpr int CMAX = 256;           // max continuation bits into the next segment
 constexpr int OVR = 64;             // bitmap bits past the last token start
@@ -115,13 +115,15 @@ constexpr uint32_t SYM_BAD = 0xfffu;
 HZ_HD uint16_t ent_sym(uint32_t len, uint32_t sym) { return (uint16_t)(len | (sym << 4)); }
 HZ_HD uint16_t ent_sub(uint32_t off, uint32_t sb) { return (uint16_t)((off << 4) | (sb << 13)); }
 
-// tokens: literal = byte; match = 0x80000000 | len<<16 | (dist-1); EOB / ERR markers
+// tokens (decoder result): literal = byte; match = 0x80000000 | len<<16 | (dist-1); EOB / ERR
 constexpr uint32_t T_MATCH = 0x80000000u;
 constexpr uint32_t T_EOB = 0x40000000u;
 constexpr uint32_t T_ERR = 0x40000001u;
+// stored token slots (16 bit): literal byte, S_EOB, S_ERR, or a match as two slots
+// 0x8000 | (len - 3) followed by (dist - 1).  A lane's token k sits at slot
+// k + popcount(match mask of tokens < k).
+constexpr uint32_t S_EOB = 0x100u, S_ERR = 0x101u, S_MATCH = 0x8000u;
 
-// stop reasons of a Phase-A lane
-constexpr int S_NONE = 0, S_EOB = 1, S_ERR = 2;
 
 struct Shared {
   uint16_t lut_ll[(1 << LL_ROOT) + LL_SUB];
@@ -129,13 +131,29 @@ struct Shared {
   uint16_t tb_first[16];
   uint16_t tb_offs[17];
   uint16_t tb_next[16];
-  uint32_t tok[TMAX][WAVE];          // token-major: lane-parallel accesses hit 64 banks
+  // token slots, lane-interleaved in pairs: slot s of lane l is half (s & 1) of dword
+  // (s >> 1) * 64 + l, so lanes reading any slots hit distinct banks
+  union {
+    uint16_t tok[SLOTS * WAVE];
+    uint32_t tokw[SLOTS / 2 * WAVE];
+  };
   // The window's decode state (input staging, token-start bitmaps, per-lane exit /
   // sync / repair flags) is dead once phase C starts building the byte reference
   // map, and is rebuilt by the next window's staging / phase A: the two share LDS.
   union {
     struct {
-      uint32_t bitmap[WAVE][BM_WORDS];
+      union {
+        uint32_t bitmap[WAVE][BM_WORDS];
+        struct {                         // Huffman table build scratch (dead while windows run)
+          uint16_t sorted_ll[288];
+          uint16_t sorted_d[32];
+          uint16_t cnt_ll[16];
+          uint16_t cnt_d[16];
+          uint16_t cnt_cl[16];
+          uint16_t sorted_cl[20];
+          uint8_t lens[320 + 32];
+        };
+      };
       uint32_t in32[IN_WORDS + 4];
       uint32_t exitpos[WAVE];
       uint32_t syncpos[WAVE];
@@ -148,13 +166,6 @@ struct Shared {
   uint32_t obase[WAVE + 1];
   uint16_t tcur_l[WAVE];
   uint16_t tend_l[WAVE];
-  uint16_t sorted_ll[288];
-  uint16_t sorted_d[32];
-  uint16_t cnt_ll[16];
-  uint16_t cnt_d[16];
-  uint16_t cnt_cl[16];
-  uint16_t sorted_cl[20];
-  uint8_t lens[320 + 32];
   // uniform scalars published by lane 0
   int32_t u_status;
   uint32_t u_pos;
@@ -291,6 +302,31 @@ HZ_HD uint32_t next_token(const Shared* sh, BitRd& r) {
   }
   return tok;
 }
+
+HZ_HD uint32_t tok_idx(uint32_t s, int lane) { return ((s >> 1) * (uint32_t)WAVE + (uint32_t)lane) * 2u + (s & 1u); }
+HZ_HD uint32_t tok_at(const Shared* sh, uint32_t s, int lane) { return sh->tok[tok_idx(s, lane)]; }
+// store decoder token tokv at slot ns of `lane`; returns the slots used (1 or 2)
+HZ_HD uint32_t put_tok(Shared* sh, int lane, uint32_t ns, uint32_t tokv) {
+  if (tokv & T_MATCH) {
+    sh->tok[tok_idx(ns, lane)] = (uint16_t)(S_MATCH | (((tokv >> 16) & 0x1ffu) - 3u));
+    sh->tok[tok_idx(ns + 1u, lane)] = (uint16_t)(tokv & 0x7fffu);
+    return 2u;
+  }
+  sh->tok[tok_idx(ns, lane)] = (uint16_t)(tokv == T_EOB ? S_EOB : tokv == T_ERR ? S_ERR : tokv);
+  return 1u;
+}
+// token at slot t of lane j: v = the slot, d = distance of a match (the next slot + 1);
+// two independent dword reads instead of two dependent 16-bit ones
+HZ_HD void tok_pair(const Shared* sh, uint32_t t, int j, uint32_t& v, uint32_t& d) {
+  const uint32_t q = t >> 1;
+  const uint32_t q1 = q + 1u < (uint32_t)(SLOTS / 2) ? q + 1u : q;
+  const uint32_t w0 = sh->tokw[q * (uint32_t)WAVE + (uint32_t)j];
+  const uint32_t w1 = sh->tokw[q1 * (uint32_t)WAVE + (uint32_t)j];
+  v = (t & 1u) ? (w0 >> 16) : (w0 & 0xffffu);
+  d = ((t & 1u) ? (w1 & 0xffffu) : (w0 >> 16)) + 1u;
+}
+// slot of token k of a lane whose match mask is mb
+HZ_HD uint32_t tok_slot(uint64_t mb, uint32_t k) { return k + popc64(k >= 64u ? mb : mb & ((1ull << k) - 1ull)); }
 
 HZ_HD void mark_bit(Shared* sh, int lane, uint32_t rel) {
   if (rel < (uint32_t)(BM_WORDS * 32)) sh->bitmap[lane][rel >> 5] |= 1u << (rel & 31u);
@@ -528,7 +564,7 @@ struct StreamJob {
 struct Tune {
   uint32_t L0;     // initial segment bits
   uint32_t W;      // warm-up bits
-  uint32_t adapt;  // 0: fixed L; 1: adapt L to the token density; n > 1: same, aiming at n/16 of TMAX tokens
+  uint32_t adapt;  // 0: fixed L; 1: adapt L to the token density; n > 1: same, aiming at n/16 of SLOTS slots
   uint32_t C;      // continuation budget (bits)
   int max_rounds;  // repair rounds per window
 };
@@ -756,7 +792,9 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       // own segment [ss, ss+L) are stored and their start bits marked.
       const uint32_t stage_base = ((win_start >= W ? win_start - W : 0u) >> 5) * 32u;
       LANE_VAR(uint32_t, seg_start);
-      LANE_VAR(uint32_t, ntok);
+      LANE_VAR(uint32_t, ntok);      // tokens stored
+      LANE_VAR(uint32_t, nslot);     // slots they use
+      LANE_VAR(uint64_t, mbits);     // bit k: token k is a match (two slots)
       LANE_VAR(int, storing);
       LANE_VAR(uint32_t, nsteps);
       LANE_LOOP {
@@ -764,14 +802,15 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
         const uint32_t se = ss + L;
         const uint32_t p0 = (lane > 0 && ss - win_start > W) ? ss - W : win_start;
         int st = p0 >= ss;
-        uint32_t nt = 0, steps = 0;
+        uint32_t nt = 0, ns = 0, steps = 0;
+        uint64_t mb = 0;
         for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
         uint32_t mw_idx = 0, mw = 0;  // bitmap word cached in a register (monotonic positions)
         BitRd r;
         br_init(&sh, r, p0, stage_base);
         while (r.pos < se) {
           if (!st && r.pos >= ss) st = 1;
-          if (st && nt >= (uint32_t)TMAX) break;
+          if (st && ns + 2u > (uint32_t)SLOTS) break;
           const uint32_t tp = r.pos;
           const uint32_t tokv = next_token(&sh, r);
           steps++;
@@ -779,7 +818,9 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             const uint32_t rel = tp - ss, wi = rel >> 5;
             if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
             mw |= 1u << (rel & 31u);
-            sh.tok[nt][lane] = tokv;
+            const uint32_t w = put_tok(&sh, lane, ns, tokv);
+            mb |= (uint64_t)(w - 1u) << nt;
+            ns += w;
             nt++;
           }
         }
@@ -789,6 +830,8 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
         }
         LV(seg_start) = ss;
         LV(ntok) = nt;
+        LV(nslot) = ns;
+        LV(mbits) = mb;
         LV(storing) = st;
         LV(nsteps) = steps;
         sh.exitpos[lane] = r.pos;
@@ -803,7 +846,8 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       // bits into segment i+1.  Tokens decoded here belong to lane i.
       LANE_LOOP {
         const uint32_t ss = LV(seg_start);
-        uint32_t nt = LV(ntok), steps = 0;
+        uint32_t nt = LV(ntok), ns = LV(nslot), steps = 0;
+        uint64_t mb = LV(mbits);
         uint32_t pend = sh.exitpos[lane];
         if (lane < 63 && LV(storing)) {
           const uint32_t ssn = ss + L;
@@ -817,13 +861,15 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
               if ((reln >> 5) != nw_idx) { nw_idx = reln >> 5; nw = sh.bitmap[lane + 1][nw_idx]; }
               if ((nw >> (reln & 31u)) & 1u) { sh.syncpos[lane + 1] = r.pos; break; }
             }
-            if (r.pos >= ssn + C || nt >= (uint32_t)TMAX) break;
+            if (r.pos >= ssn + C || ns + 2u > (uint32_t)SLOTS) break;
             const uint32_t rel = r.pos - ss, wi = rel >> 5;
             const uint32_t tokv = next_token(&sh, r);
             steps++;
             if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
             mw |= 1u << (rel & 31u);
-            sh.tok[nt][lane] = tokv;
+            const uint32_t w = put_tok(&sh, lane, ns, tokv);
+            mb |= (uint64_t)(w - 1u) << nt;
+            ns += w;
             nt++;
           }
           if (mw_idx < (uint32_t)BM_WORDS) sh.bitmap[lane][mw_idx] |= mw;
@@ -831,6 +877,8 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
           mark_bit(&sh, lane, pend - ss);     // final boundary of this lane's decode
         }
         LV(ntok) = nt;
+        LV(nslot) = ns;
+        LV(mbits) = mb;
         LV(nsteps) += steps;
         sh.contpos[lane] = pend;
       }
@@ -865,7 +913,8 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             // of that path (tokens, continuation, successor sync) is already right:
             // splice it in instead of decoding it again
             const uint32_t ss = LV(seg_start), se = ss + L;
-            const uint32_t old_nt = LV(ntok);
+            const uint32_t old_nt = LV(ntok), old_ns = LV(nslot);
+            const uint64_t old_mb = LV(mbits);
             const uint32_t start = sh.contpos[lane - 1];
             const uint32_t old_sync_next = lane < 63 ? sh.syncpos[lane + 1] : 0xffffffffu;
             if (lane < 63 && !next_failed) sh.syncpos[lane + 1] = 0xffffffffu;
@@ -877,7 +926,8 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             }
             uint32_t ow = cw < (uint32_t)BM_WORDS ? sh.bitmap[lane][cw] : 0u;   // its old marks
             uint32_t mw = 0;                          // its new marks
-            uint32_t nt = 0;
+            uint32_t nt = 0, ns = 0;
+            uint64_t mb = 0;
             int merged = 0, nomerge = 0;
             BitRd r;
             br_init(&sh, r, start, stage_base);
@@ -895,10 +945,15 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
                 ow = wi < (uint32_t)BM_WORDS ? sh.bitmap[lane][wi] : 0u;
               }
               const uint32_t jcur = oldc + popc32(ow & bmask(rel & 31u));   // old tokens before here
+              const uint32_t scur = jcur <= old_nt ? tok_slot(old_mb, jcur) : old_ns;   // their slots
               if (((ow >> (rel & 31u)) & 1u) && !nomerge && jcur <= old_nt) {
-                // nt <= jcur: new tokens only ever overwrote old slots below jcur
+                // ns <= scur: new tokens only ever overwrote old slots below scur
                 sh.bitmap[lane][cw] = mw | (ow & ~bmask(rel & 31u));
-                if (nt < jcur) { for (uint32_t t = jcur; t < old_nt; t++) sh.tok[nt + t - jcur][lane] = sh.tok[t][lane]; }
+                if (ns < scur) {
+                  for (uint32_t t = scur; t < old_ns; t++) sh.tok[tok_idx(ns + t - scur, lane)] = sh.tok[tok_idx(t, lane)];
+                }
+                mb |= (old_mb >> jcur) << nt;
+                ns += old_ns - scur;
                 nt += old_nt - jcur;
                 merged = 1;
                 break;
@@ -912,12 +967,15 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
                 }
                 if (r.pos >= se + C) break;
               }
-              if (nt >= (uint32_t)TMAX) break;
+              if (ns + 2u > (uint32_t)SLOTS) break;
               const uint32_t tokv = next_token(&sh, r);
               steps++;
               mw |= 1u << (rel & 31u);
-              if (nt >= jcur) nomerge = 1;            // slot nt may still hold a needed old token
-              sh.tok[nt][lane] = tokv;
+              const uint32_t w = (tokv & T_MATCH) ? 2u : 1u;
+              if (ns + w > scur) nomerge = 1;         // would overwrite a possibly needed old slot
+              put_tok(&sh, lane, ns, tokv);
+              mb |= (uint64_t)(w - 1u) << nt;
+              ns += w;
               nt++;
             }
 #if !HZ_GPU && defined(HZ_DEBUG)
@@ -935,7 +993,9 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             }
             sh.syncpos[lane] = start;                 // whole token list is valid
             LV(ntok) = nt;
-            if (stats) { stats->matches++; stats->match_bytes += (uint64_t)merged; stats->stored += (uint64_t)(!merged && nomerge); stats->blocks += (uint64_t)(!merged && old_nt < (uint32_t)TMAX && LV(storing) && sh.exitpos[lane] < se ); }
+            LV(nslot) = ns;
+            LV(mbits) = mb;
+            if (stats) { stats->matches++; stats->match_bytes += (uint64_t)merged; }
           }
           LV(nsteps) += steps;
 #if !HZ_GPU
@@ -983,9 +1043,11 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
         uint32_t te = LV(ntok);
         int ek = 0;
         if (ok) {
+          uint32_t sl = tok_slot(LV(mbits), tf);
           for (uint32_t t = tf; t < te; t++) {
-            const uint32_t v = sh.tok[t][lane];
-            if (v == T_EOB || v == T_ERR) { ek = v == T_EOB ? 1 : 2; te = t; break; }
+            const uint32_t v = tok_at(&sh, sl, lane);
+            if (v == S_EOB || v == S_ERR) { ek = v == S_EOB ? 1 : 2; te = t; break; }
+            sl += (v & S_MATCH) ? 2u : 1u;
           }
         }
         LV(tok_first) = ok ? tf : 0xffffffffu;
@@ -1014,11 +1076,15 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
           // bit position after the EOB token = the mark following token te
           sh.u_pos = nth_mark(&sh, lane, te + 1u) + LV(seg_start);
         }
+        const uint32_t sf = tok_slot(LV(mbits), tf);
+        uint32_t sl = sf;
         for (uint32_t t = tf; t < te; t++) {
-          const uint32_t v = sh.tok[t][lane];
-          ol += (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+          const uint32_t v = tok_at(&sh, sl, lane);
+          const uint32_t m = v & S_MATCH;
+          ol += m ? (v & 0xffu) + 3u : 1u;
+          sl += m ? 2u : 1u;
         }
-        LV(tcur) = tf; LV(tend) = te; LV(olen) = ol;
+        LV(tcur) = sf; LV(tend) = sl; LV(olen) = ol;
       }
       WAVE_SYNC();
       if (end_lane >= 0 && sh.u_status == 2) {
@@ -1042,14 +1108,15 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             // lane 0 alone overflows: keep its first tokens that fit (>= 1 token)
             LANE_LOOP {
               if (lane == 0) {
-                uint32_t t = LV(tcur), acc = 0;
-                while (t < LV(tend)) {
-                  const uint32_t v = sh.tok[t][lane];
-                  const uint32_t n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+                uint32_t sl = LV(tcur), t = 0, acc = 0;     // lane 0's tokens start at token 0
+                while (sl < LV(tend)) {
+                  const uint32_t v = tok_at(&sh, sl, lane);
+                  const uint32_t m = v & S_MATCH;
+                  const uint32_t n = m ? (v & 0xffu) + 3u : 1u;
                   if (acc + n > (uint32_t)SCAP) break;
-                  acc += n; t++;
+                  acc += n; sl += m ? 2u : 1u; t++;
                 }
-                LV(tend) = t; LV(olen) = acc;
+                LV(tend) = sl; LV(olen) = acc;
                 sh.u_pos = win_start + nth_mark(&sh, lane, t);
               }
             }
@@ -1104,32 +1171,36 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
             if (sh.obase[mid] <= x0) lo_j = mid; else hi_j = mid - 1;
           }
           int j = lo_j;
-          uint32_t t = sh.tcur_l[j], q = sh.obase[j];
-          uint32_t v = sh.tok[t][j];
-          uint32_t n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+          uint32_t t = sh.tcur_l[j], q = sh.obase[j];     // t: slot of lane j
+          uint32_t v, d;
+          tok_pair(&sh, t, j, v, d);
+          uint32_t m = v & S_MATCH;
+          uint32_t n = m ? (v & 0xffu) + 3u : 1u;
           while (q + n <= x0) {                    // token of lane j containing x0
-            q += n; t++;
-            v = sh.tok[t][j];
-            n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
+            q += n; t += m ? 2u : 1u;
+            tok_pair(&sh, t, j, v, d);
+            m = v & S_MATCH;
+            n = m ? (v & 0xffu) + 3u : 1u;
           }
-          uint32_t d = (v & 0x7fffu) + 1u;
-          uint32_t jj = (v & T_MATCH) ? (x0 - q) % d : 0u;
+          d = m ? d : 1u;
+          uint32_t jj = m ? (x0 - q) % d : 0u;
           int32_t base = (int32_t)q - (int32_t)d;
           uint32_t tend_j = sh.tend_l[j];
-          if ((v & T_MATCH) && d > wbeg + q) err = 1;
+          if (m && d > wbeg + q) err = 1;
           for (uint32_t x = x0; x < x1 && !err; x++) {
             if (x == q + n) {                      // next token (possibly of the next lane)
-              q = x; t++;
+              q = x; t += m ? 2u : 1u;
               while (t >= tend_j) { j++; t = sh.tcur_l[j]; tend_j = sh.tend_l[j]; }
-              v = sh.tok[t][j];
-              n = (v & T_MATCH) ? ((v >> 16) & 0x1ffu) : 1u;
-              d = (v & 0x7fffu) + 1u;
+              tok_pair(&sh, t, j, v, d);
+              m = v & S_MATCH;
+              n = m ? (v & 0xffu) + 3u : 1u;
+              d = m ? d : 1u;
               base = (int32_t)q - (int32_t)d;
               jj = 0;
-              if ((v & T_MATCH) && d > wbeg + q) { err = 1; break; }
+              if (m && d > wbeg + q) { err = 1; break; }
             }
             const int32_t srcq = base + (int32_t)jj;
-            const uint32_t rv = !(v & T_MATCH) ? (0x4000u | v)
+            const uint32_t rv = !m ? (0x4000u | v)
                               : srcq >= 0 ? (uint32_t)srcq : (0x8000u | (uint32_t)(-srcq - 1));
             sh.ref[x] = (uint16_t)rv;
             jj++;
@@ -1205,13 +1276,13 @@ HZ_UNROLL
       out += wtotal;
       pos = npos;
       if (end_lane >= 0) break;        // EOB: the next block header follows
-      // next segment length: about half of TMAX tokens per segment (room for the
+      // next segment length: about half of SLOTS token slots per segment (room for the
       // continuation) and an expected window output of about 3/4 of the LDS map
       if (tune.adapt) {
         const uint32_t used = npos - win_start;
         const uint32_t bpt16 = ntok_valid ? (used * 16u) / ntok_valid : 16u * 8u;   // bits/token x16
-        const uint32_t fill16 = tune.adapt > 1u ? tune.adapt : ADAPT_FILL16;   // of TMAX, /16
-        uint32_t target = (bpt16 * (uint32_t)TMAX * fill16) / (16u * 16u);
+        const uint32_t fill16 = tune.adapt > 1u ? tune.adapt : ADAPT_FILL16;   // of SLOTS, /16
+        uint32_t target = (bpt16 * (uint32_t)SLOTS * fill16) / (16u * 16u);   // bpt16: bits per slot
         if (wtotal && used) {
           const uint64_t lim = ((uint64_t)SCAP * 3u / 4u) * used / ((uint64_t)wtotal * 64u);
           if (lim < target) target = (uint32_t)lim;

@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 from hsds_amd import _native  # noqa: E402
 
-_native.LIB_PATH = os.path.join(ROOT, "tools", "libhsds_prof.so")
+_native.LIB_PATH = os.environ.get("HZ_PROF_LIB") or os.path.join(ROOT, "tools", "libhsds_prof.so")
 L = _native.lib()
 L.hsds_debug_profile.argtypes = [ctypes.c_void_p, ctypes.c_int]
 import torch  # noqa: E402
@@ -46,11 +46,13 @@ def run(fmt, n, unique, tune=None):
     assert (d_st.cpu().numpy() == 0).all()
     tot = sum(buf)
     print(f"{fmt} n={n} tune={tune} wall={el*1e3:.1f} ms  {n*CHUNK_BYTES/el/1e9:.2f} GB/s  kernel={eng.last_inflate_ms():.1f} ms")
+    streams = n * 4
     for i in range(16):
         if buf[i]:
-            print(f"   {NAMES[i]:10s} {100.0*buf[i]/tot:6.2f}%")
+            print(f"   {NAMES[i]:10s} {100.0*buf[i]/tot:6.2f}%   {buf[i]/streams/1e3:9.1f} kcyc/stream")
 
 
 if __name__ == "__main__":
-    run("F1", 1024, 256)
-    run("F2", 256, 128)
+    n1 = int(os.environ.get("HZ_PROF_N1", "1024"))
+    run("F1", n1, 256)
+    run("F2", int(os.environ.get("HZ_PROF_N2", "256")), 128)
