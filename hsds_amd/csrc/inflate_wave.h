@@ -117,8 +117,8 @@ HZ_HD uint16_t ent_sub(uint32_t off, uint32_t sb) { return (uint16_t)((off << 4)
 
 // tokens (decoder result): literal = byte; match = 0x80000000 | len<<16 | (dist-1); EOB / ERR
 constexpr uint32_t T_MATCH = 0x80000000u;
-constexpr uint32_t T_EOB = 0x40000000u;
-constexpr uint32_t T_ERR = 0x40000001u;
+constexpr uint32_t T_EOB = 0x100u;        // == its stored slot value S_EOB
+constexpr uint32_t T_ERR = 0x101u;        // == S_ERR
 // stored token slots (16 bit): literal byte, S_EOB, S_ERR, or a match as two slots
 // 0x8000 | (len - 3) followed by (dist - 1).  A lane's token k sits at slot
 // k + popcount(match mask of tokens < k).
@@ -288,7 +288,7 @@ HZ_HD uint32_t next_token(const Shared* sh, BitRd& r) {
   const uint32_t base = s < 8u ? s + 3u : s == 28u ? 258u : ((4u | (s & 3u)) << xb) + 3u;
   const uint32_t len = base + ((uint32_t)(r.bb >> nb) & bmask(xb));
   br_drop(r, nb + xb);
-  uint32_t tok = p < 256u ? p : p == 256u ? T_EOB : T_ERR;
+  uint32_t tok = p <= 256u ? p : T_ERR;     // literal byte or T_EOB (= 256)
   if (islen) {
     br_fill(sh, r);
     const uint32_t ed = lookup_d(sh, r.bb);
@@ -307,13 +307,11 @@ HZ_HD uint32_t tok_idx(uint32_t s, int lane) { return ((s >> 1) * (uint32_t)WAVE
 HZ_HD uint32_t tok_at(const Shared* sh, uint32_t s, int lane) { return sh->tok[tok_idx(s, lane)]; }
 // store decoder token tokv at slot ns of `lane`; returns the slots used (1 or 2)
 HZ_HD uint32_t put_tok(Shared* sh, int lane, uint32_t ns, uint32_t tokv) {
-  if (tokv & T_MATCH) {
-    sh->tok[tok_idx(ns, lane)] = (uint16_t)(S_MATCH | (((tokv >> 16) & 0x1ffu) - 3u));
-    sh->tok[tok_idx(ns + 1u, lane)] = (uint16_t)(tokv & 0x7fffu);
-    return 2u;
-  }
-  sh->tok[tok_idx(ns, lane)] = (uint16_t)(tokv == T_EOB ? S_EOB : tokv == T_ERR ? S_ERR : tokv);
-  return 1u;
+  const uint32_t m = tokv & T_MATCH;
+  const uint32_t i0 = tok_idx(ns, lane);
+  sh->tok[i0] = (uint16_t)(m ? (S_MATCH | (((tokv >> 16) & 0x1ffu) - 3u)) : tokv);
+  if (m) sh->tok[i0 + ((ns & 1u) ? 2u * (uint32_t)WAVE - 1u : 1u)] = (uint16_t)(tokv & 0x7fffu);
+  return m ? 2u : 1u;
 }
 // token at slot t of lane j: v = the slot, d = distance of a match (the next slot + 1);
 // two independent dword reads instead of two dependent 16-bit ones
