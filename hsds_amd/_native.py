@@ -75,6 +75,9 @@ def lib():
         "hsds_copy_batch": (I, [P, P, P, P, I64, P]),
         "hsds_compare_batch": (I, [P, P, P, P, I64, I, P, P]),
         "hsds_copy_batch_if": (I, [P, P, P, P, I64, P, P]),
+        "hsds_encode_batch": (I, [P, P, P, I64, P, U64, P, P, I, I, I, P]),
+        "hsds_compress": (I64, [P, P, I64, I, I, I, P, I64]),
+        "hsds_last_deflate_ms": (I, [P, ctypes.POINTER(ctypes.c_float)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -134,6 +137,13 @@ class Engine:
         rc = lib().hsds_last_inflate_ms(self.h, ctypes.byref(v))
         if rc != OK:
             raise NativeError(rc, "hsds_last_inflate_ms")
+        return v.value
+
+    def last_deflate_ms(self):
+        v = ctypes.c_float()
+        rc = lib().hsds_last_deflate_ms(self.h, ctypes.byref(v))
+        if rc != OK:
+            raise NativeError(rc, "hsds_last_deflate_ms")
         return v.value
 
 

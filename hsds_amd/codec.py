@@ -141,8 +141,32 @@ def _uncompress(data, compressor=None, shuffle=0, level=None, dtype=None, chunk_
 
 
 def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape=None):
-    """storUtil._compress (storUtil.py:238-281).  The GPU deflate encoder is the
-    next SURVEY.md section 8 row for this engine; until it lands this raises."""
+    """storUtil._compress (storUtil.py:238-281) on the GPU: a Blosc1 frame with the
+    zlib inner codec (gzip/deflate/zlib are all Blosc "zlib", storUtil.py:255-257),
+    typesize 1 because the reference always hands Blosc a bytes object, and the
+    byte-shuffle flag from `shuffle`.  Differences from the reference, by design:
+      * bitshuffle (shuffle=2) and other Blosc codecs are outside this engine and raise
+        NotImplementedError (the reference would bitshuffle, then Blosc-encode);
+      * an encoder failure raises instead of silently storing the raw bytes
+        (storUtil.py:266-279 logs and returns `data`, which its own reader then
+        rejects: SURVEY.md section 8b)."""
     if not compressor and shuffle != BIT_SHUFFLE:
         return data
-    raise NotImplementedError("GPU Blosc/zlib encoder not built yet (write path, BASELINE config 5)")
+    if shuffle == BIT_SHUFFLE:
+        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+    if shuffle not in (0, BYTE_SHUFFLE):
+        raise ValueError()
+    if not compressor or compressor == "scaleoffset":
+        return data        # no compressor, nothing shuffled: the bytes as given
+    if _compressor_code(compressor) != nat.COMP_ZLIB:
+        raise NotImplementedError(f"Blosc codec {compressor!r} is outside the hsds_amd engine scope")
+    if level is None:
+        level = 5
+    src = _as_bytes(data)
+    cap = src.size + 16
+    out = np.empty(cap, np.uint8)
+    n = nat.lib().hsds_compress(nat.engine().h, src.ctypes.data, src.size, int(level), int(shuffle), 1,
+                                out.ctypes.data, cap)
+    if n < 0:
+        raise nat.NativeError(n, "hsds_compress")
+    return out[:n].tobytes()

@@ -10,6 +10,12 @@
 //   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
 //   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
 //                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
+//   enc_plan_kernel     one thread per chunk: c-blosc 1.21 frame geometry of
+//                       storUtil._compress (storUtil.py:238-281), one item per split
+//   deflate_kernel      persistent waves; one wavefront encodes one zlib stream
+//                       (deflate_wave.h)
+//   frame_kernel        one workgroup per chunk: Blosc1 header, bstarts, raw-split and
+//                       memcpyed fallbacks, payload copies into the final frame
 // Every launch is asynchronous on the caller's stream; no host synchronisation
 // inside the batched entry points.
 #include <hip/hip_runtime.h>
@@ -19,6 +25,7 @@
 
 #include "../../include/hsds_amd.h"
 #include "inflate_wave.h"
+#include "deflate_wave.h"
 
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -364,6 +371,276 @@ __global__ void zero_i32_kernel(int32_t* p, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
 }
 
+
+// =========================================================================
+// encode (storUtil._compress -> c-blosc 1.21 blosc_compress_ctx, zlib codec)
+// =========================================================================
+constexpr uint64_t ENC_CHUNK_SLACK = 4352;   // per-chunk scratch slack: 16 B per item + alignment
+
+struct EncItem {       // 40 bytes
+  uint64_t src;        // block base (stream input when ts == 1)
+  uint64_t dst;        // scratch output, 4-byte aligned, cap + 8 bytes
+  uint32_t len;        // stream input bytes (neblock)
+  uint32_t cap;        // neblock - 1: an output of neblock bytes or more is stored raw
+  uint32_t off;        // stream offset inside the (shuffled) block
+  uint32_t ts;         // > 1: gather from the byte-shuffled block
+  uint32_t neb;        // elements per block plane
+  uint32_t chunk;
+};
+
+struct EncGeom {       // per-chunk frame geometry (enc_plan_kernel -> frame_kernel)
+  uint64_t nbytes;
+  uint64_t bs;
+  uint32_t nblocks;
+  uint32_t flags;
+  uint32_t ts;
+  uint32_t memcpyed;
+};
+
+// c-blosc 1.21 compute_blocksize for the zlib codec (oracle.c orc_blosc_blocksize)
+__device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint64_t nbytes) {
+  if (nbytes < ts) return 1;
+  uint64_t bs = nbytes;
+  if (nbytes >= 32 * 1024) {
+    bs = 32 * 1024 * 2;
+    switch (clevel) {
+      case 0: bs /= 4; break;
+      case 1: bs /= 2; break;
+      case 2: break;
+      case 3: bs *= 2; break;
+      case 4: case 5: bs *= 4; break;
+      case 6: case 7: case 8: bs *= 8; break;
+      default: bs *= 16; break;
+    }
+  }
+  if (clevel > 0 && ts <= 16 && bs / ts >= 128) {
+    if (bs > (1u << 18)) bs = 1u << 18;
+    bs *= ts;
+    if (bs < (1u << 16)) bs = 1u << 16;
+    if (bs > 1024u * 1024u) bs = 1024u * 1024u;
+  }
+  if (bs > nbytes) bs = nbytes;
+  if (bs > ts) bs = bs / ts * ts;
+  return bs;
+}
+
+__global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
+                                int64_t nchunks, uint8_t* scratch, EncItem* __restrict__ slots,
+                                uint32_t* __restrict__ counts, EncGeom* __restrict__ geom,
+                                int32_t* __restrict__ status, int clevel, int shuffle, int typesize) {
+  const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const hsds_chunk_desc c = chunks[ci];
+  uint32_t ts = typesize < 1 || typesize > 255 ? 1u : (uint32_t)typesize;
+  const uint64_t nbytes = c.src_len;
+  int st = HSDS_OK;
+  uint32_t cnt = 0;
+  EncGeom g = {nbytes, 0, 0, (3u << 5) | (shuffle ? 1u : 0u), ts, 0};
+  if (c.dst_len < nbytes + 16 || nbytes >= (1ull << 31) - 16) {
+    st = HSDS_ERR_ARG;
+  } else {
+    const uint64_t bs = enc_blocksize(clevel, ts, nbytes);
+    g.bs = bs;
+    if (!(ts <= 16 && bs / ts >= 128)) g.flags |= 0x10;
+    g.memcpyed = (nbytes < 128 || clevel <= 0) ? 1u : 0u;
+    const uint64_t nblocks = bs ? (nbytes + bs - 1) / bs : 0;
+    const uint64_t leftover = bs ? nbytes % bs : 0;
+    g.nblocks = (uint32_t)nblocks;
+    if (!g.memcpyed) {
+      const uint8_t* csrc = src_base + c.src_off;
+      uint8_t* cscr = scratch + c.dst_off + (uint64_t)ci * ENC_CHUNK_SLACK;
+      const int doshuffle = (g.flags & 0x01) && ts > 1;
+      for (uint64_t b = 0; b < nblocks && st == HSDS_OK; b++) {
+        const int isleft = (b == nblocks - 1) && leftover;
+        const uint64_t bsz = isleft ? leftover : bs;
+        const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? ts : 1u;
+        const uint64_t neblock = bsz / nspl;
+        for (uint32_t j = 0; j < nspl; j++) {
+          if (cnt >= (uint32_t)KSLOTS) { st = HSDS_ERR_UNSUPPORTED; break; }
+          const uint64_t raw = b * bs + j * neblock;
+          EncItem it;
+          it.src = (uint64_t)(csrc + b * bs + (doshuffle ? 0 : j * neblock));
+          it.dst = (uint64_t)(cscr + ((raw + 3) & ~3ull) + 16ull * cnt);
+          it.len = (uint32_t)neblock;
+          it.cap = neblock ? (uint32_t)neblock - 1u : 0u;
+          it.off = doshuffle ? (uint32_t)(j * neblock) : 0u;
+          it.ts = doshuffle ? ts : 1u;
+          it.neb = doshuffle ? (uint32_t)(bsz / ts) : 0u;
+          it.chunk = (uint32_t)ci;
+          slots[ci * KSLOTS + cnt++] = it;
+        }
+      }
+    }
+  }
+  if (st != HSDS_OK) cnt = 0;
+  counts[ci] = cnt;
+  status[ci] = st;
+  geom[ci] = g;
+}
+
+__global__ void __launch_bounds__(64) deflate_kernel(const EncItem* __restrict__ slots,
+                                                     const uint32_t* __restrict__ offs, int64_t nchunks,
+                                                     uint32_t* __restrict__ counter, int64_t* __restrict__ isize,
+                                                     int level) {
+  __shared__ hd::Shared sh;
+  const uint32_t total = offs[nchunks];
+  const int lane = threadIdx.x;
+  const hd::Tune tune = hd::tune_for_level(level);
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(counter, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= total) break;
+    int64_t lo = 0, hi = nchunks - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t k = item - offs[lo];
+    const EncItem it = slots[lo * KSLOTS + k];
+    hd::EncJob job = {(const uint8_t*)it.src, it.len, (uint32_t*)it.dst, it.cap, level, it.ts, it.neb, it.off};
+    const int64_t r = hd::deflate_stream(sh, job, tune);
+    if (lane == 0) isize[lo * KSLOTS + k] = r;
+    __syncthreads();
+  }
+}
+
+// bounded unaligned 32-bit load: bytes [p, p+4) of a buffer whose valid bytes are [b, e)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p, const uint8_t* b, const uint8_t* e) {
+  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
+  const uint32_t s = (uint32_t)((uintptr_t)p & 3u) * 8u;
+  const uint8_t* ab = (const uint8_t*)((uintptr_t)b & ~(uintptr_t)3);
+  const uint32_t lo = (uint32_t)((uintptr_t)b - (uintptr_t)ab), hi = (uint32_t)((uintptr_t)e - (uintptr_t)ab);
+  hz_gcu8* g = HZ_GLOBAL(hz_gcu8*, ab);
+  const uint32_t k = (uint32_t)((a - (uintptr_t)ab) >> 2);
+  const uint32_t w0 = hz::load_word(g, k, lo, hi);
+  if (!s) return w0;
+  const uint32_t w1 = hz::load_word(g, k + 1u, lo, hi);
+  return (w0 >> s) | (w1 << (32u - s));
+}
+
+// workgroup copy of n bytes, any alignment of either side; ts > 1 gathers the bytes
+// [off, off + n) of the byte-shuffled block at src (c-blosc raw split of a shuffled block)
+__device__ void wg_copy(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t ts, uint32_t neb, uint32_t off) {
+  if (ts > 1) {
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x)
+      dst[i] = src[hd::shuffled_src_index(off + (uint32_t)i, ts, neb)];
+    return;
+  }
+  uint64_t head = (4u - ((uintptr_t)dst & 3u)) & 3u;
+  if (head > n) head = n;
+  if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
+  const uint64_t nw = (n - head) >> 2;
+  uint32_t* d4 = (uint32_t*)(dst + head);
+  const uint8_t* s = src + head;
+  const uint8_t* e = src + n;
+  if (((uintptr_t)s & 3u) == 0) {
+    const uint32_t* s4 = (const uint32_t*)s;
+    for (uint64_t w = threadIdx.x; w < nw; w += blockDim.x) d4[w] = s4[w];
+  } else {
+    for (uint64_t w = threadIdx.x; w < nw; w += blockDim.x) d4[w] = ld32u(s + 4 * w, src, e);
+  }
+  const uint64_t t0 = head + 4 * nw;
+  if (t0 + threadIdx.x < n) dst[t0 + threadIdx.x] = src[t0 + threadIdx.x];
+}
+
+// one workgroup per chunk: c-blosc serial_blosc / blosc_c frame layout with the raw
+// split (csize == neblock) and memcpyed fallbacks (oracle.c orc_blosc_encode_zlib)
+__global__ void __launch_bounds__(256) frame_kernel(const uint8_t* __restrict__ src_base,
+                                                    const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
+                                                    uint8_t* dst_base, const EncItem* __restrict__ slots,
+                                                    const uint32_t* __restrict__ counts,
+                                                    const EncGeom* __restrict__ geom,
+                                                    const int64_t* __restrict__ isize,
+                                                    int64_t* __restrict__ sizes, int32_t* __restrict__ status) {
+  __shared__ uint32_t pos[KSLOTS];     // payload offset of split k in the frame
+  __shared__ uint32_t csz[KSLOTS];     // payload bytes
+  __shared__ uint32_t raw[KSLOTS];
+  __shared__ uint32_t s_memcpyed, s_ntbytes;
+  const int64_t ci = blockIdx.x;
+  if (ci >= nchunks) return;
+  if (status[ci] != HSDS_OK) {
+    if (threadIdx.x == 0) sizes[ci] = status[ci];
+    return;
+  }
+  const hsds_chunk_desc c = chunks[ci];
+  const EncGeom g = geom[ci];
+  const uint32_t cnt = counts[ci];
+  const EncItem* it = slots + ci * KSLOTS;
+  const int64_t* isz = isize + ci * KSLOTS;
+  uint8_t* out = dst_base + c.dst_off;
+  const uint8_t* csrc = src_base + c.src_off;
+  if (threadIdx.x == 0) {
+    const uint64_t maxbytes = g.nbytes + 16;
+    uint32_t memcpyed = g.memcpyed;
+    uint64_t nt = 16 + 4ull * g.nblocks;
+    if (!memcpyed && nt > maxbytes) memcpyed = 1;
+    uint32_t k = 0;
+    const uint64_t leftover = g.bs ? g.nbytes % g.bs : 0;
+    for (uint32_t b = 0; b < g.nblocks && !memcpyed; b++) {
+      const int isleft = (b == g.nblocks - 1) && leftover;
+      const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? g.ts : 1u;
+      const uint32_t first = k;
+      (void)first;
+      for (uint32_t j = 0; j < nspl && !memcpyed; j++, k++) {
+        const uint64_t neblock = it[k].len;
+        nt += 4;
+        int64_t maxout = (int64_t)neblock;
+        if (nt + neblock > maxbytes) {
+          maxout = (int64_t)maxbytes - (int64_t)nt;
+          if (maxout <= 0) { memcpyed = 1; break; }
+        }
+        int64_t cb = isz[k];
+        if (cb < 0 || cb > maxout) cb = 0;          // compress2 would not fit
+        uint32_t israw = 0;
+        if (cb == 0 || (uint64_t)cb == neblock) {
+          if (nt + neblock > maxbytes) { memcpyed = 1; break; }
+          cb = (int64_t)neblock;
+          israw = 1;
+        }
+        pos[k] = (uint32_t)nt;
+        csz[k] = (uint32_t)cb;
+        raw[k] = israw;
+        nt += (uint64_t)cb;
+      }
+    }
+    if (memcpyed) nt = g.nbytes + 16;
+    s_memcpyed = memcpyed;
+    s_ntbytes = (uint32_t)nt;
+    // header (blosc.c write header: version 2, versionlz 1, flags, typesize, sizes)
+    const uint32_t flags = g.flags | (memcpyed ? 0x02u : 0u);
+    uint8_t hdr[16] = {2, 1, (uint8_t)flags, (uint8_t)g.ts};
+    for (int i = 0; i < 4; i++) {
+      hdr[4 + i] = (uint8_t)(g.nbytes >> (8 * i));
+      hdr[8 + i] = (uint8_t)(g.bs >> (8 * i));
+      hdr[12 + i] = (uint8_t)(nt >> (8 * i));
+    }
+    for (int i = 0; i < 16; i++) out[i] = hdr[i];
+    if (!memcpyed) {
+      // bstarts: offset of each block's first split length prefix
+      uint32_t kk = 0;
+      for (uint32_t b = 0; b < g.nblocks; b++) {
+        const int isleft = (b == g.nblocks - 1) && leftover;
+        const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? g.ts : 1u;
+        const uint32_t bstart = pos[kk] - 4u;
+        for (int i = 0; i < 4; i++) out[16 + 4 * b + i] = (uint8_t)(bstart >> (8 * i));
+        for (uint32_t j = 0; j < nspl; j++, kk++)
+          for (int i = 0; i < 4; i++) out[pos[kk] - 4 + i] = (uint8_t)(csz[kk] >> (8 * i));
+      }
+    }
+  }
+  __syncthreads();
+  if (s_memcpyed) {
+    wg_copy(out + 16, csrc, g.nbytes, 1, 0, 0);
+  } else {
+    for (uint32_t k = 0; k < cnt; k++) {
+      if (raw[k]) wg_copy(out + pos[k], (const uint8_t*)it[k].src, csz[k], it[k].ts, it[k].neb, it[k].off);
+      else wg_copy(out + pos[k], (const uint8_t*)it[k].dst, csz[k], 1, 0, 0);
+    }
+  }
+  if (threadIdx.x == 0) sizes[ci] = s_ntbytes;
+}
+
 }  // namespace
 
 // =========================================================================
@@ -386,6 +663,14 @@ struct hsds_engine {
   size_t h_dev_dst_bytes = 0;
   hipEvent_t ev0, ev1;
   int ev_valid = 0;
+  // encode workspace (items, sizes, geometry) and per-split output scratch
+  int deflate_blocks_per_cu = 1;
+  uint8_t* ews = nullptr;
+  size_t ews_bytes = 0;
+  uint8_t* escr = nullptr;
+  size_t escr_bytes = 0;
+  hipEvent_t ev2, ev3;
+  int ev_enc_valid = 0;
 };
 
 static int grow(void** p, size_t* have, size_t need) {
@@ -434,12 +719,16 @@ int hsds_engine_create(int device, hsds_engine** out) {
     if (v >= 1 && v < occ) occ = v;
   }
   e->inflate_blocks_per_cu = occ;
+  int docc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc, deflate_kernel, 64, 0) != hipSuccess || docc < 1) docc = 2;
+  e->deflate_blocks_per_cu = docc;
   e->tune.L0 = 384;
   e->tune.W = 96;
   e->tune.adapt = 1;
   e->tune.C = 192;
   e->tune.max_rounds = 4;
-  if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
+  if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
+      hipEventCreate(&e->ev2) != hipSuccess || hipEventCreate(&e->ev3) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
   *out = e;
   return HSDS_OK;
 }
@@ -451,8 +740,12 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (e->tmp) hipFree(e->tmp);
   if (e->h_dev_src) hipFree(e->h_dev_src);
   if (e->h_dev_dst) hipFree(e->h_dev_dst);
+  if (e->ews) hipFree(e->ews);
+  if (e->escr) hipFree(e->escr);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
+  hipEventDestroy(e->ev2);
+  hipEventDestroy(e->ev3);
   delete e;
 }
 
@@ -651,6 +944,85 @@ int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const h
   hipLaunchKernelGGL(compare_kernel, dim3(8, gy), dim3(256), 0, st, (const uint8_t*)d_b, (const uint8_t*)d_a,
                      d_desc, n, kind, d_differs);
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+// ---- encode -----------------------------------------------------------------
+int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                      void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
+                      int shuffle, int typesize, void* stream) {
+  if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
+  if (clevel < 0 || clevel > 9 || (shuffle != HSDS_SHUFFLE_NONE && shuffle != HSDS_SHUFFLE_BYTE)) return HSDS_ERR_ARG;
+  if (nchunks == 0) return HSDS_OK;
+  if (nchunks > (int64_t)(1u << 22)) return HSDS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  const size_t sz_slots = (size_t)nchunks * KSLOTS * sizeof(EncItem);
+  const size_t sz_isz = (size_t)nchunks * KSLOTS * sizeof(int64_t);
+  const size_t sz_counts = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
+  const size_t sz_offs = ((size_t)(nchunks + 1) * 4 + 255) & ~(size_t)255;
+  const size_t sz_geom = ((size_t)nchunks * sizeof(EncGeom) + 255) & ~(size_t)255;
+  const size_t need = sz_slots + sz_isz + sz_counts + sz_offs + sz_geom + 256;
+  if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
+  uint8_t* w = e->ews;
+  EncItem* slots = (EncItem*)w; w += sz_slots;
+  int64_t* isz = (int64_t*)w; w += sz_isz;
+  uint32_t* counts = (uint32_t*)w; w += sz_counts;
+  uint32_t* offs = (uint32_t*)w; w += sz_offs;
+  EncGeom* geom = (EncGeom*)w; w += sz_geom;
+  uint32_t* ctr = (uint32_t*)w;
+  // per-split output scratch: the destination layout plus ENC_CHUNK_SLACK per chunk
+  if (grow((void**)&e->escr, &e->escr_bytes, dst_extent + (size_t)nchunks * ENC_CHUNK_SLACK + 256))
+    return HSDS_ERR_DEVICE;
+  if (hipMemsetAsync(ctr, 0, 16, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  const int tpb = 256;
+  const int nb = (int)((nchunks + tpb - 1) / tpb);
+  hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, e->escr,
+                     slots, counts, geom, d_status, clevel, shuffle, typesize);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
+  int64_t grid = (int64_t)e->num_cus * e->deflate_blocks_per_cu;
+  if (grid > nchunks * 4) grid = nchunks * 4;
+  if (grid < 1) grid = 1;
+  hipEventRecord(e->ev2, st);
+  hipLaunchKernelGGL(deflate_kernel, dim3((unsigned)grid), dim3(64), 0, st, slots, offs, nchunks, ctr, isz, clevel);
+  hipEventRecord(e->ev3, st);
+  e->ev_enc_valid = 1;
+  hipLaunchKernelGGL(frame_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
+                     nchunks, (uint8_t*)d_dst, slots, counts, geom, isz, d_sizes, d_status);
+  return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+int hsds_last_deflate_ms(hsds_engine* e, float* ms) {
+  if (!e || !ms || !e->ev_enc_valid) return HSDS_ERR_ARG;
+  if (hipEventElapsedTime(ms, e->ev2, e->ev3) != hipSuccess) return HSDS_ERR_DEVICE;
+  return HSDS_OK;
+}
+
+int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize, void* dst,
+                      int64_t cap) {
+  if (!e || n < 0 || (n && !src) || !dst || cap < n + 16) return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  const size_t desc_off = ((size_t)n + 255) & ~(size_t)255;
+  const size_t frame_cap = (size_t)n + 16;
+  const size_t stat_off = (frame_cap + 255) & ~(size_t)255;
+  if (grow((void**)&e->h_dev_src, &e->h_dev_src_bytes, desc_off + sizeof(hsds_chunk_desc))) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->h_dev_dst, &e->h_dev_dst_bytes, stat_off + 64)) return HSDS_ERR_DEVICE;
+  hsds_chunk_desc c = {0, (uint64_t)n, 0, (uint64_t)frame_cap};
+  hsds_chunk_desc* dd = (hsds_chunk_desc*)(e->h_dev_src + desc_off);
+  int64_t* dsize = (int64_t*)(e->h_dev_dst + stat_off);
+  int32_t* dstat = (int32_t*)(e->h_dev_dst + stat_off + 16);
+  if (n && hipMemcpy(e->h_dev_src, src, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (hipMemcpy(dd, &c, sizeof(c), hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
+  int r = hsds_encode_batch(e, e->h_dev_src, dd, 1, e->h_dev_dst, frame_cap, dsize, dstat, clevel, shuffle, typesize,
+                            nullptr);
+  if (r) return r;
+  int32_t status = 0;
+  int64_t size = 0;
+  if (hipMemcpy(&status, dstat, 4, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (status) return status;
+  if (hipMemcpy(&size, dsize, 8, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (size < 16 || size > cap) return HSDS_ERR_SIZE;
+  if (hipMemcpy(dst, e->h_dev_dst, (size_t)size, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  return size;
 }
 
 }  // extern "C"

@@ -72,6 +72,27 @@ class ChunkEngine:
     def last_inflate_ms(self):
         return self.eng.last_inflate_ms()
 
+    def encode(self, src, chunk_descs, dst, sizes, status, clevel=5, shuffle=1, typesize=1, stream=None):
+        """Asynchronously encode the chunks `chunk_descs` (src_off/src_len in `src`)
+        into HSDS F1 objects -- Blosc1 frames with the zlib codec, exactly what
+        storUtil._compress stores (storUtil.py:238-281) -- at dst_off in `dst`
+        (dst_len = capacity >= src_len + 16).  Frame sizes land in `sizes` (int64
+        device tensor), HSDS_* status codes in `status` (int32)."""
+        if isinstance(chunk_descs, np.ndarray):
+            n = chunk_descs.size
+            chunk_descs = to_device_bytes(chunk_descs, self.device)
+        else:
+            n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
+        rc = nat.lib().hsds_encode_batch(self.eng.h, _ptr(src), _ptr(chunk_descs), n, _ptr(dst),
+                                         dst.numel() * dst.element_size(), _ptr(sizes), _ptr(status),
+                                         int(clevel), int(shuffle), int(typesize), _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_encode_batch")
+        return chunk_descs
+
+    def last_deflate_ms(self):
+        return self.eng.last_deflate_ms()
+
     def copy(self, src, dst, copy_descs, stream=None, flags=None):
         """Asynchronous strided region copies (COPY_DESC_DTYPE records)."""
         if isinstance(copy_descs, np.ndarray):
@@ -112,6 +133,23 @@ class ChunkEngine:
                                            _stream_handle(stream))
         if rc != nat.OK:
             raise nat.NativeError(rc, "hsds_shuffle_device")
+
+
+def encode_descs(src_lens, align=256, overhead=16):
+    """Descriptors for an encode batch of chunks stored back to back (src) with one
+    frame slot of src_len + 16 bytes (c-blosc MAX_OVERHEAD) each in dst.
+    Returns (descs CHUNK_DESC_DTYPE ndarray, src_extent, dst_extent)."""
+    n = len(src_lens)
+    descs = np.zeros(n, CHUNK_DESC_DTYPE)
+    so = do = 0
+    for i, L in enumerate(src_lens):
+        descs[i]["src_off"] = so
+        descs[i]["src_len"] = L
+        descs[i]["dst_off"] = do
+        descs[i]["dst_len"] = L + overhead
+        so += (L + align - 1) // align * align
+        do += (L + overhead + align - 1) // align * align
+    return descs, so, do
 
 
 def pack_chunks(blobs, dst_lens, align=256):

@@ -15,6 +15,9 @@
  *                           chunk_crawl.py:135 arr[data_sel] (SN write gather)
  *   hsds_compare_batch + hsds_copy_batch_if
  *                        <- chunkUtil.py:932 chunkWriteSelection (ndarray_compare, then chunk_arr[slices] = data)
+ *   hsds_compress        <- storUtil.py:238  _compress(data, compressor, level, shuffle, dtype, chunk_shape)
+ *   hsds_encode_batch    <- the per-chunk _compress of putStorBytes (storUtil.py:584-600) reached from
+ *                           write_s3_obj (hsds/datanode_lib.py:126-311), batched over many dirty chunks
  *
  * Threading: an engine is bound to one device and may be used from one host thread
  * at a time (HSDS data nodes are single-threaded asyncio processes).  All *_batch
@@ -140,6 +143,28 @@ int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const h
 /* copy only the descriptors whose d_flags[k] != 0 */
 int hsds_copy_batch_if(hsds_engine* e, const void* d_src, void* d_dst, const hsds_copy_desc* d_desc,
                        int64_t n, const int32_t* d_flags, void* stream);
+
+/* ---- encode (write path) ---------------------------------------------------- */
+/* Batched, device-resident encode into HSDS F1 objects: chunk k (d_chunks[k].src_off /
+ * src_len in d_src) becomes a Blosc1 frame with the zlib codec at level `clevel`
+ * (0-9), the byte-shuffle flag `shuffle` (0 / 1) and `typesize` (the reference's
+ * _compress always uses typesize 1) at d_dst + dst_off; dst_len is the frame
+ * capacity and must be >= src_len + 16 (c-blosc MAX_OVERHEAD).  Frame geometry,
+ * raw splits and the memcpyed fallback follow c-blosc 1.21 blosc_compress; the
+ * deflate streams are produced by the GPU encoder (any valid deflate: they inflate
+ * through libz, c-blosc and storUtil._uncompress).  The frame size goes to
+ * d_sizes[k] (int64), the status to d_status[k].  dst_extent = bytes spanned by d_dst. */
+int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                      void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
+                      int shuffle, int typesize, void* stream);
+
+/* Host-buffer single object: mirrors storUtil._compress for the zlib compressor.
+ * Returns the frame size (<= cap; cap must be >= n + 16) or a negative HSDS_ERR_*. */
+int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize,
+                      void* dst, int64_t cap);
+
+/* Device time (ms) of the deflate kernel of the most recent hsds_encode_batch. */
+int hsds_last_deflate_ms(hsds_engine* e, float* ms);
 
 #ifdef __cplusplus
 }
