@@ -239,6 +239,109 @@ def run_cfg3(args, dev):
     return out
 
 
+CFG5_CHUNK = (512, 512)
+
+
+def run_cfg5(args, dev, rank=0):
+    """configs[4] write path, one GPU's share (32k chunks / 8 GPUs = 4096): a
+    float32 slab of 16 x 256 chunks of 512x512 (4 GiB, smooth rows generated on the
+    device) is scattered into 1 MiB chunk arrays (chunk_crawl.py:118-140 write
+    gather + chunkWriteSelection's copy) and every chunk is encoded into an HSDS F1
+    object (storUtil._compress: Blosc1 frame, zlib L4, shuffle flag, typesize 1).
+    One step = scatter + encode.  Algorithmic bytes:
+    slab bytes in + compressed bytes out."""
+    import torch
+    from hsds_amd.engine import ChunkEngine, COPY_DESC_DTYPE, encode_descs, to_device_bytes
+    from oracle import oracle as orc
+    R, C = 16, args.chunks // 16
+    cr, cc = CFG5_CHUNK
+    rows, cols = R * cr, C * cc
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261015 + rank)
+    slab = torch.empty((rows, cols), dtype=torch.float32, device=dev)
+    for r0 in range(0, rows, 512):   # round(cumsum(N(0,1)), 2) along rows, float64 then float32
+        z = torch.randn((512, cols), generator=g, device=dev, dtype=torch.float64)
+        slab[r0:r0 + 512] = torch.round(torch.cumsum(z, dim=1), decimals=2).to(torch.float32)
+        del z
+    n = R * C
+    cbytes = cr * cc * 4
+    cd = np.zeros(n, COPY_DESC_DTYPE)
+    for k in range(n):
+        i, j = divmod(k, C)
+        cd[k]["src_off"] = (i * cr * cols + j * cc) * 4
+        cd[k]["dst_off"] = k * cbytes
+        cd[k]["src_stride"][:2] = (cols * 4, 4)
+        cd[k]["dst_stride"][:2] = (cc * 4, 4)
+        cd[k]["count"][:2] = (cr, cc)
+        cd[k]["rank"] = 2
+        cd[k]["itemsize"] = 4
+    d_cd = to_device_bytes(cd, dev)
+    descs, _, dext = encode_descs([cbytes] * n)
+    # chunk arrays back to back (src of the encode), frames in 1 MiB + 16 slots
+    chunks = torch.empty(n * cbytes, dtype=torch.uint8, device=dev)
+    frames = torch.empty(dext, dtype=torch.uint8, device=dev)
+    sizes = torch.zeros(n, dtype=torch.int64, device=dev)
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_desc = to_device_bytes(descs, dev)
+    eng = ChunkEngine(dev.index)
+    slab_u8 = slab.view(torch.uint8).reshape(-1)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        eng.copy(slab_u8, chunks, d_cd, stream=stream)
+        eng.encode(chunks, d_desc, frames, sizes, st, clevel=4, shuffle=1, typesize=1, stream=stream)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0, "encode status errors"
+    hs = sizes.cpu().numpy()
+    host_slab = None
+    for k in (0, n // 2, n - 1):    # sampled frames decode (oracle) to the slab's chunk
+        i, j = divmod(k, C)
+        o = int(descs[k]["dst_off"])
+        fr = frames[o:o + int(hs[k])].cpu().numpy().tobytes()
+        want = slab[i * cr:(i + 1) * cr, j * cc:(j + 1) * cc].contiguous().cpu().numpy().tobytes()
+        assert orc.uncompress(fr, "zlib", 1, 1, cbytes) == want, f"cfg5 chunk {k}"
+    del host_slab
+    kern = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.steps
+    step()
+    torch.cuda.synchronize()
+    kern.append(eng.last_deflate_ms())
+    comp = int(sizes.sum())
+    slab_bytes = n * cbytes
+    # libz reference size on a sample of the same chunks (oracle = reference _compress bytes)
+    samp = [chunks[k * cbytes:(k + 1) * cbytes].cpu().numpy() for k in range(0, n, max(1, n // 16))]
+    ref = sum(len(orc.blosc_encode(x, typesize=1, clevel=4, shuffle=1)) for x in samp)
+    ours = sum(int(hs[k]) for k in range(0, n, max(1, n // 16)))
+    out = {"value": round(slab_bytes / el / 1e9, 2), "unit": "GB/s slab (scatter + encode)",
+           "ms_per_step": round(el * 1e3, 3), "chunks": n, "slab_bytes": slab_bytes, "compressed_bytes": comp,
+           "algorithmic_GBps": round((slab_bytes + comp) / el / 1e9, 2),
+           "deflate_kernel_ms": round(kern[-1], 3),
+           "deflate_kernel_GBps": round((slab_bytes + comp) / (kern[-1] / 1e3) / 1e9, 2),
+           "size_vs_libz": round(ours / ref, 4),
+           "workload": "configs[4] per-GPU share: f32 slab 8192x131072 -> 4096 chunks 512x512 -> F1 zlib L4 frames"}
+    if args.cpu_seconds > 0 and rank == 0:
+        threads = min(16, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t1 < args.cpu_seconds / 2:
+            orc.encode_batch(samp, op="blosc", typesize=1, clevel=4, shuffle=1, nthreads=threads)
+            done += len(samp)
+        cel = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": round(done * cbytes / cel / 1e9, 3), "unit": "GB/s", "cores": threads,
+                               "kind": "port", "sample": f"{done} x 1 MiB F1 encodes (oracle c-blosc + libz L4)"}
+    del slab, chunks, frames
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(args, world):
     """HBM bytes per inflate launch from the committed PMC passes (tools/pmc_traffic.sh):
     2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
@@ -279,6 +382,7 @@ def main():
     ap.add_argument("--kernel-timing", type=int, default=0)
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
+    ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -333,6 +437,8 @@ def main():
         out["e2e_pcie"] = run_e2e(r1, args, dev)
     if world == 1 and args.cfg3:
         out["cfg3"] = run_cfg3(args, dev)
+    if world == 1 and args.cfg5:
+        out["cfg5"] = run_cfg5(args, dev, rank)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = min(16, os.cpu_count() or 1)
         sample = r1["blobs"][:256]

@@ -462,7 +462,8 @@ HZ_HD uint32_t dyn_header_bits(Shared& sh) {
 // one zlib stream.  Returns compressed bytes, or R_OVERFLOW when the output would
 // exceed job.cap (the caller then stores the input raw, as c-blosc does).
 // ---------------------------------------------------------------------------
-HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
+HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune, HzProf* prof = nullptr) {
+  (void)prof;
   const uint32_t n = job.len;
   hz_gcu8* const gsrc = HZ_GLOBAL(hz_gcu8*, (uintptr_t)job.src & ~(uintptr_t)3);
   const uint32_t sa = (uint32_t)((uintptr_t)job.src & 3u);
@@ -489,6 +490,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
     const bool last = seg + 1 == nseg;
 
     // ---- 1. stage the segment (+ lookahead) into the ring, adler sums ----
+    HZ_T(1);
     LANE_LOOP {
       const uint32_t nw = (stage_hi - s0 + 3u) / 4u;
       for (uint32_t k = (uint32_t)lane; k < nw; k += WAVE) {
@@ -526,6 +528,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
     const uint32_t lo_pos = s0 > WIN ? s0 - WIN : 0u;   // farthest match source
     if (!tune.stored) {
       // ---- 2. exact hash chains, 64 positions per step ----
+      HZ_T(2);
       for (uint32_t g = s0; g < s1; g += WAVE) {
         LANE_VAR(uint32_t, key);
         LANE_VAR(uint32_t, kp);
@@ -558,6 +561,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
     }
 
     // ---- 3. lane-parallel greedy parse ----
+    HZ_T(3);
     LANE_VAR(uint32_t, nslot);
     LANE_LOOP {
       const uint32_t R = (seglen + WAVE - 1) / WAVE;
@@ -608,17 +612,20 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
     WAVE_SYNC();
 
     // ---- 4. block type and codes ----
+    HZ_T(4);
     LANE_LOOP { if (lane == 0) sh.freq[256] = 1; }
     WAVE_SYNC();
     uint64_t dyn_bits = ~0ull, fix_bits = ~0ull;
     if (!tune.stored) {
       HD_BUILD_HUFF(sh, sh.freq, NLL, 512, 15, sh.len_ll, sh.code_ll);
       HD_BUILD_HUFF(sh, (sh.freq + NLL), ND, 32, 15, sh.len_d, sh.code_d);
+      HZ_T(5);
       LANE_LOOP { if (lane == 0) build_rle(sh); }
       WAVE_SYNC();
       HD_BUILD_HUFF(sh, sh.clf, NCL, 32, 7, sh.len_cl, sh.code_cl);
       LANE_LOOP { if (lane == 0) sh.hdr_bits = dyn_header_bits(sh); }
       WAVE_SYNC();
+      HZ_T(10);
       // data bits under the dynamic and the fixed code
       LANE_VAR(uint64_t, db);
       LANE_VAR(uint64_t, fb);
@@ -658,6 +665,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
     else btype = 0;
 
     // ---- 5. emission into the staging words ----
+    HZ_T(6);
     LANE_LOOP {
       for (int w = lane; w < STAGE_WORDS; w += WAVE) sh.stage[w] = w == 0 ? carry : 0u;
       if (lane == 0 && btype == 1) set_fixed_codes(sh);
@@ -724,6 +732,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
         LV(nb) = bits;
       }
       WAVE_SYNC();
+      HZ_T(7);
       LANE_VAR(uint32_t, off);
 #if HZ_GPU
       off = hz::wave_excl_scan(nb, (int)threadIdx.x);
@@ -759,6 +768,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
     WAVE_SYNC();
 
     // ---- 6. flush full words, carry the partial one ----
+    HZ_T(8);
     const uint32_t full = total_bits >> 5;
     if ((out_words + full) * 4ull > (uint64_t)job.cap + 4u) {   // dst holds cap + 8 bytes
       overflow = true;
@@ -775,6 +785,7 @@ HZ_HD int64_t deflate_stream(Shared& sh, const EncJob& job, const Tune& tune) {
   if (overflow) return R_OVERFLOW;
 
   // ---- trailer: byte align, adler32 big-endian ----
+  HZ_T(9);
   uint64_t S1, S2;
 #if HZ_GPU
   S1 = HD_WAVE_SUM64(as1);

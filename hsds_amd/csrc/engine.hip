@@ -486,6 +486,15 @@ __global__ void __launch_bounds__(64) deflate_kernel(const EncItem* __restrict__
   const uint32_t total = offs[nchunks];
   const int lane = threadIdx.x;
   const hd::Tune tune = hd::tune_for_level(level);
+#ifdef HZ_PROFILE
+  HzProf prof_;
+  for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
+  prof_.last = __builtin_amdgcn_s_memtime();
+  prof_.cur = 0;
+  HzProf* prof = &prof_;
+#else
+  HzProf* prof = nullptr;
+#endif
   for (;;) {
     uint32_t item = 0;
     if (lane == 0) item = atomicAdd(counter, 1u);
@@ -499,10 +508,18 @@ __global__ void __launch_bounds__(64) deflate_kernel(const EncItem* __restrict__
     const uint32_t k = item - offs[lo];
     const EncItem it = slots[lo * KSLOTS + k];
     hd::EncJob job = {(const uint8_t*)it.src, it.len, (uint32_t*)it.dst, it.cap, level, it.ts, it.neb, it.off};
-    const int64_t r = hd::deflate_stream(sh, job, tune);
+    const int64_t r = hd::deflate_stream(sh, job, tune, prof);
     if (lane == 0) isize[lo * KSLOTS + k] = r;
     __syncthreads();
   }
+#ifdef HZ_PROFILE
+  {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    prof_.acc[prof_.cur] += now - prof_.last;
+    if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&hz_prof[i], (unsigned long long)prof_.acc[i]);
+  }
+#endif
+  (void)prof;
 }
 
 // bounded unaligned 32-bit load: bytes [p, p+4) of a buffer whose valid bytes are [b, e)
