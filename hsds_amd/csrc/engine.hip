@@ -375,26 +375,34 @@ __global__ void zero_i32_kernel(int32_t* p, int64_t n) {
 // =========================================================================
 // encode (storUtil._compress -> c-blosc 1.21 blosc_compress_ctx, zlib codec)
 // =========================================================================
-constexpr uint64_t ENC_CHUNK_SLACK = 4352;   // per-chunk scratch slack: 16 B per item + alignment
-
-struct EncItem {       // 40 bytes
+struct EncItem {       // 40 bytes: one zlib stream (Blosc split)
   uint64_t src;        // block base (stream input when ts == 1)
-  uint64_t dst;        // scratch output, 4-byte aligned, cap + 8 bytes
   uint32_t len;        // stream input bytes (neblock)
-  uint32_t cap;        // neblock - 1: an output of neblock bytes or more is stored raw
   uint32_t off;        // stream offset inside the (shuffled) block
   uint32_t ts;         // > 1: gather from the byte-shuffled block
   uint32_t neb;        // elements per block plane
   uint32_t chunk;
+  uint32_t seg0;       // first segment, relative to the chunk's first segment
+  uint32_t pad[2];
 };
 
-struct EncGeom {       // per-chunk frame geometry (enc_plan_kernel -> frame_kernel)
+struct EncGeom {       // per-chunk frame geometry (plan -> layout -> raw copies)
   uint64_t nbytes;
   uint64_t bs;
   uint32_t nblocks;
   uint32_t flags;
   uint32_t ts;
   uint32_t memcpyed;
+};
+
+struct ItemOut {       // layout -> raw copies
+  uint32_t pos;        // payload offset of the split in the frame
+  uint32_t raw;        // 1: stored raw (c-blosc csize == neblock)
+};
+
+struct SegMeta {       // parse -> huffman
+  uint32_t item;       // EncItem slot
+  uint32_t seglen;
 };
 
 // c-blosc 1.21 compute_blocksize for the zlib codec (oracle.c orc_blosc_blocksize)
@@ -425,18 +433,18 @@ __device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint6
 }
 
 __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
-                                int64_t nchunks, uint8_t* scratch, EncItem* __restrict__ slots,
-                                uint32_t* __restrict__ counts, EncGeom* __restrict__ geom,
+                                int64_t nchunks, EncItem* __restrict__ slots, uint32_t* __restrict__ counts,
+                                uint32_t* __restrict__ segcnt, EncGeom* __restrict__ geom,
                                 int32_t* __restrict__ status, int clevel, int shuffle, int typesize) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
   const hsds_chunk_desc c = chunks[ci];
-  uint32_t ts = typesize < 1 || typesize > 255 ? 1u : (uint32_t)typesize;
+  const uint32_t ts = typesize < 1 || typesize > 255 ? 1u : (uint32_t)typesize;
   const uint64_t nbytes = c.src_len;
   int st = HSDS_OK;
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, nseg = 0;
   EncGeom g = {nbytes, 0, 0, (3u << 5) | (shuffle ? 1u : 0u), ts, 0};
-  if (c.dst_len < nbytes + 16 || nbytes >= (1ull << 31) - 16) {
+  if (c.dst_len < nbytes + 16 || nbytes >= (1ull << 31) - 16 || (c.dst_off & 3)) {
     st = HSDS_ERR_ARG;
   } else {
     const uint64_t bs = enc_blocksize(clevel, ts, nbytes);
@@ -448,7 +456,6 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
     g.nblocks = (uint32_t)nblocks;
     if (!g.memcpyed) {
       const uint8_t* csrc = src_base + c.src_off;
-      uint8_t* cscr = scratch + c.dst_off + (uint64_t)ci * ENC_CHUNK_SLACK;
       const int doshuffle = (g.flags & 0x01) && ts > 1;
       for (uint64_t b = 0; b < nblocks && st == HSDS_OK; b++) {
         const int isleft = (b == nblocks - 1) && leftover;
@@ -457,32 +464,46 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
         const uint64_t neblock = bsz / nspl;
         for (uint32_t j = 0; j < nspl; j++) {
           if (cnt >= (uint32_t)KSLOTS) { st = HSDS_ERR_UNSUPPORTED; break; }
-          const uint64_t raw = b * bs + j * neblock;
           EncItem it;
           it.src = (uint64_t)(csrc + b * bs + (doshuffle ? 0 : j * neblock));
-          it.dst = (uint64_t)(cscr + ((raw + 3) & ~3ull) + 16ull * cnt);
           it.len = (uint32_t)neblock;
-          it.cap = neblock ? (uint32_t)neblock - 1u : 0u;
           it.off = doshuffle ? (uint32_t)(j * neblock) : 0u;
           it.ts = doshuffle ? ts : 1u;
           it.neb = doshuffle ? (uint32_t)(bsz / ts) : 0u;
           it.chunk = (uint32_t)ci;
+          it.seg0 = nseg;
+          it.pad[0] = it.pad[1] = 0;
           slots[ci * KSLOTS + cnt++] = it;
+          nseg += hd::nsegments((uint32_t)neblock);
         }
       }
     }
   }
-  if (st != HSDS_OK) cnt = 0;
+  if (st != HSDS_OK) { cnt = 0; nseg = 0; }
   counts[ci] = cnt;
+  segcnt[ci] = nseg;
   status[ci] = st;
   geom[ci] = g;
 }
 
-__global__ void __launch_bounds__(64) deflate_kernel(const EncItem* __restrict__ slots,
-                                                     const uint32_t* __restrict__ offs, int64_t nchunks,
-                                                     uint32_t* __restrict__ counter, int64_t* __restrict__ isize,
-                                                     int level) {
-  __shared__ hd::Shared sh;
+// item index -> (chunk, slot) by binary search over the exclusive item offsets
+__device__ __forceinline__ int64_t item_chunk(const uint32_t* offs, int64_t nchunks, uint32_t item) {
+  int64_t lo = 0, hi = nchunks - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// P: persistent waves, one zlib stream each
+__global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ slots,
+                                                   const uint32_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                   uint32_t* __restrict__ counter, hd::SegParse* __restrict__ sp,
+                                                   SegMeta* __restrict__ meta, uint16_t* __restrict__ tok,
+                                                   uint32_t* __restrict__ adler, uint32_t seg_cap, int level) {
+  __shared__ hd::ParseShared sh;
   const uint32_t total = offs[nchunks];
   const int lane = threadIdx.x;
   const hd::Tune tune = hd::tune_for_level(level);
@@ -500,16 +521,19 @@ __global__ void __launch_bounds__(64) deflate_kernel(const EncItem* __restrict__
     if (lane == 0) item = atomicAdd(counter, 1u);
     item = __shfl(item, 0, 64);
     if (item >= total) break;
-    int64_t lo = 0, hi = nchunks - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi + 1) >> 1;
-      if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+    const int64_t ci = item_chunk(offs, nchunks, item);
+    const uint32_t slot = (uint32_t)(ci * KSLOTS + (item - offs[ci]));
+    const EncItem it = slots[slot];
+    const uint32_t g0 = segoffs[ci] + it.seg0;
+    const uint32_t nseg = hd::nsegments(it.len);
+    if (g0 + nseg > seg_cap) continue;          // the layout phase fails the chunk
+    hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
+    const uint32_t a = hd::parse_stream(sh, job, tune, sp + g0, tok + (size_t)g0 * hd::SEG_TOK, prof);
+    for (uint32_t s = (uint32_t)lane; s < nseg; s += 64) {
+      const uint32_t s0 = s * (uint32_t)hd::SEG;
+      meta[g0 + s] = SegMeta{slot, it.len - s0 < (uint32_t)hd::SEG ? it.len - s0 : (uint32_t)hd::SEG};
     }
-    const uint32_t k = item - offs[lo];
-    const EncItem it = slots[lo * KSLOTS + k];
-    hd::EncJob job = {(const uint8_t*)it.src, it.len, (uint32_t*)it.dst, it.cap, level, it.ts, it.neb, it.off};
-    const int64_t r = hd::deflate_stream(sh, job, tune, prof);
-    if (lane == 0) isize[lo * KSLOTS + k] = r;
+    if (lane == 0) adler[slot] = a;
     __syncthreads();
   }
 #ifdef HZ_PROFILE
@@ -520,6 +544,169 @@ __global__ void __launch_bounds__(64) deflate_kernel(const EncItem* __restrict__
   }
 #endif
   (void)prof;
+}
+
+// H: one wave per segment
+__global__ void __launch_bounds__(64) huff_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                  uint32_t* __restrict__ counter,
+                                                  const hd::SegParse* __restrict__ sp,
+                                                  const SegMeta* __restrict__ meta, hd::SegCode* __restrict__ sc,
+                                                  uint32_t seg_cap, int level) {
+  __shared__ hd::HuffShared sh;
+  uint32_t total = segoffs[nchunks];
+  if (total > seg_cap) total = seg_cap;
+  const int lane = threadIdx.x;
+  for (;;) {
+    uint32_t s = 0;
+    if (lane == 0) s = atomicAdd(counter, 1u);
+    s = __shfl(s, 0, 64);
+    if (s >= total) break;
+    hd::huff_segment(sh, sp + s, sc + s, meta[s].seglen, level <= 0);
+    __syncthreads();
+  }
+}
+
+// L: one thread per chunk: stream sizes -> c-blosc frame layout (serial_blosc /
+// blosc_c with the raw split and memcpyed fallbacks, oracle.c orc_blosc_encode_zlib)
+// -> block bit positions, frame header, bstarts, split length prefixes, zlib headers
+__global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks, uint8_t* dst_base,
+                              const EncItem* __restrict__ slots, const uint32_t* __restrict__ counts,
+                              const uint32_t* __restrict__ segoffs, EncGeom* __restrict__ geom,
+                              const hd::SegCode* __restrict__ sc, const uint32_t* __restrict__ adler,
+                              ItemOut* __restrict__ iout, hd::SegOut* __restrict__ so, int64_t* __restrict__ sizes,
+                              int32_t* __restrict__ status, uint32_t seg_cap, int level) {
+  const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const uint32_t cnt = counts[ci];
+  const uint32_t g0 = segoffs[ci], g1 = segoffs[ci + 1];
+  // every segment of the chunk gets a record (E skips the ones not emitted)
+  for (uint32_t s = g0; s < g1 && s < seg_cap; s++) so[s].flags = 0;
+  if (status[ci] != HSDS_OK) { sizes[ci] = status[ci]; return; }
+  if (g1 > seg_cap) { status[ci] = HSDS_ERR_UNSUPPORTED; sizes[ci] = HSDS_ERR_UNSUPPORTED; return; }
+  const hsds_chunk_desc c = chunks[ci];
+  EncGeom g = geom[ci];
+  const EncItem* it = slots + ci * KSLOTS;
+  ItemOut* io = iout + ci * KSLOTS;
+  uint8_t* out = dst_base + c.dst_off;
+  const uint64_t maxbytes = g.nbytes + 16;
+  uint32_t memcpyed = g.memcpyed;
+  uint64_t nt = 16 + 4ull * g.nblocks;
+  if (!memcpyed && nt > maxbytes) memcpyed = 1;
+  const uint64_t leftover = g.bs ? g.nbytes % g.bs : 0;
+  uint32_t k = 0;
+  for (uint32_t b = 0; b < g.nblocks && !memcpyed; b++) {
+    const int isleft = (b == g.nblocks - 1) && leftover;
+    const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? g.ts : 1u;
+    for (uint32_t j = 0; j < nspl && !memcpyed; j++, k++) {
+      const uint64_t neblock = it[k].len;
+      nt += 4;
+      int64_t maxout = (int64_t)neblock;
+      if (nt + neblock > maxbytes) {
+        maxout = (int64_t)maxbytes - (int64_t)nt;
+        if (maxout <= 0) { memcpyed = 1; break; }
+      }
+      int64_t cb = (int64_t)hd::stream_layout(sc + g0 + it[k].seg0, it[k].len, nullptr);
+      if (cb > maxout) cb = 0;                     // compress2 would not fit
+      uint32_t israw = 0;
+      if (cb == 0 || (uint64_t)cb >= neblock) {    // c-blosc: csize == neblock is raw
+        if (nt + neblock > maxbytes) { memcpyed = 1; break; }
+        cb = (int64_t)neblock;
+        israw = 1;
+      }
+      io[k].pos = (uint32_t)nt;
+      io[k].raw = israw;
+      nt += (uint64_t)cb;
+    }
+  }
+  if (memcpyed) nt = g.nbytes + 16;
+  g.memcpyed = memcpyed;
+  geom[ci] = g;
+  uint32_t* dw = (uint32_t*)dst_base;
+  if (!memcpyed) {
+    // block bit positions; zero the two edge words of every emitted block
+    for (uint32_t kk = 0; kk < cnt; kk++) {
+      if (io[kk].raw) continue;
+      const hd::SegCode* scs = sc + g0 + it[kk].seg0;
+      const uint32_t len = it[kk].len;
+      const uint32_t nseg = hd::nsegments(len);
+      const uint64_t base = (c.dst_off + io[kk].pos) * 8ull;
+      uint64_t bpos = 16;
+      for (uint32_t s = 0; s < nseg; s++) {
+        const uint32_t s0 = s * (uint32_t)hd::SEG;
+        const uint32_t seglen = len - s0 < (uint32_t)hd::SEG ? len - s0 : (uint32_t)hd::SEG;
+        const uint64_t start = bpos;
+        if (scs[s].btype == 0) bpos = ((bpos + 3u + 7u) & ~7ull) + 32u + 8ull * seglen;
+        else bpos += scs[s].bits;
+        const bool last = s + 1 == nseg;
+        uint64_t end = bpos;
+        if (last) end = ((bpos + 7u) & ~7ull) + 32u;
+        hd::SegOut& o = so[g0 + it[kk].seg0 + s];
+        o.bitpos = base + start;
+        o.item = (uint32_t)(ci * KSLOTS + kk);
+        o.seg = s;
+        o.flags = 1u | (last ? 2u : 0u);
+        o.adler = adler[ci * KSLOTS + kk];
+        dw[(base + start) >> 5] = 0;
+        dw[(base + end - 1) >> 5] = 0;
+      }
+    }
+  }
+  // frame header (blosc write header: version 2, versionlz 1, flags, typesize, sizes)
+  const uint32_t flags = g.flags | (memcpyed ? 0x02u : 0u);
+  uint8_t hdr[16] = {2, 1, (uint8_t)flags, (uint8_t)g.ts};
+  for (int i = 0; i < 4; i++) {
+    hdr[4 + i] = (uint8_t)(g.nbytes >> (8 * i));
+    hdr[8 + i] = (uint8_t)(g.bs >> (8 * i));
+    hdr[12 + i] = (uint8_t)(nt >> (8 * i));
+  }
+  for (int i = 0; i < 16; i++) out[i] = hdr[i];
+  if (!memcpyed) {
+    uint32_t kk = 0;
+    for (uint32_t b = 0; b < g.nblocks; b++) {
+      const int isleft = (b == g.nblocks - 1) && leftover;
+      const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? g.ts : 1u;
+      const uint32_t bstart = io[kk].pos - 4u;
+      for (int i = 0; i < 4; i++) out[16 + 4 * b + i] = (uint8_t)(bstart >> (8 * i));
+      for (uint32_t j = 0; j < nspl; j++, kk++) {
+        const uint32_t p = io[kk].pos;
+        const uint32_t cs = io[kk].raw ? it[kk].len
+                                       : (uint32_t)hd::stream_layout(sc + g0 + it[kk].seg0, it[kk].len, nullptr);
+        for (int i = 0; i < 4; i++) out[p - 4 + i] = (uint8_t)(cs >> (8 * i));
+        if (!io[kk].raw) {
+          out[p] = 0x78;
+          out[p + 1] = (uint8_t)hd::zlib_flg(level);
+        }
+      }
+    }
+  }
+  sizes[ci] = (int64_t)nt;
+}
+
+// E: one wave per segment
+__global__ void __launch_bounds__(64) emit_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                  uint32_t* __restrict__ counter,
+                                                  const hd::SegOut* __restrict__ so,
+                                                  const hd::SegCode* __restrict__ sc,
+                                                  const hd::SegParse* __restrict__ sp,
+                                                  const uint16_t* __restrict__ tok,
+                                                  const EncItem* __restrict__ slots, uint32_t* dst_words,
+                                                  uint32_t seg_cap, int level) {
+  __shared__ hd::EmitShared sh;
+  uint32_t total = segoffs[nchunks];
+  if (total > seg_cap) total = seg_cap;
+  const int lane = threadIdx.x;
+  for (;;) {
+    uint32_t s = 0;
+    if (lane == 0) s = atomicAdd(counter, 1u);
+    s = __shfl(s, 0, 64);
+    if (s >= total) break;
+    const hd::SegOut o = so[s];
+    if (!(o.flags & 1u)) continue;
+    const EncItem it = slots[o.item];
+    hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
+    hd::emit_segment(sh, o, sc + s, sp + s, tok + (size_t)s * hd::SEG_TOK, job, dst_words);
+    __syncthreads();
+  }
 }
 
 // bounded unaligned 32-bit load: bytes [p, p+4) of a buffer whose valid bytes are [b, e)
@@ -561,101 +748,28 @@ __device__ void wg_copy(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t t
   if (t0 + threadIdx.x < n) dst[t0 + threadIdx.x] = src[t0 + threadIdx.x];
 }
 
-// one workgroup per chunk: c-blosc serial_blosc / blosc_c frame layout with the raw
-// split (csize == neblock) and memcpyed fallbacks (oracle.c orc_blosc_encode_zlib)
-__global__ void __launch_bounds__(256) frame_kernel(const uint8_t* __restrict__ src_base,
-                                                    const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
-                                                    uint8_t* dst_base, const EncItem* __restrict__ slots,
-                                                    const uint32_t* __restrict__ counts,
-                                                    const EncGeom* __restrict__ geom,
-                                                    const int64_t* __restrict__ isize,
-                                                    int64_t* __restrict__ sizes, int32_t* __restrict__ status) {
-  __shared__ uint32_t pos[KSLOTS];     // payload offset of split k in the frame
-  __shared__ uint32_t csz[KSLOTS];     // payload bytes
-  __shared__ uint32_t raw[KSLOTS];
-  __shared__ uint32_t s_memcpyed, s_ntbytes;
+// R: one workgroup per chunk: raw splits and memcpyed frames
+__global__ void __launch_bounds__(256) raw_copy_kernel(const uint8_t* __restrict__ src_base,
+                                                       const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
+                                                       uint8_t* dst_base, const EncItem* __restrict__ slots,
+                                                       const uint32_t* __restrict__ counts,
+                                                       const EncGeom* __restrict__ geom,
+                                                       const ItemOut* __restrict__ iout,
+                                                       const int32_t* __restrict__ status) {
   const int64_t ci = blockIdx.x;
-  if (ci >= nchunks) return;
-  if (status[ci] != HSDS_OK) {
-    if (threadIdx.x == 0) sizes[ci] = status[ci];
-    return;
-  }
+  if (ci >= nchunks || status[ci] != HSDS_OK) return;
   const hsds_chunk_desc c = chunks[ci];
   const EncGeom g = geom[ci];
+  uint8_t* out = dst_base + c.dst_off;
+  if (g.memcpyed) {
+    wg_copy(out + 16, src_base + c.src_off, g.nbytes, 1, 0, 0);
+    return;
+  }
   const uint32_t cnt = counts[ci];
   const EncItem* it = slots + ci * KSLOTS;
-  const int64_t* isz = isize + ci * KSLOTS;
-  uint8_t* out = dst_base + c.dst_off;
-  const uint8_t* csrc = src_base + c.src_off;
-  if (threadIdx.x == 0) {
-    const uint64_t maxbytes = g.nbytes + 16;
-    uint32_t memcpyed = g.memcpyed;
-    uint64_t nt = 16 + 4ull * g.nblocks;
-    if (!memcpyed && nt > maxbytes) memcpyed = 1;
-    uint32_t k = 0;
-    const uint64_t leftover = g.bs ? g.nbytes % g.bs : 0;
-    for (uint32_t b = 0; b < g.nblocks && !memcpyed; b++) {
-      const int isleft = (b == g.nblocks - 1) && leftover;
-      const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? g.ts : 1u;
-      const uint32_t first = k;
-      (void)first;
-      for (uint32_t j = 0; j < nspl && !memcpyed; j++, k++) {
-        const uint64_t neblock = it[k].len;
-        nt += 4;
-        int64_t maxout = (int64_t)neblock;
-        if (nt + neblock > maxbytes) {
-          maxout = (int64_t)maxbytes - (int64_t)nt;
-          if (maxout <= 0) { memcpyed = 1; break; }
-        }
-        int64_t cb = isz[k];
-        if (cb < 0 || cb > maxout) cb = 0;          // compress2 would not fit
-        uint32_t israw = 0;
-        if (cb == 0 || (uint64_t)cb == neblock) {
-          if (nt + neblock > maxbytes) { memcpyed = 1; break; }
-          cb = (int64_t)neblock;
-          israw = 1;
-        }
-        pos[k] = (uint32_t)nt;
-        csz[k] = (uint32_t)cb;
-        raw[k] = israw;
-        nt += (uint64_t)cb;
-      }
-    }
-    if (memcpyed) nt = g.nbytes + 16;
-    s_memcpyed = memcpyed;
-    s_ntbytes = (uint32_t)nt;
-    // header (blosc.c write header: version 2, versionlz 1, flags, typesize, sizes)
-    const uint32_t flags = g.flags | (memcpyed ? 0x02u : 0u);
-    uint8_t hdr[16] = {2, 1, (uint8_t)flags, (uint8_t)g.ts};
-    for (int i = 0; i < 4; i++) {
-      hdr[4 + i] = (uint8_t)(g.nbytes >> (8 * i));
-      hdr[8 + i] = (uint8_t)(g.bs >> (8 * i));
-      hdr[12 + i] = (uint8_t)(nt >> (8 * i));
-    }
-    for (int i = 0; i < 16; i++) out[i] = hdr[i];
-    if (!memcpyed) {
-      // bstarts: offset of each block's first split length prefix
-      uint32_t kk = 0;
-      for (uint32_t b = 0; b < g.nblocks; b++) {
-        const int isleft = (b == g.nblocks - 1) && leftover;
-        const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? g.ts : 1u;
-        const uint32_t bstart = pos[kk] - 4u;
-        for (int i = 0; i < 4; i++) out[16 + 4 * b + i] = (uint8_t)(bstart >> (8 * i));
-        for (uint32_t j = 0; j < nspl; j++, kk++)
-          for (int i = 0; i < 4; i++) out[pos[kk] - 4 + i] = (uint8_t)(csz[kk] >> (8 * i));
-      }
-    }
-  }
-  __syncthreads();
-  if (s_memcpyed) {
-    wg_copy(out + 16, csrc, g.nbytes, 1, 0, 0);
-  } else {
-    for (uint32_t k = 0; k < cnt; k++) {
-      if (raw[k]) wg_copy(out + pos[k], (const uint8_t*)it[k].src, csz[k], it[k].ts, it[k].neb, it[k].off);
-      else wg_copy(out + pos[k], (const uint8_t*)it[k].dst, csz[k], 1, 0, 0);
-    }
-  }
-  if (threadIdx.x == 0) sizes[ci] = s_ntbytes;
+  const ItemOut* io = iout + ci * KSLOTS;
+  for (uint32_t k = 0; k < cnt; k++)
+    if (io[k].raw) wg_copy(out + io[k].pos, (const uint8_t*)it[k].src, it[k].len, it[k].ts, it[k].neb, it[k].off);
 }
 
 }  // namespace
@@ -681,7 +795,9 @@ struct hsds_engine {
   hipEvent_t ev0, ev1;
   int ev_valid = 0;
   // encode workspace (items, sizes, geometry) and per-split output scratch
-  int deflate_blocks_per_cu = 1;
+  int parse_blocks_per_cu = 1;
+  int huff_blocks_per_cu = 1;
+  int emit_blocks_per_cu = 1;
   uint8_t* ews = nullptr;
   size_t ews_bytes = 0;
   uint8_t* escr = nullptr;
@@ -736,9 +852,13 @@ int hsds_engine_create(int device, hsds_engine** out) {
     if (v >= 1 && v < occ) occ = v;
   }
   e->inflate_blocks_per_cu = occ;
-  int docc = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc, deflate_kernel, 64, 0) != hipSuccess || docc < 1) docc = 2;
-  e->deflate_blocks_per_cu = docc;
+  int o1 = 0, o2 = 0, o3 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, parse_kernel, 64, 0) != hipSuccess || o1 < 1) o1 = 2;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, huff_kernel, 64, 0) != hipSuccess || o2 < 1) o2 = 4;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o3, emit_kernel, 64, 0) != hipSuccess || o3 < 1) o3 = 4;
+  e->parse_blocks_per_cu = o1;
+  e->huff_blocks_per_cu = o2;
+  e->emit_blocks_per_cu = o3;
   e->tune.L0 = 384;
   e->tune.W = 96;
   e->tune.adapt = 1;
@@ -969,42 +1089,73 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
                       int shuffle, int typesize, void* stream) {
   if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
   if (clevel < 0 || clevel > 9 || (shuffle != HSDS_SHUFFLE_NONE && shuffle != HSDS_SHUFFLE_BYTE)) return HSDS_ERR_ARG;
+  if (((uintptr_t)d_dst & 3u) != 0) return HSDS_ERR_ARG;
   if (nchunks == 0) return HSDS_OK;
   if (nchunks > (int64_t)(1u << 22)) return HSDS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
-  const size_t sz_slots = (size_t)nchunks * KSLOTS * sizeof(EncItem);
-  const size_t sz_isz = (size_t)nchunks * KSLOTS * sizeof(int64_t);
-  const size_t sz_counts = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
-  const size_t sz_offs = ((size_t)(nchunks + 1) * 4 + 255) & ~(size_t)255;
-  const size_t sz_geom = ((size_t)nchunks * sizeof(EncGeom) + 255) & ~(size_t)255;
-  const size_t need = sz_slots + sz_isz + sz_counts + sz_offs + sz_geom + 256;
+  // segment capacity: every byte of every chunk at most once per SEG, plus the
+  // partial last segment of up to 16 streams per chunk (chunks beyond it fail)
+  const uint64_t seg_cap64 = dst_extent / hd::SEG + (uint64_t)nchunks * 16 + 64;
+  if (seg_cap64 > 0xffffffffull) return HSDS_ERR_ARG;
+  const uint32_t seg_cap = (uint32_t)seg_cap64;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t ns = (size_t)nchunks * KSLOTS;
+  const size_t sz_slots = al(ns * sizeof(EncItem));
+  const size_t sz_adler = al(ns * 4);
+  const size_t sz_iout = al(ns * sizeof(ItemOut));
+  const size_t sz_counts = al((size_t)nchunks * 4);
+  const size_t sz_offs = al((size_t)(nchunks + 1) * 4);
+  const size_t sz_geom = al((size_t)nchunks * sizeof(EncGeom));
+  const size_t sz_sp = al((size_t)seg_cap * sizeof(hd::SegParse));
+  const size_t sz_sc = al((size_t)seg_cap * sizeof(hd::SegCode));
+  const size_t sz_so = al((size_t)seg_cap * sizeof(hd::SegOut));
+  const size_t sz_meta = al((size_t)seg_cap * sizeof(SegMeta));
+  const size_t need = sz_slots + sz_adler + sz_iout + 2 * sz_counts + 2 * sz_offs + sz_geom + sz_sp + sz_sc + sz_so +
+                      sz_meta + 256;
   if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
   uint8_t* w = e->ews;
   EncItem* slots = (EncItem*)w; w += sz_slots;
-  int64_t* isz = (int64_t*)w; w += sz_isz;
+  uint32_t* adler = (uint32_t*)w; w += sz_adler;
+  ItemOut* iout = (ItemOut*)w; w += sz_iout;
   uint32_t* counts = (uint32_t*)w; w += sz_counts;
+  uint32_t* segcnt = (uint32_t*)w; w += sz_counts;
   uint32_t* offs = (uint32_t*)w; w += sz_offs;
+  uint32_t* segoffs = (uint32_t*)w; w += sz_offs;
   EncGeom* geom = (EncGeom*)w; w += sz_geom;
-  uint32_t* ctr = (uint32_t*)w;
-  // per-split output scratch: the destination layout plus ENC_CHUNK_SLACK per chunk
-  if (grow((void**)&e->escr, &e->escr_bytes, dst_extent + (size_t)nchunks * ENC_CHUNK_SLACK + 256))
-    return HSDS_ERR_DEVICE;
+  hd::SegParse* sp = (hd::SegParse*)w; w += sz_sp;
+  hd::SegCode* sc = (hd::SegCode*)w; w += sz_sc;
+  hd::SegOut* so = (hd::SegOut*)w; w += sz_so;
+  SegMeta* meta = (SegMeta*)w; w += sz_meta;
+  uint32_t* ctr = (uint32_t*)w;    // [0] parse items, [1] huffman segments, [2] emit segments
+  // token slots: SEG_TOK per segment
+  if (grow((void**)&e->escr, &e->escr_bytes, (size_t)seg_cap * hd::SEG_TOK * 2 + 256)) return HSDS_ERR_DEVICE;
+  uint16_t* tok = (uint16_t*)e->escr;
   if (hipMemsetAsync(ctr, 0, 16, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
-  hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, e->escr,
-                     slots, counts, geom, d_status, clevel, shuffle, typesize);
+  hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, slots,
+                     counts, segcnt, geom, d_status, clevel, shuffle, typesize);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
-  int64_t grid = (int64_t)e->num_cus * e->deflate_blocks_per_cu;
-  if (grid > nchunks * 4) grid = nchunks * 4;
-  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, segcnt, segoffs, nchunks);
+  auto grid_for = [&](int per_cu, int64_t cap) {
+    int64_t g = (int64_t)e->num_cus * per_cu;
+    if (g > cap) g = cap;
+    return (unsigned)(g < 1 ? 1 : g);
+  };
   hipEventRecord(e->ev2, st);
-  hipLaunchKernelGGL(deflate_kernel, dim3((unsigned)grid), dim3(64), 0, st, slots, offs, nchunks, ctr, isz, clevel);
+  hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, nchunks * KSLOTS)), dim3(64), 0, st, slots,
+                     offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, clevel);
+  hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs, nchunks,
+                     ctr + 1, sp, meta, sc, seg_cap, clevel);
+  hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
+                     segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel);
+  hipLaunchKernelGGL(emit_kernel, dim3(grid_for(e->emit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs, nchunks,
+                     ctr + 2, so, sc, sp, tok, slots, (uint32_t*)d_dst, seg_cap, clevel);
+  hipLaunchKernelGGL(raw_copy_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
+                     nchunks, (uint8_t*)d_dst, slots, counts, geom, iout, d_status);
   hipEventRecord(e->ev3, st);
   e->ev_enc_valid = 1;
-  hipLaunchKernelGGL(frame_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
-                     nchunks, (uint8_t*)d_dst, slots, counts, geom, isz, d_sizes, d_status);
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
 }
 

@@ -1,31 +1,74 @@
 // CPU emulation driver for hsds_amd/csrc/deflate_wave.h (TEST INFRASTRUCTURE ONLY).
-// Runs the exact single-source wave encoder with LANE_LOOP iterating the 64 lanes
-// in order, so its orchestration is checked against libz inflate on CPU.  Never
+// Runs the exact single-source phases of the wave encoder (parse -> Huffman ->
+// layout -> emit) with LANE_LOOP iterating the 64 lanes in order, for one zlib
+// stream, so that the orchestration is checked against libz inflate on CPU.  Never
 // used by the product.
 #include <stdlib.h>
+#include <string.h>
+#include <vector>
 #include "../../hsds_amd/csrc/deflate_wave.h"
 
-// dst: 4-byte aligned, cap + 8 bytes writable.  Returns compressed bytes or -1.
-extern "C" int64_t emu_deflate(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level,
-                               int chain_override) {
-  hd::Shared* sh = (hd::Shared*)calloc(1, sizeof(hd::Shared));
-  hd::Tune tune = hd::tune_for_level(level);
-  if (chain_override > 0) tune.chain = (uint32_t)chain_override;
-  hd::EncJob job = {src, n, (uint32_t*)dst, cap, level, 1u, 0u, 0u};
-  const int64_t r = hd::deflate_stream(*sh, job, tune);
-  free(sh);
+static int64_t run(const hd::EncJob& job, const hd::Tune& tune, uint8_t* dst, uint32_t cap) {
+  const uint32_t nseg = hd::nsegments(job.len);
+  std::vector<hd::SegParse> sp(nseg);
+  std::vector<hd::SegCode> sc(nseg);
+  std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
+  hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
+  hd::HuffShared* hs = (hd::HuffShared*)calloc(1, sizeof(hd::HuffShared));
+  hd::EmitShared* es = (hd::EmitShared*)calloc(1, sizeof(hd::EmitShared));
+  const uint32_t adler = hd::parse_stream(*ps, job, tune, sp.data(), tok.data());
+  for (uint32_t s = 0; s < nseg; s++) {
+    const uint32_t s0 = s * (uint32_t)hd::SEG;
+    const uint32_t seglen = job.len - s0 < (uint32_t)hd::SEG ? job.len - s0 : (uint32_t)hd::SEG;
+    hd::huff_segment(*hs, &sp[s], &sc[s], seglen, tune.stored);
+  }
+  const uint64_t total = hd::stream_layout(sc.data(), job.len, nullptr);
+  int64_t r = -1;
+  if (total <= cap) {
+    // the layout phase: block bit positions from bit 16, zlib header bytes
+    std::vector<uint32_t> words((total + 8) / 4 + 8, 0u);
+    uint8_t* wb = (uint8_t*)words.data();
+    wb[0] = 0x78;
+    wb[1] = (uint8_t)hd::zlib_flg(job.level);
+    uint64_t bpos = 16;
+    for (uint32_t s = 0; s < nseg; s++) {
+      const uint32_t s0 = s * (uint32_t)hd::SEG;
+      const uint32_t seglen = job.len - s0 < (uint32_t)hd::SEG ? job.len - s0 : (uint32_t)hd::SEG;
+      hd::SegOut o;
+      o.bitpos = bpos;
+      o.item = 0;
+      o.seg = s;
+      o.flags = 1u | (s + 1 == nseg ? 2u : 0u);
+      o.adler = adler;
+      hd::emit_segment(*es, o, &sc[s], &sp[s], tok.data() + (size_t)s * hd::SEG_TOK, job, words.data());
+      if (sc[s].btype == 0) bpos = ((bpos + 3u + 7u) & ~7ull) + 32u + 8ull * seglen;
+      else bpos += sc[s].bits;
+    }
+    memcpy(dst, wb, total);
+    r = (int64_t)total;
+  }
+  free(ps);
+  free(hs);
+  free(es);
   return r;
 }
 
-extern "C" int emu_deflate_shared_bytes() { return (int)sizeof(hd::Shared); }
+// Returns compressed bytes or -1 when they would exceed cap.
+extern "C" int64_t emu_deflate(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level,
+                               int chain_override) {
+  hd::Tune tune = hd::tune_for_level(level);
+  if (chain_override > 0) tune.chain = (uint32_t)chain_override;
+  hd::EncJob job = {src, n, level, 1u, 0u, 0u};
+  return run(job, tune, dst, cap);
+}
 
 // gather mode: the stream is bytes [off, off + n) of the byte-shuffled block at src
 extern "C" int64_t emu_deflate_shuffled(const uint8_t* block, uint32_t n, uint8_t* dst, uint32_t cap, int level,
                                         uint32_t ts, uint32_t neb, uint32_t off) {
-  hd::Shared* sh = (hd::Shared*)calloc(1, sizeof(hd::Shared));
-  hd::Tune tune = hd::tune_for_level(level);
-  hd::EncJob job = {block, n, (uint32_t*)dst, cap, level, ts, neb, off};
-  const int64_t r = hd::deflate_stream(*sh, job, tune);
-  free(sh);
-  return r;
+  hd::EncJob job = {block, n, level, ts, neb, off};
+  return run(job, hd::tune_for_level(level), dst, cap);
 }
+
+extern "C" int emu_parse_shared_bytes() { return (int)sizeof(hd::ParseShared); }
+extern "C" int emu_huff_shared_bytes() { return (int)sizeof(hd::HuffShared); }
+extern "C" int emu_emit_shared_bytes() { return (int)sizeof(hd::EmitShared); }
