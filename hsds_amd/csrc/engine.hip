@@ -245,16 +245,70 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
 // -------------------------------------------------------------------------
 // unshuffle of staged chunks: work items = (listed chunk, 4 KiB output tile)
 // -------------------------------------------------------------------------
-__device__ __forceinline__ void unshuffle_range(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                uint64_t len, uint32_t n, uint64_t beg, uint64_t end) {
+// Byte (un)shuffle of one span (numcodecs.Shuffle / HDF5 shuffle filter): element-
+// major `elem` (count = len / n elements of n bytes, then len % n tail bytes) <->
+// plane-major `plane` (byte k of every element in plane k).  Word path: a thread
+// owns 4 consecutive elements, reads one dword per plane (coalesced across the
+// group) and writes the 4 elements as n whole dwords (16 B per lane for n = 4), a
+// register byte transpose instead of per-byte gathers.  `tid`/`nthr` stride the
+// groups over whatever set of threads shares the span.
+template <bool UNSHUFFLE, int NT>
+__device__ __forceinline__ void shuffle_span_n(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t len,
+                                               uint32_t n_rt, uint64_t tid, uint64_t nthr) {
+  const uint32_t n = NT ? (uint32_t)NT : n_rt;   // compile-time plane count for the common dtypes
   const uint64_t count = len / n, body = count * n;
-  for (uint64_t q = beg; q < end; q++) {
-    out[q] = q < body ? in[(q % n) * count + q / n] : in[q];
+  const bool words = n >= 2 && n <= 16 && (count & 3) == 0 && (((uintptr_t)in | (uintptr_t)out) & 3) == 0;
+  uint64_t done = 0;
+  if (words) {
+    const uint64_t groups = count / 4;
+    for (uint64_t g = tid; g < groups; g += nthr) {
+      uint32_t p[16], w[16];
+      if (UNSHUFFLE) {
+        for (uint32_t k = 0; k < n; k++) p[k] = ((const uint32_t*)(in + k * count))[g];
+        for (uint32_t i = 0; i < n; i++) w[i] = 0;
+        for (uint32_t e = 0; e < 4; e++)
+          for (uint32_t k = 0; k < n; k++) {
+            const uint32_t ob = e * n + k;                       // output byte within the 4 elements
+            w[ob >> 2] |= ((p[k] >> (8 * e)) & 0xffu) << (8 * (ob & 3));
+          }
+        uint32_t* o = (uint32_t*)out + g * n;
+        for (uint32_t i = 0; i < n; i++) o[i] = w[i];
+      } else {
+        const uint32_t* ip = (const uint32_t*)in + g * n;
+        for (uint32_t i = 0; i < n; i++) w[i] = ip[i];
+        for (uint32_t k = 0; k < n; k++) p[k] = 0;
+        for (uint32_t e = 0; e < 4; e++)
+          for (uint32_t k = 0; k < n; k++) {
+            const uint32_t ib = e * n + k;
+            p[k] |= ((w[ib >> 2] >> (8 * (ib & 3))) & 0xffu) << (8 * e);
+          }
+        for (uint32_t k = 0; k < n; k++) ((uint32_t*)(out + k * count))[g] = p[k];
+      }
+    }
+    done = body;
+  }
+  for (uint64_t q = done + tid; q < len; q += nthr) {
+    if (q >= body) { out[q] = in[q]; continue; }
+    if (UNSHUFFLE) out[q] = in[(q % n) * count + q / n];
+    else out[(q % n) * count + q / n] = in[q];
   }
 }
 
-__global__ void unshuffle_kernel(const ChunkMeta* __restrict__ meta, const uint32_t* __restrict__ meta_list,
-                                 const uint32_t* __restrict__ meta_count, const int32_t* __restrict__ status) {
+template <bool UNSHUFFLE>
+__device__ __forceinline__ void shuffle_span(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t len,
+                                             uint32_t n, uint64_t tid, uint64_t nthr) {
+  switch (n) {
+    case 2: shuffle_span_n<UNSHUFFLE, 2>(in, out, len, n, tid, nthr); break;
+    case 4: shuffle_span_n<UNSHUFFLE, 4>(in, out, len, n, tid, nthr); break;
+    case 8: shuffle_span_n<UNSHUFFLE, 8>(in, out, len, n, tid, nthr); break;
+    default: shuffle_span_n<UNSHUFFLE, 0>(in, out, len, n, tid, nthr); break;
+  }
+}
+
+__global__ void __launch_bounds__(256) unshuffle_kernel(const ChunkMeta* __restrict__ meta,
+                                                        const uint32_t* __restrict__ meta_list,
+                                                        const uint32_t* __restrict__ meta_count,
+                                                        const int32_t* __restrict__ status) {
   const uint32_t nlist = *meta_count;
   for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
     const uint32_t ci = meta_list[li];
@@ -263,18 +317,11 @@ __global__ void unshuffle_kernel(const ChunkMeta* __restrict__ meta, const uint3
     const uint8_t* in = (const uint8_t*)m.tmp;
     uint8_t* out = (uint8_t*)m.dst;
     if (m.mode == 2) {
-      const uint32_t n = m.ts;
-      const uint64_t count = m.nbytes / n, body = count * n;
-      for (uint64_t q = threadIdx.x; q < m.nbytes; q += blockDim.x)
-        out[q] = q < body ? in[(q % n) * count + q / n] : in[q];
+      shuffle_span<true>(in, out, m.nbytes, m.ts, threadIdx.x, blockDim.x);
     } else {
-      const uint64_t nb = m.nbytes, bs = m.bs;
-      for (uint64_t b0 = 0; b0 < nb; b0 += bs) {
-        const uint64_t bsz = nb - b0 < bs ? nb - b0 : bs;
-        const uint32_t n = m.ts;
-        const uint64_t count = bsz / n, body = count * n;
-        for (uint64_t q = threadIdx.x; q < bsz; q += blockDim.x)
-          out[b0 + q] = q < body ? in[b0 + (q % n) * count + q / n] : in[b0 + q];
+      for (uint64_t b0 = 0; b0 < m.nbytes; b0 += m.bs) {
+        const uint64_t bsz = m.nbytes - b0 < m.bs ? m.nbytes - b0 : m.bs;
+        shuffle_span<true>(in + b0, out + b0, bsz, m.ts, threadIdx.x, blockDim.x);
       }
     }
   }
@@ -283,12 +330,9 @@ __global__ void unshuffle_kernel(const ChunkMeta* __restrict__ meta, const uint3
 // plain device shuffle / unshuffle of one buffer (numcodecs.Shuffle semantics)
 __global__ void shuffle_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t len,
                                uint32_t n, int inverse) {
-  const uint64_t count = len / n, body = count * n;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x) {
-    if (q >= body) { out[q] = in[q]; continue; }
-    if (inverse) out[q] = in[(q % n) * count + q / n];          // unshuffle: element-major out
-    else out[(q % n) * count + q / n] = in[q];                  // shuffle:   plane-major out
-  }
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nthr = (uint64_t)gridDim.x * blockDim.x;
+  if (inverse) shuffle_span<true>(in, out, len, n, tid, nthr);
+  else shuffle_span<false>(in, out, len, n, tid, nthr);
 }
 
 // -------------------------------------------------------------------------
