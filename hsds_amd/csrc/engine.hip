@@ -32,7 +32,7 @@
 namespace {
 
 constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
-constexpr int INFLATE_WAVES_PER_CU = 7;   // LDS-bound: sizeof(hz::Shared) <= 22.8 KiB
+constexpr int INFLATE_WAVES_PER_CU = 8;   // LDS-bound: sizeof(hz::Shared) <= 20 KiB
 static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
 
 enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_INEXACT = 0x100 };

@@ -80,17 +80,35 @@ namespace hz {
 constexpr int WAVE = 64;
 constexpr int LL_ROOT = 10;
 constexpr int D_ROOT = 8;
-// second-level entries (codes longer than the root).  Sized above zlib's exact
+// second-level entries (codes longer than the root).  Sized at or above zlib's exact
 // worst cases (ENOUGH: 286 symbols / root 10 -> 308 extra entries; 30 symbols /
 // root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
-constexpr int LL_SUB = 512;
+// Window sizes (LMAX, SCAP, SLOTS) are set so that sizeof(Shared) = 20480 B: eight
+// wavefronts per CU (A/B on MI355X: 7 -> 8 waves/CU gave F1 +7 %, F2 +14 %; smaller
+// windows at 9-10 waves/CU lost more to per-window overhead than they gained).
+#ifndef HZ_LL_SUB
+#define HZ_LL_SUB 320
+#endif
+constexpr int LL_SUB = HZ_LL_SUB;
 constexpr int D_SUB = 384;
-constexpr int SLOTS = 58;           // 16-bit token slots per lane per window (a match takes two)
-constexpr int LMAX = 384;           // max segment length (bits)
+#ifndef HZ_SLOTS
+#define HZ_SLOTS 50
+#endif
+constexpr int SLOTS = HZ_SLOTS;           // 16-bit token slots per lane per window (a match takes two)
+#ifndef HZ_LMAX
+#define HZ_LMAX 288
+#endif
+constexpr int LMAX = HZ_LMAX;           // max segment length (bits)
 constexpr int LMIN = 64;
 constexpr uint32_t ADAPT_FILL16 = 11; // adaptive L aims at this many 16ths of SLOTS token slots per segment
-constexpr int SCAP = 5120;           // window output bytes resolved in LDS
-constexpr int CMAX = 256;           // max continuation bits into the next segment
+#ifndef HZ_SCAP
+#define HZ_SCAP 4608
+#endif
+constexpr int SCAP = HZ_SCAP;           // window output bytes resolved in LDS
+#ifndef HZ_CMAX
+#define HZ_CMAX 256
+#endif
+constexpr int CMAX = HZ_CMAX;           // max continuation bits into the next segment
 constexpr int OVR = 64;             // bitmap bits past the last token start
 constexpr int BM_WORDS = (LMAX + CMAX + OVR) / 32 + 1;
 // staged input dwords: window (64 L) + warm-up (<= L) + alignment + overrun/peek
@@ -518,8 +536,11 @@ struct TableArgs {
               lmax = l2; k2++;                                                          \
             }                                                                           \
             const int sb = lmax - _R;                                                   \
+            /* <= nsub for every complete code (see LL_SUB/D_SUB); a table that would  \
+               not fit is rejected instead of written past its end */                   \
+            if (used + (1 << sb) > (A).nsub) { (sh).u_status = hz::ST_DATA; break; }    \
             (A).lut[hz::rev_bits((uint32_t)p, _R)] = hz::ent_sub((uint32_t)used, (uint32_t)sb); \
-            used += 1 << sb;  /* <= nsub for every complete code (see LL_SUB/D_SUB) */  \
+            used += 1 << sb;                                                            \
             k = k2;                                                                     \
           }                                                                             \
         }                                                                               \
@@ -527,7 +548,7 @@ struct TableArgs {
       WAVE_SYNC();                                                                      \
       /* fill subtables by symbol (zlib-style replication) */                           \
       LANE_LOOP {                                                                       \
-        for (int k = _k0 + lane; k < _k1; k += 64) {                                    \
+        for (int k = _k0 + lane; k < _k1 && (sh).u_status == hz::ST_OK; k += 64) {      \
           const uint32_t sym = (A).sorted[k];                                           \
           const int len = (A).lens[sym];                                                \
           const int c = (int)(sh).tb_first[len] + (k - (int)(sh).tb_offs[len]);         \

@@ -127,3 +127,27 @@ def test_wrong_expected_size(emu):
     c = zlib.compress(data, 4)
     assert run(emu, c, len(data) - 1)[0] < 0
     assert run(emu, c, len(data) + 1)[0] < 0
+
+
+def test_deep_codes_use_second_level_tables(emu):
+    # Fibonacci symbol frequencies make zlib build length-limited codes that reach
+    # 15 bits for both literals and distances: the longest codes and the largest
+    # second-level table usage the LDS tables are sized for (LL_SUB / D_SUB).
+    import zlib
+    rng = np.random.default_rng(77)
+    fib = [1, 1]
+    while len(fib) < 40:
+        fib.append(fib[-1] + fib[-2])
+    lits = np.concatenate([np.full(min(f, 20000), s % 256, np.uint8) for s, f in enumerate(fib[:24])])
+    rare = rng.permutation(256).astype(np.uint8)          # every other byte value once
+    data = np.concatenate([rng.permutation(lits), rare]).tobytes()
+    # matches at Fibonacci-distributed distances
+    parts = [data]
+    for k, f in enumerate(fib[:20]):
+        d = 1 + (k * 1543) % 30000
+        parts.append(data[-d:][:8] * max(1, min(f, 50)))
+    data = b"".join(parts)[:400000]
+    for level in (1, 6, 9):
+        comp = zlib.compress(data, level)
+        r, out = run(emu, comp, len(data))
+        assert r == 0 and out == data, (level, r)
