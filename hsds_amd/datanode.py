@@ -1,0 +1,663 @@
+"""Data-node read side of the hot path, batched on the GPU (SURVEY.md section 8a rows
+a8-a12 and section 8f items 1-2).
+
+Reference flow, one chunk per request:
+  get_chunk (hsds/datanode_lib.py:948-1142): chunk cache lookup, in-flight read dedupe,
+  get_chunk_bytes (datanode_lib.py:796-945):
+    * plain objects: getStorBytes -> _uncompress (storUtil.py:450-522), bytesToArray,
+      H5D_CONTIGUOUS_REF reads zero-extended to the chunk size (:833-844);
+    * H5D_CHUNKED_REF_INDIRECT "hyper chunks": a chunk made of k HDF5 chunks at byte
+      offsets of an HDF5 file; the array is prefilled (fill value or zeros), empty
+      ranges are skipped, the locations are coalesced by chunkMunge
+      (rangegetUtil.py:111-159) into range reads, and getHyperChunks
+      (storUtil.py:525-580) decodes every HDF5 chunk and places it at
+      hyper_index * hyper_dims;
+  then the array goes into the chunk LruCache (lruCache.py:37-410) if there is room.
+
+Here a whole request's chunks are one batch: every stored object and every HDF5 chunk
+of the batch is decoded by ONE hsds_decode_batch call into a contiguous device buffer,
+and ONE hsds_copy_batch launch per destination places plain chunks and hyper chunks
+into their slots of an HBM-resident cache arena (DeviceChunkCache).  The
+storage read itself (POSIX / S3 / Azure drivers) stays outside this engine: callers
+pass `fetch(key, offset, length) -> bytes | None` (None = object not found).
+"""
+import time
+from collections import OrderedDict, namedtuple
+from operator import attrgetter
+
+import numpy as np
+
+from . import _native as nat
+from .codec import HTTPInternalServerError
+
+# HDF5 file chunk location (rangegetUtil.py:9): index = hyper-chunk index tuple,
+# offset / length = byte range in the HDF5 file
+ChunkLocation = namedtuple("ChunkLocation", ["index", "offset", "length"])
+
+H5D_CONTIGUOUS_REF = "H5D_CONTIGUOUS_REF"
+
+
+class HTTPNotFound(Exception):
+    """Stored object missing (the reference raises aiohttp's HTTPNotFound -> 404)."""
+
+
+# ---------------------------------------------------------------------------
+# rangegetUtil restatement (pure logic, pinned by tests/golden/rangeget_cases.json)
+# ---------------------------------------------------------------------------
+def getHyperChunkFactors(chunk_dims, hyper_dims):
+    """Per-dimension ratio chunk extent / hyper-chunk extent (rangegetUtil.py:24-38);
+    ValueError when the ranks differ or an extent does not divide."""
+    if len(hyper_dims) != len(chunk_dims):
+        raise ValueError("unexpected length for hyper_dims")
+    factors = []
+    for c, h in zip(chunk_dims, hyper_dims):
+        if c % h:
+            raise ValueError("unexpected value for hyper_dims")
+        factors.append(c // h)
+    return factors
+
+
+def getHyperChunkIndex(i, factors):
+    """Index tuple of the i-th hyper chunk, C order over `factors` (rangegetUtil.py:41-52)."""
+    idx = []
+    for d in range(len(factors)):
+        stride = int(np.prod(factors[d + 1:], dtype=np.int64))
+        idx.append((i // stride) % factors[d])
+    return tuple(idx)
+
+
+def _span(c):
+    if isinstance(c, list):
+        return min(e.offset for e in c), max(e.offset + e.length for e in c)
+    return c.offset, c.offset + c.length
+
+
+def chunkMunge(h5chunks, max_gap=1024):
+    """Coalesce ChunkLocations into range-read groups (rangegetUtil.py:111-159).
+
+    Sorted by offset; repeatedly the closest adjacent pair (gap = start of the right
+    item minus end of the left item, first pair on ties, a zero gap wins at once) whose
+    gap is <= max_gap is merged into one list, until no pair qualifies.  Items that
+    never merge stay bare ChunkLocations, merged ones become lists in offset order."""
+    items = sorted(h5chunks, key=attrgetter("offset"))
+    while len(items) > 1:
+        best, best_d = None, None
+        for i in range(1, len(items)):
+            ls, le = _span(items[i - 1])
+            rs, re = _span(items[i])
+            d = rs - le if ls < rs else ls - re
+            if d < 0:
+                raise ValueError("unexpected chunk position")
+            if d == 0:
+                best = i
+                break
+            if d <= max_gap and (best_d is None or d < best_d):
+                best, best_d = i, d
+        if best is None:
+            break
+        left, right = items[best - 1], items[best]
+        merged = (list(left) if isinstance(left, list) else [left])
+        merged += right if isinstance(right, list) else [right]
+        items = items[:best - 1] + [merged] + items[best + 1:]
+    return items
+
+
+# ---------------------------------------------------------------------------
+# HBM arena + chunk cache (lruCache.LruCache semantics, device-resident)
+# ---------------------------------------------------------------------------
+class DeviceArena:
+    """One preallocated uint8 HBM tensor carved into 256-byte aligned slots.  Freed
+    slots go to an exact-size free list (HSDS datasets have a handful of chunk sizes)
+    and are reused first; the bump pointer serves the rest."""
+
+    ALIGN = 256
+
+    def __init__(self, nbytes, device):
+        import torch
+        self.capacity = int(nbytes)
+        self.buf = torch.empty(self.capacity, dtype=torch.uint8, device=device)
+        self.top = 0
+        self.free_lists = {}
+        self.used = 0
+
+    def _round(self, n):
+        return max(self.ALIGN, (int(n) + self.ALIGN - 1) // self.ALIGN * self.ALIGN)
+
+    def alloc(self, nbytes):
+        n = self._round(nbytes)
+        fl = self.free_lists.get(n)
+        if fl:
+            off = fl.pop()
+        elif self.top + n <= self.capacity:
+            off = self.top
+            self.top += n
+        else:
+            return None
+        self.used += n
+        return off
+
+    def free(self, off, nbytes):
+        n = self._round(nbytes)
+        self.free_lists.setdefault(n, []).append(off)
+        self.used -= n
+
+    def view(self, off, nbytes):
+        return self.buf[off:off + int(nbytes)]
+
+
+class _Node:
+    __slots__ = ("off", "nbytes", "shape", "dtype", "dirty", "pinned", "last_access")
+
+    def __init__(self, off, nbytes, shape, dtype):
+        self.off, self.nbytes, self.shape, self.dtype = off, int(nbytes), tuple(shape), np.dtype(dtype)
+        self.dirty = False
+        self.pinned = False      # slot of a read batch in flight: not evictable
+        self.last_access = time.time()
+
+
+def device_view(u8, shape, dtype):
+    """Typed torch view of a uint8 device slice (falls back to the uint8 bytes for
+    numpy dtypes torch has no equivalent of, e.g. compound types)."""
+    import torch
+    m = {np.dtype(k): v for k, v in ((np.float32, torch.float32), (np.float64, torch.float64),
+                                     (np.float16, torch.float16), (np.int8, torch.int8), (np.uint8, torch.uint8),
+                                     (np.int16, torch.int16), (np.int32, torch.int32), (np.int64, torch.int64),
+                                     (np.uint16, torch.uint16), (np.uint32, torch.uint32),
+                                     (np.uint64, torch.uint64), (np.bool_, torch.bool))}
+    dt = np.dtype(dtype)
+    td = m.get(dt.newbyteorder("=")) if dt.isnative or dt.itemsize == 1 else None
+    if td is None:
+        return u8
+    return u8.view(td).reshape(shape)
+
+
+class DeviceChunkCache:
+    """HBM-resident replacement of the DN chunk LruCache (lruCache.py:37-410): the same
+    operations and accounting (mem_target, dirty set, memFree = target - dirty bytes,
+    cacheUtilizationPercent, dirty nodes never evicted, clearCache refuses dirty
+    nodes), but entries are slots of one DeviceArena, so decodes land in place.  The
+    reference's default 128 MiB target (config.yml:58) becomes an HBM-sized one.
+
+    Deviation (documented): the reference's __setitem__ on an existing key computes
+    its size delta from the already-updated node (always 0, lruCache.py:181-183);
+    here the delta is applied."""
+
+    def __init__(self, mem_target, device, name="ChunkCache", expire_time=None, arena_bytes=None):
+        self._target = int(mem_target)
+        self._name = name
+        self._expire = expire_time
+        self._lru = OrderedDict()        # key -> _Node, most recent last
+        self._mem = 0
+        self._dirty = set()
+        self._dirty_size = 0
+        self.arena = DeviceArena(arena_bytes or int(mem_target * 1.25) + (1 << 20), device)
+
+    # -- LruCache surface --
+    def __len__(self):
+        return len(self._lru)
+
+    def __iter__(self):
+        return iter(reversed(list(self._lru.keys())))    # most recent first, like the LRU list
+
+    def _has(self, key):
+        n = self._lru.get(key)
+        if n is None:
+            return False
+        if self._expire and not n.dirty and time.time() - n.last_access > self._expire:
+            return False
+        return True
+
+    def __contains__(self, key):
+        return self._has(key)
+
+    def __getitem__(self, key):
+        if not self._has(key):
+            raise KeyError(key)
+        self._lru.move_to_end(key)
+        n = self._lru[key]
+        return device_view(self.arena.view(n.off, n.nbytes), n.shape, n.dtype)
+
+    def node_bytes(self, key):
+        n = self._lru[key]
+        return self.arena.view(n.off, n.nbytes)
+
+    def __delitem__(self, key):
+        n = self._lru.pop(key)
+        self._mem -= n.nbytes
+        if key in self._dirty:
+            self._dirty.discard(key)
+            self._dirty_size = max(0, self._dirty_size - n.nbytes)
+        self.arena.free(n.off, n.nbytes)
+
+    def reserve(self, key, shape, dtype, pin=False):
+        """Slot for `key` (existing or new, moved to the front), evicting clean LRU
+        nodes until the arena has room; None when nothing more can be evicted.  A
+        pinned slot (a read batch in flight) is not evicted until unpin()."""
+        nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
+        if key in self._lru:
+            n = self._lru[key]
+            if n.nbytes == nbytes:
+                self._lru.move_to_end(key)
+                n.shape, n.dtype, n.last_access = tuple(shape), np.dtype(dtype), time.time()
+                n.pinned = n.pinned or pin
+                return self.arena.view(n.off, n.nbytes)
+            dirty = n.dirty
+            del self[key]
+        else:
+            dirty = False
+        off = self.arena.alloc(nbytes)
+        while off is None and self._evict_one(exclude=key):
+            off = self.arena.alloc(nbytes)
+        if off is None:
+            return None
+        node = _Node(off, nbytes, shape, dtype)
+        node.pinned = pin
+        self._lru[key] = node
+        self._mem += nbytes
+        if dirty:
+            self.setDirty(key)
+        if self._mem > self._target:
+            keep = node.dirty
+            node.dirty = True        # never evict the node just added (lruCache.py:215-222)
+            self._reduce()
+            node.dirty = keep
+        return self.arena.view(off, nbytes)
+
+    def __setitem__(self, key, arr):
+        """Store a host ndarray or a device tensor (copied into the arena)."""
+        import torch
+        if isinstance(arr, np.ndarray):
+            shape, dtype = arr.shape, arr.dtype
+            src = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).reshape(-1))
+        else:
+            raise TypeError("DeviceChunkCache stores numpy arrays or uses reserve() for device data")
+        slot = self.reserve(key, shape, dtype)
+        if slot is None:
+            raise MemoryError("chunk cache full of dirty chunks")
+        slot.copy_(src, non_blocking=False)
+
+    def unpin(self, key):
+        n = self._lru.get(key)
+        if n is not None:
+            n.pinned = False
+
+    def _evict_one(self, exclude=None):
+        for k, n in self._lru.items():          # least recent first
+            if not n.dirty and not n.pinned and k != exclude:
+                del self[k]
+                return True
+        return False
+
+    def _reduce(self):
+        for k in [k for k, n in self._lru.items() if not n.dirty and not n.pinned]:
+            if self._mem <= self._target:
+                break
+            del self[k]
+
+    def clearCache(self):
+        if any(n.dirty for n in self._lru.values()):
+            raise ValueError("Unable to clear cache")
+        for k in list(self._lru):
+            del self[k]
+
+    def setDirty(self, key):
+        self._lru.move_to_end(key)
+        n = self._lru[key]
+        if not n.dirty:
+            self._dirty_size += n.nbytes
+        n.dirty = True
+        self._dirty.add(key)
+
+    def clearDirty(self, key):
+        self._lru.move_to_end(key)
+        n = self._lru[key]
+        if n.dirty:
+            self._dirty_size -= n.nbytes
+        n.dirty = False
+        if key in self._dirty:
+            self._dirty.discard(key)
+            if self._mem > self._target:
+                self._reduce()
+
+    def isDirty(self, key):
+        return key in self._dirty
+
+    @property
+    def cacheUtilizationPercent(self):
+        return int(self._mem / self._target * 100.0)
+
+    @property
+    def dirtyCount(self):
+        return len(self._dirty)
+
+    @property
+    def memUsed(self):
+        return self._mem
+
+    @property
+    def memFree(self):
+        return max(0, self._target - self._dirty_size)
+
+    @property
+    def memTarget(self):
+        return self._target
+
+    @property
+    def memDirty(self):
+        return self._dirty_size
+
+
+# ---------------------------------------------------------------------------
+# batched get_chunk_bytes / get_chunk
+# ---------------------------------------------------------------------------
+class ChunkRead:
+    """One chunk of a read batch.  Plain object: offset / length ints (0, 0 = whole
+    object).  Hyper chunk (H5D_CHUNKED_REF_INDIRECT): offset and length are lists, one
+    entry per hyper chunk in C order (datanode_lib.py:857-906)."""
+
+    def __init__(self, chunk_id, key, offset=0, length=0):
+        self.chunk_id, self.key, self.offset, self.length = chunk_id, key, offset, length
+
+
+def _filter_args(filter_ops, dtype):
+    """(compressor code, shuffle, itemsize) for hsds_decode_batch from getFilterOps."""
+    if not filter_ops:
+        return nat.COMP_NONE, 0, np.dtype(dtype).itemsize
+    comp = filter_ops.get("compressor")
+    code = nat.COMP_NONE if not comp or comp == "scaleoffset" else \
+        nat.COMP_ZLIB if comp in ("gzip", "deflate", "zlib") else nat.COMP_OTHER
+    shuffle = int(filter_ops.get("shuffle") or 0)
+    if shuffle == 2:
+        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+    dt = filter_ops.get("dtype", dtype)
+    return code, shuffle, np.dtype(dt if dt is not None else dtype).itemsize
+
+
+class ChunkReader:
+    """Batched get_chunk / get_chunk_bytes for one dataset (datanode_lib.py:796-1142).
+
+    `fetch(key, offset, length)` is the storage read (storUtil.getStorBytes without
+    the codec): bytes, or None when the object does not exist."""
+
+    def __init__(self, fetch, cache=None, device=None, max_gap=1024):
+        import torch
+        from .engine import ChunkEngine
+        self.fetch = fetch
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.eng = ChunkEngine(self.device.index)
+        self.cache = cache
+        self.max_gap = int(max_gap)
+        self.stats = {"decode_calls": 0, "objects": 0, "h5_chunks": 0, "range_reads": 0, "cache_hits": 0}
+
+    # -- host side: gather every stored byte range of the batch --
+    def _plan(self, reads, dtype, chunk_dims, hyper_dims):
+        itemsize = np.dtype(dtype).itemsize
+        chunk_size = int(np.prod(chunk_dims, dtype=np.int64)) * itemsize
+        blobs, jobs = [], []          # jobs: (read index, kind, blob index, hyper index or None)
+        errors = {}
+        for ri, r in enumerate(reads):
+            if not isinstance(r.offset, list):
+                data = self.fetch(r.key, r.offset, r.length)
+                self.stats["range_reads"] += 1
+                if data is None:
+                    errors[ri] = HTTPNotFound(r.chunk_id)
+                    continue
+                if r.length and r.length > 0 and len(data) != r.length:
+                    data = bytes(r.length)      # storUtil.py:480-485 (bytearray(length), data not copied)
+                blobs.append(bytes(data))
+                jobs.append((ri, "plain", len(blobs) - 1, None))
+                continue
+            # hyper chunk (datanode_lib.py:851-906)
+            if hyper_dims is None or len(hyper_dims) != len(chunk_dims):
+                errors[ri] = ValueError(f"invalid hyper_dims: {hyper_dims}")
+                continue
+            factors = getHyperChunkFactors(chunk_dims, hyper_dims)
+            n = len(r.offset)
+            h5_size = int(np.prod(hyper_dims, dtype=np.int64)) * itemsize
+            if int(np.prod(factors)) != n or not isinstance(r.length, list) or len(r.length) != n \
+                    or n > chunk_size // h5_size:
+                errors[ri] = ValueError(f"unexpected number of hyperchunks: {n}")
+                continue
+            locs = [ChunkLocation(getHyperChunkIndex(i, factors), r.offset[i], r.length[i])
+                    for i in range(n) if r.length[i] != 0]
+            jobs.append((ri, "hyper_init", None, None))
+            for group in chunkMunge(locs, max_gap=self.max_gap):
+                group = group if isinstance(group, list) else [group]
+                lo = min(c.offset for c in group)
+                hi = max(c.offset + c.length for c in group)
+                data = self.fetch(r.key, lo, hi - lo)
+                self.stats["range_reads"] += 1
+                if not data:
+                    continue                     # storUtil.py:544-546: no data, leave the prefill
+                for c in group:
+                    o = c.offset - lo
+                    if o + c.length > len(data):     # edge chunk: zero-padded to h5_size (:559-563)
+                        piece = bytearray(h5_size)
+                        k = len(data) - o
+                        piece[:k] = data[o:o + k]
+                        piece = bytes(piece)
+                    else:
+                        piece = bytes(data[o:o + c.length])
+                    blobs.append(piece)
+                    jobs.append((ri, "h5", len(blobs) - 1, c.index))
+        return blobs, jobs, errors, chunk_size
+
+    def get_stor_bytes(self, key, chunk_locations, h5_size, filter_ops=None, offset=None, length=None):
+        """getStorBytes with chunk_locations (storUtil.py:450-522): one range read
+        [offset, offset + length) (default: the span of the locations), every location
+        decoded by one batch call; locations before `offset` and decodes whose size is
+        not h5_size are skipped, a codec failure raises HTTPInternalServerError."""
+        import torch
+        from .engine import pack_chunks
+        locs = [c if isinstance(c, ChunkLocation) else ChunkLocation(*c) for c in chunk_locations]
+        if offset is None:
+            offset = min(c.offset for c in locs)
+            length = max(c.offset + c.length for c in locs) - offset
+        data = self.fetch(key, offset, length)
+        self.stats["range_reads"] += 1
+        if data is None or len(data) == 0:
+            return data
+        if length and length > 0 and len(data) != length:
+            data = bytes(length)
+        pieces = [data[c.offset - offset:c.offset - offset + c.length] for c in locs if c.offset >= offset]
+        if not pieces:
+            return []
+        comp, shuffle, isz = _filter_args(filter_ops, (filter_ops or {}).get("dtype", np.uint8))
+        src, descs, ext = pack_chunks(pieces, [int(h5_size)] * len(pieces))
+        dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
+        status = torch.full((len(pieces),), 99, dtype=torch.int32, device=self.device)
+        self.eng.decode(torch.from_numpy(src).to(self.device), descs, dbuf, status, compressor=_comp_name(comp),
+                        shuffle=shuffle, itemsize=isz)
+        self.stats["decode_calls"] += 1
+        st = status.cpu().numpy()
+        host = dbuf.cpu().numpy()
+        out = []
+        for k in range(len(pieces)):
+            if st[k] == nat.ERR_SIZE:
+                continue                       # "expected chunk ... to have size", skipped
+            if st[k] != nat.OK:
+                raise HTTPInternalServerError()
+            o = int(descs[k]["dst_off"])
+            out.append(host[o:o + int(h5_size)].tobytes())
+        return out
+
+    def read(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
+             hyper_dims=None):
+        """Decode a batch of chunks.  Returns a list (one entry per read) of device
+        arrays (typed torch views of chunk_dims), or an exception instance:
+        HTTPNotFound (object missing), HTTPInternalServerError (codec failure or a
+        decoded size that is not the chunk size -- get_chunk's 500), ValueError (a
+        malformed hyper-chunk request)."""
+        import torch
+        from .engine import COPY_DESC_DTYPE, pack_chunks
+        dtype = np.dtype(dtype)
+        chunk_dims = tuple(int(c) for c in chunk_dims)
+        comp, shuffle, isz = _filter_args(filter_ops, dtype)
+        blobs, jobs, errors, chunk_size = self._plan(reads, dtype, chunk_dims, hyper_dims)
+        h5_size = int(np.prod(hyper_dims, dtype=np.int64)) * dtype.itemsize if hyper_dims is not None else 0
+        if layout_class == H5D_CONTIGUOUS_REF and not filter_ops:
+            # short contiguous reads near the end of the file are zero-extended (:833-844)
+            for ri, kind, bi, _ in jobs:
+                if kind == "plain" and len(blobs[bi]) < chunk_size:
+                    blobs[bi] = blobs[bi] + bytes(chunk_size - len(blobs[bi]))
+        results = [None] * len(reads)
+        for ri, e in errors.items():
+            results[ri] = e
+        # destination slots (base tensor, byte offset): cache arena, else a batch tensor
+        need = [ri for ri in range(len(reads)) if ri not in errors]
+        slots = {}
+        pinned = []
+        if self.cache is not None:
+            abase = self.cache.arena.buf
+            for ri in need:
+                cid = reads[ri].chunk_id
+                # get_chunk caches when `chunk_id in cache or memFree >= size` (:1094-1103)
+                if cid not in self.cache and self.cache.memFree < chunk_size:
+                    continue
+                v = self.cache.reserve(cid, chunk_dims, dtype, pin=True)
+                if v is not None:
+                    slots[ri] = (abase, v.data_ptr() - abase.data_ptr())
+                    pinned.append(cid)
+        rest = [ri for ri in need if ri not in slots]
+        if rest:
+            tmp = torch.empty(len(rest) * chunk_size, dtype=torch.uint8, device=self.device)
+            for k, ri in enumerate(rest):
+                slots[ri] = (tmp, k * chunk_size)
+        # prefill hyper chunks with the fill value or zeros (datanode_lib.py:884-888)
+        fill_chunk = None
+        for ri, kind, _, _ in jobs:
+            if kind != "hyper_init":
+                continue
+            base, off = slots[ri]
+            view = base[off:off + chunk_size]
+            if fill_value is None or not np.array(fill_value, dtype=dtype).reshape(1).view(np.uint8).any():
+                view.zero_()
+            else:
+                if fill_chunk is None:
+                    fill_chunk = torch.from_numpy(np.full(chunk_dims, fill_value, dtype=dtype).view(np.uint8)
+                                                  .reshape(-1).copy()).to(self.device)
+                view.copy_(fill_chunk)
+        # ONE decode batch into a contiguous buffer (plain objects and HDF5 chunks)
+        dec = [j for j in jobs if j[1] in ("plain", "h5")]
+        if dec:
+            sizes = [chunk_size if kind == "plain" else h5_size for _, kind, _, _ in dec]
+            src, descs, ext = pack_chunks([blobs[bi] for _, _, bi, _ in dec], sizes)
+            d_src = torch.from_numpy(src).to(self.device)
+            dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
+            status = torch.full((len(dec),), 99, dtype=torch.int32, device=self.device)
+            self.eng.decode(d_src, descs, dbuf, status, compressor=_comp_name(comp), shuffle=shuffle, itemsize=isz)
+            self.stats["decode_calls"] += 1
+            self.stats["objects"] += sum(1 for _, k, _, _ in dec if k == "plain")
+            self.stats["h5_chunks"] += sum(1 for _, k, _, _ in dec if k == "h5")
+            st = status.cpu().numpy()
+            # placement: ONE copy batch per destination tensor
+            groups = {}
+            for k, (ri, kind, bi, hidx) in enumerate(dec):
+                if st[k] != nat.OK:
+                    results[ri] = HTTPInternalServerError()
+                    continue
+                base, off = slots[ri]
+                so = int(descs[k]["dst_off"])
+                if kind == "plain":
+                    d = _flat_desc(so, off, chunk_size)
+                else:
+                    d = _place_desc(so, off, chunk_dims, hyper_dims, hidx, dtype.itemsize)
+                groups.setdefault(id(base), (base, []))[1].append(d)
+            for base, ds in groups.values():
+                arr = np.zeros(len(ds), COPY_DESC_DTYPE)
+                for k, d in enumerate(ds):
+                    arr[k] = d
+                self.eng.copy(dbuf, base, arr)
+        torch.cuda.synchronize(self.device)
+        for cid in pinned:
+            self.cache.unpin(cid)
+        for ri in need:
+            base, off = slots[ri]
+            if results[ri] is None:
+                results[ri] = device_view(base[off:off + chunk_size], chunk_dims, dtype)
+            elif self.cache is not None and reads[ri].chunk_id in self.cache:
+                del self.cache[reads[ri].chunk_id]     # failed reads are not cached
+        if self.cache is not None and self.cache.memUsed > self.cache.memTarget:
+            self.cache._reduce()
+        return results
+
+
+def _comp_name(code):
+    return {nat.COMP_NONE: None, nat.COMP_ZLIB: "zlib"}.get(code, "other")
+
+
+def _copy_rec():
+    return np.zeros((), dtype=[("src_off", "<u8"), ("dst_off", "<u8"), ("src_stride", "<i8", (8,)),
+                               ("dst_stride", "<i8", (8,)), ("count", "<i8", (8,)), ("rank", "<i4"),
+                               ("itemsize", "<i4")])
+
+
+def _flat_desc(src_off, dst_off, nbytes):
+    """1-d copy of nbytes (8-byte elements when the sizes and offsets allow)."""
+    d = _copy_rec()
+    w = 8 if not (nbytes | src_off | dst_off) & 7 else 4 if not (nbytes | src_off | dst_off) & 3 else 1
+    d["src_off"], d["dst_off"] = src_off, dst_off
+    d["src_stride"][0] = d["dst_stride"][0] = w
+    d["count"][0] = nbytes // w
+    d["rank"], d["itemsize"] = 1, w
+    return d
+
+
+def _place_desc(src_off, dst_off, chunk_dims, hyper_dims, hidx, itemsize):
+    """copy for `chunk_arr[hidx*hyper : (hidx+1)*hyper] = hyper_chunk` (storUtil.py:568-580)."""
+    rank = len(chunk_dims)
+    d = _copy_rec()
+    cstr = [itemsize] * rank
+    hstr = [itemsize] * rank
+    for k in range(rank - 2, -1, -1):
+        cstr[k] = cstr[k + 1] * chunk_dims[k + 1]
+        hstr[k] = hstr[k + 1] * hyper_dims[k + 1]
+    d["src_off"] = src_off
+    d["dst_off"] = dst_off + sum(int(hidx[k]) * hyper_dims[k] * cstr[k] for k in range(rank))
+    d["src_stride"][:rank] = hstr
+    d["dst_stride"][:rank] = cstr
+    d["count"][:rank] = hyper_dims
+    d["rank"] = rank
+    d["itemsize"] = itemsize
+    return d
+
+
+class ChunkStore:
+    """get_chunk for many chunks at once (datanode_lib.py:948-1142).  The returned
+    device arrays are views of HBM cache slots: valid until the next call that may
+    evict them (the DN uses a chunk right after get_chunk).  Cache hits are
+    served from HBM, the misses are read as one batch by ChunkReader and cached when
+    there is room (`chunk_id in cache or memFree >= nbytes`), duplicates in a batch
+    are read once (the reference's pending_s3_read dedupe), and a missing object
+    with chunk_init yields a fill-value (or zero) chunk of the full layout dims."""
+
+    def __init__(self, fetch, mem_target=1 << 30, device=None, max_gap=1024):
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.cache = DeviceChunkCache(mem_target, dev)
+        self.reader = ChunkReader(fetch, cache=self.cache, device=dev, max_gap=max_gap)
+
+    def get_chunks(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
+                   hyper_dims=None, chunk_init=False):
+        out = {}
+        todo, seen = [], set()
+        for r in reads:
+            if r.chunk_id in self.cache:
+                out[r.chunk_id] = self.cache[r.chunk_id]
+                self.reader.stats["cache_hits"] += 1
+            elif r.chunk_id not in seen:
+                seen.add(r.chunk_id)
+                todo.append(r)
+        if todo:
+            res = self.reader.read(todo, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
+                                   layout_class=layout_class, hyper_dims=hyper_dims)
+            for r, v in zip(todo, res):
+                if isinstance(v, HTTPNotFound) and chunk_init:
+                    arr = np.full(chunk_dims, fill_value, dtype=dtype) if fill_value is not None \
+                        else np.zeros(chunk_dims, dtype=dtype)
+                    self.cache[r.chunk_id] = arr
+                    v = self.cache[r.chunk_id]
+                elif isinstance(v, HTTPNotFound):
+                    v = None                               # 404: no chunk
+                out[r.chunk_id] = v
+        return [out[r.chunk_id] for r in reads]
