@@ -342,6 +342,74 @@ def run_cfg5(args, dev, rank=0):
     return out
 
 
+CFG4_DIMS, CFG4_LAYOUT = (131072, 131072), (512, 512)
+CFG4_SEL = (slice(0, 131072, 4), slice(0, 131072, 4))
+
+
+def run_cfg4(args, dev, rank, world):
+    """configs[3]: f32 dataset 131072 x 131072 in 1 MiB chunks (65 536 chunks), strided
+    selection [::4, ::4] (4 GiB slab), chunks sharded by getObjPartition(chunk_id,
+    world) -- HSDS's own DN rule -- over the ranks.  One step = every rank decodes its
+    chunks (one batch), packs their selected sub-blocks (one copy launch) and sends
+    them to rank 0 over RCCL (one grouped P2P call), rank 0 places every piece into the
+    slab (one copy launch).  value = decoded bytes of all ranks / max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+    from hsds_amd import crawl
+    threads = max(1, min(16, (os.cpu_count() or 1) // max(1, world)))
+    sc = max(1, args.cfg4_scale)
+    dims = tuple(d // sc for d in CFG4_DIMS)
+    sel = tuple(slice(0, d, 4) for d in dims)
+    plan = crawl.SelectionPlan("d-5a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", dims, CFG4_LAYOUT, sel,
+                               np.float32, world)
+    ids = plan.chunk_ids(rank)
+    nuniq = min(args.cfg4_unique, len(ids))
+    raw, enc = make_corpus("F1", nuniq, 20261015 + 7919 * rank, threads)
+    blobs = {cid: enc[k % nuniq] for k, cid in enumerate(ids)}
+    rd = crawl.ShardedReader(plan, rank, dev)
+    st = rd.upload(blobs)
+    gathered = torch.empty(max(plan.gathered_nbytes, 1), dtype=torch.uint8, device=dev) if rank == 0 else None
+    slab = torch.zeros(max(plan.slab_nbytes, 1), dtype=torch.uint8, device=dev) if rank == 0 else None
+    rd.read(st, slab=slab, gathered=gathered, check=True)          # warm-up (+ statuses checked)
+    torch.cuda.synchronize()
+    ok = 1
+    if rank == 0:
+        host = slab[:plan.slab_nbytes].view(torch.float32).reshape(plan.slab_shape)
+        for r in range(world):                                      # one piece per rank vs its raw chunk
+            if not plan.by_rank[r]:
+                continue
+            p = plan.pieces[plan.by_rank[r][0]]
+            if r == 0:
+                c = raw[0].view(np.float32).reshape(CFG4_LAYOUT)
+                ok &= int(np.array_equal(host[p.data_slices].cpu().numpy(), c[p.chunk_slices]))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.cfg4_steps):
+        rd.read(st, slab=slab, gathered=gathered, check=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    el /= args.cfg4_steps
+    n_all = len(plan.pieces)
+    out = {"value": round(n_all * (1 << 20) / el / 1e9, 2), "unit": "GB/s decoded (all ranks)",
+           "selected_GBps": round(plan.slab_nbytes / el / 1e9, 2), "ms_per_step": round(el * 1e3, 3),
+           "chunks": n_all, "chunks_per_rank": [len(b) for b in plan.by_rank],
+           "gathered_bytes_from_peers": int(sum(plan.rank_bytes[r] for r in range(1, world))),
+           "root_piece_check": bool(ok), "steps": args.cfg4_steps,
+           "workload": f"configs[3]: f32 {dims[0]}x{dims[1]}, 512x512 chunks (F1 L4), select [::4, ::4], "
+                       "md5-sharded decode + pack + RCCL P2P gather + place on rank 0"}
+    del st, gathered, slab
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(args, world):
     """HBM bytes per inflate launch from the committed PMC passes (tools/pmc_traffic.sh):
     2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
@@ -383,6 +451,11 @@ def main():
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
+    ap.add_argument("--cfg4", type=int, default=-1,
+                    help="configs[3] sharded decode+select+RCCL gather (default: on when N > 1)")
+    ap.add_argument("--cfg4-steps", type=int, default=3)
+    ap.add_argument("--cfg4-unique", type=int, default=256)
+    ap.add_argument("--cfg4-scale", type=int, default=1, help="divide the cfg4 dataset extents (local checks)")
     args = ap.parse_args()
 
     import torch
@@ -390,7 +463,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.distributed.init_process_group("nccl")
+        import datetime
+        torch.distributed.init_process_group("nccl", timeout=datetime.timedelta(seconds=300))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -439,6 +513,11 @@ def main():
         out["cfg3"] = run_cfg3(args, dev)
     if world == 1 and args.cfg5:
         out["cfg5"] = run_cfg5(args, dev, rank)
+    if (args.cfg4 == 1) or (args.cfg4 == -1 and world > 1):
+        try:
+            out["cfg4"] = run_cfg4(args, dev, rank, world)
+        except Exception as e:   # the headline stands even if this leg fails
+            out["cfg4"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = min(16, os.cpu_count() or 1)
         sample = r1["blobs"][:256]

@@ -139,7 +139,12 @@ def exchange(packed, plan, rank, root=0, group=None, gathered=None):
     import torch.distributed as dist
     if rank != root:
         if plan.rank_bytes[rank]:
-            dist.send(packed[:plan.rank_bytes[rank]], root, group=group)
+            if dist.get_backend(group) == "nccl":
+                for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed[:plan.rank_bytes[rank]], root,
+                                                            group=group)]):
+                    q.wait()
+            else:
+                dist.send(packed[:plan.rank_bytes[rank]], root, group=group)
         return None
     if gathered is None:
         gathered = torch.empty(plan.gathered_nbytes, dtype=torch.uint8, device=packed.device)
@@ -147,12 +152,17 @@ def exchange(packed, plan, rank, root=0, group=None, gathered=None):
     own = gathered[b0:b0 + plan.rank_bytes[root]]
     if plan.rank_bytes[root] and packed.data_ptr() != own.data_ptr():
         own.copy_(packed[:plan.rank_bytes[root]])
-    reqs = []
-    for r in range(plan.world):
-        if r == root or not plan.rank_bytes[r]:
-            continue
-        b = int(plan.rank_base[r])
-        reqs.append(dist.irecv(gathered[b:b + plan.rank_bytes[r]], r, group=group))
+    peers = [r for r in range(plan.world) if r != root and plan.rank_bytes[r]]
+    if dist.get_backend(group) == "nccl" and peers:
+        # one RCCL group call: the receives from every peer run concurrently (one
+        # xGMI link per peer) instead of one after another
+        ops = [dist.P2POp(dist.irecv, gathered[int(plan.rank_base[r]):int(plan.rank_base[r]) + plan.rank_bytes[r]],
+                          r, group=group) for r in peers]
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+        return gathered
+    reqs = [dist.irecv(gathered[int(plan.rank_base[r]):int(plan.rank_base[r]) + plan.rank_bytes[r]], r, group=group)
+            for r in peers]
     for q in reqs:
         q.wait()
     return gathered
