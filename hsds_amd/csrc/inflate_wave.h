@@ -42,7 +42,20 @@ typedef __attribute__((address_space(1))) const uint32_t hz_gcu32;
 #define LANE_VAR(T, name) T name
 #define LV(name) name
 #define LANE_LOOP for (int lane = (int)threadIdx.x, _once = 1; _once; _once = 0)
+#if defined(HZ_LIGHT_SYNC)
+// one-wavefront workgroups: the LDS executes a wave's instructions in order, so
+// cross-lane LDS hand-offs only need the compiler not to move or cache memory
+// accesses across this point (wavefront-scope acquire/release fences), not the
+// s_waitcnt vmcnt(0) lgkmcnt(0) + s_barrier of __syncthreads
+#define WAVE_SYNC()                                              \
+  do {                                                           \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       \
+    __builtin_amdgcn_wave_barrier();                             \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       \
+  } while (0)
+#else
 #define WAVE_SYNC() __syncthreads()
+#endif
 #define WAVE_SYNC_GLOBAL() \
   do { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); __syncthreads(); \
        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); } while (0)

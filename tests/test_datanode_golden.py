@@ -74,3 +74,25 @@ def test_device_cache_lru_semantics_on_cpu():
     # arena slots are reused after eviction
     c[f"x"] = np.zeros((1024,), np.float64)
     assert c.arena.used == 8 * kb
+
+
+def test_filter_ops_match_reference(rg_golden):
+    from hsds_amd.filters import getFilterOps
+    vlen = np.dtype("O", metadata={"vlen": str})
+    dts = {"<f4": np.dtype("<f4"), "vlen": vlen, "cmpd_vlen": np.dtype([("a", "<i4"), ("s", vlen)]), "none": None}
+    fdefs = rg_golden["filter_defs"]
+    assert len(rg_golden["filter_ops"]) >= 40
+    for case in rg_golden["filter_ops"]:
+        app = {"filter_map": {}}
+        dt = dts[case["dtype"]]
+        if "error" in case:
+            with pytest.raises(Exception) as ei:
+                getFilterOps(app, "d-x", [fdefs[k] for k in case["filters"]], dtype=dt, chunk_shape=(4, 5))
+            assert type(ei.value).__name__ == case["error"]
+            continue
+        ops = getFilterOps(app, "d-x", [fdefs[k] for k in case["filters"]], dtype=dt, chunk_shape=(4, 5))
+        again = getFilterOps(app, "d-x", [], dtype=dt, chunk_shape=(4, 5))
+        enc = {k: (list(v) if k == "chunk_shape" else (None if v is None else str(v)) if k == "dtype" else v)
+               for k, v in ops.items()}
+        assert enc == case["ops"], case
+        assert (again is ops) == case["cached"]
