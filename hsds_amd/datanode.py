@@ -661,3 +661,115 @@ class ChunkStore:
                     v = None                               # 404: no chunk
                 out[r.chunk_id] = v
         return [out[r.chunk_id] for r in reads]
+
+    # ---- write side (PUT_Chunk -> save_chunk -> s3sync / write_s3_obj) ------------
+    def put_selections(self, writes, dtype, chunk_dims, filter_ops=None, fill_value=None, write_zero_chunks=False):
+        """PUT_Chunk for many chunks at once (chunk_dn.py:55-314).  `writes` is a list
+        of (ChunkRead, slices, data) with data a host ndarray of the selection shape.
+        Every target chunk is fetched (get_chunk with chunk_init: missing chunks start
+        from the fill value), then ONE compare launch (chunkWriteSelection's
+        ndarray_compare, chunkUtil.py:983) and ONE conditional copy launch update the
+        chunks in HBM; changed chunks (or all with write_zero_chunks,
+        chunk_dn.py:306) are marked dirty for the next flush (save_chunk,
+        datanode_lib.py:1145-1183).  Returns one is_dirty flag per write."""
+        import torch
+        from .engine import COPY_DESC_DTYPE
+        from .selection import _contig_slices, _kind, copy_desc
+        dtype = np.dtype(dtype)
+        chunk_dims = tuple(int(c) for c in chunk_dims)
+        # requests are applied in order: writes to the same chunk go to later rounds
+        seen, first, later = set(), [], []
+        for i, w in enumerate(writes):
+            (later if w[0].chunk_id in seen else first).append(i)
+            seen.add(w[0].chunk_id)
+        if later:
+            res = dict(zip(first, self.put_selections([writes[i] for i in first], dtype, chunk_dims, filter_ops,
+                                                      fill_value, write_zero_chunks)))
+            res.update(zip(later, self.put_selections([writes[i] for i in later], dtype, chunk_dims, filter_ops,
+                                                      fill_value, write_zero_chunks)))
+            return [res[i] for i in range(len(writes))]
+        reads = [w[0] for w in writes]
+        arrs = self.get_chunks(reads, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
+                               chunk_init=True)
+        # pin the target slots while the update runs
+        for r in reads:
+            n = self.cache._lru.get(r.chunk_id)
+            if n is None:
+                raise MemoryError("chunk cache cannot hold the write batch")
+            n.pinned = True
+        try:
+            abase = self.cache.arena.buf
+            data_parts, descs, offs = [], [], 0
+            for (r, slices, data) in writes:
+                data = np.ascontiguousarray(data, dtype=dtype)
+                slot = self.cache.node_bytes(r.chunk_id)
+                slot_off = slot.data_ptr() - abase.data_ptr()
+                descs.append(copy_desc(data.shape, _contig_slices(data.shape), chunk_dims, tuple(slices),
+                                       dtype.itemsize, src_base=offs, dst_base=slot_off))
+                data_parts.append(data.view(np.uint8).reshape(-1))
+                offs += (data.nbytes + 255) // 256 * 256
+            host = np.zeros(max(offs, 1), np.uint8)
+            o = 0
+            for part in data_parts:
+                host[o:o + part.size] = part
+                o += (part.size + 255) // 256 * 256
+            d_data = torch.from_numpy(host).to(abase.device)
+            dd = np.concatenate(descs) if descs else np.zeros(0, COPY_DESC_DTYPE)
+            differs = torch.zeros(max(len(writes), 1), dtype=torch.int32, device=abase.device)
+            d_desc = self.reader.eng.compare(d_data, abase, dd, _kind(dtype), differs)
+            self.reader.eng.copy(d_data, abase, d_desc, flags=differs)
+            dirty = differs[:len(writes)].cpu().numpy().astype(bool)
+        finally:
+            for r in reads:
+                self.cache.unpin(r.chunk_id)
+        out = []
+        for (r, _, _), d in zip(writes, dirty):
+            if d or write_zero_chunks:
+                self.cache.setDirty(r.chunk_id)
+            out.append(bool(d))
+        del arrs
+        return out
+
+    def flush(self, put, filter_ops=None, keys=None):
+        """s3sync for every dirty chunk (datanode_lib.py:1186-1318, 126-311): ONE
+        hsds_encode_batch straight from the HBM cache slots (storUtil._compress's
+        F1 Blosc-zlib frames with the dataset's level and shuffle flag; no compressor
+        -> the raw bytes, putStorBytes semantics), one device-to-host copy of the
+        frames, `put(key, bytes)` per chunk, then clearDirty.  `keys` maps chunk id ->
+        storage key (default: hsds_amd.partition.getS3Key).  Returns the flushed ids."""
+        import torch
+        from .engine import encode_descs
+        from .partition import getS3Key
+        ids = [k for k in list(self.cache._lru) if self.cache.isDirty(k)]
+        if not ids:
+            return []
+        abase = self.cache.arena.buf
+        nodes = [self.cache._lru[k] for k in ids]
+        comp = (filter_ops or {}).get("compressor")
+        if comp and comp not in ("gzip", "deflate", "zlib"):
+            raise NotImplementedError(f"Blosc codec {comp!r} is outside the hsds_amd engine scope")
+        if (filter_ops or {}).get("shuffle") == 2:
+            raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+        if comp:
+            level = filter_ops.get("level", 5)
+            level = 5 if level is None else int(level)
+            descs, _, dext = encode_descs([n.nbytes for n in nodes])
+            for d, n in zip(descs, nodes):
+                d["src_off"] = n.off
+            frames = torch.empty(max(dext, 1), dtype=torch.uint8, device=abase.device)
+            sizes = torch.zeros(len(ids), dtype=torch.int64, device=abase.device)
+            status = torch.full((len(ids),), 99, dtype=torch.int32, device=abase.device)
+            self.reader.eng.encode(abase, descs, frames, sizes, status, clevel=level,
+                                   shuffle=int(filter_ops.get("shuffle") or 0), typesize=1)
+            st = status.cpu().numpy()
+            if (st != 0).any():
+                raise HTTPInternalServerError()
+            host = frames.cpu().numpy()
+            sz = sizes.cpu().numpy()
+            blobs = [host[int(d["dst_off"]):int(d["dst_off"]) + int(s)].tobytes() for d, s in zip(descs, sz)]
+        else:
+            blobs = [self.cache.node_bytes(k).cpu().numpy().tobytes() for k in ids]
+        for k, b in zip(ids, blobs):
+            put(keys[k] if keys else getS3Key(k), b)
+            self.cache.clearDirty(k)
+        return ids

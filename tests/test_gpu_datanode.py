@@ -168,3 +168,56 @@ def test_getstorbytes_chunk_locations_skip_mismatch(dev, rg):
     r = ChunkReader(lambda k, o, n: body[o - base:o - base + n].tobytes(), device=dev)
     got = r.get_stor_bytes("f", [(tuple(x[0]), x[1], x[2]) for x in locs], sb["h5_size"], _ops(sb["filter_ops"]))
     assert got == want
+
+
+def test_put_selections_and_flush(dev, oracle_lib):
+    """PUT_Chunk + s3sync, batched: chunkWriteSelection semantics (no change -> not
+    dirty, NaN always an update), missing chunks start from the fill value, the
+    flush encodes every dirty chunk in one batch from HBM, and the stored objects
+    decode (oracle: c-blosc frame walk + libz) to numpy's result of the same writes."""
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    from hsds_amd.filters import getFilterOps
+    orc = oracle_lib
+    dims = (64, 96)
+    dt = np.dtype("<f4")
+    rng = np.random.default_rng(11)
+    ops = getFilterOps({"filter_map": {}}, "d-w", [{"class": "H5Z_FILTER_SHUFFLE", "id": 2, "name": "shuffle"},
+                                                   {"class": "H5Z_FILTER_DEFLATE", "id": 1, "level": 4}],
+                       dtype=dt, chunk_shape=dims)
+    truth, store = {}, {}
+    for i in range(3):
+        a = np.round(np.cumsum(rng.normal(size=dims[0] * dims[1])), 2).astype(dt).reshape(dims)
+        truth[f"c-w_{i}_0"] = a
+        store[f"k{i}"] = orc.blosc_encode(a.tobytes(), typesize=1, clevel=4, shuffle=1)
+    keys = {f"c-w_{i}_0": f"k{i}" for i in range(5)}
+    cs = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    s1 = (slice(3, 40, 2), slice(10, 90, 7))
+    d1 = rng.normal(size=(len(range(3, 40, 2)), len(range(10, 90, 7)))).astype(dt)
+    s2 = (slice(0, 64, 1), slice(0, 96, 1))
+    s3 = (slice(5, 9, 1), slice(0, 4, 1))
+    d3 = np.full((4, 4), np.nan, dt)
+    writes = [(ChunkRead("c-w_0_0", "k0"), s1, d1),                          # changes
+              (ChunkRead("c-w_1_0", "k1"), s2, truth["c-w_1_0"].copy()),     # identical: not dirty
+              (ChunkRead("c-w_3_0", "k3"), s1, d1),                          # missing -> fill, changes
+              (ChunkRead("c-w_2_0", "k2"), s3, d3),                          # NaN: always an update
+              (ChunkRead("c-w_2_0", "k2"), s3, d3)]                          # again (next round)
+    dirty = cs.put_selections(writes, dt, dims, filter_ops=ops, fill_value=1.5)
+    assert dirty == [True, False, True, True, True]
+    want = {k: v.copy() for k, v in truth.items()}
+    want["c-w_0_0"][s1] = d1
+    want["c-w_3_0"] = np.full(dims, 1.5, dt)
+    want["c-w_3_0"][s1] = d1
+    want["c-w_2_0"][s3] = d3
+    flushed = {}
+    ids = cs.flush(lambda k, b: flushed.__setitem__(k, b), filter_ops=ops, keys=keys)
+    assert sorted(ids) == ["c-w_0_0", "c-w_2_0", "c-w_3_0"]
+    assert cs.cache.dirtyCount == 0
+    for cid in ids:
+        got = orc.uncompress(flushed[keys[cid]], "zlib", 1, 4, dims[0] * dims[1] * 4)
+        assert np.frombuffer(got, dt).reshape(dims).tobytes() == want[cid].tobytes(), cid
+    # the flushed objects read back through the GPU path
+    store.update(flushed)
+    cs2 = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in ids], dt, dims, filter_ops=ops)
+    for cid, r in zip(ids, res):
+        assert r.cpu().numpy().tobytes() == want[cid].tobytes()
