@@ -127,7 +127,7 @@ class Engine:
         except Exception:
             pass
 
-    def set_tuning(self, seg_bits=384, warmup_bits=96, cont_bits=192, rounds=4):
+    def set_tuning(self, seg_bits=288, warmup_bits=384, cont_bits=192, rounds=4):
         rc = lib().hsds_set_tuning(self.h, seg_bits, warmup_bits, cont_bits, rounds)
         if rc != OK:
             raise NativeError(rc, "hsds_set_tuning")

@@ -20,6 +20,7 @@
 // inside the batched entry points.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -903,11 +904,22 @@ int hsds_engine_create(int device, hsds_engine** out) {
   e->parse_blocks_per_cu = o1;
   e->huff_blocks_per_cu = o2;
   e->emit_blocks_per_cu = o3;
-  e->tune.L0 = 384;
-  e->tune.W = 96;
-  e->tune.adapt = 1;
+  e->tune.L0 = hz::LMAX;
+  // A/B on MI355X (tools/ab_tune.sh): warm-up 96 -> 384 bits and a fill target of
+  // 12/16 slots cut the repair rounds: F1 +8 %, F2 +21 % over (96, 11/16)
+  e->tune.W = 384;
+  e->tune.adapt = 12;
   e->tune.C = 192;
   e->tune.max_rounds = 4;
+  // development override (A/B experiments): "L0,W,adapt,C,rounds", validated like hsds_set_tuning
+  if (const char* ev = getenv("HSDS_INFLATE_TUNE")) {
+    unsigned l0, w, ad, c; int rd;
+    if (sscanf(ev, "%u,%u,%u,%u,%d", &l0, &w, &ad, &c, &rd) == 5 && l0 >= (unsigned)hz::LMIN &&
+        w <= (unsigned)hz::WMAX && c <= (unsigned)hz::CMAX && ad <= 16 && rd >= 0 && rd <= 64) {
+      e->tune.L0 = l0 < (unsigned)hz::LMAX ? l0 : (unsigned)hz::LMAX; e->tune.W = w; e->tune.adapt = ad; e->tune.C = c; e->tune.max_rounds = rd;
+      fprintf(stderr, "hsds_amd: inflate tune override %s\n", ev);
+    }
+  }
   if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
       hipEventCreate(&e->ev2) != hipSuccess || hipEventCreate(&e->ev3) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
   *out = e;

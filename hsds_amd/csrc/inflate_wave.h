@@ -121,7 +121,10 @@ constexpr int SCAP = HZ_SCAP;           // window output bytes resolved in LDS
 #ifndef HZ_CMAX
 #define HZ_CMAX 256
 #endif
-constexpr int CMAX = HZ_CMAX;           // max continuation bits into the next segment
+constexpr int CMAX = HZ_CMAX;
+#ifndef HZ_SCAP_FILL8
+#define HZ_SCAP_FILL8 7                 // adaptive L aims at this many 8ths of SCAP output bytes per window
+#endif           // max continuation bits into the next segment
 constexpr int OVR = 64;             // bitmap bits past the last token start
 constexpr int BM_WORDS = (LMAX + CMAX + OVR) / 32 + 1;
 // staged input dwords: window (64 L) + warm-up (<= L) + alignment + overrun/peek
@@ -811,7 +814,9 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       if (stats) stats->windows++;
       HZ_T(4);
       const uint32_t win_start = pos;
-      const uint32_t W = tune.W, C = tune.C;
+      // a continuation never runs past its successor's segment: phase B counts a
+      // lane's valid tokens from the point where its predecessor met its marks
+      const uint32_t W = tune.W, C = tune.C < L ? tune.C : L;
       {
         const uint32_t first_bit = win_start >= W ? win_start - W : 0u;
         const uint32_t words = (64u * L + W + C + 256u) / 32u + 3u;
@@ -1316,7 +1321,7 @@ HZ_UNROLL
         const uint32_t fill16 = tune.adapt > 1u ? tune.adapt : ADAPT_FILL16;   // of SLOTS, /16
         uint32_t target = (bpt16 * (uint32_t)SLOTS * fill16) / (16u * 16u);   // bpt16: bits per slot
         if (wtotal && used) {
-          const uint64_t lim = ((uint64_t)SCAP * 3u / 4u) * used / ((uint64_t)wtotal * 64u);
+          const uint64_t lim = ((uint64_t)SCAP * HZ_SCAP_FILL8 / 8u) * used / ((uint64_t)wtotal * 64u);
           if (lim < target) target = (uint32_t)lim;
         }
         L = target < (uint32_t)LMIN ? (uint32_t)LMIN : target > (uint32_t)LMAX ? (uint32_t)LMAX : target;
