@@ -44,6 +44,12 @@ def make_corpus(fmt, n_unique, base_seed, threads):
         raw = list(ex.map(lambda i: smooth_chunk(base_seed + i).view(np.uint8), range(n_unique)))
     if fmt == "F1":
         blobs = orc.encode_batch(raw, op="blosc", typesize=1, clevel=4, shuffle=1, nthreads=threads)
+    elif fmt == "LZ4":
+        # Blosc-lz4 frames as _compress(compressor="lz4", level=5) lays them out
+        # (typesize 1, 128 KiB blocks); the payload is the oracle's greedy LZ4 writer
+        with ThreadPoolExecutor(threads) as ex:
+            blobs = [np.frombuffer(b, np.uint8) for b in
+                     ex.map(lambda r: orc.blosc_encode_lz4(r, typesize=1, blocksize=131072, shuffle=1), raw)]
     else:
         shuf = [np.frombuffer(orc.shuffle(r, 4), np.uint8) for r in raw]
         blobs = orc.encode_batch(shuf, op="zlib", clevel=4, nthreads=threads)
@@ -68,8 +74,10 @@ def run_format(fmt, args, dev, rank, world):
     d_desc = to_device_bytes(descs, dev)
     stream = torch.cuda.current_stream()
 
+    comp = "lz4" if fmt == "LZ4" else "zlib"
+
     def step():
-        eng.decode(d_src, d_desc, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4, stream=stream)
+        eng.decode(d_src, d_desc, d_dst, d_st, compressor=comp, shuffle=1, itemsize=4, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -422,16 +430,16 @@ def load_traffic(args, world):
     return t
 
 
-def cpu_baseline(blobs, seconds, threads):
-    """Oracle decode (c-blosc frame walk + libz, same as the reference path) on the
-    box's host cores, bounded to about `seconds` of wall time."""
+def cpu_baseline(blobs, seconds, threads, compressor="zlib"):
+    """Oracle decode (c-blosc frame walk + libz / LZ4, same as the reference path) on
+    the box's host cores, bounded to about `seconds` of wall time."""
     from oracle import oracle as orc
     exp = [CHUNK_BYTES] * len(blobs)
     out = [np.empty(CHUNK_BYTES, np.uint8) for _ in blobs]
     done = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        _, status = orc.uncompress_batch(blobs, exp, "zlib", 1, 4, nthreads=threads, out=out)
+        _, status = orc.uncompress_batch(blobs, exp, compressor, 1, 4, nthreads=threads, out=out)
         assert (status == CHUNK_BYTES).all()
         done += len(blobs)
     el = time.perf_counter() - t0
@@ -450,6 +458,7 @@ def main():
     ap.add_argument("--kernel-timing", type=int, default=0)
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
+    ap.add_argument("--lz4", type=int, default=1, help="also measure Blosc-lz4 1 MiB chunks (N=1)")
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
     ap.add_argument("--cfg4", type=int, default=-1,
                     help="configs[3] sharded decode+select+RCCL gather (default: on when N > 1)")
@@ -507,6 +516,19 @@ def main():
         v2 = r2["dec_bytes"] * world * args.steps / r2["elapsed_s"] / 1e9
         out["f2"] = {"value": round(v2, 2), "unit": "GB/s", "format": "HDF5 chunk: zlib L4 of byte-shuffled f32",
                      "compressed_bytes_per_gpu": r2["comp_bytes"], "inflate_kernel_ms": round(r2["kernel_ms"], 3)}
+    if world == 1 and args.lz4:
+        r3 = run_format("LZ4", args, dev, rank, world)
+        v3 = r3["dec_bytes"] * args.steps / r3["elapsed_s"] / 1e9
+        out["lz4"] = {"value": round(v3, 2), "unit": "GB/s", "format": "Blosc-lz4 frames (typesize 1, 128 KiB blocks)",
+                      "compressed_bytes_per_gpu": r3["comp_bytes"], "lz_kernel_ms": round(r3["kernel_ms"], 3),
+                      "algorithmic_GBps": round((r3["comp_bytes"] + r3["dec_bytes"]) / (r3["kernel_ms"] / 1e3) / 1e9, 2)}
+        if args.cpu_seconds > 0:
+            threads = min(16, os.cpu_count() or 1)
+            v, n = cpu_baseline(r3["blobs"][:256], min(args.cpu_seconds, 4.0), threads, compressor="lz4")
+            out["lz4"]["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+                                          "sample": f"{n} x 1 MiB Blosc-lz4 chunk decodes, oracle frame walk + LZ4, "
+                                                    f"{threads} threads"}
+        del r3
     if world == 1 and args.e2e:
         out["e2e_pcie"] = run_e2e(r1, args, dev)
     if world == 1 and args.cfg3:

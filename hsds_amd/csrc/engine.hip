@@ -7,6 +7,7 @@
 //   scan_kernel         exclusive scan of items per chunk (single workgroup)
 //   inflate_kernel      persistent waves pull stream items from a device counter;
 //                       one wavefront decodes one zlib stream (inflate_wave.h)
+//   lz_kernel           the same for LZ4 / BloscLZ Blosc splits (lz_wave.h)
 //   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
 //   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
 //                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
@@ -27,6 +28,7 @@
 #include "../../include/hsds_amd.h"
 #include "inflate_wave.h"
 #include "deflate_wave.h"
+#include "lz_wave.h"
 
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -35,8 +37,10 @@ namespace {
 constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
 constexpr int INFLATE_WAVES_PER_CU = 8;   // LDS-bound: sizeof(hz::Shared) <= 20 KiB
 static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
+static_assert(sizeof(lz::Shared) <= sizeof(hz::Shared), "the LZ decoder reuses the inflate LDS block");
 
-enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_INEXACT = 0x100 };
+// ITEM_LZ4 / ITEM_BLOSCLZ: Blosc splits of the byte-LZ77 codecs (lz_wave.h)
+enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_INEXACT = 0x100 };
 
 struct Item {          // 32 bytes
   uint64_t src;
@@ -70,8 +74,8 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
                                   int64_t nchunks, uint8_t* dst_base, uint8_t* tmp_base, Item* __restrict__ slots,
                                   uint32_t* __restrict__ counts, ChunkMeta* __restrict__ meta,
                                   uint32_t* __restrict__ meta_list, uint32_t* __restrict__ meta_count,
-                                  int32_t* __restrict__ status, int compressor, int shuffle, int itemsize,
-                                  int inexact) {
+                                  uint32_t* __restrict__ kind_counts, int32_t* __restrict__ status,
+                                  int compressor, int shuffle, int itemsize, int inexact) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
   const hsds_chunk_desc c = chunks[ci];
@@ -104,13 +108,15 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
     if (L < 16) st = HSDS_ERR_FRAME;
     else {
       const uint32_t ver = rd8(s), verlz = rd8(s + 1), flags = rd8(s + 2), ts = rd8(s + 3);
+      const uint32_t codec = (flags >> 5) & 7;   // 0 blosclz, 1 lz4/lz4hc, 2 snappy, 3 zlib, 4 zstd
+      const uint32_t kind = codec == 3 ? ITEM_ZLIB : codec == 1 ? ITEM_LZ4 : ITEM_BLOSCLZ;
       const uint64_t nbytes = rd32le(s + 4), bs = rd32le(s + 8), cbytes = rd32le(s + 12);
       if (ver != 2 || cbytes > L || cbytes < 16) st = HSDS_ERR_FRAME;
       else if (nbytes != n) st = HSDS_ERR_SIZE;
       else if (flags & 0x02) {
         if (nbytes + 16 > cbytes) st = HSDS_ERR_FRAME;
         else emit(ITEM_RAW, s + 16, nbytes, out, nbytes);
-      } else if (((flags >> 5) & 7) != 3) st = HSDS_ERR_UNSUPPORTED;
+      } else if (codec != 3 && codec != 1 && codec != 0) st = HSDS_ERR_UNSUPPORTED;   // zstd, snappy
       else if (verlz != 1) st = HSDS_ERR_FRAME;
       else if (flags & 0x04) st = HSDS_ERR_UNSUPPORTED;
       else if (nbytes > 0) {
@@ -133,7 +139,7 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
               const int64_t cs = (int32_t)rd32le(s + p);
               p += 4;
               if (cs < 0 || p + cs > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
-              emit((uint64_t)cs == neblock ? ITEM_RAW : ITEM_ZLIB, s + p, (uint64_t)cs,
+              emit((uint64_t)cs == neblock ? ITEM_RAW : kind, s + p, (uint64_t)cs,
                    target + b * bs + j * neblock, neblock);
               if (st != HSDS_OK) break;
               p += cs;
@@ -153,6 +159,12 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
     st = HSDS_ERR_UNSUPPORTED;
   }
   if (st != HSDS_OK) { cnt = 0; m.mode = 0; }
+  // items per decoder (kind_counts[0]: LZ splits for lz_kernel, [1]: the rest for
+  // inflate_kernel), so that a kernel with nothing to do exits at once
+  uint32_t nlz = 0;
+  for (uint32_t k = 0; k < cnt; k++) nlz += (slot[k].kind & 0xff) == ITEM_LZ4 || (slot[k].kind & 0xff) == ITEM_BLOSCLZ;
+  if (nlz) atomicAdd(&kind_counts[0], nlz);
+  if (cnt - nlz) atomicAdd(&kind_counts[1], cnt - nlz);
   counts[ci] = cnt;
   status[ci] = st;
   meta[ci] = m;
@@ -194,8 +206,9 @@ __global__ void scan_kernel(const uint32_t* __restrict__ counts, uint32_t* __res
 __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
                                                      int64_t nchunks, uint32_t* __restrict__ counter,
                                                      int32_t* __restrict__ status, uint32_t* __restrict__ sizes,
-                                                     hz::Tune tune) {
+                                                     const uint32_t* __restrict__ kind_counts, hz::Tune tune) {
   __shared__ hz::Shared sh;
+  if (kind_counts[1] == 0) return;   // only LZ splits in this batch (lz_kernel)
   const uint32_t total = offs[nchunks];
   const int lane = threadIdx.x;
 #ifdef HZ_PROFILE
@@ -225,6 +238,8 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
       uint8_t* dp = (uint8_t*)it.dst;
       for (uint32_t i = lane; i < it.dst_len; i += 64) dp[i] = sp[i];
       st = HSDS_OK;
+    } else if ((it.kind & 0xff) == ITEM_LZ4 || (it.kind & 0xff) == ITEM_BLOSCLZ) {
+      continue;                        // lz_kernel's item
     } else {
       hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
                            (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr};
@@ -241,6 +256,38 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
   }
 #endif
   (void)prof;
+}
+
+// -------------------------------------------------------------------------
+// LZ4 / BloscLZ splits (lz_wave.h): persistent 64-thread workgroups over the same
+// item table as inflate_kernel, taking only the LZ items (own counter).
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
+                                                int64_t nchunks, uint32_t* __restrict__ counter,
+                                                int32_t* __restrict__ status,
+                                                const uint32_t* __restrict__ kind_counts) {
+  __shared__ lz::Shared ls;
+  if (kind_counts[0] == 0) return;
+  const uint32_t total = offs[nchunks];
+  const int lane = threadIdx.x;
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(counter, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= total) break;
+    int64_t lo = 0, hi = nchunks - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const Item it = slots[lo * KSLOTS + (item - offs[lo])];
+    const uint32_t kind = it.kind & 0xff;
+    if (kind != ITEM_LZ4 && kind != ITEM_BLOSCLZ) continue;
+    hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len, 1u, nullptr};
+    const int st = lz::lz_stream(ls, job, kind == ITEM_LZ4 ? lz::FMT_LZ4 : lz::FMT_BLOSCLZ);
+    if (lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
+    __syncthreads();
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -826,6 +873,7 @@ struct hsds_engine {
   int device;
   int num_cus;
   int inflate_blocks_per_cu;   // occupancy of inflate_kernel (LDS-bound)
+  int lz_blocks_per_cu;        // occupancy of lz_kernel
   hz::Tune tune;
   // workspace (grown on demand)
   uint8_t* ws = nullptr;
@@ -897,6 +945,9 @@ int hsds_engine_create(int device, hsds_engine** out) {
     if (v >= 1 && v < occ) occ = v;
   }
   e->inflate_blocks_per_cu = occ;
+  int olz = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olz, lz_kernel, 64, 0) != hipSuccess || olz < 1) olz = 8;
+  e->lz_blocks_per_cu = olz;
   int o1 = 0, o2 = 0, o3 = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, parse_kernel, 64, 0) != hipSuccess || o1 < 1) o1 = 2;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, huff_kernel, 64, 0) != hipSuccess || o2 < 1) o2 = 4;
@@ -976,23 +1027,30 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   uint32_t* offs = (uint32_t*)w; w += sz_offs;
   ChunkMeta* meta = (ChunkMeta*)w; w += sz_meta;
   uint32_t* list = (uint32_t*)w; w += sz_list;
-  uint32_t* ctr = (uint32_t*)w;   // [0] inflate item counter, [1] meta list count, [2] inexact size
+  // [0] inflate item counter, [1] meta list count, [2] inexact size, [3] LZ item counter,
+  // [4] LZ items, [5] other items
+  uint32_t* ctr = (uint32_t*)w;
   // staging for shuffled outputs (F2 chunks, Blosc typesize > 1): same offsets as
   // the destination buffer, so it spans the destination extent
   if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
-  if (hipMemsetAsync(ctr, 0, 16, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
   hipLaunchKernelGGL(frame_walk_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
-                     (uint8_t*)d_dst, e->tmp, slots, counts, meta, list, ctr + 1, d_status, compressor, shuffle,
-                     itemsize, inexact);
+                     (uint8_t*)d_dst, e->tmp, slots, counts, meta, list, ctr + 1, ctr + 4, d_status, compressor,
+                     shuffle, itemsize, inexact);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
   int64_t grid = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
   if (grid > nchunks * 4) grid = nchunks * 4;
   if (grid < 1) grid = 1;
   hipEventRecord(e->ev0, st);
   hipLaunchKernelGGL(inflate_kernel, dim3((unsigned)grid), dim3(64), 0, st, slots, offs, nchunks, ctr, d_status,
-                     ctr + 2, e->tune);
+                     ctr + 2, ctr + 4, e->tune);
+  int64_t lgrid = (int64_t)e->num_cus * e->lz_blocks_per_cu;
+  if (lgrid > nchunks * 16) lgrid = nchunks * 16;
+  if (lgrid < 1) lgrid = 1;
+  hipLaunchKernelGGL(lz_kernel, dim3((unsigned)lgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 3, d_status,
+                     ctr + 4);
   hipEventRecord(e->ev1, st);
   e->ev_valid = 1;
   hipLaunchKernelGGL(unshuffle_kernel, dim3(2048), dim3(256), 0, st, meta, list, ctr + 1, d_status);
@@ -1187,7 +1245,7 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
   // token slots: SEG_TOK per segment
   if (grow((void**)&e->escr, &e->escr_bytes, (size_t)seg_cap * hd::SEG_TOK * 2 + 256)) return HSDS_ERR_DEVICE;
   uint16_t* tok = (uint16_t*)e->escr;
-  if (hipMemsetAsync(ctr, 0, 16, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
   hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, slots,

@@ -16,6 +16,10 @@
  *     tests/golden/make_golden.py probes).
  *   - zlib inflate/deflate: the reference calls CPython zlib 1.2.11 and c-blosc's
  *     zlib_wrap_{compress,decompress}; this file calls the same system libz 1.2.11.
+ *   - the other Blosc inner codecs the reference writes with cname = the dataset's
+ *     compressor (storUtil.py:255-262): LZ4 block decode (lz4 1.9.x) and BloscLZ
+ *     (c-blosc 1.21), restated from their published formats (orc_lz4_decode,
+ *     orc_blosclz_decode).  zstd and snappy stay unsupported.
  *
  * Parity pinning: tests/test_oracle_golden.py checks every function here against the
  * golden vectors in tests/golden/ that were produced by the reference's own
@@ -92,6 +96,96 @@ int64_t orc_zlib_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64_
   return ORC_ERR_SIZE;
 }
 
+/* ---- LZ4 block decode (lz4 1.9.x LZ4_decompress_safe, third-party: the lz4 that
+ * c-blosc 1.21 vendors and calls from lz4_wrap_decompress for codec 1, "lz4" and
+ * "lz4hc").  Restated from the published block format: token (literal length high
+ * nibble, match length - 4 low nibble, 15 = extended by bytes until one != 255),
+ * literals, 16-bit little-endian offset, extended match length.  End-of-block rules of
+ * the safe decoder: a literal run reaching oend - MFLIMIT(12) or iend - 8 must be the
+ * last sequence and end exactly at iend; a match must end at least LASTLITERALS(5)
+ * bytes before oend; offset 0 or an offset before the output start is corrupt.
+ * Pinned by tests/golden/codec2_cases (frames written by libblosc 1.21.0's lz4).
+ * Returns the decoded length or a negative status. */
+int64_t orc_lz4_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  for (;;) {
+    if (ip >= srclen) return ORC_ERR_TRUNC;
+    unsigned t = src[ip++];
+    int64_t lit = t >> 4;
+    if (lit == 15) {
+      unsigned b;
+      do { if (ip >= srclen) return ORC_ERR_TRUNC; b = src[ip++]; lit += b; } while (b == 255);
+    }
+    if (lit > srclen - ip) return ORC_ERR_TRUNC;
+    if (lit > cap - op) return ORC_ERR_SIZE;
+    memcpy(dst + op, src + ip, (size_t)lit);
+    ip += lit;
+    op += lit;
+    if (op + 12 > cap || ip + 8 > srclen) {
+      if (ip != srclen) return ORC_ERR_DATA;
+      return op;
+    }
+    if (ip + 1 >= srclen) return ORC_ERR_TRUNC;
+    int64_t off = src[ip] | (src[ip + 1] << 8);
+    ip += 2;
+    int64_t ml = t & 15;
+    if (ml == 15) {
+      unsigned b;
+      do { if (ip >= srclen) return ORC_ERR_TRUNC; b = src[ip++]; ml += b; } while (b == 255);
+    }
+    ml += 4;
+    if (off == 0 || off > op) return ORC_ERR_DATA;
+    if (op + ml + 5 > cap) return ORC_ERR_DATA;
+    for (int64_t k = 0; k < ml; k++) dst[op + k] = dst[op + k - off];   /* overlapping copy */
+    op += ml;
+  }
+}
+
+/* ---- BloscLZ decode (c-blosc 1.21 blosclz_decompress, third-party, in-tree in
+ * c-blosc).  Control byte c (the first one masked to 5 bits): c < 32 -> c + 1 literal
+ * bytes; else a match of (c >> 5) + 2 bytes (c >> 5 == 7: plus extension bytes until
+ * one != 255), distance ((c & 31) << 8) + next byte + 1, or, when that byte is 255 and
+ * c & 31 == 31, 8192 + a 16-bit big-endian distance.  The stream ends when the input
+ * is exhausted after an item.  Pinned by tests/golden/codec2_cases (libblosc 1.21.0). */
+int64_t orc_blosclz_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  if (srclen <= 0) return ORC_ERR_TRUNC;
+  unsigned c = src[ip++] & 31u;
+  for (;;) {
+    if (c >= 32) {
+      int64_t len = (c >> 5) - 1;
+      int64_t dist = (int64_t)(c & 31u) << 8;
+      unsigned code;
+      if (len == 6) {
+        do { if (ip >= srclen) return ORC_ERR_TRUNC; code = src[ip++]; len += code; } while (code == 255);
+      }
+      if (ip >= srclen) return ORC_ERR_TRUNC;
+      code = src[ip++];
+      len += 3;
+      if (code == 255 && dist == (31 << 8)) {
+        if (ip + 1 >= srclen) return ORC_ERR_TRUNC;
+        dist = ((int64_t)src[ip] << 8 | src[ip + 1]) + 8192;
+        ip += 2;
+      } else {
+        dist += code + 1;
+      }
+      if (len > cap - op) return ORC_ERR_SIZE;
+      if (dist > op) return ORC_ERR_DATA;
+      for (int64_t k = 0; k < len; k++) dst[op + k] = dst[op + k - dist];
+      op += len;
+    } else {
+      int64_t n = (int64_t)c + 1;
+      if (n > cap - op) return ORC_ERR_SIZE;
+      if (n > srclen - ip) return ORC_ERR_TRUNC;
+      memcpy(dst + op, src + ip, (size_t)n);
+      op += n;
+      ip += n;
+    }
+    if (ip >= srclen) return op;
+    c = src[ip++];
+  }
+}
+
 /* ---- Blosc1 frame decode (c-blosc 1.21 blosc_decompress semantics) --------- */
 
 int orc_is_blosc(const uint8_t *src, int64_t srclen) {
@@ -123,8 +217,8 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
     memcpy(dst, src + 16, (size_t)nbytes);
     return nbytes;
   }
-  int codec = (flags >> 5) & 7;
-  if (codec != 3) return ORC_ERR_UNSUPPORTED; /* only the zlib inner codec */
+  int codec = (flags >> 5) & 7;   /* 0 blosclz, 1 lz4/lz4hc, 3 zlib; 2 snappy, 4 zstd unsupported */
+  if (codec != 3 && codec != 1 && codec != 0) return ORC_ERR_UNSUPPORTED;
   if (verlz != 1) return ORC_ERR_FRAME;
   if (flags & 0x04) return ORC_ERR_UNSUPPORTED; /* bitshuffle inside Blosc */
   if (nbytes == 0) return 0;
@@ -152,7 +246,9 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
       if (cs == neblock) {
         memcpy(out + j * neblock, src + p, (size_t)neblock);
       } else {
-        int64_t r = orc_zlib_decode(src + p, cs, out + j * neblock, neblock);
+        int64_t r = codec == 3 ? orc_zlib_decode(src + p, cs, out + j * neblock, neblock)
+                  : codec == 1 ? orc_lz4_decode(src + p, cs, out + j * neblock, neblock)
+                               : orc_blosclz_decode(src + p, cs, out + j * neblock, neblock);
         if (r < 0) { result = r == ORC_ERR_SIZE ? ORC_ERR_SIZE : r; goto done; }
         if (r != neblock) { result = ORC_ERR_SIZE; goto done; }
       }
@@ -241,15 +337,57 @@ int64_t orc_blosc_blocksize(int clevel, int ts, int64_t nbytes) {
   return bs;
 }
 
-int64_t orc_blosc_encode_zlib(const uint8_t *src, int64_t nbytes, int ts, int clevel,
-                              int doshuffle_flag, uint8_t *dst, int64_t dstcap) {
+/* Greedy LZ4 block writer (4-byte hash, distance <= 65535) obeying the block end
+ * rules LZ4_decompress_safe checks: the last match starts at least MFLIMIT (12) bytes
+ * before the end and ends at least LASTLITERALS (5) bytes before it.  Corpus writer
+ * only: parity is judged on decoding, and any valid block decodes identically.
+ * Returns the block size, or ORC_ERR_SIZE when it would exceed cap. */
+int64_t orc_lz4_encode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+  enum { HB = 14 };
+  int32_t *ht = (int32_t *)calloc((size_t)1 << HB, sizeof(int32_t));
+  int64_t ip = 0, anchor = 0, op = 0;
+#define PUT(b) do { if (op >= cap) { free(ht); return ORC_ERR_SIZE; } dst[op++] = (uint8_t)(b); } while (0)
+#define PUTLEN(v) do { int64_t _v = (v); while (_v >= 255) { PUT(255); _v -= 255; } PUT(_v); } while (0)
+  while (n >= 13 && ip < n - 12) {
+    uint32_t seq = rd32(src + ip);
+    uint32_t h = (seq * 2654435761u) >> (32 - HB);
+    int64_t ref = (int64_t)ht[h] - 1;
+    ht[h] = (int32_t)(ip + 1);
+    if (ref < 0 || ip - ref > 65535 || rd32(src + ref) != seq) { ip++; continue; }
+    int64_t ml = 4;
+    while (ip + ml < n - 5 && src[ref + ml] == src[ip + ml]) ml++;
+    int64_t lit = ip - anchor;
+    PUT(((lit < 15 ? lit : 15) << 4) | (ml - 4 < 15 ? ml - 4 : 15));
+    if (lit >= 15) PUTLEN(lit - 15);
+    if (op + lit > cap) { free(ht); return ORC_ERR_SIZE; }
+    memcpy(dst + op, src + anchor, (size_t)lit);
+    op += lit;
+    PUT((ip - ref) & 0xff);
+    PUT((ip - ref) >> 8);
+    if (ml - 4 >= 15) PUTLEN(ml - 4 - 15);
+    ip += ml;
+    anchor = ip;
+  }
+  int64_t lit = n - anchor;
+  PUT((lit < 15 ? lit : 15) << 4);
+  if (lit >= 15) PUTLEN(lit - 15);
+  if (op + lit > cap) { free(ht); return ORC_ERR_SIZE; }
+  memcpy(dst + op, src + anchor, (size_t)lit);
+  op += lit;
+#undef PUT
+#undef PUTLEN
+  free(ht);
+  return op;
+}
+
+static int64_t blosc_encode(int codec, const uint8_t *src, int64_t nbytes, int ts, int clevel, int64_t bs,
+                            int doshuffle_flag, uint8_t *dst, int64_t dstcap) {
   if (ts < 1) ts = 1;
   if (ts > 255) ts = 1; /* c-blosc: typesize > BLOSC_MAX_TYPESIZE -> 1 */
   if (dstcap < nbytes + 16) return ORC_ERR_ARG;
   int64_t maxbytes = nbytes + 16;
-  int flags = (3 << 5); /* zlib format code */
+  int flags = codec << 5;
   if (doshuffle_flag) flags |= 0x01;
-  int64_t bs = orc_blosc_blocksize(clevel, ts, nbytes);
   if (!split_ok(ts, bs)) flags |= 0x10;
   int memcpyed = (nbytes < 128) || clevel == 0;
   int64_t nblocks = bs > 0 ? (nbytes + bs - 1) / bs : 0;
@@ -277,10 +415,14 @@ int64_t orc_blosc_encode_zlib(const uint8_t *src, int64_t nbytes, int ts, int cl
           maxout = maxbytes - ntbytes;
           if (maxout <= 0) { ntbytes = 0; break; }
         }
-        uLongf cl = (uLongf)maxout;
         int64_t cb = 0;
-        if (compress2(dst + ntbytes, &cl, blk + j * neblock, (uLong)neblock, clevel) == Z_OK)
-          cb = (int64_t)cl;
+        if (codec == 3) {
+          uLongf cl = (uLongf)maxout;
+          if (compress2(dst + ntbytes, &cl, blk + j * neblock, (uLong)neblock, clevel) == Z_OK) cb = (int64_t)cl;
+        } else {
+          cb = orc_lz4_encode(blk + j * neblock, neblock, dst + ntbytes, maxout);
+          if (cb < 0 || cb >= neblock) cb = 0;
+        }
         if (cb == 0 || cb == neblock) {
           if (ntbytes + neblock > maxbytes) { ntbytes = 0; break; }
           memcpy(dst + ntbytes, blk + j * neblock, (size_t)neblock);
@@ -301,6 +443,24 @@ int64_t orc_blosc_encode_zlib(const uint8_t *src, int64_t nbytes, int ts, int cl
   dst[2] = (uint8_t)flags;
   wr32(dst + 12, (uint32_t)ntbytes);
   return ntbytes;
+}
+
+
+int64_t orc_blosc_encode_zlib(const uint8_t *src, int64_t nbytes, int ts, int clevel,
+                              int doshuffle_flag, uint8_t *dst, int64_t dstcap) {
+  if (ts < 1 || ts > 255) ts = 1;
+  return blosc_encode(3, src, nbytes, ts, clevel, orc_blosc_blocksize(clevel, ts, nbytes), doshuffle_flag,
+                      dst, dstcap);
+}
+
+/* Blosc1 frame with LZ4 splits (codec 1) at an explicit blocksize: the corpus writer for
+ * lz4 tests and the bench (its payload bytes differ from lz4's own compressor; every
+ * valid LZ4 block decodes the same way, and the frame layout follows c-blosc 1.21). */
+int64_t orc_blosc_encode_lz4(const uint8_t *src, int64_t nbytes, int ts, int64_t bs, int doshuffle_flag,
+                             uint8_t *dst, int64_t dstcap) {
+  if (ts < 1 || ts > 255) ts = 1;
+  if (bs <= 0 || bs > nbytes) bs = nbytes;
+  return blosc_encode(1, src, nbytes, ts, 5, bs, doshuffle_flag, dst, dstcap);
 }
 
 /* zlib.compress(data, level) equivalent (the F2 stream producer for fixtures) */

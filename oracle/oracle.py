@@ -42,6 +42,10 @@ def lib():
         P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.orc_zlib_decode.argtypes = [P, I64, P, I64]
         L.orc_zlib_decode.restype = I64
+        L.orc_lz4_decode.argtypes = [P, I64, P, I64]
+        L.orc_lz4_decode.restype = I64
+        L.orc_blosclz_decode.argtypes = [P, I64, P, I64]
+        L.orc_blosclz_decode.restype = I64
         L.orc_blosc_decode.argtypes = [P, I64, P, I64]
         L.orc_blosc_decode.restype = I64
         L.orc_is_blosc.argtypes = [P, I64]
@@ -50,6 +54,10 @@ def lib():
         L.orc_uncompress.restype = I64
         L.orc_blosc_encode_zlib.argtypes = [P, I64, I, I, I, P, I64]
         L.orc_blosc_encode_zlib.restype = I64
+        L.orc_blosc_encode_lz4.argtypes = [P, I64, I, I64, I, P, I64]
+        L.orc_blosc_encode_lz4.restype = I64
+        L.orc_lz4_encode.argtypes = [P, I64, P, I64]
+        L.orc_lz4_encode.restype = I64
         L.orc_blosc_blocksize.argtypes = [I, I, I64]
         L.orc_blosc_blocksize.restype = I64
         L.orc_zlib_encode.argtypes = [P, I64, I, P, I64]
@@ -84,6 +92,26 @@ def zlib_decode(data, cap):
     return n if n < 0 else out[:n].tobytes()
 
 
+def _split_decode(fn, data, n):
+    """one Blosc split: exactly n bytes (c-blosc rejects any other size) or a status"""
+    s = _u8(data)
+    if s.size == 0:
+        s = np.zeros(1, np.uint8)[:0]
+    out = np.empty(max(n, 1), np.uint8)
+    r = fn(s.ctypes.data, len(data), out.ctypes.data, n)
+    if r < 0:
+        return r
+    return out[:n].tobytes() if r == n else ERR_SIZE
+
+
+def lz4_decode(data, n):
+    return _split_decode(lib().orc_lz4_decode, data, n)
+
+
+def blosclz_decode(data, n):
+    return _split_decode(lib().orc_blosclz_decode, data, n)
+
+
 def blosc_decode(data, cap):
     s = _u8(data)
     out = np.empty(max(cap, 1), np.uint8)
@@ -115,6 +143,25 @@ def blosc_encode(data, typesize=1, clevel=5, shuffle=1):
                                     out.ctypes.data, out.size)
     if n < 0:
         raise RuntimeError(f"blosc encode error {n}")
+    return out[:n].tobytes()
+
+
+def blosc_encode_lz4(data, typesize=1, blocksize=131072, shuffle=1):
+    """Blosc1 frame with LZ4 splits (corpus writer for lz4 tests and the bench)."""
+    s = _u8(data)
+    out = np.empty(s.size + 16, np.uint8)
+    n = lib().orc_blosc_encode_lz4(s.ctypes.data, s.size, typesize, blocksize, shuffle, out.ctypes.data, out.size)
+    if n < 0:
+        raise RuntimeError(f"blosc lz4 encode error {n}")
+    return out[:n].tobytes()
+
+
+def lz4_encode(data):
+    s = _u8(data)
+    out = np.empty(s.size + s.size // 255 + 64, np.uint8)
+    n = lib().orc_lz4_encode(s.ctypes.data, s.size, out.ctypes.data, out.size)
+    if n < 0:
+        raise RuntimeError(f"lz4 encode error {n}")
     return out[:n].tobytes()
 
 

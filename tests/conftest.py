@@ -22,6 +22,16 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden2():
+    """lz4 / lz4hc / blosclz / zstd Blosc objects (tests/golden/make_codec2_golden.py)"""
+    import json
+    import numpy as np
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "codec2_cases.json")))
+    arrs = np.load(os.path.join(ROOT, "tests", "golden", "codec2_cases.npz"))
+    return d, arrs
+
+
+@pytest.fixture(scope="session")
 def selection_golden():
     import json
     return json.load(open(os.path.join(ROOT, "tests", "golden", "selection_cases.json")))

@@ -160,3 +160,96 @@ def test_error_statuses(oracle_lib, torch_dev):
             assert st[k] == 0, (k, st[k])
             o = int(descs[k]["dst_off"])
             assert out[o:o + sizes[k]].tobytes() == ref
+
+
+def test_other_blosc_codecs_match_reference_goldens(golden2, torch_dev):
+    """lz4 / lz4hc / blosclz objects of the reference (codec2 goldens) through _uncompress
+    on the GPU: every byte and every error; zstd raises NotImplementedError (outside the
+    engine); a truncated object is rejected (the reference reads past its end)."""
+    from hsds_amd import codec
+    meta, arrs = golden2
+    checked = 0
+    for c in meta["cases"]:
+        blob = arrs[c["name"] + "__in"].tobytes()
+        kw = dict(compressor=c["compressor"], shuffle=c["shuffle"], level=c["level"],
+                  dtype=np.dtype(c["dtype"]), chunk_shape=tuple(c["chunk_shape"]))
+        if c["codec"] not in (0, 1, 3) and not c["memcpyed"]:
+            with pytest.raises(NotImplementedError):
+                codec._uncompress(blob, **kw)
+            continue
+        if c["status"] == "error" or c["name"].endswith("_trunc"):
+            with pytest.raises(codec.HTTPInternalServerError):
+                codec._uncompress(blob, **kw)
+            continue
+        out = codec._uncompress(blob, **kw)
+        assert len(out) == c["out_len"] and _sha(out) == c["out_sha256"], c["name"]
+        checked += 1
+    assert checked >= 45
+
+
+@pytest.mark.parametrize("kind,size,ts,bs", [
+    ("smooth", 1 << 20, 1, 131072), ("smooth", 1 << 20, 4, 262144), ("int16", 262144, 2, 65536),
+    ("zeros", 1 << 20, 1, 131072), ("random", 65536, 1, 32768), ("mixed", 300000 + 5, 1, 65536),
+    ("mixed", 500000, 8, 524288),
+])
+def test_batch_decode_lz4_matches_oracle(kind, size, ts, bs, oracle_lib, torch_dev):
+    import torch
+    from hsds_amd.engine import ChunkEngine, pack_chunks
+    orc = oracle_lib
+    rng = np.random.default_rng(abs(hash(("lz4", kind, size, ts))) % (1 << 32))
+    chunks = _corpus(rng, 16, size, kind)
+    blobs = [orc.blosc_encode_lz4(c, typesize=ts, blocksize=bs, shuffle=1) for c in chunks]
+    src, descs, ext = pack_chunks(blobs, [len(c) for c in chunks])
+    eng = ChunkEngine(0)
+    d_src = torch.from_numpy(src).to(torch_dev)
+    d_dst = torch.zeros(ext, dtype=torch.uint8, device=torch_dev)
+    d_st = torch.full((len(blobs),), 77, dtype=torch.int32, device=torch_dev)
+    eng.decode(d_src, descs, d_dst, d_st, compressor="lz4", shuffle=1, itemsize=ts)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    out = d_dst.cpu().numpy()
+    for k, c in enumerate(chunks):
+        assert orc.uncompress(blobs[k], "lz4", 1, ts, len(c)) == c
+        assert st[k] == 0, (k, st[k])
+        o = int(descs[k]["dst_off"])
+        assert out[o:o + len(c)].tobytes() == c, k
+
+
+def test_lz4_blosclz_error_statuses(golden2, oracle_lib, torch_dev):
+    """corrupted lz4 / blosclz frames in one batch: status < 0 exactly where the oracle
+    fails, identical bytes where it decodes."""
+    import torch
+    from hsds_amd.engine import ChunkEngine, pack_chunks
+    orc = oracle_lib
+    meta, arrs = golden2
+    rng = np.random.default_rng(11)
+    blobs, sizes = [], []
+    for c in meta["cases"]:
+        if c["codec"] not in (0, 1) or c["memcpyed"] or c["in_len"] > 300000:
+            continue
+        good = arrs[c["name"] + "__in"].tobytes()
+        n = int(np.prod(c["chunk_shape"])) * np.dtype(c["dtype"]).itemsize
+        for t in range(3):
+            b = bytearray(good)
+            i = int(rng.integers(16, len(b)))
+            b[i] ^= int(rng.integers(1, 256))
+            blobs.append(bytes(b))
+            sizes.append(n)
+    src, descs, ext = pack_chunks(blobs, sizes)
+    eng = ChunkEngine(0)
+    d_src = torch.from_numpy(src).to(torch_dev)
+    d_dst = torch.zeros(ext, dtype=torch.uint8, device=torch_dev)
+    d_st = torch.full((len(blobs),), 77, dtype=torch.int32, device=torch_dev)
+    eng.decode(d_src, descs, d_dst, d_st, compressor="lz4", shuffle=1, itemsize=1)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    out = d_dst.cpu().numpy()
+    assert len(blobs) >= 60
+    for k, b in enumerate(blobs):
+        ref = orc.uncompress(b, "lz4", 1, 1, sizes[k])
+        if isinstance(ref, int):
+            assert st[k] < 0, (k, ref, st[k])
+        else:
+            assert st[k] == 0, (k, st[k])
+            o = int(descs[k]["dst_off"])
+            assert out[o:o + sizes[k]].tobytes() == ref, k
