@@ -37,7 +37,6 @@ namespace {
 constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
 constexpr int INFLATE_WAVES_PER_CU = 8;   // LDS-bound: sizeof(hz::Shared) <= 20 KiB
 static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
-static_assert(sizeof(lz::Shared) <= sizeof(hz::Shared), "the LZ decoder reuses the inflate LDS block");
 
 // ITEM_LZ4 / ITEM_BLOSCLZ: Blosc splits of the byte-LZ77 codecs (lz_wave.h)
 enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_INEXACT = 0x100 };
@@ -260,7 +259,8 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
 
 // -------------------------------------------------------------------------
 // LZ4 / BloscLZ splits (lz_wave.h): persistent 64-thread workgroups over the same
-// item table as inflate_kernel, taking only the LZ items (own counter).
+// item table as inflate_kernel; a wave takes lz::GROUP consecutive items at a time
+// and decodes the LZ ones among them together (one split per header-walking lane).
 // -------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
                                                 int64_t nchunks, uint32_t* __restrict__ counter,
@@ -270,24 +270,51 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, 
   if (kind_counts[0] == 0) return;
   const uint32_t total = offs[nchunks];
   const int lane = threadIdx.x;
+#ifdef HZ_PROFILE
+  HzProf prof_;
+  for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
+  prof_.last = __builtin_amdgcn_s_memtime();
+  prof_.cur = 0;
+  HzProf* prof = &prof_;
+#else
+  HzProf* prof = nullptr;
+#endif
   for (;;) {
-    uint32_t item = 0;
-    if (lane == 0) item = atomicAdd(counter, 1u);
-    item = __shfl(item, 0, 64);
-    if (item >= total) break;
-    int64_t lo = 0, hi = nchunks - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi + 1) >> 1;
-      if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(counter, (uint32_t)lz::GROUP);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(base, 0, 64));
+    if (base >= total) break;
+    const uint32_t item = base + (uint32_t)lane;
+    lz::LaneJob j = {nullptr, nullptr, 0u, 0u, 0u, 0u};
+    uint32_t chunk = 0;
+    if (lane < lz::GROUP && item < total) {
+      int64_t lo = 0, hi = nchunks - 1;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+      }
+      const Item it = slots[lo * KSLOTS + (item - offs[lo])];
+      const uint32_t kind = it.kind & 0xff;
+      if (kind == ITEM_LZ4 || kind == ITEM_BLOSCLZ) {
+        j = {(const uint8_t*)it.src, (uint8_t*)it.dst, it.src_len, it.dst_len,
+             kind == ITEM_LZ4 ? lz::FMT_LZ4 : lz::FMT_BLOSCLZ, 1u};
+        chunk = it.chunk;
+      }
     }
-    const Item it = slots[lo * KSLOTS + (item - offs[lo])];
-    const uint32_t kind = it.kind & 0xff;
-    if (kind != ITEM_LZ4 && kind != ITEM_BLOSCLZ) continue;
-    hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len, 1u, nullptr};
-    const int st = lz::lz_stream(ls, job, kind == ITEM_LZ4 ? lz::FMT_LZ4 : lz::FMT_BLOSCLZ);
-    if (lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
+    if (lane < lz::GROUP) ls.job[lane] = j;
+    __syncthreads();
+    lz::lz_group(ls, prof);
+    if (j.valid && ls.m_st[lane] != HSDS_OK) atomicMin(&status[chunk], ls.m_st[lane]);
     __syncthreads();
   }
+#ifdef HZ_PROFILE
+  {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    prof_.acc[prof_.cur] += now - prof_.last;
+    if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&hz_prof[i], (unsigned long long)prof_.acc[i]);
+  }
+#endif
+  (void)prof;
 }
 
 // -------------------------------------------------------------------------
@@ -1047,7 +1074,7 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   hipLaunchKernelGGL(inflate_kernel, dim3((unsigned)grid), dim3(64), 0, st, slots, offs, nchunks, ctr, d_status,
                      ctr + 2, ctr + 4, e->tune);
   int64_t lgrid = (int64_t)e->num_cus * e->lz_blocks_per_cu;
-  if (lgrid > nchunks * 16) lgrid = nchunks * 16;
+  if (lgrid > (nchunks * KSLOTS + lz::GROUP - 1) / lz::GROUP) lgrid = (nchunks * KSLOTS + lz::GROUP - 1) / lz::GROUP;
   if (lgrid < 1) lgrid = 1;
   hipLaunchKernelGGL(lz_kernel, dim3((unsigned)lgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 3, d_status,
                      ctr + 4);

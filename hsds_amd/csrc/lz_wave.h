@@ -1,5 +1,5 @@
-// lz_wave.h -- one-wavefront-per-stream decoder for the byte-aligned LZ77 codecs a
-// Blosc1 frame can carry besides zlib:
+// lz_wave.h -- decoder for the byte-aligned LZ77 codecs a Blosc1 frame can carry
+// besides zlib:
 //   * codec 1, "lz4" / "lz4hc": LZ4 block format (lz4 1.9.x LZ4_decompress_safe, which
 //     c-blosc 1.21 calls from lz4_wrap_decompress for every split);
 //   * codec 0, "blosclz": c-blosc 1.21's BloscLZ (blosclz_decompress).
@@ -8,15 +8,18 @@
 // cname = the dataset's compressor (storUtil.py:255-262, dsetUtil.py:38-44).
 //
 // Algorithm (DESIGN.md "LZ4 / BloscLZ"):
-//   A window is a run of up to NSEQ sequences (literal run + match).  Their headers are
-//   parsed serially from a 4 KiB LDS stage of the input (uniform code: every lane
-//   walks the same bytes), which fixes every sequence's absolute output offset.  Then
-//   every output byte of the window is a pure function of the sequence table: a literal
-//   byte is read from the input; a match byte at offset k into a match of distance d
-//   starting at m is the byte at m - d + (k mod d) (the periodic extension of an
-//   overlapping copy), which lies in an earlier sequence or before the window (already
-//   stored), so each lane resolves its bytes independently in a few hops and stores
-//   them as aligned dwords.  No LDS output buffer, no rounds.
+//   One wavefront decodes GROUP (8) splits at once, in rounds.
+//   * Parse: lane i < GROUP walks the sequence headers of ITS split (literal length,
+//     literal source, match distance, match length) for up to GK sequences, reading the
+//     input through an 8-byte register window.  This serial, latency-bound walk runs on
+//     GROUP splits in parallel instead of one lane walking one split.
+//   * Resolve: the round's output of the GROUP splits is cut into 16-byte destination
+//     groups that the 64 lanes share.  Every output byte is a pure function of its
+//     split's sequence table: a literal byte is read from the input; a match byte at
+//     offset k into a match of distance d starting at m is the byte at
+//     m - d + (k mod d) (the periodic extension of an overlapping copy), which lies in
+//     an earlier sequence of the round or before it (already stored).  Bytes are
+//     stored as aligned dwords.
 //
 // Single source, like inflate_wave.h: tests/emu/lz_emu.cpp runs the same code on CPU.
 #pragma once
@@ -24,193 +27,292 @@
 
 namespace lz {
 
-constexpr int NSEQ = 256;            // sequences per window
-constexpr int STAGE_WORDS = 1024;    // 4 KiB input stage
-constexpr uint32_t FMT_BLOSCLZ = 0, FMT_LZ4 = 1;   // Blosc1 codec numbers (flags >> 5)
+#ifndef LZ_GK
+#define LZ_GK 32
+#endif
+constexpr int GK = LZ_GK;                           // sequences per split per round
+#ifndef LZ_GROUP
+#define LZ_GROUP 8
+#endif
+// splits per wavefront: lanes [0, GROUP) walk headers, all 64 lanes resolve.  A batch
+// has only ~8 splits per 1 MiB chunk, so a small group keeps enough wavefronts per CU
+// to hide the resolve's LDS and memory latency (MI355X A/B, 4096 x 1 MiB lz4 chunks:
+// GROUP 64 / 16 / 8 / 4 -> 23 / 62 / 79 / 67 GB/s; GK 16 / 32 / 64 -> 77 / 79 / 79).
+constexpr int GROUP = LZ_GROUP;
+constexpr uint32_t FMT_BLOSCLZ = 0, FMT_LZ4 = 1;    // Blosc1 codec numbers (flags >> 5)
 
-struct Shared {
-  uint32_t in32[STAGE_WORDS + 4];
-  uint32_t s_out[NSEQ + 1];   // absolute output offset of each sequence; [nseq] = window end
-  uint32_t s_lit[NSEQ];       // literal bytes
-  uint32_t s_src[NSEQ];       // stream offset of the literals
-  uint32_t s_off[NSEQ];       // match distance (0: literals only)
+// one split per lane
+struct LaneJob {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint32_t src_len, dst_len;
+  uint32_t fmt, valid;
 };
 
-HZ_HD uint32_t sbyte(const Shared& ls, uint32_t idx) { return (ls.in32[idx >> 2] >> ((idx & 3u) * 8u)) & 0xffu; }
+struct Shared {
+  uint32_t t_out[GK][GROUP];   // [k][split]: output offset of the split's k-th sequence this round
+  uint32_t t_lit[GK][GROUP];   // literal bytes
+  uint32_t t_src[GK][GROUP];   // input offset of the literals
+  uint32_t t_off[GK][GROUP];   // match distance (0: literals only)
+  LaneJob job[GROUP];
+  uint32_t m_lo[GROUP], m_hi[GROUP], m_nk[GROUP];   // round output [lo, hi) and sequence count
+  int32_t m_st[GROUP];                               // per-split status
+  uint32_t gpre[GROUP + 1];                          // exclusive prefix of 16-byte groups per split
+};
 
-#if HZ_GPU
-#define LZ_LANE0 if (threadIdx.x == 0)
-#else
-#define LZ_LANE0
-#endif
+// per-lane input window: 8 bytes at a dword-aligned position of the split
+struct ByteRd {
+  hz_gcu8* base;      // split start rounded down to 4 bytes
+  uint32_t lo, hi;    // valid byte range in base coordinates
+  uint32_t bpos;      // base offset of buf
+  uint64_t buf;
+};
 
-// Decode one Blosc split.  Returns hz::ST_OK or an error status (uniform).
+HZ_HD uint32_t rd_byte(ByteRd& r, uint32_t pos) {
+  const uint32_t ap = pos + r.lo;
+  if (ap - r.bpos >= 8u) {
+    r.bpos = ap & ~3u;
+    r.buf = (uint64_t)hz::load_word(r.base, r.bpos >> 2, r.lo, r.hi) |
+            ((uint64_t)hz::load_word(r.base, (r.bpos >> 2) + 1u, r.lo, r.hi) << 32);
+  }
+  return (uint32_t)(r.buf >> (8u * (ap - r.bpos))) & 0xffu;
+}
+
+struct PState { uint32_t ip, op, done; };
+
+#define LZ_NEED(pos) if ((pos) >= iend) return hz::ST_TRUNC;
+
+// One LZ4 sequence (LZ4_decompress_safe rules; oracle.c orc_lz4_decode).  1: parsed
+// (ps.done set after the last one), < 0: status.
+HZ_HD int parse_lz4(ByteRd& r, PState& ps, uint32_t iend, uint32_t oend, uint32_t& lit, uint32_t& lsrc,
+                    uint32_t& off, uint32_t& ml) {
+  uint32_t x = ps.ip;
+  LZ_NEED(x);
+  const uint32_t t = rd_byte(r, x); x++;
+  lit = t >> 4;
+  if (lit == 15) {
+    uint32_t b;
+    do { LZ_NEED(x); b = rd_byte(r, x); x++; lit += b; } while (b == 255 && lit < 0x7fffffffu);
+  }
+  lsrc = x;
+  if (lit > iend - x) return hz::ST_TRUNC;
+  if (lit > oend - ps.op) return hz::ST_SIZE;
+  x += lit;
+  // a literal run reaching oend - MFLIMIT (12) or iend - 8 is the last sequence and
+  // must end exactly at iend
+  if (ps.op + lit + 12u > oend || x + 8u > iend) {
+    if (x != iend) return hz::ST_DATA;
+    off = 0; ml = 0; ps.ip = x; ps.done = 1;
+    return 1;
+  }
+  off = rd_byte(r, x);
+  off |= rd_byte(r, x + 1u) << 8;
+  x += 2;
+  ml = t & 15u;
+  if (ml == 15) {
+    uint32_t b;
+    do { LZ_NEED(x); b = rd_byte(r, x); x++; ml += b; } while (b == 255 && ml < 0x7fffffffu);
+  }
+  ml += 4;
+  const uint32_t oe = ps.op + lit;
+  if (off == 0 || off > oe) return hz::ST_DATA;
+  if (ml > oend - oe || oe + ml + 5u > oend) return hz::ST_DATA;   // LASTLITERALS
+  ps.ip = x;
+  return 1;
+}
+
+// One BloscLZ item (c-blosc 1.21 blosclz_decompress; oracle.c orc_blosclz_decode)
+HZ_HD int parse_blosclz(ByteRd& r, PState& ps, uint32_t iend, uint32_t oend, uint32_t& lit, uint32_t& lsrc,
+                        uint32_t& off, uint32_t& ml) {
+  uint32_t x = ps.ip;
+  LZ_NEED(x);
+  uint32_t c = rd_byte(r, x); x++;
+  if (ps.ip == 0) c &= 31u;
+  lit = 0; lsrc = 0; off = 0; ml = 0;
+  if (c >= 32) {
+    ml = (c >> 5) - 1u;
+    const uint32_t ofs = (c & 31u) << 8;
+    uint32_t code;
+    if (ml == 6) {
+      do { LZ_NEED(x); code = rd_byte(r, x); x++; ml += code; } while (code == 255 && ml < 0x7fffffffu);
+    }
+    LZ_NEED(x);
+    code = rd_byte(r, x); x++;
+    ml += 3;
+    off = ofs + code + 1u;
+    if (code == 255 && ofs == (31u << 8)) {
+      LZ_NEED(x + 1u);
+      off = ((rd_byte(r, x) << 8) | rd_byte(r, x + 1u)) + 8192u;
+      x += 2;
+    }
+    if (ml > oend - ps.op) return hz::ST_SIZE;
+    if (off > ps.op) return hz::ST_DATA;
+  } else {
+    lit = c + 1u;
+    lsrc = x;
+    if (lit > oend - ps.op) return hz::ST_SIZE;
+    if (lit > iend - x) return hz::ST_TRUNC;
+    x += lit;
+  }
+  ps.ip = x;
+  if (x >= iend) ps.done = 1;
+  return 1;
+}
+#undef LZ_NEED
+
+// largest k <= hi with t_out[k][s] <= p (non-decreasing in k, t_out[0][s] <= p)
+HZ_HD uint32_t find_seq(const Shared& ls, uint32_t s, uint32_t hi, uint32_t p) {
+  uint32_t lo = 0;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1u) >> 1;
+    if (ls.t_out[mid][s] <= p) lo = mid; else hi = mid - 1u;
+  }
+  return lo;
+}
+
+// largest s < GROUP with gpre[s] <= g
+HZ_HD uint32_t find_split(const Shared& ls, uint32_t g) {
+  uint32_t lo = 0, hi = GROUP - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1u) >> 1;
+    if (ls.gpre[mid] <= g) lo = mid; else hi = mid - 1u;
+  }
+  return lo;
+}
+
+// Decode the splits in ls.job[0..GROUP) (valid ones); statuses land in ls.m_st.
 #if HZ_GPU
 __device__
 #else
 static
 #endif
-inline int lz_stream(Shared& ls, const hz::StreamJob job, uint32_t fmt) {
-  const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 3u);
-  hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, job.src - a);
-  hz_gcu8* src = HZ_GLOBAL(hz_gcu8*, job.src);
-  hz_gu8* const dst = HZ_GLOBAL(hz_gu8*, job.dst);
-  const uint32_t iend = job.src_len, oend = job.dst_len;
-  const uint32_t dmis = (uint32_t)(((uintptr_t)job.dst) & 3u);
-  uint32_t ip = 0, op = 0;
-  int done = 0;
-  if (iend == 0) return hz::ST_TRUNC;
-  while (!done) {
-    // ---- stage 4 KiB of input at ip (dword-aligned) ----
-    const uint32_t w0 = (ip + a) >> 2;
-    WAVE_SYNC();
+inline void lz_group(Shared& ls, HzProf* prof = nullptr) {
+  (void)prof;
+  LANE_VAR(PState, ps);
+  LANE_VAR(ByteRd, rd);
+  LANE_VAR(int, active);
+  LANE_VAR(uint32_t, gc);
+  LANE_LOOP {
+    LV(active) = 0;
+    LV(gc) = 0;
+    if (lane >= GROUP) continue;
+    const LaneJob j = ls.job[lane];
+    const uint32_t a = (uint32_t)(((uintptr_t)j.src) & 3u);
+    LV(ps).ip = 0; LV(ps).op = 0; LV(ps).done = 0;
+    LV(rd).base = HZ_GLOBAL(hz_gcu8*, j.src - a);
+    LV(rd).lo = a; LV(rd).hi = a + j.src_len;
+    LV(rd).bpos = 0x80000000u; LV(rd).buf = 0;
+    LV(active) = j.valid != 0;
+    ls.m_st[lane] = hz::ST_OK;
+    if (j.valid && j.src_len == 0) { ls.m_st[lane] = hz::ST_TRUNC; LV(active) = 0; }
+  }
+  WAVE_SYNC();
+  for (;;) {
+    if (!WAVE_BALLOT(LV(active))) break;
+    HZ_T(1);
+    // ---- parse: every lane walks up to GK sequence headers of its own split ----
     LANE_LOOP {
-      for (uint32_t k = (uint32_t)lane; k < (uint32_t)STAGE_WORDS + 4u; k += 64)
-        ls.in32[k] = k < (uint32_t)STAGE_WORDS ? hz::load_word(base, w0 + k, a, a + iend) : 0u;
-    }
-    WAVE_SYNC();
-    // stream offsets [slo, shi) are in the stage; byte x is at stage index x - slo + sfix
-    const uint32_t sfix = (ip + a) & 3u, slo = ip;
-    const uint32_t shi = ip + (uint32_t)STAGE_WORDS * 4u - sfix;
-    const uint32_t win_base = op;
-    uint32_t nseq = 0;
-    int err = hz::ST_OK;
-    // ---- serial parse of sequence headers (uniform) ----
-    // A window takes sequences while their first byte is staged; header bytes past
-    // the stage (the tail of a window's last sequence, after a long literal run) are
-    // read from the input directly.
-    while (!done && nseq < (uint32_t)NSEQ && ip < shi) {
-      uint32_t x = ip, lit = 0, lsrc = 0, off = 0, ml = 0;
-#define LZ_NEED(pos) \
-  if ((pos) >= iend) { err = hz::ST_TRUNC; break; }
-#define LZ_B(pos) ((pos) < shi ? sbyte(ls, (pos) - slo + sfix) : (uint32_t)src[pos])
-      int last = 0;
-      do {
-        if (fmt == FMT_LZ4) {
-          LZ_NEED(x);
-          const uint32_t t = LZ_B(x); x++;
-          lit = t >> 4;
-          if (lit == 15) {
-            uint32_t b;
-            do { LZ_NEED(x); b = LZ_B(x); x++; lit += b; } while (b == 255 && lit < 0x7fffffffu);
-            if (err != hz::ST_OK) break;
-          }
-          lsrc = x;
-          if (lit > iend - x) { err = hz::ST_TRUNC; break; }
-          x += lit;
-          const uint32_t oe = op + lit;
-          if (lit > oend - op) { err = hz::ST_SIZE; break; }
-          // LZ4_decompress_safe: a literal run that reaches oend - MFLIMIT (12) or
-          // iend - 8 must be the last sequence and end exactly at iend
-          if (oe + 12u > oend || x + 8u > iend) {
-            if (x != iend) { err = hz::ST_DATA; break; }
-            last = 1;
-            break;
-          }
-          LZ_NEED(x + 1u);
-          off = LZ_B(x) | (LZ_B(x + 1u) << 8); x += 2;
-          ml = t & 15u;
-          if (ml == 15) {
-            uint32_t b;
-            do { LZ_NEED(x); b = LZ_B(x); x++; ml += b; } while (b == 255 && ml < 0x7fffffffu);
-            if (err != hz::ST_OK) break;
-          }
-          ml += 4;
-          if (off == 0 || off > oe) { err = hz::ST_DATA; break; }
-          if (ml > oend - oe || oe + ml + 5u > oend) { err = hz::ST_DATA; break; }   // LASTLITERALS
-        } else {
-          LZ_NEED(x);
-          uint32_t c = LZ_B(x); x++;
-          if (ip == 0) c &= 31u;
-          if (c >= 32) {
-            ml = (c >> 5) - 1u;
-            const uint32_t ofs = (c & 31u) << 8;
-            uint32_t code;
-            if (ml == 6) {
-              do { LZ_NEED(x); code = LZ_B(x); x++; ml += code; } while (code == 255 && ml < 0x7fffffffu);
-              if (err != hz::ST_OK) break;
-            }
-            LZ_NEED(x);
-            code = LZ_B(x); x++;
-            ml += 3;
-            off = ofs + code + 1u;
-            if (code == 255 && ofs == (31u << 8)) {
-              LZ_NEED(x + 1u);
-              off = ((LZ_B(x) << 8) | LZ_B(x + 1u)) + 8192u;
-              x += 2;
-            }
-            if (ml > oend - op) { err = hz::ST_SIZE; break; }
-            if (off > op) { err = hz::ST_DATA; break; }
-          } else {
-            lit = c + 1u;
-            lsrc = x;
-            if (lit > oend - op) { err = hz::ST_SIZE; break; }
-            if (lit > iend - x) { err = hz::ST_TRUNC; break; }
-            x += lit;
-          }
-          if (x >= iend) last = 1;
+      if (lane >= GROUP) continue;
+      const LaneJob j = ls.job[lane];
+      const uint32_t op0 = LV(ps).op;
+      uint32_t k = 0;
+      if (LV(active)) {
+        for (; k < (uint32_t)GK && !LV(ps).done; k++) {
+          uint32_t lit, lsrc, off, ml;
+          const int r = j.fmt == FMT_LZ4 ? parse_lz4(LV(rd), LV(ps), j.src_len, j.dst_len, lit, lsrc, off, ml)
+                                         : parse_blosclz(LV(rd), LV(ps), j.src_len, j.dst_len, lit, lsrc, off, ml);
+          if (r < 0) { ls.m_st[lane] = r; LV(active) = 0; break; }
+          ls.t_out[k][lane] = LV(ps).op;
+          ls.t_lit[k][lane] = lit;
+          ls.t_src[k][lane] = lsrc;
+          ls.t_off[k][lane] = off;
+          LV(ps).op += lit + ml;
         }
-      } while (0);
-#undef LZ_NEED
-#undef LZ_B
-      if (err != hz::ST_OK) return err;
-      LZ_LANE0 {
-        ls.s_out[nseq] = op;
-        ls.s_lit[nseq] = lit;
-        ls.s_src[nseq] = lsrc;
-        ls.s_off[nseq] = off;
       }
-      nseq++;
-      op += lit + ml;
-      ip = x;
-      if (last) done = 1;
+      const uint32_t hi = LV(active) ? LV(ps).op : op0;
+      ls.m_lo[lane] = op0;
+      ls.m_hi[lane] = hi;
+      ls.m_nk[lane] = LV(active) ? k : 0u;
+      const uint32_t dmis = (uint32_t)(((uintptr_t)j.dst) & 3u);
+      LV(gc) = hi > op0 ? ((hi + dmis + 15u) >> 4) - ((op0 + dmis) >> 4) : 0u;
     }
-    LZ_LANE0 { ls.s_out[nseq] = op; }
+    HZ_T(2);
+    // ---- groups of all splits, exclusive prefix ----
+    {
+      LANE_VAR(uint32_t, gx);
+#if HZ_GPU
+      gx = hz::wave_excl_scan(gc, (int)threadIdx.x);
+#else
+      { uint32_t acc = 0; for (int lane = 0; lane < 64; lane++) { gx[lane] = acc; acc += gc[lane]; } }
+#endif
+      LANE_LOOP {
+        if (lane < GROUP) ls.gpre[lane] = LV(gx);
+        if (lane == GROUP - 1) ls.gpre[GROUP] = LV(gx) + LV(gc);
+      }
+    }
     WAVE_SYNC();
-    // ---- resolve and store the window's bytes [win_base, op) ----
-    const uint32_t wb = win_base, we = op;
-    const uint32_t g0 = (wb + dmis) >> 2, g1 = (we + dmis + 3u) >> 2;
+    const uint32_t total = ls.gpre[GROUP];
+    // ---- resolve: 16-byte destination groups shared by all lanes ----
     LANE_LOOP {
-      uint32_t s = 0;                              // cursor: sequence holding the current byte
-      uint32_t s_beg = ls.s_out[0], s_end = ls.s_out[1];
-      for (uint32_t g = g0 + (uint32_t)lane; g < g1; g += 64u) {
-        uint32_t word = 0, have = 0;
-        for (uint32_t k = 0; k < 4u; k++) {
-          const uint32_t p = g * 4u + k - dmis;    // wraps below 0 for the first group
-          if (g * 4u + k < wb + dmis || p >= we) continue;
-          while (p >= s_end) { s++; s_beg = s_end; s_end = ls.s_out[s + 1]; }
-          uint32_t q = p, t = s, tb = s_beg, v = 0;
+      for (uint32_t g = (uint32_t)lane; g < total; g += 64u) {
+        const uint32_t s = find_split(ls, g);
+        const LaneJob j = ls.job[s];
+        hz_gcu8* src = HZ_GLOBAL(hz_gcu8*, j.src);
+        hz_gu8* dst = HZ_GLOBAL(hz_gu8*, j.dst);
+        const uint32_t dmis = (uint32_t)(((uintptr_t)j.dst) & 3u);
+        const uint32_t wb = ls.m_lo[s], we = ls.m_hi[s], nk = ls.m_nk[s];
+        const uint32_t a0 = (((wb + dmis) >> 4) + (g - ls.gpre[s])) * 16u;   // dst - dmis offset of the group
+        const uint32_t pb = a0 > wb + dmis ? a0 - dmis : wb;                  // first window byte in it
+        uint32_t t = find_seq(ls, s, nk - 1u, pb);
+        uint32_t t_beg = ls.t_out[t][s], t_end = t + 1u < nk ? ls.t_out[t + 1u][s] : we;
+        // pass 1: the source address of every byte (no loads: no waits inside chains)
+        hz_gcu8* sp[16];
+        uint32_t have = 0;
+        HZ_UNROLL
+        for (uint32_t k = 0; k < 16u; k++) {
+          const uint32_t ak = a0 + k;
+          sp[k] = src;
+          if (ak < wb + dmis || ak >= we + dmis) continue;
+          const uint32_t p = ak - dmis;
+          while (p >= t_end) { t++; t_beg = t_end; t_end = t + 1u < nk ? ls.t_out[t + 1u][s] : we; }
+          uint32_t q = p, u = t, ub = t_beg;
           for (;;) {
-            const uint32_t rel = q - tb, nl = ls.s_lit[t];
-            if (rel < nl) { v = src[ls.s_src[t] + rel]; break; }
-            const uint32_t m = tb + nl, d = ls.s_off[t], kk = q - m;
+            const uint32_t rel = q - ub, nl = ls.t_lit[u][s];
+            if (rel < nl) { sp[k] = src + ls.t_src[u][s] + rel; break; }
+            const uint32_t m = ub + nl, d = ls.t_off[u][s], kk = q - m;
             const uint32_t q2 = m - d + (kk < d ? kk : kk % d);
-            if (q2 < wb) { v = dst[q2]; break; }
-            // q2 lies in an earlier (or this) sequence of the window: largest t2 <= t
-            // with s_out[t2] <= q2
-            uint32_t lo2 = 0, hi2 = t;
-            while (lo2 < hi2) {
-              const uint32_t mid = (lo2 + hi2 + 1u) >> 1;
-              if (ls.s_out[mid] <= q2) lo2 = mid; else hi2 = mid - 1u;
-            }
-            q = q2; t = lo2; tb = ls.s_out[lo2];
+            if (q2 < wb) { sp[k] = (hz_gcu8*)dst + q2; break; }
+            u = find_seq(ls, s, u, q2);                // an earlier (or this) sequence
+            q = q2; ub = ls.t_out[u][s];
           }
-          word |= v << (8u * k);
           have |= 1u << k;
         }
-        if (have == 15u) {
-          *(hz_gu32*)(dst + (g * 4u - dmis)) = word;
-        } else {
-          for (uint32_t k = 0; k < 4u; k++)
-            if (have & (1u << k)) dst[g * 4u + k - dmis] = (uint8_t)(word >> (8u * k));
+        // pass 2: 16 independent byte loads in flight together
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        HZ_UNROLL
+        for (uint32_t k = 0; k < 16u; k++) w[k >> 2] |= (uint32_t)*sp[k] << (8u * (k & 3u));
+        for (uint32_t i = 0; i < 4u; i++) {
+          const uint32_t hm = (have >> (4u * i)) & 15u;
+          if (hm == 15u) {
+            *(hz_gu32*)(dst + (a0 + 4u * i - dmis)) = w[i];
+          } else if (hm) {
+            for (uint32_t k = 0; k < 4u; k++)
+              if (hm & (1u << k)) dst[a0 + 4u * i + k - dmis] = (uint8_t)(w[i] >> (8u * k));
+          }
         }
       }
     }
+    HZ_T(3);
     WAVE_SYNC_GLOBAL();
+    HZ_T(0);
+    LANE_LOOP {
+      if (lane < GROUP && LV(active) && LV(ps).done) {
+        if (LV(ps).op != ls.job[lane].dst_len) ls.m_st[lane] = hz::ST_SIZE;
+        LV(active) = 0;
+      }
+    }
   }
-  if (op != oend) return hz::ST_SIZE;
-  if (job.out_len) { LZ_LANE0 { *job.out_len = op; } }
-  return hz::ST_OK;
+  WAVE_SYNC();
 }
 
 }  // namespace lz

@@ -206,3 +206,69 @@ def test_corrupt_streams_fail_like_the_oracle(emu, oracle_lib):
                 assert r != 0, (fmt, k)
             else:
                 assert r == 0 and got == want, (fmt, k)
+
+
+def _ext(v):
+    return bytes([255] * (v // 255) + [v % 255])
+
+
+def test_headers_longer_than_the_stage(emu, oracle_lib):
+    """LZ4 / BloscLZ items whose length-extension bytes exceed the 4 KiB LDS stage
+    (runs of several MB): the parser falls back to global reads for that item."""
+    rng = np.random.default_rng(9)
+    # LZ4: 2 MB literal run, then a 3 MB overlapping match (distance 1), then 6 literals
+    lits = rng.integers(0, 256, 2_000_000, dtype=np.uint8).tobytes()
+    tail = b"abcdef"
+    ml = 3_000_000
+    comp = (bytes([0xFF]) + _ext(len(lits) - 15) + lits + struct.pack("<H", 1) + _ext(ml - 4 - 15)
+            + bytes([len(tail) << 4]) + tail)
+    raw = lits + lits[-1:] * ml + tail
+    assert oracle_lib.lz4_decode(comp, len(raw)) == raw
+    r, got = split(emu, comp, len(raw), 1)
+    assert r == 0 and got == raw
+    # BloscLZ: 3 literals, then a 2 MB match of distance 3
+    ln = 2_000_000
+    comp = bytes([2]) + b"xyz" + bytes([7 << 5]) + _ext(ln - 9) + bytes([2])
+    raw = b"xyz" * ((ln + 3) // 3 + 1)
+    raw = raw[:3 + ln]
+    assert oracle_lib.blosclz_decode(comp, len(raw)) == raw
+    r, got = split(emu, comp, len(raw), 0)
+    assert r == 0 and got == raw
+
+
+def test_group_of_splits_shares_the_resolve(emu, oracle_lib):
+    """Up to 64 splits decoded together (mixed formats, sizes, corrupt ones): the
+    resolve interleaves every split's 16-byte groups across the lanes."""
+    emu.emu_lz_group.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    rng = np.random.default_rng(21)
+    for n in (64, 37, 1):
+        comps, raws, fmts = [], [], []
+        for i in range(n):
+            fmt = int(rng.integers(0, 2))
+            comp, raw = (lz4_write if fmt else blosclz_write)(rng, int(rng.integers(1, 30000)))
+            if i % 9 == 4:
+                b = bytearray(comp)
+                b[int(rng.integers(0, len(b)))] ^= 0x5A
+                comp = bytes(b)
+            comps.append(np.frombuffer(comp, np.uint8).copy())
+            raws.append(raw)
+            fmts.append(fmt)
+        # destinations at odd offsets of one buffer: unaligned dword groups
+        offs = np.cumsum([0] + [len(r) + 3 for r in raws])
+        out = np.zeros(int(offs[-1]) + 16, np.uint8)
+        src_p = (ctypes.c_void_p * n)(*[c.ctypes.data for c in comps])
+        dst_p = (ctypes.c_void_p * n)(*[out.ctypes.data + int(offs[i]) + 1 for i in range(n)])
+        slen = np.array([len(c) for c in comps], np.uint32)
+        dlen = np.array([len(r) for r in raws], np.uint32)
+        fm = np.array(fmts, np.uint32)
+        st = np.zeros(n, np.int32)
+        emu.emu_lz_group(src_p, slen.ctypes.data, dst_p, dlen.ctypes.data, fm.ctypes.data, n, st.ctypes.data)
+        for i in range(n):
+            dec = oracle_lib.lz4_decode if fmts[i] else oracle_lib.blosclz_decode
+            want = dec(comps[i].tobytes(), len(raws[i]))
+            if isinstance(want, int):
+                assert st[i] != 0, (n, i)
+            else:
+                o = int(offs[i]) + 1
+                assert st[i] == 0 and out[o:o + len(raws[i])].tobytes() == want, (n, i)

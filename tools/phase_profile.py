@@ -23,6 +23,9 @@ NAMES = ["other", "blk-stage", "hdr-lens", "tables", "win-stage", "A", "A'", "re
          "C-ref", "C-chase", "C-flush", "C-rounds", "C-end", "trailer"]
 
 
+LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
+
+
 def run(fmt, n, unique, tune=None):
     raw, blobs = make_corpus(fmt, unique, 20261015, 16)
     order = [i % unique for i in range(n)]
@@ -34,12 +37,13 @@ def run(fmt, n, unique, tune=None):
     d_src = torch.from_numpy(src).to(dev)
     d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
-    eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
+    comp = "lz4" if fmt == "LZ4" else "zlib"
+    eng.decode(d_src, descs, d_dst, d_st, compressor=comp, shuffle=1, itemsize=4)
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
     L.hsds_debug_profile(buf, 1)
     t = time.perf_counter()
-    eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
+    eng.decode(d_src, descs, d_dst, d_st, compressor=comp, shuffle=1, itemsize=4)
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     L.hsds_debug_profile(buf, 1)
@@ -49,10 +53,12 @@ def run(fmt, n, unique, tune=None):
     streams = n * 4
     for i in range(16):
         if buf[i]:
-            print(f"   {NAMES[i]:10s} {100.0*buf[i]/tot:6.2f}%   {buf[i]/streams/1e3:9.1f} kcyc/stream")
+            print(f"   {(LZ_NAMES if fmt == 'LZ4' else NAMES)[i]:10s} {100.0*buf[i]/tot:6.2f}%   {buf[i]/streams/1e3:9.1f} kcyc/stream")
 
 
 if __name__ == "__main__":
     n1 = int(os.environ.get("HZ_PROF_N1", "1024"))
     run("F1", n1, 256)
     run("F2", int(os.environ.get("HZ_PROF_N2", "256")), 128)
+    if os.environ.get("HZ_PROF_LZ", "1") == "1":
+        run("LZ4", int(os.environ.get("HZ_PROF_NLZ", "1024")), 256)
