@@ -335,6 +335,29 @@ def run_cfg5(args, dev, rank=0):
            "deflate_kernel_GBps": round((slab_bytes + comp) / (kern[-1] / 1e3) / 1e9, 2),
            "size_vs_libz": round(ours / ref, 4),
            "workload": "configs[4] per-GPU share: f32 slab 8192x131072 -> 4096 chunks 512x512 -> F1 zlib L4 frames"}
+    # the same scatter + encode for an lz4 dataset (Blosc-lz4 frames, level 5)
+    def step_lz4():
+        eng.copy(slab_u8, chunks, d_cd, stream=stream)
+        eng.encode(chunks, d_desc, frames, sizes, st, clevel=5, shuffle=1, typesize=1, stream=stream,
+                   compressor="lz4")
+
+    step_lz4()
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0, "lz4 encode status errors"
+    o = int(descs[n // 3]["dst_off"])
+    fr = frames[o:o + int(sizes[n // 3])].cpu().numpy().tobytes()
+    assert orc.uncompress(fr, "lz4", 1, 1, cbytes) == chunks[(n // 3) * cbytes:(n // 3 + 1) * cbytes].cpu().numpy().tobytes()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_lz4()
+    torch.cuda.synchronize()
+    el4 = (time.perf_counter() - t0) / args.steps
+    comp4 = int(sizes.sum())
+    out["lz4_encode"] = {"value": round(slab_bytes / el4 / 1e9, 2), "unit": "GB/s slab (scatter + encode)",
+                         "ms_per_step": round(el4 * 1e3, 3), "compressed_bytes": comp4,
+                         "encode_ms": round(eng.last_deflate_ms(), 3),
+                         "format": "Blosc-lz4 frames (typesize 1, c-blosc lz4 blocksize), parse tokens -> LZ4 blocks"}
     if args.cpu_seconds > 0 and rank == 0:
         threads = min(16, os.cpu_count() or 1)
         t1 = time.perf_counter()

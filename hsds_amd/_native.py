@@ -22,6 +22,14 @@ ERR_ARG = -6
 ERR_DEVICE = -7
 
 COMP_NONE, COMP_ZLIB, COMP_OTHER = 0, 1, 2
+CNAME_ZLIB, CNAME_LZ4, CNAME_LZ4HC = 0, 1, 2
+
+
+def cname_code(compressor):
+    """storUtil._compress compressor -> HSDS_CNAME_* (None when the engine has no encoder for it)"""
+    if compressor in ("gzip", "deflate", "zlib"):
+        return CNAME_ZLIB
+    return {"lz4": CNAME_LZ4, "lz4hc": CNAME_LZ4HC}.get(compressor)
 SHUFFLE_NONE, SHUFFLE_BYTE, SHUFFLE_BIT = 0, 1, 2
 MAX_RANK = 8
 KIND_BYTES, KIND_F16, KIND_F32, KIND_F64, KIND_C64, KIND_C128 = 0, 1, 2, 3, 4, 5
@@ -76,7 +84,9 @@ def lib():
         "hsds_compare_batch": (I, [P, P, P, P, I64, I, P, P]),
         "hsds_copy_batch_if": (I, [P, P, P, P, I64, P, P]),
         "hsds_encode_batch": (I, [P, P, P, I64, P, U64, P, P, I, I, I, P]),
+        "hsds_encode_batch_codec": (I, [P, P, P, I64, P, U64, P, P, I, I, I, I, P]),
         "hsds_compress": (I64, [P, P, I64, I, I, I, P, I64]),
+        "hsds_compress_codec": (I64, [P, P, I64, I, I, I, I, P, I64]),
         "hsds_last_deflate_ms": (I, [P, ctypes.POINTER(ctypes.c_float)]),
     }
     for name, (res, args) in sig.items():

@@ -145,11 +145,12 @@ def _uncompress(data, compressor=None, shuffle=0, level=None, dtype=None, chunk_
 
 def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape=None):
     """storUtil._compress (storUtil.py:238-281) on the GPU: a Blosc1 frame with the
-    zlib inner codec (gzip/deflate/zlib are all Blosc "zlib", storUtil.py:255-257),
-    typesize 1 because the reference always hands Blosc a bytes object, and the
-    byte-shuffle flag from `shuffle`.  Differences from the reference, by design:
-      * bitshuffle (shuffle=2) and other Blosc codecs are outside this engine and raise
-        NotImplementedError (the reference would bitshuffle, then Blosc-encode);
+    inner codec cname = compressor (gzip/deflate/zlib are all Blosc "zlib",
+    storUtil.py:255-257; lz4 and lz4hc carry LZ4 blocks), typesize 1 because the
+    reference always hands Blosc a bytes object, and the byte-shuffle flag from
+    `shuffle`.  Differences from the reference, by design:
+      * bitshuffle (shuffle=2) and the blosclz / zstd encoders are outside this engine
+        and raise NotImplementedError (the reference would encode them with c-blosc);
       * an encoder failure raises instead of silently storing the raw bytes
         (storUtil.py:266-279 logs and returns `data`, which its own reader then
         rejects: SURVEY.md section 8b)."""
@@ -161,15 +162,16 @@ def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape
         raise ValueError()
     if not compressor or compressor == "scaleoffset":
         return data        # no compressor, nothing shuffled: the bytes as given
-    if _compressor_code(compressor) != nat.COMP_ZLIB:
-        raise NotImplementedError(f"Blosc codec {compressor!r} is outside the hsds_amd engine scope")
+    cname = nat.cname_code(compressor)
+    if cname is None:
+        raise NotImplementedError(f"Blosc codec {compressor!r} has no encoder in the hsds_amd engine")
     if level is None:
         level = 5
     src = _as_bytes(data)
     cap = src.size + 16
     out = np.empty(cap, np.uint8)
-    n = nat.lib().hsds_compress(nat.engine().h, src.ctypes.data, src.size, int(level), int(shuffle), 1,
-                                out.ctypes.data, cap)
+    n = nat.lib().hsds_compress_codec(nat.engine().h, src.ctypes.data, src.size, int(level), int(shuffle), 1, cname,
+                                      out.ctypes.data, cap)
     if n < 0:
-        raise nat.NativeError(n, "hsds_compress")
+        raise nat.NativeError(n, "hsds_compress_codec")
     return out[:n].tobytes()

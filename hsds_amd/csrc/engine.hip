@@ -29,6 +29,7 @@
 #include "inflate_wave.h"
 #include "deflate_wave.h"
 #include "lz_wave.h"
+#include "lz4_enc.h"
 
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -524,12 +525,13 @@ struct SegMeta {       // parse -> huffman
   uint32_t seglen;
 };
 
-// c-blosc 1.21 compute_blocksize for the zlib codec (oracle.c orc_blosc_blocksize)
-__device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint64_t nbytes) {
+// c-blosc 1.21 compute_blocksize (oracle.c orc_blosc_blocksize_codec): the HCR codecs
+// (zlib, lz4hc) start from 2 x L1 and double again at level 9, lz4 from L1
+__device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint64_t nbytes, int hcr) {
   if (nbytes < ts) return 1;
   uint64_t bs = nbytes;
   if (nbytes >= 32 * 1024) {
-    bs = 32 * 1024 * 2;
+    bs = hcr ? 32 * 1024 * 2 : 32 * 1024;
     switch (clevel) {
       case 0: bs /= 4; break;
       case 1: bs /= 2; break;
@@ -537,7 +539,7 @@ __device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint6
       case 3: bs *= 2; break;
       case 4: case 5: bs *= 4; break;
       case 6: case 7: case 8: bs *= 8; break;
-      default: bs *= 16; break;
+      default: bs *= hcr ? 16 : 8; break;
     }
   }
   if (clevel > 0 && ts <= 16 && bs / ts >= 128) {
@@ -554,7 +556,7 @@ __device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint6
 __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
                                 int64_t nchunks, EncItem* __restrict__ slots, uint32_t* __restrict__ counts,
                                 uint32_t* __restrict__ segcnt, EncGeom* __restrict__ geom,
-                                int32_t* __restrict__ status, int clevel, int shuffle, int typesize) {
+                                int32_t* __restrict__ status, int clevel, int shuffle, int typesize, int cname) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
   const hsds_chunk_desc c = chunks[ci];
@@ -562,11 +564,12 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
   const uint64_t nbytes = c.src_len;
   int st = HSDS_OK;
   uint32_t cnt = 0, nseg = 0;
-  EncGeom g = {nbytes, 0, 0, (3u << 5) | (shuffle ? 1u : 0u), ts, 0};
+  const uint32_t fmt = cname == HSDS_CNAME_ZLIB ? 3u : 1u;   // Blosc1 codec: zlib 3, lz4 / lz4hc 1
+  EncGeom g = {nbytes, 0, 0, (fmt << 5) | (shuffle ? 1u : 0u), ts, 0};
   if (c.dst_len < nbytes + 16 || nbytes >= (1ull << 31) - 16 || (c.dst_off & 3)) {
     st = HSDS_ERR_ARG;
   } else {
-    const uint64_t bs = enc_blocksize(clevel, ts, nbytes);
+    const uint64_t bs = enc_blocksize(clevel, ts, nbytes, cname != HSDS_CNAME_LZ4);
     g.bs = bs;
     if (!(ts <= 16 && bs / ts >= 128)) g.flags |= 0x10;
     g.memcpyed = (nbytes < 128 || clevel <= 0) ? 1u : 0u;
@@ -693,7 +696,8 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
                               const uint32_t* __restrict__ segoffs, EncGeom* __restrict__ geom,
                               const hd::SegCode* __restrict__ sc, const uint32_t* __restrict__ adler,
                               ItemOut* __restrict__ iout, hd::SegOut* __restrict__ so, int64_t* __restrict__ sizes,
-                              int32_t* __restrict__ status, uint32_t seg_cap, int level) {
+                              int32_t* __restrict__ status, uint32_t seg_cap, int level,
+                              const uint32_t* __restrict__ lzsize) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
   const uint32_t cnt = counts[ci];
@@ -724,8 +728,9 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
         maxout = (int64_t)maxbytes - (int64_t)nt;
         if (maxout <= 0) { memcpyed = 1; break; }
       }
-      int64_t cb = (int64_t)hd::stream_layout(sc + g0 + it[k].seg0, it[k].len, nullptr);
-      if (cb > maxout) cb = 0;                     // compress2 would not fit
+      int64_t cb = lzsize ? (int64_t)lzsize[ci * KSLOTS + k]
+                          : (int64_t)hd::stream_layout(sc + g0 + it[k].seg0, it[k].len, nullptr);
+      if (cb > maxout) cb = 0;                     // compress2 / LZ4_compress would not fit
       uint32_t israw = 0;
       if (cb == 0 || (uint64_t)cb >= neblock) {    // c-blosc: csize == neblock is raw
         if (nt + neblock > maxbytes) { memcpyed = 1; break; }
@@ -741,7 +746,7 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
   g.memcpyed = memcpyed;
   geom[ci] = g;
   uint32_t* dw = (uint32_t*)dst_base;
-  if (!memcpyed) {
+  if (!memcpyed && !lzsize) {
     // block bit positions; zero the two edge words of every emitted block
     for (uint32_t kk = 0; kk < cnt; kk++) {
       if (io[kk].raw) continue;
@@ -789,9 +794,10 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
       for (uint32_t j = 0; j < nspl; j++, kk++) {
         const uint32_t p = io[kk].pos;
         const uint32_t cs = io[kk].raw ? it[kk].len
-                                       : (uint32_t)hd::stream_layout(sc + g0 + it[kk].seg0, it[kk].len, nullptr);
+                            : lzsize ? lzsize[ci * KSLOTS + kk]
+                                     : (uint32_t)hd::stream_layout(sc + g0 + it[kk].seg0, it[kk].len, nullptr);
         for (int i = 0; i < 4; i++) out[p - 4 + i] = (uint8_t)(cs >> (8 * i));
-        if (!io[kk].raw) {
+        if (!io[kk].raw && !lzsize) {
           out[p] = 0x78;
           out[p + 1] = (uint8_t)hd::zlib_flg(level);
         }
@@ -825,6 +831,35 @@ __global__ void __launch_bounds__(64) emit_kernel(const uint32_t* __restrict__ s
     hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
     hd::emit_segment(sh, o, sc + s, sp + s, tok + (size_t)s * hd::SEG_TOK, job, dst_words);
     __syncthreads();
+  }
+}
+
+// LZ4 write path (lz4_enc.h): one thread per split walks its parse tokens, first
+// for the block size (-> layout_kernel), then to write the block into the frame
+__global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict__ slots,
+                                                       const uint32_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                       const hd::SegParse* __restrict__ sp,
+                                                       const uint16_t* __restrict__ tok,
+                                                       uint32_t* __restrict__ lzsize, uint32_t seg_cap, int level,
+                                                       const hsds_chunk_desc* __restrict__ chunks, uint8_t* dst_base,
+                                                       const EncGeom* __restrict__ geom,
+                                                       const ItemOut* __restrict__ iout,
+                                                       const int32_t* __restrict__ status, int write) {
+  const uint32_t total = offs[nchunks];
+  for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < total; item += gridDim.x * blockDim.x) {
+    const int64_t ci = item_chunk(offs, nchunks, item);
+    const uint32_t slot = (uint32_t)(ci * KSLOTS + (item - offs[ci]));
+    const EncItem it = slots[slot];
+    const uint32_t g0 = segoffs[ci] + it.seg0;
+    if (g0 + hd::nsegments(it.len) > seg_cap) continue;   // the layout phase fails the chunk
+    hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
+    if (!write) {
+      lzsize[slot] = lze::lz4_block(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, nullptr, 0);
+    } else {
+      if (status[ci] != HSDS_OK || geom[ci].memcpyed || iout[slot].raw) continue;
+      lze::lz4_block(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, dst_base + chunks[ci].dst_off + iout[slot].pos, 1);
+    }
   }
 }
 
@@ -1225,10 +1260,11 @@ int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const h
 }
 
 // ---- encode -----------------------------------------------------------------
-int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
-                      void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
-                      int shuffle, int typesize, void* stream) {
+int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                            void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
+                            int shuffle, int typesize, int cname, void* stream) {
   if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
+  if (cname != HSDS_CNAME_ZLIB && cname != HSDS_CNAME_LZ4 && cname != HSDS_CNAME_LZ4HC) return HSDS_ERR_ARG;
   if (clevel < 0 || clevel > 9 || (shuffle != HSDS_SHUFFLE_NONE && shuffle != HSDS_SHUFFLE_BYTE)) return HSDS_ERR_ARG;
   if (((uintptr_t)d_dst & 3u) != 0) return HSDS_ERR_ARG;
   if (nchunks == 0) return HSDS_OK;
@@ -1252,8 +1288,9 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
   const size_t sz_sc = al((size_t)seg_cap * sizeof(hd::SegCode));
   const size_t sz_so = al((size_t)seg_cap * sizeof(hd::SegOut));
   const size_t sz_meta = al((size_t)seg_cap * sizeof(SegMeta));
+  const size_t sz_lzsize = al(ns * 4);
   const size_t need = sz_slots + sz_adler + sz_iout + 2 * sz_counts + 2 * sz_offs + sz_geom + sz_sp + sz_sc + sz_so +
-                      sz_meta + 256;
+                      sz_meta + sz_lzsize + 256;
   if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
   uint8_t* w = e->ews;
   EncItem* slots = (EncItem*)w; w += sz_slots;
@@ -1268,6 +1305,7 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
   hd::SegCode* sc = (hd::SegCode*)w; w += sz_sc;
   hd::SegOut* so = (hd::SegOut*)w; w += sz_so;
   SegMeta* meta = (SegMeta*)w; w += sz_meta;
+  uint32_t* lzsize = (uint32_t*)w; w += sz_lzsize;
   uint32_t* ctr = (uint32_t*)w;    // [0] parse items, [1] huffman segments, [2] emit segments
   // token slots: SEG_TOK per segment
   if (grow((void**)&e->escr, &e->escr_bytes, (size_t)seg_cap * hd::SEG_TOK * 2 + 256)) return HSDS_ERR_DEVICE;
@@ -1276,7 +1314,7 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
   hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, slots,
-                     counts, segcnt, geom, d_status, clevel, shuffle, typesize);
+                     counts, segcnt, geom, d_status, clevel, shuffle, typesize, cname);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, segcnt, segoffs, nchunks);
   auto grid_for = [&](int per_cu, int64_t cap) {
@@ -1287,17 +1325,34 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
   hipEventRecord(e->ev2, st);
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, nchunks * KSLOTS)), dim3(64), 0, st, slots,
                      offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, clevel);
-  hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs, nchunks,
-                     ctr + 1, sp, meta, sc, seg_cap, clevel);
-  hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
-                     segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel);
-  hipLaunchKernelGGL(emit_kernel, dim3(grid_for(e->emit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs, nchunks,
-                     ctr + 2, so, sc, sp, tok, slots, (uint32_t*)d_dst, seg_cap, clevel);
+  if (cname == HSDS_CNAME_ZLIB) {
+    hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
+                       nchunks, ctr + 1, sp, meta, sc, seg_cap, clevel);
+    hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
+                       segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(emit_kernel, dim3(grid_for(e->emit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
+                       nchunks, ctr + 2, so, sc, sp, tok, slots, (uint32_t*)d_dst, seg_cap, clevel);
+  } else {
+    const unsigned lgrid = grid_for(4, (nchunks * KSLOTS + 63) / 64);
+    hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
+                       seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0);
+    hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
+                       segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)lzsize);
+    hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
+                       seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 1);
+  }
   hipLaunchKernelGGL(raw_copy_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
                      nchunks, (uint8_t*)d_dst, slots, counts, geom, iout, d_status);
   hipEventRecord(e->ev3, st);
   e->ev_enc_valid = 1;
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                      void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
+                      int shuffle, int typesize, void* stream) {
+  return hsds_encode_batch_codec(e, d_src, d_chunks, nchunks, d_dst, dst_extent, d_sizes, d_status, clevel, shuffle,
+                                 typesize, HSDS_CNAME_ZLIB, stream);
 }
 
 int hsds_last_deflate_ms(hsds_engine* e, float* ms) {
@@ -1306,8 +1361,8 @@ int hsds_last_deflate_ms(hsds_engine* e, float* ms) {
   return HSDS_OK;
 }
 
-int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize, void* dst,
-                      int64_t cap) {
+int64_t hsds_compress_codec(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize,
+                            int cname, void* dst, int64_t cap) {
   if (!e || n < 0 || (n && !src) || !dst || cap < n + 16) return HSDS_ERR_ARG;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
   const size_t desc_off = ((size_t)n + 255) & ~(size_t)255;
@@ -1321,8 +1376,8 @@ int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, in
   int32_t* dstat = (int32_t*)(e->h_dev_dst + stat_off + 16);
   if (n && hipMemcpy(e->h_dev_src, src, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
   if (hipMemcpy(dd, &c, sizeof(c), hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
-  int r = hsds_encode_batch(e, e->h_dev_src, dd, 1, e->h_dev_dst, frame_cap, dsize, dstat, clevel, shuffle, typesize,
-                            nullptr);
+  int r = hsds_encode_batch_codec(e, e->h_dev_src, dd, 1, e->h_dev_dst, frame_cap, dsize, dstat, clevel, shuffle,
+                                  typesize, cname, nullptr);
   if (r) return r;
   int32_t status = 0;
   int64_t size = 0;
@@ -1332,6 +1387,11 @@ int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, in
   if (size < 16 || size > cap) return HSDS_ERR_SIZE;
   if (hipMemcpy(dst, e->h_dev_dst, (size_t)size, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
   return size;
+}
+
+int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize, void* dst,
+                      int64_t cap) {
+  return hsds_compress_codec(e, src, n, clevel, shuffle, typesize, HSDS_CNAME_ZLIB, dst, cap);
 }
 
 }  // extern "C"

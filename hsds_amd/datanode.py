@@ -732,8 +732,8 @@ class ChunkStore:
 
     def flush(self, put, filter_ops=None, keys=None):
         """s3sync for every dirty chunk (datanode_lib.py:1186-1318, 126-311): ONE
-        hsds_encode_batch straight from the HBM cache slots (storUtil._compress's
-        F1 Blosc-zlib frames with the dataset's level and shuffle flag; no compressor
+        hsds_encode_batch_codec straight from the HBM cache slots (storUtil._compress's
+        Blosc frames with the dataset's codec (zlib, lz4, lz4hc), level and shuffle flag; no compressor
         -> the raw bytes, putStorBytes semantics), one device-to-host copy of the
         frames, `put(key, bytes)` per chunk, then clearDirty.  `keys` maps chunk id ->
         storage key (default: hsds_amd.partition.getS3Key).  Returns the flushed ids."""
@@ -746,8 +746,10 @@ class ChunkStore:
         abase = self.cache.arena.buf
         nodes = [self.cache._lru[k] for k in ids]
         comp = (filter_ops or {}).get("compressor")
-        if comp and comp not in ("gzip", "deflate", "zlib"):
-            raise NotImplementedError(f"Blosc codec {comp!r} is outside the hsds_amd engine scope")
+        if comp == "scaleoffset":
+            comp = None
+        if comp and nat.cname_code(comp) is None:
+            raise NotImplementedError(f"Blosc codec {comp!r} has no encoder in the hsds_amd engine")
         if (filter_ops or {}).get("shuffle") == 2:
             raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
         if comp:
@@ -760,7 +762,7 @@ class ChunkStore:
             sizes = torch.zeros(len(ids), dtype=torch.int64, device=abase.device)
             status = torch.full((len(ids),), 99, dtype=torch.int32, device=abase.device)
             self.reader.eng.encode(abase, descs, frames, sizes, status, clevel=level,
-                                   shuffle=int(filter_ops.get("shuffle") or 0), typesize=1)
+                                   shuffle=int(filter_ops.get("shuffle") or 0), typesize=1, compressor=comp)
             st = status.cpu().numpy()
             if (st != 0).any():
                 raise HTTPInternalServerError()

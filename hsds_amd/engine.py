@@ -72,22 +72,27 @@ class ChunkEngine:
     def last_inflate_ms(self):
         return self.eng.last_inflate_ms()
 
-    def encode(self, src, chunk_descs, dst, sizes, status, clevel=5, shuffle=1, typesize=1, stream=None):
+    def encode(self, src, chunk_descs, dst, sizes, status, clevel=5, shuffle=1, typesize=1, stream=None,
+               compressor="zlib"):
         """Asynchronously encode the chunks `chunk_descs` (src_off/src_len in `src`)
-        into HSDS F1 objects -- Blosc1 frames with the zlib codec, exactly what
-        storUtil._compress stores (storUtil.py:238-281) -- at dst_off in `dst`
+        into HSDS objects -- Blosc1 frames with the zlib (default), lz4 or lz4hc codec,
+        what storUtil._compress stores (storUtil.py:238-281) -- at dst_off in `dst`
         (dst_len = capacity >= src_len + 16).  Frame sizes land in `sizes` (int64
         device tensor), HSDS_* status codes in `status` (int32)."""
+        cname = nat.cname_code(compressor)
+        if cname is None:
+            raise NotImplementedError(f"Blosc codec {compressor!r} has no encoder in the hsds_amd engine")
         if isinstance(chunk_descs, np.ndarray):
             n = chunk_descs.size
             chunk_descs = to_device_bytes(chunk_descs, self.device)
         else:
             n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
-        rc = nat.lib().hsds_encode_batch(self.eng.h, _ptr(src), _ptr(chunk_descs), n, _ptr(dst),
-                                         dst.numel() * dst.element_size(), _ptr(sizes), _ptr(status),
-                                         int(clevel), int(shuffle), int(typesize), _stream_handle(stream))
+        rc = nat.lib().hsds_encode_batch_codec(self.eng.h, _ptr(src), _ptr(chunk_descs), n, _ptr(dst),
+                                               dst.numel() * dst.element_size(), _ptr(sizes), _ptr(status),
+                                               int(clevel), int(shuffle), int(typesize), cname,
+                                               _stream_handle(stream))
         if rc != nat.OK:
-            raise nat.NativeError(rc, "hsds_encode_batch")
+            raise nat.NativeError(rc, "hsds_encode_batch_codec")
         return chunk_descs
 
     def last_deflate_ms(self):

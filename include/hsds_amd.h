@@ -18,6 +18,8 @@
  *   hsds_compress        <- storUtil.py:238  _compress(data, compressor, level, shuffle, dtype, chunk_shape)
  *   hsds_encode_batch    <- the per-chunk _compress of putStorBytes (storUtil.py:584-600) reached from
  *                           write_s3_obj (hsds/datanode_lib.py:126-311), batched over many dirty chunks
+ *   hsds_encode_batch_codec / hsds_compress_codec
+ *                        <- the same with Blosc(cname = "lz4" / "lz4hc") (storUtil.py:255-262)
  *
  * Threading: an engine is bound to one device and may be used from one host thread
  * at a time (HSDS data nodes are single-threaded asyncio processes).  All *_batch
@@ -47,6 +49,11 @@ extern "C" {
 #define HSDS_COMP_NONE 0        /* None / "scaleoffset"                           */
 #define HSDS_COMP_ZLIB 1        /* "gzip" / "deflate" / "zlib"                    */
 #define HSDS_COMP_OTHER 2       /* lz4 / lz4hc / blosclz / ...: Blosc frames only  */
+
+/* Blosc inner codec of the write path (storUtil._compress cname) */
+#define HSDS_CNAME_ZLIB 0       /* "gzip" / "deflate" / "zlib": Blosc codec 3      */
+#define HSDS_CNAME_LZ4 1        /* "lz4": Blosc codec 1, c-blosc's lz4 blocksize   */
+#define HSDS_CNAME_LZ4HC 2      /* "lz4hc": Blosc codec 1, HCR blocksize           */
 
 /* shuffle codes (storUtil.BYTE_SHUFFLE / BIT_SHUFFLE) */
 #define HSDS_SHUFFLE_NONE 0
@@ -158,10 +165,20 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
                       void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
                       int shuffle, int typesize, void* stream);
 
+/* The same with the Blosc inner codec `cname` (HSDS_CNAME_*): lz4 / lz4hc frames
+ * carry LZ4 blocks (any valid block; the frame layout follows c-blosc 1.21 for that
+ * codec).  hsds_encode_batch == cname HSDS_CNAME_ZLIB. */
+int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
+                            void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
+                            int shuffle, int typesize, int cname, void* stream);
+
 /* Host-buffer single object: mirrors storUtil._compress for the zlib compressor.
  * Returns the frame size (<= cap; cap must be >= n + 16) or a negative HSDS_ERR_*. */
 int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize,
                       void* dst, int64_t cap);
+/* ... and for any HSDS_CNAME_* */
+int64_t hsds_compress_codec(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize,
+                            int cname, void* dst, int64_t cap);
 
 /* Device time (ms) of the deflate kernel of the most recent hsds_encode_batch. */
 int hsds_last_deflate_ms(hsds_engine* e, float* ms);

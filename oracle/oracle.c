@@ -311,11 +311,14 @@ int64_t orc_uncompress(const uint8_t *src, int64_t srclen, int compressor, int s
  * split exactly as c-blosc's zlib_wrap_compress.  dst must hold nbytes + 16. */
 static int split_ok(int ts, int64_t bs) { return ts <= 16 && bs / ts >= 128; }
 
-int64_t orc_blosc_blocksize(int clevel, int ts, int64_t nbytes) {
+/* c-blosc 1.21 compute_blocksize.  hcr: the high-compression-ratio codecs (zlib,
+ * lz4hc, zstd) start from L1 x 2 and double again at level 9; lz4 / blosclz start
+ * from L1 (32 KiB).  Pinned against libblosc 1.21.0 by the codec2 golden table. */
+int64_t orc_blosc_blocksize_codec(int clevel, int ts, int64_t nbytes, int hcr) {
   if (nbytes < ts) return 1;
   int64_t bs = nbytes;
   if (nbytes >= 32 * 1024) {
-    bs = 32 * 1024 * 2; /* L1 x 2 for the HCR zlib codec */
+    bs = hcr ? 32 * 1024 * 2 : 32 * 1024;
     switch (clevel) {
       case 0: bs /= 4; break;
       case 1: bs /= 2; break;
@@ -323,7 +326,7 @@ int64_t orc_blosc_blocksize(int clevel, int ts, int64_t nbytes) {
       case 3: bs *= 2; break;
       case 4: case 5: bs *= 4; break;
       case 6: case 7: case 8: bs *= 8; break;
-      default: bs *= 16; break; /* 9: x8, x2 for HCR codecs */
+      default: bs *= hcr ? 16 : 8; break; /* 9: x8, x2 for HCR codecs */
     }
   }
   if (clevel > 0 && split_ok(ts, bs)) {
@@ -336,6 +339,8 @@ int64_t orc_blosc_blocksize(int clevel, int ts, int64_t nbytes) {
   if (bs > ts) bs = bs / ts * ts;
   return bs;
 }
+
+int64_t orc_blosc_blocksize(int clevel, int ts, int64_t nbytes) { return orc_blosc_blocksize_codec(clevel, ts, nbytes, 1); }
 
 /* Greedy LZ4 block writer (4-byte hash, distance <= 65535) obeying the block end
  * rules LZ4_decompress_safe checks: the last match starts at least MFLIMIT (12) bytes

@@ -58,6 +58,8 @@ def lib():
         L.orc_blosc_encode_lz4.restype = I64
         L.orc_lz4_encode.argtypes = [P, I64, P, I64]
         L.orc_lz4_encode.restype = I64
+        L.orc_blosc_blocksize_codec.argtypes = [I, I, I64, I]
+        L.orc_blosc_blocksize_codec.restype = I64
         L.orc_blosc_blocksize.argtypes = [I, I, I64]
         L.orc_blosc_blocksize.restype = I64
         L.orc_zlib_encode.argtypes = [P, I64, I, P, I64]
@@ -163,6 +165,11 @@ def lz4_encode(data):
     if n < 0:
         raise RuntimeError(f"lz4 encode error {n}")
     return out[:n].tobytes()
+
+
+def blosc_blocksize_codec(clevel, typesize, nbytes, cname):
+    """c-blosc 1.21 compute_blocksize for cname (zlib / lz4hc / zstd are HCR codecs)"""
+    return lib().orc_blosc_blocksize_codec(clevel, typesize, nbytes, 0 if cname in ("lz4", "blosclz") else 1)
 
 
 def blosc_blocksize(clevel, typesize, nbytes):

@@ -7,6 +7,7 @@
 #include <string.h>
 #include <vector>
 #include "../../hsds_amd/csrc/deflate_wave.h"
+#include "../../hsds_amd/csrc/lz4_enc.h"
 
 static int64_t run(const hd::EncJob& job, const hd::Tune& tune, uint8_t* dst, uint32_t cap) {
   const uint32_t nseg = hd::nsegments(job.len);
@@ -67,6 +68,22 @@ extern "C" int64_t emu_deflate_shuffled(const uint8_t* block, uint32_t n, uint8_
                                         uint32_t ts, uint32_t neb, uint32_t off) {
   hd::EncJob job = {block, n, level, ts, neb, off};
   return run(job, hd::tune_for_level(level), dst, cap);
+}
+
+// LZ4 block of one split: the parse phase, then the lz4_enc.h token walk (size pass,
+// then write pass).  Returns the block size or -1 when it would exceed cap.
+extern "C" int64_t emu_lz4_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level) {
+  const uint32_t nseg = hd::nsegments(n);
+  std::vector<hd::SegParse> sp(nseg);
+  std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
+  hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
+  hd::EncJob job = {src, n, level, 1u, 0u, 0u};
+  hd::parse_stream(*ps, job, hd::tune_for_level(level), sp.data(), tok.data());
+  free(ps);
+  const uint32_t sz = lze::lz4_block(sp.data(), tok.data(), job, nullptr, 0);
+  if (sz > cap) return -1;
+  const uint32_t sz2 = lze::lz4_block(sp.data(), tok.data(), job, dst, 1);
+  return sz2 == sz ? (int64_t)sz : -2;
 }
 
 extern "C" int emu_parse_shared_bytes() { return (int)sizeof(hd::ParseShared); }

@@ -128,9 +128,19 @@ def main():
         # c-blosc 1.21 blosc_decompress takes no source size and reads past the end of a
         # truncated object; the engine rejects it (header cbytes > object length)
         add(f"err_{comp}_trunc", good[:-7], ops, "truncated frame: reference reads past the object end")
+    # ---- c-blosc 1.21 frame header fields per codec (compute_blocksize, split flag)
+    hdr = []
+    base = data("smooth", 1 << 20, "<i4", 5).tobytes()
+    for cname in ("lz4", "lz4hc", "blosclz", "zlib"):
+        for lv in range(10):
+            for ts in (1, 2, 4, 8, 16, 32):
+                for nb in (1 << 22, 1 << 20, 262144, 100000, 40000, 32768, 5000, 100):
+                    f = refshim.blosc_compress_raw(base[:nb], lv, 1, ts, cname=cname)
+                    hdr.append({"cname": cname, "clevel": lv, "typesize": ts, "nbytes": nb, "flags": f[2],
+                                "blocksize": int(np.frombuffer(f[8:12], "<u4")[0])})
     np.savez_compressed(os.path.join(HERE, "codec2_cases.npz"), **arrays)
     with open(os.path.join(HERE, "codec2_cases.json"), "w") as fh:
-        json.dump({"cases": cases}, fh, indent=1)
+        json.dump({"cases": cases, "headers": hdr}, fh, indent=1)
     print("wrote", len(cases), "cases;", sum(c["status"] == "error" for c in cases), "errors")
 
 

@@ -221,3 +221,48 @@ def test_put_selections_and_flush(dev, oracle_lib):
     res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in ids], dt, dims, filter_ops=ops)
     for cid, r in zip(ids, res):
         assert r.cpu().numpy().tobytes() == want[cid].tobytes()
+
+
+def test_put_and_flush_lz4_dataset(dev, oracle_lib):
+    """An lz4-filtered dataset (getFilterOps -> compressor "lz4"): PUT_Chunk on stored
+    Blosc-lz4 objects, flush through the GPU lz4 encoder, objects decode through the
+    oracle (frame walk + LZ4) and read back through the GPU LZ4 decoder."""
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    from hsds_amd.filters import getFilterOps
+    orc = oracle_lib
+    dims = (128, 256)
+    dt = np.dtype("<i4")
+    rng = np.random.default_rng(12)
+    ops = getFilterOps({"filter_map": {}}, "d-l", [{"class": "H5Z_FILTER_SHUFFLE", "id": 2, "name": "shuffle"},
+                                                   {"class": "H5Z_FILTER_LZ4", "id": 32004, "name": "lz4"}],
+                       dtype=dt, chunk_shape=dims)
+    assert ops["compressor"] == "lz4" and ops["level"] == 5
+    truth, store = {}, {}
+    for i in range(4):
+        a = (np.cumsum(rng.normal(size=dims[0] * dims[1])) * 10).astype(dt).reshape(dims)
+        truth[f"c-l_{i}_0"] = a
+        store[f"k{i}"] = orc.blosc_encode_lz4(a.tobytes(), typesize=1, blocksize=131072, shuffle=1)
+    keys = {f"c-l_{i}_0": f"k{i}" for i in range(4)}
+    cs = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    sel = (slice(7, 120, 3), slice(0, 256, 5))
+    d = rng.integers(-1000, 1000, size=(len(range(7, 120, 3)), len(range(0, 256, 5)))).astype(dt)
+    writes = [(ChunkRead(f"c-l_{i}_0", f"k{i}"), sel, d) for i in (0, 2, 3)]
+    assert cs.put_selections(writes, dt, dims, filter_ops=ops) == [True, True, True]
+    flushed = {}
+    ids = cs.flush(lambda k, b: flushed.__setitem__(k, b), filter_ops=ops, keys=keys)
+    assert sorted(ids) == ["c-l_0_0", "c-l_2_0", "c-l_3_0"]
+    for cid in ids:
+        f = flushed[keys[cid]]
+        assert f[2] >> 5 == 1                      # Blosc codec 1: lz4
+        want = truth[cid].copy()
+        want[sel] = d
+        got = orc.uncompress(f, "lz4", 1, 4, want.nbytes)
+        assert got == want.tobytes(), cid
+    store.update(flushed)
+    cs2 = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in sorted(keys)], dt, dims, filter_ops=ops)
+    for cid, r in zip(sorted(keys), res):
+        want = truth[cid].copy()
+        if cid in ids:
+            want[sel] = d
+        assert r.cpu().numpy().tobytes() == want.tobytes(), cid

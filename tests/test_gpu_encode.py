@@ -97,7 +97,9 @@ def test_compress_passthrough_and_errors(dev):
     with pytest.raises(NotImplementedError):
         codec._compress(data, compressor="zlib", shuffle=2)
     with pytest.raises(NotImplementedError):
-        codec._compress(data, compressor="lz4")
+        codec._compress(data, compressor="zstd")
+    with pytest.raises(NotImplementedError):
+        codec._compress(data, compressor="blosclz")
 
 
 @pytest.mark.parametrize("ts", [2, 4, 8, 32])
@@ -217,3 +219,91 @@ def test_streams_equal_cpu_emulation(dev):
             r = L.emu_deflate(blk.ctypes.data, len(blk), out.ctypes.data, len(blk) + 4096, level, 0)
             assert r == cs, (seed, b, r, cs)
             assert out.view(np.uint8)[:r].tobytes() == fb[start + 4:start + 4 + cs].tobytes(), (seed, b)
+
+
+# ---- the lz4 / lz4hc write path (Blosc codec 1, LZ4 blocks from the parse tokens) ----
+
+@pytest.mark.parametrize("name", sorted(INPUTS))
+@pytest.mark.parametrize("cname,level", [("lz4", 5), ("lz4hc", 5), ("lz4", 1), ("lz4", 9)])
+def test_lz4_compress_decodes_through_oracle_and_gpu(dev, oracle_lib, name, cname, level):
+    """storUtil._compress(compressor="lz4"/"lz4hc"): header fields as c-blosc 1.21
+    writes them for that codec (blocksize rule pinned by the codec2 golden table),
+    and the object decodes to the input through the oracle and the GPU decoder."""
+    from hsds_amd import codec
+    data = INPUTS[name]()
+    frame = codec._compress(data, compressor=cname, level=level, shuffle=1)
+    h = header(frame)
+    n = len(data)
+    bs = oracle_lib.blosc_blocksize_codec(level, 1, n, cname)
+    assert (h["version"], h["versionlz"], h["typesize"], h["nbytes"], h["blocksize"]) == (2, 1, 1, n, bs)
+    assert h["cbytes"] == len(frame) <= n + 16
+    assert h["flags"] & 0xE1 == 0x21                   # codec 1 (lz4), shuffle flag
+    assert bool(h["flags"] & 0x02) == (n < 128 or h["flags"] & 0x02 != 0)
+    assert oracle_lib.uncompress(frame, cname, 1, 1, n) == data
+    if n:
+        assert codec._uncompress(frame, compressor=cname, shuffle=1, dtype=np.dtype("u1"), chunk_shape=(n,)) == data
+
+
+@pytest.mark.parametrize("ts", [2, 4, 8, 32])
+def test_lz4_batch_typesize_shuffle(dev, oracle_lib, ts):
+    import torch
+    from hsds_amd.engine import ChunkEngine, encode_descs
+    data = [smooth(500 + ts, 1 << 18), smooth(600 + ts, 65536 * 3 + 4 * ts), bytes(70000 // ts * ts)]
+    descs, sext, dext = encode_descs([len(d) for d in data])
+    src = np.zeros(max(sext, 1), np.uint8)
+    for d, r in zip(data, descs):
+        src[int(r["src_off"]):int(r["src_off"]) + len(d)] = np.frombuffer(d, np.uint8)
+    d_src = torch.from_numpy(src).to(dev)
+    d_dst = torch.zeros(dext, dtype=torch.uint8, device=dev)
+    sizes = torch.zeros(len(data), dtype=torch.int64, device=dev)
+    st = torch.full((len(data),), 99, dtype=torch.int32, device=dev)
+    eng = ChunkEngine(0)
+    eng.encode(d_src, descs, d_dst, sizes, st, clevel=5, shuffle=1, typesize=ts, compressor="lz4")
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    out = d_dst.cpu().numpy()
+    for d, r, n in zip(data, descs, sizes.cpu().numpy()):
+        frame = out[int(r["dst_off"]):int(r["dst_off"]) + int(n)].tobytes()
+        h = header(frame)
+        assert h["typesize"] == ts and h["blocksize"] == oracle_lib.blosc_blocksize_codec(5, ts, len(d), "lz4")
+        assert bool(h["flags"] & 0x10) == (not (ts <= 16 and h["blocksize"] // ts >= 128))
+        assert oracle_lib.uncompress(frame, "lz4", 1, ts, len(d)) == d
+
+
+def test_lz4_batch_mixed_gpu_roundtrip(dev, oracle_lib):
+    import torch
+    from hsds_amd.engine import ChunkEngine, encode_descs, pack_chunks
+    rng = np.random.default_rng(19)
+    data = []
+    for i in range(40):
+        k = i % 4
+        data.append(smooth(700 + i, 1 << 20) if k == 0 else
+                    (np.cumsum(rng.normal(size=131072)) * 100).astype("<i2").tobytes() if k == 1 else
+                    rng.integers(0, 256, 1 << 18, dtype=np.uint8).tobytes() if k == 2 else
+                    np.repeat(rng.integers(0, 9, 4000), 97).astype("<i4").tobytes())
+    descs, sext, dext = encode_descs([len(d) for d in data])
+    src = np.zeros(sext, np.uint8)
+    for d, r in zip(data, descs):
+        src[int(r["src_off"]):int(r["src_off"]) + len(d)] = np.frombuffer(d, np.uint8)
+    d_src = torch.from_numpy(src).to(dev)
+    d_dst = torch.zeros(dext, dtype=torch.uint8, device=dev)
+    sizes = torch.zeros(len(data), dtype=torch.int64, device=dev)
+    st = torch.full((len(data),), 99, dtype=torch.int32, device=dev)
+    eng = ChunkEngine(0)
+    eng.encode(d_src, descs, d_dst, sizes, st, clevel=5, shuffle=1, typesize=1, compressor="lz4")
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    out = d_dst.cpu().numpy()
+    frames = [out[int(r["dst_off"]):int(r["dst_off"]) + int(n)].tobytes() for r, n in zip(descs, sizes.cpu().numpy())]
+    for d, f in zip(data, frames):
+        assert oracle_lib.uncompress(f, "lz4", 1, 1, len(d)) == d
+    psrc, pdescs, ext = pack_chunks(frames, [len(d) for d in data])
+    g_src = torch.from_numpy(psrc).to(dev)
+    g_dst = torch.zeros(ext, dtype=torch.uint8, device=dev)
+    g_st = torch.full((len(data),), 99, dtype=torch.int32, device=dev)
+    eng.decode(g_src, pdescs, g_dst, g_st, compressor="lz4", shuffle=1, itemsize=1)
+    torch.cuda.synchronize()
+    assert (g_st.cpu().numpy() == 0).all()
+    dec = g_dst.cpu().numpy()
+    for d, r in zip(data, pdescs):
+        assert dec[int(r["dst_off"]):int(r["dst_off"]) + len(d)].tobytes() == d

@@ -132,3 +132,17 @@ def test_zlib_roundtrip(oracle_lib, level):
     assert zlib.decompress(c) == data
     assert oracle_lib.uncompress(c, "zlib", 0, 1, len(data)) == data
     assert oracle_lib.adler32(data) == zlib.adler32(data)
+
+
+def test_blosc_header_rule_all_codecs(golden2, oracle_lib):
+    """c-blosc 1.21 compute_blocksize and the dont-split flag for lz4 / lz4hc /
+    blosclz / zlib frames: 960 headers written by libblosc 1.21.0."""
+    meta, _ = golden2
+    rows = meta["headers"]
+    assert len(rows) >= 900
+    for r in rows:
+        bs = oracle_lib.blosc_blocksize_codec(r["clevel"], r["typesize"], r["nbytes"], r["cname"])
+        assert bs == r["blocksize"], r
+        ts = r["typesize"] if r["typesize"] <= 255 else 1
+        split = ts <= 16 and bs // ts >= 128
+        assert bool(r["flags"] & 0x10) == (not split), r
