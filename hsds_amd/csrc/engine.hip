@@ -834,8 +834,9 @@ __global__ void __launch_bounds__(64) emit_kernel(const uint32_t* __restrict__ s
   }
 }
 
-// LZ4 write path (lz4_enc.h): one thread per split walks its parse tokens, first
-// for the block size (-> layout_kernel), then to write the block into the frame
+// LZ4 write path (lz4_enc.h): one wavefront per split walks its parse tokens (each
+// lane its own token range), first for the block size (-> layout_kernel), then to
+// write the block into the frame
 __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict__ slots,
                                                        const uint32_t* __restrict__ offs,
                                                        const uint32_t* __restrict__ segoffs, int64_t nchunks,
@@ -847,7 +848,7 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
                                                        const ItemOut* __restrict__ iout,
                                                        const int32_t* __restrict__ status, int write) {
   const uint32_t total = offs[nchunks];
-  for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < total; item += gridDim.x * blockDim.x) {
+  for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
     const int64_t ci = item_chunk(offs, nchunks, item);
     const uint32_t slot = (uint32_t)(ci * KSLOTS + (item - offs[ci]));
     const EncItem it = slots[slot];
@@ -855,10 +856,12 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
     if (g0 + hd::nsegments(it.len) > seg_cap) continue;   // the layout phase fails the chunk
     hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
     if (!write) {
-      lzsize[slot] = lze::lz4_block(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, nullptr, 0);
+      const uint32_t sz = lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, nullptr, 0);
+      if (threadIdx.x == 0) lzsize[slot] = sz;
     } else {
       if (status[ci] != HSDS_OK || geom[ci].memcpyed || iout[slot].raw) continue;
-      lze::lz4_block(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, dst_base + chunks[ci].dst_off + iout[slot].pos, 1);
+      lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job,
+                          dst_base + chunks[ci].dst_off + iout[slot].pos, 1);
     }
   }
 }
@@ -1333,7 +1336,7 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
     hipLaunchKernelGGL(emit_kernel, dim3(grid_for(e->emit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 2, so, sc, sp, tok, slots, (uint32_t*)d_dst, seg_cap, clevel);
   } else {
-    const unsigned lgrid = grid_for(4, (nchunks * KSLOTS + 63) / 64);
+    const unsigned lgrid = grid_for(16, nchunks * KSLOTS);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                        seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,

@@ -8,12 +8,12 @@
 //
 // The match finding is the deflate encoder's parse phase (deflate_wave.h P: exact hash
 // chains over an 8 KiB window, lane-parallel greedy parse, tokens in HBM).  This file
-// turns one split's token list into an LZ4 block: one lane per split walks the tokens
-// in order (a serial, byte-granular walk over ~10^4 sequences, which the batch runs on
-// thousands of splits at once), length-3 matches become literals, and the block end
-// rules LZ4_decompress_safe enforces are kept (the last match starts at least MFLIMIT
-// = 12 bytes before the end and ends at least LASTLITERALS = 5 bytes before it).
-// The walk runs twice: once for the size (frame layout), once to write.
+// turns one split's token list into an LZ4 block, one wavefront per split (each lane
+// keeps the token range the parse gave it; see lz4_block_wave), length-3 matches
+// become literals, and the block end rules LZ4_decompress_safe enforces are kept (the
+// last match starts at least MFLIMIT = 12 bytes before the end and ends at least
+// LASTLITERALS = 5 bytes before it).  The walk runs twice: once for the size (frame
+// layout), once to write.
 //
 // Single source: tests/emu/deflate_emu.cpp runs the same walk on CPU.
 #pragma once
@@ -75,62 +75,143 @@ HZ_HD void sequence(Out& o, InRd& in, uint32_t l0, uint32_t l1, uint32_t dist, u
   }
 }
 
+HZ_HD uint32_t ext_len(uint32_t v) { return v >= 15u ? (v - 15u) / 255u + 1u : 0u; }
+// bytes of a sequence with `run` literals and a match of ml bytes (ml == 0: none)
+HZ_HD uint32_t seq_size(uint32_t run, uint32_t ml) { return 1u + ext_len(run) + run + (ml ? 2u + ext_len(ml - 4u) : 0u); }
+
+// Walk lane `lane`'s parse tokens of one segment (input [p0, p1)); calls
+// f(pos, ml, dist) for every match the LZ4 block keeps, in order.  Length-3 matches
+// and matches breaking the block end rules (start within MFLIMIT = 12 bytes of the
+// end, or ending within LASTLITERALS = 5) become literals / are shortened.
+template <class F>
+HZ_HD void lane_matches(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, uint32_t n, F&& f) {
+  uint32_t pos = p0, pend = 0;
+  bool have = false;
+  for (uint32_t s = 0; s < ns; s++) {
+    uint32_t t;
+    if (!have) {
+      const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)hd::tslot(s, lane) * 2u);
+      t = pr & 0xffffu; pend = pr >> 16; have = true;
+    } else {
+      t = pend; have = false;
+    }
+    if (!(t & 0x8000u)) { pos++; continue; }
+    uint32_t dv;
+    s++;
+    if (!have) {
+      const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)hd::tslot(s, lane) * 2u);
+      dv = pr & 0xffffu; pend = pr >> 16; have = true;
+    } else {
+      dv = pend; have = false;
+    }
+    const uint32_t len = (t & 0x7fffu) + 3u;
+    if (len >= 4u && pos + 12u <= n) f(pos, pos + len + 5u > n ? n - 5u - pos : len, dv + 1u);   // ml >= 7 when cut
+    pos += len;
+  }
+}
+
 // The LZ4 block of one split from its parse tokens (sp / tok: the split's first
-// segment).  Returns the block size; writes it to out when `write`.
-HZ_HD uint32_t lz4_block(const hd::SegParse* sp, const uint16_t* tok, const hd::EncJob& job, uint8_t* out,
-                         int write) {
+// segment), one wavefront: the 64 lanes take the token ranges the parse gave them
+// (an equal 1/64 of each segment).  A sequence belongs to the lane holding its match;
+// its literal run may begin in earlier lanes or segments, so each lane's run-in
+// length comes from a segmented scan (reset at every lane with a match), and lane
+// output offsets from a prefix sum.  write == 0: returns the block size; write == 1:
+// writes the block to out (and returns the size).
+HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const hd::EncJob& job, uint8_t* out,
+                              int write) {
   const uint32_t n = job.len;
   const uint32_t nseg = hd::nsegments(n);
-  Out o = {HZ_GLOBAL(hz_gu8*, out), 0u, write};
-  InRd in;
-  in_init(in, job);
-  uint32_t pos = 0, lit0 = 0;
-  // the last sequence is held back: a match that continues it (no literals in
-  // between, same distance) extends it, so runs longer than deflate's 258-byte
-  // matches become one LZ4 match
-  uint32_t q0 = 0, q1 = 0, qd = 0, qml = 0;
-  int have_q = 0;
+  uint32_t carry = 0;      // literals pending from earlier segments
+  uint32_t base = 0;       // output bytes of earlier segments
+  LANE_VAR(uint32_t, sv);  // scan value: literals carried past this lane
+  LANE_VAR(uint32_t, sr);  // 1: the lane has a match (the scan resets)
+  LANE_VAR(uint32_t, osz); // output bytes of the lane's sequences
+  LANE_VAR(uint32_t, hh);  // literals before the lane's first match
+  LANE_VAR(uint32_t, fml); // first match length
+  LANE_VAR(uint32_t, rest);
+  LANE_VAR(uint32_t, cin); // literal run entering the lane
   for (uint32_t sg = 0; sg < nseg; sg++) {
+    const uint32_t s0 = sg * (uint32_t)hd::SEG;
+    const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
+    const uint32_t R = (seglen + hd::WAVE - 1) / hd::WAVE;
     hz_gcu8* const gtok = HZ_GLOBAL(hz_gcu8*, tok + (size_t)sg * hd::SEG_TOK);
-    for (int lane = 0; lane < hd::WAVE; lane++) {
-      const uint32_t ns = sp[sg].nslot[lane];
-      uint32_t pend = 0;
-      bool have = false;
-      for (uint32_t s = 0; s < ns; s++) {
-        uint32_t t;
-        if (!have) {
-          const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)hd::tslot(s, lane) * 2u);
-          t = pr & 0xffffu; pend = pr >> 16; have = true;
-        } else {
-          t = pend; have = false;
+    LANE_LOOP {
+      const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
+      const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+      uint32_t has = 0, h = 0, ml0 = 0, rs = 0, lit0 = s0 + a0;
+      lane_matches(gtok, sp[sg].nslot[lane], lane, s0 + a0, n, [&](uint32_t pos, uint32_t ml, uint32_t) {
+        if (!has) { has = 1; h = pos - lit0; ml0 = ml; } else { rs += seq_size(pos - lit0, ml); }
+        lit0 = pos + ml;
+      });
+      LV(sr) = has;
+      LV(sv) = has ? s0 + a1 - lit0 : a1 - a0;
+      LV(hh) = h; LV(fml) = ml0; LV(rest) = rs;
+    }
+    // segmented exclusive scan of the carried literals, seeded with `carry`
+    uint32_t seg_carry, seg_total;
+#if HZ_GPU
+    {
+      const int lane = (int)threadIdx.x;
+      uint32_t v = sv, r = sr;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t pv = __shfl_up(v, o, 64), pr = __shfl_up(r, o, 64);
+        if (lane >= o && !r) { v += pv; r = pr; }
+      }
+      uint32_t ev = __shfl_up(v, 1, 64), er = __shfl_up(r, 1, 64);
+      if (lane == 0) { ev = 0; er = 0; }
+      cin = er ? ev : carry + ev;
+      const uint32_t lv = __shfl(v, 63, 64), lr = __shfl(r, 63, 64);
+      seg_carry = lr ? lv : carry + lv;
+      osz = sr ? seq_size(cin + hh, fml) + rest : 0u;
+      const uint32_t ox = hz::wave_excl_scan(osz, lane);
+      seg_total = __shfl(ox + osz, 63, 64);
+      osz = ox;               // from here on: the lane's output offset in the segment
+    }
+#else
+    {
+      uint32_t v = carry;
+      for (int lane = 0; lane < 64; lane++) { cin[lane] = v; v = sr[lane] ? sv[lane] : v + sv[lane]; }
+      seg_carry = v;
+      uint32_t acc = 0;
+      for (int lane = 0; lane < 64; lane++) {
+        const uint32_t z = sr[lane] ? seq_size(cin[lane] + hh[lane], fml[lane]) + rest[lane] : 0u;
+        osz[lane] = acc;
+        acc += z;
+      }
+      seg_total = acc;
+    }
+#endif
+    if (write) {
+      LANE_LOOP {
+        if (LV(sr)) {
+          const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
+          Out o = {HZ_GLOBAL(hz_gu8*, out + base + LV(osz)), 0u, 1};
+          InRd in;
+          in_init(in, job);
+          uint32_t lit0 = s0 + a0 - LV(cin);
+          lane_matches(gtok, sp[sg].nslot[lane], lane, s0 + a0, n, [&](uint32_t pos, uint32_t ml, uint32_t dist) {
+            sequence(o, in, lit0, pos, dist, ml);
+            lit0 = pos + ml;
+          });
         }
-        if (!(t & 0x8000u)) { pos++; continue; }
-        uint32_t dv;
-        s++;
-        if (!have) {
-          const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)hd::tslot(s, lane) * 2u);
-          dv = pr & 0xffffu; pend = pr >> 16; have = true;
-        } else {
-          dv = pend; have = false;
-        }
-        const uint32_t len = (t & 0x7fffu) + 3u;
-        if (len >= 4u && pos + 12u <= n) {
-          const uint32_t ml = pos + len + 5u > n ? n - 5u - pos : len;   // >= 7 here
-          if (have_q && lit0 == pos && q1 + qml == pos && qd == dv + 1u) {
-            qml += ml;
-          } else {
-            if (have_q) sequence(o, in, q0, q1, qd, qml);
-            q0 = lit0; q1 = pos; qd = dv + 1u; qml = ml; have_q = 1;
-          }
-          lit0 = pos + ml;
-        }
-        pos += len;
+      }
+      WAVE_SYNC();
+    }
+    carry = seg_carry;
+    base += seg_total;
+  }
+  // the final literals-only sequence
+  if (write) {
+    LANE_LOOP {
+      if (lane == 0) {
+        Out o = {HZ_GLOBAL(hz_gu8*, out + base), 0u, 1};
+        InRd in;
+        in_init(in, job);
+        sequence(o, in, n - carry, n, 0u, 0u);
       }
     }
   }
-  if (have_q) sequence(o, in, q0, q1, qd, qml);
-  sequence(o, in, lit0, n, 0u, 0u);
-  return o.n;
+  return base + seq_size(carry, 0u);
 }
 
 }  // namespace lze

@@ -80,9 +80,9 @@ extern "C" int64_t emu_lz4_block(const uint8_t* src, uint32_t n, uint8_t* dst, u
   hd::EncJob job = {src, n, level, 1u, 0u, 0u};
   hd::parse_stream(*ps, job, hd::tune_for_level(level), sp.data(), tok.data());
   free(ps);
-  const uint32_t sz = lze::lz4_block(sp.data(), tok.data(), job, nullptr, 0);
+  const uint32_t sz = lze::lz4_block_wave(sp.data(), tok.data(), job, nullptr, 0);
   if (sz > cap) return -1;
-  const uint32_t sz2 = lze::lz4_block(sp.data(), tok.data(), job, dst, 1);
+  const uint32_t sz2 = lze::lz4_block_wave(sp.data(), tok.data(), job, dst, 1);
   return sz2 == sz ? (int64_t)sz : -2;
 }
 
