@@ -146,10 +146,10 @@ def _uncompress(data, compressor=None, shuffle=0, level=None, dtype=None, chunk_
 def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape=None):
     """storUtil._compress (storUtil.py:238-281) on the GPU: a Blosc1 frame with the
     inner codec cname = compressor (gzip/deflate/zlib are all Blosc "zlib",
-    storUtil.py:255-257; lz4 and lz4hc carry LZ4 blocks), typesize 1 because the
+    storUtil.py:255-257; lz4 and lz4hc carry LZ4 blocks, blosclz BloscLZ), typesize 1 because the
     reference always hands Blosc a bytes object, and the byte-shuffle flag from
     `shuffle`.  Differences from the reference, by design:
-      * bitshuffle (shuffle=2) and the blosclz / zstd encoders are outside this engine
+      * bitshuffle (shuffle=2) and the zstd encoder are outside this engine
         and raise NotImplementedError (the reference would encode them with c-blosc);
       * an encoder failure raises instead of silently storing the raw bytes
         (storUtil.py:266-279 logs and returns `data`, which its own reader then

@@ -564,12 +564,13 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
   const uint64_t nbytes = c.src_len;
   int st = HSDS_OK;
   uint32_t cnt = 0, nseg = 0;
-  const uint32_t fmt = cname == HSDS_CNAME_ZLIB ? 3u : 1u;   // Blosc1 codec: zlib 3, lz4 / lz4hc 1
+  // Blosc1 codec: zlib 3, lz4 / lz4hc 1, blosclz 0
+  const uint32_t fmt = cname == HSDS_CNAME_ZLIB ? 3u : cname == HSDS_CNAME_BLOSCLZ ? 0u : 1u;
   EncGeom g = {nbytes, 0, 0, (fmt << 5) | (shuffle ? 1u : 0u), ts, 0};
   if (c.dst_len < nbytes + 16 || nbytes >= (1ull << 31) - 16 || (c.dst_off & 3)) {
     st = HSDS_ERR_ARG;
   } else {
-    const uint64_t bs = enc_blocksize(clevel, ts, nbytes, cname != HSDS_CNAME_LZ4);
+    const uint64_t bs = enc_blocksize(clevel, ts, nbytes, cname == HSDS_CNAME_ZLIB || cname == HSDS_CNAME_LZ4HC);
     g.bs = bs;
     if (!(ts <= 16 && bs / ts >= 128)) g.flags |= 0x10;
     g.memcpyed = (nbytes < 128 || clevel <= 0) ? 1u : 0u;
@@ -846,7 +847,7 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
                                                        const hsds_chunk_desc* __restrict__ chunks, uint8_t* dst_base,
                                                        const EncGeom* __restrict__ geom,
                                                        const ItemOut* __restrict__ iout,
-                                                       const int32_t* __restrict__ status, int write) {
+                                                       const int32_t* __restrict__ status, int write, int blosclz) {
   const uint32_t total = offs[nchunks];
   for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
     const int64_t ci = item_chunk(offs, nchunks, item);
@@ -856,12 +857,14 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
     if (g0 + hd::nsegments(it.len) > seg_cap) continue;   // the layout phase fails the chunk
     hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
     if (!write) {
-      const uint32_t sz = lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, nullptr, 0);
+      const uint32_t sz = blosclz ? lze::blosclz_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, nullptr, 0)
+                                  : lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, nullptr, 0);
       if (threadIdx.x == 0) lzsize[slot] = sz;
     } else {
       if (status[ci] != HSDS_OK || geom[ci].memcpyed || iout[slot].raw) continue;
-      lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job,
-                          dst_base + chunks[ci].dst_off + iout[slot].pos, 1);
+      uint8_t* o = dst_base + chunks[ci].dst_off + iout[slot].pos;
+      if (blosclz) lze::blosclz_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, o, 1);
+      else lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, o, 1);
     }
   }
 }
@@ -1267,7 +1270,8 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
                             void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
                             int shuffle, int typesize, int cname, void* stream) {
   if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
-  if (cname != HSDS_CNAME_ZLIB && cname != HSDS_CNAME_LZ4 && cname != HSDS_CNAME_LZ4HC) return HSDS_ERR_ARG;
+  if (cname != HSDS_CNAME_ZLIB && cname != HSDS_CNAME_LZ4 && cname != HSDS_CNAME_LZ4HC && cname != HSDS_CNAME_BLOSCLZ)
+    return HSDS_ERR_ARG;
   if (clevel < 0 || clevel > 9 || (shuffle != HSDS_SHUFFLE_NONE && shuffle != HSDS_SHUFFLE_BYTE)) return HSDS_ERR_ARG;
   if (((uintptr_t)d_dst & 3u) != 0) return HSDS_ERR_ARG;
   if (nchunks == 0) return HSDS_OK;
@@ -1338,11 +1342,13 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   } else {
     const unsigned lgrid = grid_for(16, nchunks * KSLOTS);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
-                       seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0);
+                       seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0,
+                       (int)(cname == HSDS_CNAME_BLOSCLZ));
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
                        segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)lzsize);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
-                       seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 1);
+                       seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 1,
+                       (int)(cname == HSDS_CNAME_BLOSCLZ));
   }
   hipLaunchKernelGGL(raw_copy_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
                      nchunks, (uint8_t*)d_dst, slots, counts, geom, iout, d_status);

@@ -1,4 +1,4 @@
-// lz4_enc.h -- LZ4 block writer for the Blosc-lz4 write path.
+// lz4_enc.h -- LZ4 and BloscLZ block writers for the Blosc-lz4 / -lz4hc / -blosclz write path.
 //
 // storUtil._compress (hsds/util/storUtil.py:238-281) encodes with
 // Blosc(cname=<the dataset's compressor>); for "lz4" / "lz4hc" c-blosc 1.21 calls
@@ -79,12 +79,10 @@ HZ_HD uint32_t ext_len(uint32_t v) { return v >= 15u ? (v - 15u) / 255u + 1u : 0
 // bytes of a sequence with `run` literals and a match of ml bytes (ml == 0: none)
 HZ_HD uint32_t seq_size(uint32_t run, uint32_t ml) { return 1u + ext_len(run) + run + (ml ? 2u + ext_len(ml - 4u) : 0u); }
 
-// Walk lane `lane`'s parse tokens of one segment (input [p0, p1)); calls
-// f(pos, ml, dist) for every match the LZ4 block keeps, in order.  Length-3 matches
-// and matches breaking the block end rules (start within MFLIMIT = 12 bytes of the
-// end, or ending within LASTLITERALS = 5) become literals / are shortened.
+// Walk lane `lane`'s parse tokens of one segment (input from p0): f(pos, len, dist)
+// for every match of the parse, in order.
 template <class F>
-HZ_HD void lane_matches(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, uint32_t n, F&& f) {
+HZ_HD void lane_tokens(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, F&& f) {
   uint32_t pos = p0, pend = 0;
   bool have = false;
   for (uint32_t s = 0; s < ns; s++) {
@@ -105,9 +103,19 @@ HZ_HD void lane_matches(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, uint3
       dv = pend; have = false;
     }
     const uint32_t len = (t & 0x7fffu) + 3u;
-    if (len >= 4u && pos + 12u <= n) f(pos, pos + len + 5u > n ? n - 5u - pos : len, dv + 1u);   // ml >= 7 when cut
+    f(pos, len, dv + 1u);
     pos += len;
   }
+}
+
+// The matches an LZ4 block keeps: length-3 matches and matches breaking the block end
+// rules (start within MFLIMIT = 12 bytes of the end, or ending within LASTLITERALS =
+// 5) become literals / are shortened.  f(pos, ml, dist).
+template <class F>
+HZ_HD void lane_matches(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, uint32_t n, F&& f) {
+  lane_tokens(gtok, ns, lane, p0, [&](uint32_t pos, uint32_t len, uint32_t dist) {
+    if (len >= 4u && pos + 12u <= n) f(pos, pos + len + 5u > n ? n - 5u - pos : len, dist);   // ml >= 7 when cut
+  });
 }
 
 // The LZ4 block of one split from its parse tokens (sp / tok: the split's first
@@ -212,6 +220,96 @@ HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const
     }
   }
   return base + seq_size(carry, 0u);
+}
+
+// ---- BloscLZ (Blosc codec 0, c-blosc 1.21 blosclz_decompress's format) ----------
+// items: c < 32 -> c + 1 literals; else a match of (c >> 5) + 2 bytes ((c >> 5) == 7:
+// plus extension bytes), distance ((c & 31) << 8) + next byte + 1, or for distances
+// from 8192 on (the parse reaches ~16 KiB back) c & 31 == 31, byte 255 and a 16-bit
+// big-endian distance - 8192.
+HZ_HD uint32_t blz_lit_size(uint32_t r) { return r + (r + 31u) / 32u; }
+HZ_HD uint32_t blz_match_size(uint32_t len, uint32_t dist) {
+  return 2u + (len >= 9u ? (len - 9u) / 255u + 1u : 0u) + (dist > 8191u ? 2u : 0u);
+}
+HZ_HD void blz_literals(Out& o, InRd& in, uint32_t l0, uint32_t l1) {
+  for (uint32_t p = l0; p < l1; p += 32u) {
+    const uint32_t k = l1 - p < 32u ? l1 - p : 32u;
+    put(o, k - 1u);
+    for (uint32_t i = 0; i < k; i++) put(o, in_byte(in, p + i));
+  }
+}
+HZ_HD void blz_match(Out& o, uint32_t len, uint32_t dist) {
+  const uint32_t cl = len - 2u < 7u ? len - 2u : 7u;
+  const int far = dist > 8191u;                     // (31, 255) marks the 16-bit form
+  put(o, (cl << 5) | (far ? 31u : (dist - 1u) >> 8));
+  if (cl == 7u) put_len(o, len - 9u);
+  if (far) {
+    put(o, 255u);
+    put(o, (dist - 8192u) >> 8);
+    put(o, (dist - 8192u) & 255u);
+  } else {
+    put(o, (dist - 1u) & 255u);
+  }
+}
+
+// The BloscLZ block of one split, one wavefront: a literal run is cut at lane
+// boundaries (consecutive literal items are valid), so every lane's bytes follow
+// from its own tokens and a prefix sum places them.
+HZ_HD uint32_t blosclz_block_wave(const hd::SegParse* sp, const uint16_t* tok, const hd::EncJob& job, uint8_t* out,
+                                  int write) {
+  const uint32_t n = job.len;
+  const uint32_t nseg = hd::nsegments(n);
+  uint32_t base = 0;
+  LANE_VAR(uint32_t, osz);
+  for (uint32_t sg = 0; sg < nseg; sg++) {
+    const uint32_t s0 = sg * (uint32_t)hd::SEG;
+    const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
+    const uint32_t R = (seglen + hd::WAVE - 1) / hd::WAVE;
+    hz_gcu8* const gtok = HZ_GLOBAL(hz_gcu8*, tok + (size_t)sg * hd::SEG_TOK);
+    LANE_LOOP {
+      const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
+      const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+      uint32_t lit0 = s0 + a0, sz = 0;
+      lane_tokens(gtok, sp[sg].nslot[lane], lane, s0 + a0, [&](uint32_t pos, uint32_t len, uint32_t dist) {
+        sz += blz_lit_size(pos - lit0) + blz_match_size(len, dist);
+        lit0 = pos + len;
+      });
+      LV(osz) = sz + blz_lit_size(s0 + a1 - lit0);
+    }
+    uint32_t seg_total;
+#if HZ_GPU
+    {
+      const uint32_t ox = hz::wave_excl_scan(osz, (int)threadIdx.x);
+      seg_total = __shfl(ox + osz, 63, 64);
+      osz = ox;
+    }
+#else
+    {
+      uint32_t acc = 0;
+      for (int lane = 0; lane < 64; lane++) { const uint32_t z = osz[lane]; osz[lane] = acc; acc += z; }
+      seg_total = acc;
+    }
+#endif
+    if (write) {
+      LANE_LOOP {
+        const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
+        const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+        Out o = {HZ_GLOBAL(hz_gu8*, out + base + LV(osz)), 0u, 1};
+        InRd in;
+        in_init(in, job);
+        uint32_t lit0 = s0 + a0;
+        lane_tokens(gtok, sp[sg].nslot[lane], lane, s0 + a0, [&](uint32_t pos, uint32_t len, uint32_t dist) {
+          blz_literals(o, in, lit0, pos);
+          blz_match(o, len, dist);
+          lit0 = pos + len;
+        });
+        blz_literals(o, in, lit0, s0 + a1);
+      }
+      WAVE_SYNC();
+    }
+    base += seg_total;
+  }
+  return base;
 }
 
 }  // namespace lze

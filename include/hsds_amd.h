@@ -19,7 +19,7 @@
  *   hsds_encode_batch    <- the per-chunk _compress of putStorBytes (storUtil.py:584-600) reached from
  *                           write_s3_obj (hsds/datanode_lib.py:126-311), batched over many dirty chunks
  *   hsds_encode_batch_codec / hsds_compress_codec
- *                        <- the same with Blosc(cname = "lz4" / "lz4hc") (storUtil.py:255-262)
+ *                        <- the same with Blosc(cname = "lz4" / "lz4hc" / "blosclz") (storUtil.py:255-262)
  *
  * Threading: an engine is bound to one device and may be used from one host thread
  * at a time (HSDS data nodes are single-threaded asyncio processes).  All *_batch
@@ -54,6 +54,7 @@ extern "C" {
 #define HSDS_CNAME_ZLIB 0       /* "gzip" / "deflate" / "zlib": Blosc codec 3      */
 #define HSDS_CNAME_LZ4 1        /* "lz4": Blosc codec 1, c-blosc's lz4 blocksize   */
 #define HSDS_CNAME_LZ4HC 2      /* "lz4hc": Blosc codec 1, HCR blocksize           */
+#define HSDS_CNAME_BLOSCLZ 3    /* "blosclz": Blosc codec 0, c-blosc's L1 blocksize */
 
 /* shuffle codes (storUtil.BYTE_SHUFFLE / BIT_SHUFFLE) */
 #define HSDS_SHUFFLE_NONE 0
@@ -166,8 +167,8 @@ int hsds_encode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
                       int shuffle, int typesize, void* stream);
 
 /* The same with the Blosc inner codec `cname` (HSDS_CNAME_*): lz4 / lz4hc frames
- * carry LZ4 blocks (any valid block; the frame layout follows c-blosc 1.21 for that
- * codec).  hsds_encode_batch == cname HSDS_CNAME_ZLIB. */
+ * carry LZ4 blocks, blosclz frames BloscLZ blocks (any valid block; the frame layout
+ * follows c-blosc 1.21 for that codec).  hsds_encode_batch == cname HSDS_CNAME_ZLIB. */
 int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
                             void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
                             int shuffle, int typesize, int cname, void* stream);

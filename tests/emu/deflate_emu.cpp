@@ -86,6 +86,21 @@ extern "C" int64_t emu_lz4_block(const uint8_t* src, uint32_t n, uint8_t* dst, u
   return sz2 == sz ? (int64_t)sz : -2;
 }
 
+// BloscLZ block of one split (parse phase, then lz4_enc.h blosclz_block_wave)
+extern "C" int64_t emu_blosclz_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level) {
+  const uint32_t nseg = hd::nsegments(n);
+  std::vector<hd::SegParse> sp(nseg);
+  std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
+  hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
+  hd::EncJob job = {src, n, level, 1u, 0u, 0u};
+  hd::parse_stream(*ps, job, hd::tune_for_level(level), sp.data(), tok.data());
+  free(ps);
+  const uint32_t sz = lze::blosclz_block_wave(sp.data(), tok.data(), job, nullptr, 0);
+  if (sz > cap) return -1;
+  const uint32_t sz2 = lze::blosclz_block_wave(sp.data(), tok.data(), job, dst, 1);
+  return sz2 == sz ? (int64_t)sz : -2;
+}
+
 extern "C" int emu_parse_shared_bytes() { return (int)sizeof(hd::ParseShared); }
 extern "C" int emu_huff_shared_bytes() { return (int)sizeof(hd::HuffShared); }
 extern "C" int emu_emit_shared_bytes() { return (int)sizeof(hd::EmitShared); }

@@ -98,8 +98,7 @@ def test_compress_passthrough_and_errors(dev):
         codec._compress(data, compressor="zlib", shuffle=2)
     with pytest.raises(NotImplementedError):
         codec._compress(data, compressor="zstd")
-    with pytest.raises(NotImplementedError):
-        codec._compress(data, compressor="blosclz")
+
 
 
 @pytest.mark.parametrize("ts", [2, 4, 8, 32])
@@ -224,7 +223,8 @@ def test_streams_equal_cpu_emulation(dev):
 # ---- the lz4 / lz4hc write path (Blosc codec 1, LZ4 blocks from the parse tokens) ----
 
 @pytest.mark.parametrize("name", sorted(INPUTS))
-@pytest.mark.parametrize("cname,level", [("lz4", 5), ("lz4hc", 5), ("lz4", 1), ("lz4", 9)])
+@pytest.mark.parametrize("cname,level", [("lz4", 5), ("lz4hc", 5), ("lz4", 1), ("lz4", 9), ("blosclz", 5),
+                                         ("blosclz", 9)])
 def test_lz4_compress_decodes_through_oracle_and_gpu(dev, oracle_lib, name, cname, level):
     """storUtil._compress(compressor="lz4"/"lz4hc"): header fields as c-blosc 1.21
     writes them for that codec (blocksize rule pinned by the codec2 golden table),
@@ -237,7 +237,7 @@ def test_lz4_compress_decodes_through_oracle_and_gpu(dev, oracle_lib, name, cnam
     bs = oracle_lib.blosc_blocksize_codec(level, 1, n, cname)
     assert (h["version"], h["versionlz"], h["typesize"], h["nbytes"], h["blocksize"]) == (2, 1, 1, n, bs)
     assert h["cbytes"] == len(frame) <= n + 16
-    assert h["flags"] & 0xE1 == 0x21                   # codec 1 (lz4), shuffle flag
+    assert h["flags"] & 0xE1 == (0x01 if cname == "blosclz" else 0x21)    # codec 0 / 1, shuffle flag
     assert bool(h["flags"] & 0x02) == (n < 128 or h["flags"] & 0x02 != 0)
     assert oracle_lib.uncompress(frame, cname, 1, 1, n) == data
     if n:
@@ -245,7 +245,8 @@ def test_lz4_compress_decodes_through_oracle_and_gpu(dev, oracle_lib, name, cnam
 
 
 @pytest.mark.parametrize("ts", [2, 4, 8, 32])
-def test_lz4_batch_typesize_shuffle(dev, oracle_lib, ts):
+@pytest.mark.parametrize("cname", ["lz4", "blosclz"])
+def test_lz4_batch_typesize_shuffle(dev, oracle_lib, ts, cname):
     import torch
     from hsds_amd.engine import ChunkEngine, encode_descs
     data = [smooth(500 + ts, 1 << 18), smooth(600 + ts, 65536 * 3 + 4 * ts), bytes(70000 // ts * ts)]
@@ -258,16 +259,16 @@ def test_lz4_batch_typesize_shuffle(dev, oracle_lib, ts):
     sizes = torch.zeros(len(data), dtype=torch.int64, device=dev)
     st = torch.full((len(data),), 99, dtype=torch.int32, device=dev)
     eng = ChunkEngine(0)
-    eng.encode(d_src, descs, d_dst, sizes, st, clevel=5, shuffle=1, typesize=ts, compressor="lz4")
+    eng.encode(d_src, descs, d_dst, sizes, st, clevel=5, shuffle=1, typesize=ts, compressor=cname)
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     out = d_dst.cpu().numpy()
     for d, r, n in zip(data, descs, sizes.cpu().numpy()):
         frame = out[int(r["dst_off"]):int(r["dst_off"]) + int(n)].tobytes()
         h = header(frame)
-        assert h["typesize"] == ts and h["blocksize"] == oracle_lib.blosc_blocksize_codec(5, ts, len(d), "lz4")
+        assert h["typesize"] == ts and h["blocksize"] == oracle_lib.blosc_blocksize_codec(5, ts, len(d), cname)
         assert bool(h["flags"] & 0x10) == (not (ts <= 16 and h["blocksize"] // ts >= 128))
-        assert oracle_lib.uncompress(frame, "lz4", 1, ts, len(d)) == d
+        assert oracle_lib.uncompress(frame, cname, 1, ts, len(d)) == d
 
 
 def test_lz4_batch_mixed_gpu_roundtrip(dev, oracle_lib):

@@ -57,3 +57,21 @@ def test_lz4_blocks_decode(emu, oracle_lib, name, level):
     data = inputs()[name]
     comp = block(emu, data, level)
     assert oracle_lib.lz4_decode(comp, len(data)) == data
+
+
+def blz_block(L, data, level):
+    L.emu_blosclz_block.restype = ctypes.c_int64
+    L.emu_blosclz_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+    src = np.frombuffer(data, np.uint8).copy() if data else np.zeros(1, np.uint8)
+    dst = np.zeros(len(data) + len(data) // 16 + 64, np.uint8)
+    r = L.emu_blosclz_block(src.ctypes.data, len(data), dst.ctypes.data, dst.size, level)
+    assert r >= 0, r
+    return dst[:r].tobytes()
+
+
+@pytest.mark.parametrize("name", sorted(inputs()))
+@pytest.mark.parametrize("level", [1, 5, 9])
+def test_blosclz_blocks_decode(emu, oracle_lib, name, level):
+    data = inputs()[name]
+    comp = blz_block(emu, data, level)
+    assert oracle_lib.blosclz_decode(comp, len(data)) == data
