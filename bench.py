@@ -247,6 +247,70 @@ def run_cfg3(args, dev):
     return out
 
 
+CFG1_DIMS, CFG1_LAYOUT = (4096, 4096), (64, 64)
+CFG1_SEL = (slice(1000, 3000, 1), slice(500, 3500, 1))
+
+
+def run_cfg1(args, dev):
+    """configs[0], the reference's CPU-runnable case: f32 4096x4096 in 64x64 chunks
+    (16 KiB, stored uncompressed), selection [1000:3000,500:3500] (32 x 48 = 1536
+    chunks, 24 MB out).  One step = the chunks' read selections + placement into the
+    slab (no codec).  The reference's rate here is bounded by HTTP per chunk."""
+    import torch
+    from hsds_amd import crawl
+    plan = crawl.SelectionPlan("d-0a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", CFG1_DIMS, CFG1_LAYOUT, CFG1_SEL,
+                               np.float32, 1)
+    ids = plan.chunk_ids(0)
+    csz = int(np.prod(CFG1_LAYOUT)) * 4
+    raw = {}
+    for k, cid in enumerate(ids):
+        g = np.random.default_rng(20261015 + k)
+        raw[cid] = np.round(np.cumsum(g.normal(size=csz // 4)), 2).astype(np.float32).view(np.uint8)
+    rd = crawl.ShardedReader(plan, 0, dev, compressor=None, shuffle=0)
+    st = rd.upload(raw)
+    gathered = torch.empty(plan.gathered_nbytes, dtype=torch.uint8, device=dev)
+    slab = torch.zeros(plan.slab_nbytes, dtype=torch.uint8, device=dev)
+    for _ in range(max(1, args.warmup)):
+        rd.read(st, slab=slab, gathered=gathered, check=False)
+    torch.cuda.synchronize()
+    assert int(st["d_status"].abs().sum()) == 0
+    host = slab.cpu().numpy().view(np.float32).reshape(plan.slab_shape)
+    for k in (0, len(ids) // 2, len(ids) - 1):
+        p = plan.pieces[plan.by_rank[0][k]]
+        c = raw[ids[k]].view(np.float32).reshape(CFG1_LAYOUT)
+        assert np.array_equal(host[p.data_slices], c[p.chunk_slices]), f"cfg1 piece {k}"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rd.read(st, slab=slab, gathered=gathered, check=False)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.steps
+    out = {"value": round(plan.slab_nbytes / el / 1e9, 3), "unit": "GB/s selected", "ms_per_step": round(el * 1e3, 3),
+           "chunks": len(ids), "selected_bytes": plan.slab_nbytes,
+           "workload": "configs[0]: f32 4096x4096, 64x64 chunks stored uncompressed, select [1000:3000,500:3500], "
+                       "gather+place"}
+    if args.cpu_seconds > 0:
+        # the reference's per-chunk path on one core: bytesToArray + chunkReadSelection
+        # (numpy slicing, chunkUtil.py:882-929) + the SN slab assignment (chunk_crawl.py:418)
+        arrs = [raw[c].view(np.float32).reshape(CFG1_LAYOUT) for c in ids]
+        pieces = [plan.pieces[plan.by_rank[0][k]] for k in range(len(ids))]
+        cpu_slab = np.zeros(plan.slab_shape, np.float32)
+        t1 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t1 < min(args.cpu_seconds, 2.0):
+            for a, p in zip(arrs, pieces):
+                cpu_slab[p.data_slices] = a[p.chunk_slices]
+            reps += 1
+        cel = (time.perf_counter() - t1) / reps
+        assert np.array_equal(cpu_slab, host)
+        out["cpu_baseline"] = {"value": round(plan.slab_nbytes / cel / 1e9, 3), "unit": "GB/s selected", "cores": 1,
+                               "kind": "port", "sample": f"{reps} x the full 1536-chunk selection, numpy slicing "
+                                                         "(chunkReadSelection + slab assignment), 1 thread"}
+    del gathered, slab, st
+    torch.cuda.empty_cache()
+    return out
+
+
 CFG5_CHUNK = (512, 512)
 
 
@@ -482,6 +546,7 @@ def main():
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     ap.add_argument("--lz4", type=int, default=1, help="also measure Blosc-lz4 1 MiB chunks (N=1)")
+    ap.add_argument("--cfg1", type=int, default=1, help="also measure configs[0] uncompressed read selection (N=1)")
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
     ap.add_argument("--cfg4", type=int, default=-1,
                     help="configs[3] sharded decode+select+RCCL gather (default: on when N > 1)")
@@ -554,6 +619,8 @@ def main():
         del r3
     if world == 1 and args.e2e:
         out["e2e_pcie"] = run_e2e(r1, args, dev)
+    if world == 1 and args.cfg1:
+        out["cfg1"] = run_cfg1(args, dev)
     if world == 1 and args.cfg3:
         out["cfg3"] = run_cfg3(args, dev)
     if world == 1 and args.cfg5:
