@@ -106,9 +106,9 @@ def _uncompress(data, compressor=None, shuffle=0, level=None, dtype=None, chunk_
         return bytes(src)
     if shuffle == BIT_SHUFFLE:
         raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
-    if comp != nat.COMP_NONE and _blosc_nbytes(src) is not None and (src[2] >> 5) not in (0, 1, 3):
-        # zstd / snappy inner codec: decodable by the reference, not by this engine
-        raise NotImplementedError(f"Blosc inner codec {int(src[2] >> 5)} (zstd/snappy) is outside the hsds_amd engine scope")
+    if comp != nat.COMP_NONE and _blosc_nbytes(src) is not None and (src[2] >> 5) not in (0, 1, 3, 4):
+        # snappy inner codec: not built into the numcodecs the reference pins either
+        raise NotImplementedError(f"Blosc inner codec {int(src[2] >> 5)} (snappy) is outside the hsds_amd engine scope")
     if comp == nat.COMP_NONE:
         expected = src.size              # shuffle only: _unshuffle of the bytes as given
     elif chunk_shape is not None:

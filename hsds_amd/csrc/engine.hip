@@ -8,6 +8,7 @@
 //   inflate_kernel      persistent waves pull stream items from a device counter;
 //                       one wavefront decodes one zlib stream (inflate_wave.h)
 //   lz_kernel           the same for LZ4 / BloscLZ Blosc splits (lz_wave.h)
+//   zstd_kernel         zstd Blosc splits, one lane per split (zstd_lane.h)
 //   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
 //   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
 //                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
@@ -30,6 +31,7 @@
 #include "deflate_wave.h"
 #include "lz_wave.h"
 #include "lz4_enc.h"
+#include "zstd_lane.h"
 
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -40,7 +42,7 @@ constexpr int INFLATE_WAVES_PER_CU = 8;   // LDS-bound: sizeof(hz::Shared) <= 20
 static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
 
 // ITEM_LZ4 / ITEM_BLOSCLZ: Blosc splits of the byte-LZ77 codecs (lz_wave.h)
-enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_INEXACT = 0x100 };
+enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_ZSTD = 4, ITEM_INEXACT = 0x100 };
 
 struct Item {          // 32 bytes
   uint64_t src;
@@ -109,14 +111,14 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
     else {
       const uint32_t ver = rd8(s), verlz = rd8(s + 1), flags = rd8(s + 2), ts = rd8(s + 3);
       const uint32_t codec = (flags >> 5) & 7;   // 0 blosclz, 1 lz4/lz4hc, 2 snappy, 3 zlib, 4 zstd
-      const uint32_t kind = codec == 3 ? ITEM_ZLIB : codec == 1 ? ITEM_LZ4 : ITEM_BLOSCLZ;
+      const uint32_t kind = codec == 3 ? ITEM_ZLIB : codec == 1 ? ITEM_LZ4 : codec == 4 ? ITEM_ZSTD : ITEM_BLOSCLZ;
       const uint64_t nbytes = rd32le(s + 4), bs = rd32le(s + 8), cbytes = rd32le(s + 12);
       if (ver != 2 || cbytes > L || cbytes < 16) st = HSDS_ERR_FRAME;
       else if (nbytes != n) st = HSDS_ERR_SIZE;
       else if (flags & 0x02) {
         if (nbytes + 16 > cbytes) st = HSDS_ERR_FRAME;
         else emit(ITEM_RAW, s + 16, nbytes, out, nbytes);
-      } else if (codec != 3 && codec != 1 && codec != 0) st = HSDS_ERR_UNSUPPORTED;   // zstd, snappy
+      } else if (codec != 3 && codec != 1 && codec != 0 && codec != 4) st = HSDS_ERR_UNSUPPORTED;   // snappy
       else if (verlz != 1) st = HSDS_ERR_FRAME;
       else if (flags & 0x04) st = HSDS_ERR_UNSUPPORTED;
       else if (nbytes > 0) {
@@ -161,10 +163,14 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
   if (st != HSDS_OK) { cnt = 0; m.mode = 0; }
   // items per decoder (kind_counts[0]: LZ splits for lz_kernel, [1]: the rest for
   // inflate_kernel), so that a kernel with nothing to do exits at once
-  uint32_t nlz = 0;
-  for (uint32_t k = 0; k < cnt; k++) nlz += (slot[k].kind & 0xff) == ITEM_LZ4 || (slot[k].kind & 0xff) == ITEM_BLOSCLZ;
+  uint32_t nlz = 0, nzs = 0;
+  for (uint32_t k = 0; k < cnt; k++) {
+    nlz += (slot[k].kind & 0xff) == ITEM_LZ4 || (slot[k].kind & 0xff) == ITEM_BLOSCLZ;
+    nzs += (slot[k].kind & 0xff) == ITEM_ZSTD;
+  }
   if (nlz) atomicAdd(&kind_counts[0], nlz);
-  if (cnt - nlz) atomicAdd(&kind_counts[1], cnt - nlz);
+  if (cnt - nlz - nzs) atomicAdd(&kind_counts[1], cnt - nlz - nzs);
+  if (nzs) atomicAdd(&kind_counts[2], nzs);
   counts[ci] = cnt;
   status[ci] = st;
   meta[ci] = m;
@@ -172,6 +178,16 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
     const uint32_t k = atomicAdd(meta_count, 1u);
     meta_list[k] = (uint32_t)ci;
   }
+}
+
+// item index -> (chunk, slot) by binary search over the exclusive item offsets
+__device__ __forceinline__ int64_t item_chunk(const uint32_t* offs, int64_t nchunks, uint32_t item) {
+  int64_t lo = 0, hi = nchunks - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (offs[mid] <= item) lo = mid; else hi = mid - 1;
+  }
+  return lo;
 }
 
 // exclusive scan of counts[0..n) into offs[0..n], single workgroup of 1024 threads
@@ -238,8 +254,8 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
       uint8_t* dp = (uint8_t*)it.dst;
       for (uint32_t i = lane; i < it.dst_len; i += 64) dp[i] = sp[i];
       st = HSDS_OK;
-    } else if ((it.kind & 0xff) == ITEM_LZ4 || (it.kind & 0xff) == ITEM_BLOSCLZ) {
-      continue;                        // lz_kernel's item
+    } else if ((it.kind & 0xff) == ITEM_LZ4 || (it.kind & 0xff) == ITEM_BLOSCLZ || (it.kind & 0xff) == ITEM_ZSTD) {
+      continue;                        // lz_kernel's / zstd_kernel's item
     } else {
       hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
                            (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr};
@@ -316,6 +332,28 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, 
   }
 #endif
   (void)prof;
+}
+
+// -------------------------------------------------------------------------
+// zstd splits (zstd_lane.h): one LANE per split; each lane owns a decode-table slot
+// in global scratch and pulls items from its own counter until the batch is done
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) zstd_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
+                                                  int64_t nchunks, uint32_t* __restrict__ counter,
+                                                  int32_t* __restrict__ status,
+                                                  const uint32_t* __restrict__ kind_counts, uint8_t* scratch) {
+  if (kind_counts[2] == 0) return;
+  const uint32_t total = offs[nchunks];
+  zs::Tables& t = *(zs::Tables*)(scratch + ((size_t)blockIdx.x * 64 + threadIdx.x) * zs::ZTAB_BYTES);
+  for (;;) {
+    const uint32_t item = atomicAdd(counter, 1u);
+    if (item >= total) break;
+    const int64_t ci = item_chunk(offs, nchunks, item);
+    const Item it = slots[ci * KSLOTS + (item - offs[ci])];
+    if ((it.kind & 0xff) != ITEM_ZSTD) continue;
+    const int st = zs::frame(t, (const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len);
+    if (st != HSDS_OK) atomicMin(&status[it.chunk], st);
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -609,15 +647,6 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
   geom[ci] = g;
 }
 
-// item index -> (chunk, slot) by binary search over the exclusive item offsets
-__device__ __forceinline__ int64_t item_chunk(const uint32_t* offs, int64_t nchunks, uint32_t item) {
-  int64_t lo = 0, hi = nchunks - 1;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (offs[mid] <= item) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
 
 // P: persistent waves, one zlib stream each
 __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ slots,
@@ -963,6 +992,8 @@ struct hsds_engine {
   size_t ews_bytes = 0;
   uint8_t* escr = nullptr;
   size_t escr_bytes = 0;
+  uint8_t* zscr = nullptr;       // zstd decode tables: one slot per lane of zstd_kernel
+  size_t zscr_bytes = 0;
   hipEvent_t ev2, ev3;
   int ev_enc_valid = 0;
 };
@@ -1054,6 +1085,7 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (e->h_dev_dst) hipFree(e->h_dev_dst);
   if (e->ews) hipFree(e->ews);
   if (e->escr) hipFree(e->escr);
+  if (e->zscr) hipFree(e->zscr);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
   hipEventDestroy(e->ev2);
@@ -1096,12 +1128,13 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   ChunkMeta* meta = (ChunkMeta*)w; w += sz_meta;
   uint32_t* list = (uint32_t*)w; w += sz_list;
   // [0] inflate item counter, [1] meta list count, [2] inexact size, [3] LZ item counter,
-  // [4] LZ items, [5] other items
+  // [4] LZ items, [5] other items, [6] zstd items, [7] zstd item counter
   uint32_t* ctr = (uint32_t*)w;
   // staging for shuffled outputs (F2 chunks, Blosc typesize > 1): same offsets as
   // the destination buffer, so it spans the destination extent
   if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
   if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->zscr, &e->zscr_bytes, (size_t)e->num_cus * 64 * zs::ZTAB_BYTES)) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
   hipLaunchKernelGGL(frame_walk_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
@@ -1119,6 +1152,8 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   if (lgrid < 1) lgrid = 1;
   hipLaunchKernelGGL(lz_kernel, dim3((unsigned)lgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 3, d_status,
                      ctr + 4);
+  hipLaunchKernelGGL(zstd_kernel, dim3((unsigned)e->num_cus), dim3(64), 0, st, slots, offs, nchunks, ctr + 7, d_status,
+                     ctr + 4, e->zscr);
   hipEventRecord(e->ev1, st);
   e->ev_valid = 1;
   hipLaunchKernelGGL(unshuffle_kernel, dim3(2048), dim3(256), 0, st, meta, list, ctr + 1, d_status);

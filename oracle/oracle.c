@@ -186,6 +186,428 @@ int64_t orc_blosclz_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int
   }
 }
 
+/* ---- Zstandard frame decode (RFC 8878; third-party: the zstd that c-blosc 1.21
+ * vendors and calls from zstd_wrap_decompress for codec 4).  Restated from the RFC:
+ * frame header, raw / RLE / compressed blocks, literals (raw, RLE, Huffman with 1 or
+ * 4 streams, FSE-compressed or direct weights, treeless reuse), sequences (predefined,
+ * RLE, FSE and repeat tables; three repeat offsets) and the optional XXH64 checksum.
+ * Pinned by tests/golden/codec2_cases (zstd objects written by the reference's
+ * _compress over libblosc 1.21.0).  Returns the decoded size or a negative status. */
+
+typedef struct { uint8_t sym, nb; uint16_t base; } zfse_t;            /* FSE decode entry */
+typedef struct { uint8_t sym, nb; } zhuf_t;                            /* Huffman decode entry */
+
+/* backward bitstream (read from the last byte towards the first) */
+typedef struct { const uint8_t *p; int64_t nbits; int64_t pos; } zbits_t;  /* pos: bits left */
+static int zb_init(zbits_t *b, const uint8_t *p, int64_t n) {
+  if (n <= 0 || p[n - 1] == 0) return -1;
+  int hb = 7; while (!(p[n - 1] >> hb)) hb--;
+  b->p = p; b->nbits = 8 * n; b->pos = 8 * (n - 1) + hb;   /* bits below the marker */
+  return 0;
+}
+static uint64_t zb_read(zbits_t *b, int n) {   /* n <= 56; bits past the start read as 0 */
+  uint64_t v = 0;
+  for (int i = 0; i < n; i++) {
+    b->pos--;
+    int bit = 0;
+    if (b->pos >= 0) bit = (b->p[b->pos >> 3] >> (b->pos & 7)) & 1;
+    v = (v << 1) | (uint64_t)bit;
+  }
+  return v;
+}
+static int zb_overflow(const zbits_t *b) { return b->pos < 0; }
+
+static int zhighbit(uint32_t v) { int r = 0; while (v >>= 1) r++; return r; }
+
+/* FSE table description (NCount): returns bytes used, or -1 */
+static int64_t z_ncount(const uint8_t *src, int64_t n, int16_t *norm, int *maxsym, int *al, int maxal) {
+  if (n < 1) return -1;
+  int64_t bitpos = 0;
+#define ZRD(k) ({ uint32_t _v = 0; for (int _i = 0; _i < (k); _i++) { int64_t _q = bitpos + _i; \
+    if ((_q >> 3) < n) _v |= (uint32_t)((src[_q >> 3] >> (_q & 7)) & 1) << _i; } _v; })
+  int log = (int)ZRD(4) + 5;
+  bitpos = 4;
+  if (log > maxal) return -1;
+  *al = log;
+  int remaining = (1 << log) + 1, threshold = 1 << log, nbits = log + 1, s = 0, prev0 = 0;
+  while (remaining > 1 && s <= *maxsym) {
+    if (prev0) {
+      int n0 = s;
+      for (;;) {
+        uint32_t r = ZRD(2); bitpos += 2;
+        n0 += (int)r;
+        if (r != 3) break;
+      }
+      if (n0 > *maxsym + 1) return -1;
+      while (s < n0) norm[s++] = 0;
+      if (s > *maxsym) break;
+    }
+    int maxv = (2 * threshold - 1) - remaining;
+    int count;
+    uint32_t low = ZRD(nbits - 1);
+    if ((int)low < maxv) { count = (int)low; bitpos += nbits - 1; }
+    else {
+      count = (int)ZRD(nbits);
+      if (count >= threshold) count -= maxv;
+      bitpos += nbits;
+    }
+    count--;
+    remaining -= count < 0 ? -count : count;
+    norm[s++] = (int16_t)count;
+    prev0 = count == 0;
+    while (remaining < threshold) { nbits--; threshold >>= 1; }
+  }
+#undef ZRD
+  if (remaining != 1) return -1;
+  *maxsym = s - 1;
+  return (bitpos + 7) >> 3;
+}
+
+static int z_build_fse(zfse_t *t, const int16_t *norm, int maxsym, int al) {
+  const int size = 1 << al;
+  int high = size - 1;
+  uint16_t next[256];
+  for (int s = 0; s <= maxsym; s++) {
+    if (norm[s] == -1) { t[high--].sym = (uint8_t)s; next[s] = 1; }
+    else next[s] = (uint16_t)norm[s];
+  }
+  const int step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+  int pos = 0;
+  for (int s = 0; s <= maxsym; s++) {
+    for (int i = 0; i < norm[s]; i++) {
+      t[pos].sym = (uint8_t)s;
+      do pos = (pos + step) & mask; while (pos > high);
+    }
+  }
+  if (pos != 0) return -1;
+  for (int u = 0; u < size; u++) {
+    const int s = t[u].sym;
+    const uint32_t ns = next[s]++;
+    const int nb = al - zhighbit(ns);
+    t[u].nb = (uint8_t)nb;
+    t[u].base = (uint16_t)((ns << nb) - size);
+  }
+  return 0;
+}
+
+static const int16_t z_ll_def[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+static const int16_t z_ml_def[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+static const int16_t z_of_def[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+static const uint32_t z_ll_base[36] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 28, 32, 40,
+                                       48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+static const uint8_t z_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3,
+                                      4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+static const uint32_t z_ml_base[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26,
+                                       27, 28, 29, 30, 31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259,
+                                       515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+static const uint8_t z_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                      1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+
+typedef struct {
+  zfse_t ll[512], of[256], ml[512];
+  int ll_al, of_al, ml_al, have_tables;
+  zhuf_t huf[1 << 11];
+  int huf_bits, have_huf;
+  uint32_t rep[3];
+} zstate_t;
+
+/* one of LL / OF / ML: mode 0 predefined, 1 RLE, 2 FSE, 3 repeat; returns bytes used */
+static int64_t z_table(zfse_t *t, int *al, int mode, const uint8_t *p, int64_t n, const int16_t *def, int defmax,
+                       int defal, int maxsym, int maxal, int have) {
+  int16_t norm[256];
+  if (mode == 0) { memcpy(norm, def, sizeof(int16_t) * (defmax + 1)); *al = defal; return z_build_fse(t, norm, defmax, defal) ? -1 : 0; }
+  if (mode == 1) {
+    if (n < 1 || p[0] > maxsym) return -1;
+    t[0].sym = p[0]; t[0].nb = 0; t[0].base = 0; *al = 0;
+    return 1;
+  }
+  if (mode == 2) {
+    int ms = maxsym, l;
+    int64_t used = z_ncount(p, n, norm, &ms, &l, maxal);
+    if (used < 0 || z_build_fse(t, norm, ms, l)) return -1;
+    *al = l;
+    return used;
+  }
+  return have ? 0 : -1;
+}
+
+/* Huffman tree description; returns bytes used */
+static int64_t z_huf_tree(zstate_t *z, const uint8_t *p, int64_t n) {
+  uint8_t w[256];
+  int nw = 0;
+  if (n < 1) return -1;
+  int64_t used;
+  if (p[0] >= 128) {
+    nw = p[0] - 127;
+    used = 1 + (nw + 1) / 2;
+    if (used > n) return -1;
+    for (int i = 0; i < nw; i++) w[i] = (i & 1) ? (p[1 + i / 2] & 15) : (p[1 + i / 2] >> 4);
+  } else {
+    const int64_t cs = p[0];
+    used = 1 + cs;
+    if (used > n || cs < 1) return -1;
+    int16_t norm[256];
+    int ms = 255, al;
+    int64_t u = z_ncount(p + 1, cs, norm, &ms, &al, 6);
+    if (u < 0) return -1;
+    zfse_t t[64];
+    if (z_build_fse(t, norm, ms, al)) return -1;
+    zbits_t b;
+    if (zb_init(&b, p + 1 + u, cs - u)) return -1;
+    uint32_t s1 = (uint32_t)zb_read(&b, al), s2 = (uint32_t)zb_read(&b, al);
+    for (;;) {
+      if (nw >= 255) return -1;
+      w[nw++] = t[s1].sym;
+      s1 = t[s1].base + (uint32_t)zb_read(&b, t[s1].nb);
+      if (zb_overflow(&b)) { w[nw++] = t[s2].sym; break; }
+      if (nw >= 255) return -1;
+      w[nw++] = t[s2].sym;
+      s2 = t[s2].base + (uint32_t)zb_read(&b, t[s2].nb);
+      if (zb_overflow(&b)) { if (nw >= 255) return -1; w[nw++] = t[s1].sym; break; }
+    }
+  }
+  /* last weight implied: the weight sum becomes a power of two */
+  uint32_t total = 0;
+  for (int i = 0; i < nw; i++) { if (w[i] > 11) return -1; if (w[i]) total += 1u << (w[i] - 1); }
+  if (total == 0) return -1;
+  const int maxb = zhighbit(total) + 1;
+  const uint32_t rest = (1u << maxb) - total;
+  if (rest & (rest - 1)) return -1;
+  w[nw++] = (uint8_t)(zhighbit(rest) + 1);
+  if (maxb > 11) return -1;
+  /* decode table: weights ascending, symbols in order inside a weight */
+  uint32_t rank[13] = {0}, start[13];
+  for (int i = 0; i < nw; i++) rank[w[i]]++;
+  uint32_t nxt = 0;
+  for (int k = 1; k <= maxb; k++) { start[k] = nxt; nxt += rank[k] << (k - 1); }
+  for (int i = 0; i < nw; i++) {
+    if (!w[i]) continue;
+    const uint32_t len = 1u << (w[i] - 1);
+    for (uint32_t u = start[w[i]]; u < start[w[i]] + len; u++) { z->huf[u].sym = (uint8_t)i; z->huf[u].nb = (uint8_t)(maxb + 1 - w[i]); }
+    start[w[i]] += len;
+  }
+  z->huf_bits = maxb;
+  z->have_huf = 1;
+  return used;
+}
+
+static int z_huf_stream(const zstate_t *z, const uint8_t *p, int64_t n, uint8_t *out, int64_t cnt) {
+  zbits_t b;
+  if (zb_init(&b, p, n)) return -1;
+  for (int64_t i = 0; i < cnt; i++) {
+    const int64_t save = b.pos;
+    const uint32_t peek = (uint32_t)zb_read(&b, z->huf_bits);
+    const zhuf_t e = z->huf[peek];
+    b.pos = save - e.nb;
+    out[i] = e.sym;
+  }
+  return b.pos == 0 ? 0 : -1;   /* every bit consumed */
+}
+
+static uint64_t xxh_rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static uint64_t xxh_rd64(const uint8_t *p) { uint64_t v = 0; for (int i = 7; i >= 0; i--) v = (v << 8) | p[i]; return v; }
+static uint64_t orc_xxh64(const uint8_t *p, int64_t len) {
+  const uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P3 = 1609587929392839161ull,
+                 P4 = 9650029242287828579ull, P5 = 2870177450012600261ull;
+  int64_t i = 0;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+    for (; i + 32 <= len; i += 32) {
+      v1 = xxh_rotl(v1 + xxh_rd64(p + i) * P2, 31) * P1;
+      v2 = xxh_rotl(v2 + xxh_rd64(p + i + 8) * P2, 31) * P1;
+      v3 = xxh_rotl(v3 + xxh_rd64(p + i + 16) * P2, 31) * P1;
+      v4 = xxh_rotl(v4 + xxh_rd64(p + i + 24) * P2, 31) * P1;
+    }
+    h = xxh_rotl(v1, 1) + xxh_rotl(v2, 7) + xxh_rotl(v3, 12) + xxh_rotl(v4, 18);
+    uint64_t vs[4] = {v1, v2, v3, v4};
+    for (int k = 0; k < 4; k++) { h ^= xxh_rotl(vs[k] * P2, 31) * P1; h = h * P1 + P4; }
+  } else {
+    h = P5;
+  }
+  h += (uint64_t)len;
+  for (; i + 8 <= len; i += 8) { h ^= xxh_rotl(xxh_rd64(p + i) * P2, 31) * P1; h = xxh_rotl(h, 27) * P1 + P4; }
+  if (i + 4 <= len) {
+    uint64_t v = (uint64_t)p[i] | (uint64_t)p[i + 1] << 8 | (uint64_t)p[i + 2] << 16 | (uint64_t)p[i + 3] << 24;
+    h ^= v * P1; h = xxh_rotl(h, 23) * P2 + P3; i += 4;
+  }
+  for (; i < len; i++) { h ^= p[i] * P5; h = xxh_rotl(h, 11) * P1; }
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return h;
+}
+
+static int64_t z_block(zstate_t *z, const uint8_t *p, int64_t n, uint8_t *dst, int64_t op, int64_t cap,
+                       uint8_t *lit) {
+  /* ---- literals section ---- */
+  if (n < 1) return ORC_ERR_DATA;
+  const int lt = p[0] & 3, sf = (p[0] >> 2) & 3;
+  int64_t rsz, csz = 0, hl;
+  int nstreams = 1;
+  if (lt < 2) {
+    if (sf == 0 || sf == 2) { rsz = p[0] >> 3; hl = 1; }
+    else if (sf == 1) { if (n < 2) return ORC_ERR_DATA; rsz = (p[0] >> 4) | (p[1] << 4); hl = 2; }
+    else { if (n < 3) return ORC_ERR_DATA; rsz = (p[0] >> 4) | (p[1] << 4) | ((int64_t)p[2] << 12); hl = 3; }
+  } else {
+    hl = sf < 2 ? 3 : sf == 2 ? 4 : 5;
+    if (n < hl) return ORC_ERR_DATA;
+    uint64_t v = 0;
+    for (int i = (int)hl - 1; i >= 0; i--) v = (v << 8) | p[i];
+    const int bits = sf < 2 ? 10 : sf == 2 ? 14 : 18;
+    rsz = (int64_t)((v >> 4) & ((1u << bits) - 1));
+    csz = (int64_t)((v >> (4 + bits)) & ((1u << bits) - 1));
+    nstreams = sf == 0 ? 1 : 4;
+  }
+  if (rsz > (1 << 17)) return ORC_ERR_DATA;
+  int64_t q = hl;
+  if (lt == 0) { if (q + rsz > n) return ORC_ERR_TRUNC; memcpy(lit, p + q, (size_t)rsz); q += rsz; }
+  else if (lt == 1) { if (q + 1 > n) return ORC_ERR_TRUNC; memset(lit, p[q], (size_t)rsz); q += 1; }
+  else {
+    if (q + csz > n) return ORC_ERR_TRUNC;
+    const uint8_t *h = p + q;
+    int64_t tsz = 0;
+    if (lt == 2) { tsz = z_huf_tree(z, h, csz); if (tsz < 0) return ORC_ERR_DATA; }
+    else if (!z->have_huf) return ORC_ERR_DATA;
+    const uint8_t *s = h + tsz;
+    const int64_t ssz = csz - tsz;
+    if (nstreams == 1) {
+      if (z_huf_stream(z, s, ssz, lit, rsz)) return ORC_ERR_DATA;
+    } else {
+      if (ssz < 6) return ORC_ERR_DATA;
+      const int64_t l1 = s[0] | (s[1] << 8), l2 = s[2] | (s[3] << 8), l3 = s[4] | (s[5] << 8);
+      const int64_t l4 = ssz - 6 - l1 - l2 - l3;
+      if (l4 < 0) return ORC_ERR_DATA;
+      const int64_t seg = (rsz + 3) / 4;
+      if (rsz < 3 * seg) return ORC_ERR_DATA;
+      const uint8_t *s1 = s + 6;
+      if (z_huf_stream(z, s1, l1, lit, seg) || z_huf_stream(z, s1 + l1, l2, lit + seg, seg) ||
+          z_huf_stream(z, s1 + l1 + l2, l3, lit + 2 * seg, seg) ||
+          z_huf_stream(z, s1 + l1 + l2 + l3, l4, lit + 3 * seg, rsz - 3 * seg))
+        return ORC_ERR_DATA;
+    }
+    q += csz;
+  }
+  /* ---- sequences section ---- */
+  if (q >= n) return ORC_ERR_TRUNC;
+  int64_t nseq = p[q++];
+  if (nseq >= 128) {
+    if (nseq < 255) { if (q >= n) return ORC_ERR_TRUNC; nseq = ((nseq - 128) << 8) + p[q++]; }
+    else { if (q + 1 >= n) return ORC_ERR_TRUNC; nseq = p[q] + (p[q + 1] << 8) + 0x7F00; q += 2; }
+  }
+  int64_t lp = 0;
+  if (nseq > 0) {
+    if (q >= n) return ORC_ERR_TRUNC;
+    const int modes = p[q++];
+    if (modes & 3) return ORC_ERR_DATA;
+    int64_t u;
+    u = z_table(z->ll, &z->ll_al, (modes >> 6) & 3, p + q, n - q, z_ll_def, 35, 6, 35, 9, z->have_tables);
+    if (u < 0) return ORC_ERR_DATA;
+    q += u;
+    u = z_table(z->of, &z->of_al, (modes >> 4) & 3, p + q, n - q, z_of_def, 28, 5, 31, 8, z->have_tables);
+    if (u < 0) return ORC_ERR_DATA;
+    q += u;
+    u = z_table(z->ml, &z->ml_al, (modes >> 2) & 3, p + q, n - q, z_ml_def, 52, 6, 52, 9, z->have_tables);
+    if (u < 0) return ORC_ERR_DATA;
+    q += u;
+    z->have_tables = 1;
+    zbits_t b;
+    if (zb_init(&b, p + q, n - q)) return ORC_ERR_DATA;
+    uint32_t sll = (uint32_t)zb_read(&b, z->ll_al), sof = (uint32_t)zb_read(&b, z->of_al),
+             sml = (uint32_t)zb_read(&b, z->ml_al);
+    for (int64_t k = 0; k < nseq; k++) {
+      const int llc = z->ll[sll].sym, ofc = z->of[sof].sym, mlc = z->ml[sml].sym;
+      if (llc > 35 || mlc > 52 || ofc > 31) return ORC_ERR_DATA;
+      const uint64_t ofv = (1ull << ofc) + zb_read(&b, ofc);
+      const uint64_t ml = z_ml_base[mlc] + zb_read(&b, z_ml_bits[mlc]);
+      const uint64_t ll = z_ll_base[llc] + zb_read(&b, z_ll_bits[llc]);
+      uint64_t off;
+      if (ofv > 3) {
+        off = ofv - 3;
+        z->rep[2] = z->rep[1]; z->rep[1] = z->rep[0]; z->rep[0] = (uint32_t)off;
+      } else {
+        const int idx = (int)ofv - 1 + (ll == 0);   /* LL == 0 shifts the repeat index by one */
+        if (idx == 0) off = z->rep[0];
+        else {
+          off = idx == 3 ? (uint64_t)z->rep[0] - 1 : z->rep[idx];
+          if (idx == 1) { z->rep[1] = z->rep[0]; }
+          else { z->rep[2] = z->rep[1]; z->rep[1] = z->rep[0]; }
+          z->rep[0] = (uint32_t)off;
+        }
+      }
+      if (k + 1 < nseq) {
+        sll = z->ll[sll].base + (uint32_t)zb_read(&b, z->ll[sll].nb);
+        sml = z->ml[sml].base + (uint32_t)zb_read(&b, z->ml[sml].nb);
+        sof = z->of[sof].base + (uint32_t)zb_read(&b, z->of[sof].nb);
+      }
+      if (lp + (int64_t)ll > rsz) return ORC_ERR_DATA;
+      if (op + (int64_t)ll + (int64_t)ml > cap) return ORC_ERR_SIZE;
+      memcpy(dst + op, lit + lp, (size_t)ll);
+      op += (int64_t)ll; lp += (int64_t)ll;
+      if (off == 0 || (int64_t)off > op) return ORC_ERR_DATA;
+      for (uint64_t i = 0; i < ml; i++) dst[op + (int64_t)i] = dst[op + (int64_t)i - (int64_t)off];
+      op += (int64_t)ml;
+    }
+    if (b.pos != 0) return ORC_ERR_DATA;
+  }
+  if (op + (rsz - lp) > cap) return ORC_ERR_SIZE;
+  memcpy(dst + op, lit + lp, (size_t)(rsz - lp));
+  return op + (rsz - lp);
+}
+
+int64_t orc_zstd_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64_t cap) {
+  if (srclen < 5) return ORC_ERR_TRUNC;
+  if (rd32(src) != 0xFD2FB528u) return ORC_ERR_DATA;
+  const int fhd = src[4];
+  const int fcsf = fhd >> 6, single = (fhd >> 5) & 1, cks = (fhd >> 2) & 1, didf = fhd & 3;
+  if (fhd & 8) return ORC_ERR_DATA;
+  int64_t q = 5 + (single ? 0 : 1);
+  q += didf == 0 ? 0 : didf == 1 ? 1 : didf == 2 ? 2 : 4;
+  if (didf) return ORC_ERR_UNSUPPORTED;                     /* dictionaries: not used by c-blosc */
+  const int fcsb = fcsf == 0 ? (single ? 1 : 0) : fcsf == 1 ? 2 : fcsf == 2 ? 4 : 8;
+  if (q + fcsb > srclen) return ORC_ERR_TRUNC;
+  int64_t fcs = -1;
+  if (fcsb) {
+    uint64_t v = 0;
+    for (int i = fcsb - 1; i >= 0; i--) v = (v << 8) | src[q + i];
+    fcs = (int64_t)(fcsb == 2 ? v + 256 : v);
+  }
+  q += fcsb;
+  zstate_t *z = (zstate_t *)calloc(1, sizeof(zstate_t));
+  uint8_t *lit = (uint8_t *)malloc(1 << 17);
+  z->rep[0] = 1; z->rep[1] = 4; z->rep[2] = 8;
+  int64_t op = 0, r = 0;
+  for (;;) {
+    if (q + 3 > srclen) { r = ORC_ERR_TRUNC; break; }
+    const uint32_t bh = src[q] | (src[q + 1] << 8) | (src[q + 2] << 16);
+    q += 3;
+    const int last = bh & 1, type = (bh >> 1) & 3;
+    const int64_t bsz = bh >> 3;
+    if (type == 3 || bsz > (1 << 17)) { r = ORC_ERR_DATA; break; }
+    if (type == 0) {
+      if (q + bsz > srclen) { r = ORC_ERR_TRUNC; break; }
+      if (op + bsz > cap) { r = ORC_ERR_SIZE; break; }
+      memcpy(dst + op, src + q, (size_t)bsz); op += bsz; q += bsz;
+    } else if (type == 1) {
+      if (q + 1 > srclen) { r = ORC_ERR_TRUNC; break; }
+      if (op + bsz > cap) { r = ORC_ERR_SIZE; break; }
+      memset(dst + op, src[q], (size_t)bsz); op += bsz; q += 1;
+    } else {
+      if (q + bsz > srclen) { r = ORC_ERR_TRUNC; break; }
+      const int64_t o2 = z_block(z, src + q, bsz, dst, op, cap, lit);
+      if (o2 < 0) { r = o2; break; }
+      op = o2; q += bsz;
+    }
+    if (last) break;
+  }
+  if (r == 0 && fcs >= 0 && fcs != op) r = ORC_ERR_SIZE;
+  if (r == 0 && cks) {
+    if (q + 4 > srclen) r = ORC_ERR_TRUNC;
+    else if ((uint32_t)orc_xxh64(dst, op) != rd32(src + q)) r = ORC_ERR_DATA;
+  }
+  free(lit);
+  free(z);
+  return r < 0 ? r : op;
+}
+
 /* ---- Blosc1 frame decode (c-blosc 1.21 blosc_decompress semantics) --------- */
 
 int orc_is_blosc(const uint8_t *src, int64_t srclen) {
@@ -217,8 +639,8 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
     memcpy(dst, src + 16, (size_t)nbytes);
     return nbytes;
   }
-  int codec = (flags >> 5) & 7;   /* 0 blosclz, 1 lz4/lz4hc, 3 zlib; 2 snappy, 4 zstd unsupported */
-  if (codec != 3 && codec != 1 && codec != 0) return ORC_ERR_UNSUPPORTED;
+  int codec = (flags >> 5) & 7;   /* 0 blosclz, 1 lz4/lz4hc, 3 zlib, 4 zstd; 2 snappy unsupported */
+  if (codec != 3 && codec != 1 && codec != 0 && codec != 4) return ORC_ERR_UNSUPPORTED;
   if (verlz != 1) return ORC_ERR_FRAME;
   if (flags & 0x04) return ORC_ERR_UNSUPPORTED; /* bitshuffle inside Blosc */
   if (nbytes == 0) return 0;
@@ -248,6 +670,7 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
       } else {
         int64_t r = codec == 3 ? orc_zlib_decode(src + p, cs, out + j * neblock, neblock)
                   : codec == 1 ? orc_lz4_decode(src + p, cs, out + j * neblock, neblock)
+                  : codec == 4 ? orc_zstd_decode(src + p, cs, out + j * neblock, neblock)
                                : orc_blosclz_decode(src + p, cs, out + j * neblock, neblock);
         if (r < 0) { result = r == ORC_ERR_SIZE ? ORC_ERR_SIZE : r; goto done; }
         if (r != neblock) { result = ORC_ERR_SIZE; goto done; }

@@ -44,6 +44,8 @@ def lib():
         L.orc_zlib_decode.restype = I64
         L.orc_lz4_decode.argtypes = [P, I64, P, I64]
         L.orc_lz4_decode.restype = I64
+        L.orc_zstd_decode.argtypes = [P, I64, P, I64]
+        L.orc_zstd_decode.restype = I64
         L.orc_blosclz_decode.argtypes = [P, I64, P, I64]
         L.orc_blosclz_decode.restype = I64
         L.orc_blosc_decode.argtypes = [P, I64, P, I64]
@@ -108,6 +110,10 @@ def _split_decode(fn, data, n):
 
 def lz4_decode(data, n):
     return _split_decode(lib().orc_lz4_decode, data, n)
+
+
+def zstd_decode(data, n):
+    return _split_decode(lib().orc_zstd_decode, data, n)
 
 
 def blosclz_decode(data, n):

@@ -102,8 +102,20 @@ def main():
             blob = su._compress(arr.tobytes(), **ops)
             add(f"{comp}_{kind}_{np.dtype(dt).name}_{'x'.join(map(str, shape))}_L{level}", blob, ops,
                 "reference getFilterOps + _compress -> _uncompress", seed, arr.tobytes())
+    # ---- zstd at every level (block types, literal modes and table modes vary)
+    for level in range(1, 10):
+        for kind, dt, shape in (("smooth", "<f4", (256, 512)), ("lowent", "|u1", (150000,)), ("steps", "<i2", (70000,))):
+            seed += 1
+            arr = data(kind, int(np.prod(shape)), dt, seed).reshape(shape)
+            f = [{"class": "H5Z_FILTER_SHUFFLE", "id": 2, "name": "shuffle"},
+                 {"class": "H5Z_FILTER_ZSTD", "id": 32015, "level": level, "name": "zstd"}]
+            ops = getFilterOps(app, f"d-zstd-{seed}", f, dtype=arr.dtype, chunk_shape=shape)
+            app["filter_map"].clear()
+            blob = su._compress(arr.tobytes(), **ops)
+            add(f"zstd_L{level}_{kind}_{np.dtype(dt).name}", blob, ops, "reference getFilterOps + _compress -> _uncompress",
+                seed, arr.tobytes())
     # ---- frames with typesize > 1 and in-frame shuffle (HDF5 Blosc filter writers)
-    for comp in ("lz4", "lz4hc", "blosclz"):
+    for comp in ("lz4", "lz4hc", "blosclz", "zstd"):
         for kind, dt, n, level in (("smooth", "<f4", 65536, 5), ("smooth", "<i2", 131072, 9), ("smooth", "<f8", 40000, 5),
                                    ("steps", "<i4", 262144 + 333, 5), ("lowent", "<f4", 8192 + 3, 5)):
             seed += 1
@@ -115,7 +127,7 @@ def main():
                 "libblosc typesize>1 frame -> reference _uncompress", seed, raw)
     # ---- corrupted frames: whatever the reference does (error, or decoded bytes)
     rng = np.random.default_rng(77)
-    for comp, kind in (("lz4", "lowent"), ("blosclz", "steps")):
+    for comp, kind in (("lz4", "lowent"), ("blosclz", "steps"), ("zstd", "lowent"), ("zstd", "text")):
         arr = data(kind, 65536, "|u1", 4242)
         ops = {"compressor": comp, "shuffle": 0, "level": 5, "dtype": np.dtype("u1"), "chunk_shape": (65536,)}
         good = su._compress(arr.tobytes(), **ops)
@@ -124,10 +136,10 @@ def main():
             bad = bytearray(good)
             pos = int(rng.integers(40, len(bad)))
             bad[pos] ^= int(rng.integers(1, 256))
-            add(f"err_{comp}_flip{k}", bytes(bad), ops, f"byte {pos} corrupted")
+            add(f"err_{comp}_{kind}_flip{k}", bytes(bad), ops, f"byte {pos} corrupted")
         # c-blosc 1.21 blosc_decompress takes no source size and reads past the end of a
         # truncated object; the engine rejects it (header cbytes > object length)
-        add(f"err_{comp}_trunc", good[:-7], ops, "truncated frame: reference reads past the object end")
+        add(f"err_{comp}_{kind}_trunc", good[:-7], ops, "truncated frame: reference reads past the object end")
     # ---- c-blosc 1.21 frame header fields per codec (compute_blocksize, split flag)
     hdr = []
     base = data("smooth", 1 << 20, "<i4", 5).tobytes()

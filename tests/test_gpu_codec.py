@@ -163,9 +163,9 @@ def test_error_statuses(oracle_lib, torch_dev):
 
 
 def test_other_blosc_codecs_match_reference_goldens(golden2, torch_dev):
-    """lz4 / lz4hc / blosclz objects of the reference (codec2 goldens) through _uncompress
-    on the GPU: every byte and every error; zstd raises NotImplementedError (outside the
-    engine); a truncated object is rejected (the reference reads past its end)."""
+    """lz4 / lz4hc / blosclz / zstd objects of the reference (codec2 goldens) through
+    _uncompress on the GPU: every byte and every error; a truncated object is rejected
+    (the reference reads past its end)."""
     from hsds_amd import codec
     meta, arrs = golden2
     checked = 0
@@ -173,10 +173,6 @@ def test_other_blosc_codecs_match_reference_goldens(golden2, torch_dev):
         blob = arrs[c["name"] + "__in"].tobytes()
         kw = dict(compressor=c["compressor"], shuffle=c["shuffle"], level=c["level"],
                   dtype=np.dtype(c["dtype"]), chunk_shape=tuple(c["chunk_shape"]))
-        if c["codec"] not in (0, 1, 3) and not c["memcpyed"]:
-            with pytest.raises(NotImplementedError):
-                codec._uncompress(blob, **kw)
-            continue
         if c["status"] == "error" or c["name"].endswith("_trunc"):
             with pytest.raises(codec.HTTPInternalServerError):
                 codec._uncompress(blob, **kw)
@@ -184,7 +180,7 @@ def test_other_blosc_codecs_match_reference_goldens(golden2, torch_dev):
         out = codec._uncompress(blob, **kw)
         assert len(out) == c["out_len"] and _sha(out) == c["out_sha256"], c["name"]
         checked += 1
-    assert checked >= 45
+    assert checked >= 90
 
 
 @pytest.mark.parametrize("kind,size,ts,bs", [
@@ -253,3 +249,39 @@ def test_lz4_blosclz_error_statuses(golden2, oracle_lib, torch_dev):
             assert st[k] == 0, (k, st[k])
             o = int(descs[k]["dst_off"])
             assert out[o:o + sizes[k]].tobytes() == ref, k
+
+
+def test_batch_decode_zstd_goldens_with_oracle(golden2, oracle_lib, torch_dev):
+    """every zstd golden object (and mixed lz4 / zlib neighbours) in ONE batch: status
+    and bytes against the oracle's zstd restatement"""
+    import torch
+    from hsds_amd.engine import ChunkEngine, pack_chunks
+    orc = oracle_lib
+    meta, arrs = golden2
+    blobs, sizes, names = [], [], []
+    for c in meta["cases"]:
+        if c["codec"] not in (1, 4) or c["name"].endswith("_trunc"):
+            continue
+        blobs.append(arrs[c["name"] + "__in"].tobytes())
+        sizes.append(int(np.prod(c["chunk_shape"])) * np.dtype(c["dtype"]).itemsize)
+        names.append(c["name"])
+    src, descs, ext = pack_chunks(blobs, sizes)
+    eng = ChunkEngine(0)
+    d_src = torch.from_numpy(src).to(torch_dev)
+    d_dst = torch.zeros(ext, dtype=torch.uint8, device=torch_dev)
+    d_st = torch.full((len(blobs),), 77, dtype=torch.int32, device=torch_dev)
+    eng.decode(d_src, descs, d_dst, d_st, compressor="zstd", shuffle=1, itemsize=1)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    out = d_dst.cpu().numpy()
+    nz = 0
+    for k, b in enumerate(blobs):
+        ref = orc.uncompress(b, "zstd", 1, 1, sizes[k])
+        if isinstance(ref, int):
+            assert st[k] < 0, names[k]
+        else:
+            assert st[k] == 0, (names[k], st[k])
+            o = int(descs[k]["dst_off"])
+            assert out[o:o + sizes[k]].tobytes() == ref, names[k]
+            nz += "zstd" in names[k]
+    assert nz >= 40

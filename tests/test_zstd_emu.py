@@ -1,0 +1,91 @@
+"""CPU emulation of the GPU zstd split decoder (hsds_amd/csrc/zstd_lane.h, the code
+each lane runs, compiled for CPU by tests/emu/zstd_emu.cpp): every zstd object of the
+reference goldens (tests/golden/codec2_cases: the reference's _compress at levels 1-9,
+typesize 2-8 frames, corrupted frames) against the reference's sha256 and errors, and
+every split against the oracle's independent restatement (oracle.c orc_zstd_decode)."""
+import ctypes
+import hashlib
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU = os.path.join(ROOT, "tests", "emu", "libzstd_emu.so")
+SRC = os.path.join(ROOT, "tests", "emu", "zstd_emu.cpp")
+
+
+@pytest.fixture(scope="module")
+def emu():
+    hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("zstd_lane.h", "inflate_wave.h")]
+    if not os.path.exists(EMU) or os.path.getmtime(EMU) < max(os.path.getmtime(p) for p in [SRC] + hdrs):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", EMU, SRC])
+    L = ctypes.CDLL(EMU)
+    L.emu_zstd_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+    return L
+
+
+def split(L, comp, n):
+    src = np.frombuffer(comp, np.uint8).copy() if comp else np.zeros(1, np.uint8)
+    dst = np.zeros(max(n, 1), np.uint8)
+    r = L.emu_zstd_frame(src.ctypes.data, len(comp), dst.ctypes.data, n)
+    return r, dst[:n].tobytes()
+
+
+def frame_decode(L, f, oracle_lib=None):
+    if len(f) < 16:
+        return -1
+    flags, ts = f[2], f[3]
+    nb, bs, cb = struct.unpack("<III", f[4:16])
+    if cb > len(f):
+        return -1
+    if flags & 2:
+        return f[16:16 + nb]
+    nblocks = (nb + bs - 1) // bs
+    left = nb % bs
+    out = bytearray()
+    for b in range(nblocks):
+        isl = b == nblocks - 1 and left
+        bsz = left if isl else bs
+        nspl = ts if (not flags & 0x10 and ts <= 16 and bs // ts >= 128 and not isl) else 1
+        ne = bsz // nspl
+        p = struct.unpack("<i", f[16 + 4 * b:20 + 4 * b])[0]
+        blk = bytearray()
+        for _ in range(nspl):
+            cs = struct.unpack("<i", f[p:p + 4])[0]
+            p += 4
+            if cs == ne:
+                blk += f[p:p + cs]
+            else:
+                r, d = split(L, f[p:p + cs], ne)
+                if oracle_lib is not None:
+                    want = oracle_lib.zstd_decode(f[p:p + cs], ne)
+                    assert (r != 0) == isinstance(want, int) and (r != 0 or d == want)
+                if r != 0:
+                    return r
+                blk += d
+            p += cs
+        if flags & 1 and ts > 1:
+            cnt = bsz // ts
+            blk = np.frombuffer(bytes(blk[:cnt * ts]), np.uint8).reshape(ts, cnt).T.tobytes() + bytes(blk[cnt * ts:])
+        out += blk
+    return bytes(out)
+
+
+def test_zstd_reference_goldens(emu, golden2, oracle_lib):
+    meta, arrs = golden2
+    checked = 0
+    for c in meta["cases"]:
+        if c["codec"] != 4 or c["memcpyed"]:
+            continue
+        blob = arrs[c["name"] + "__in"].tobytes()
+        got = frame_decode(emu, blob, oracle_lib if not c["name"].endswith("_trunc") else None)
+        if c["status"] == "error" or c["name"].endswith("_trunc"):
+            assert isinstance(got, int), c["name"]
+            continue
+        assert not isinstance(got, int), (c["name"], got)
+        assert hashlib.sha256(got).hexdigest() == c["out_sha256"], c["name"]
+        checked += 1
+    assert checked >= 35
