@@ -44,6 +44,22 @@ def make_corpus(fmt, n_unique, base_seed, threads):
         raw = list(ex.map(lambda i: smooth_chunk(base_seed + i).view(np.uint8), range(n_unique)))
     if fmt == "F1":
         blobs = orc.encode_batch(raw, op="blosc", typesize=1, clevel=4, shuffle=1, nthreads=threads)
+    elif fmt == "ZSTD":
+        # Blosc-zstd frames as _compress(compressor="zstd", level=5) writes them: the
+        # image's libblosc 1.21 (the c-blosc the reference's numcodecs vendors), 16 threads
+        import ctypes
+        lb = ctypes.CDLL("/opt/conda/lib/libblosc.so.1")
+        lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
+                                          ctypes.c_size_t, ctypes.c_int]
+
+        def enc(r):
+            out = np.empty(r.size + 16, np.uint8)
+            k = lb.blosc_compress_ctx(5, 1, 1, r.size, r.ctypes.data, out.ctypes.data, out.size, b"zstd", 0, 1)
+            assert k > 0
+            return out[:k].copy()
+        with ThreadPoolExecutor(threads) as ex:
+            blobs = list(ex.map(enc, raw))
     elif fmt == "LZ4":
         # Blosc-lz4 frames as _compress(compressor="lz4", level=5) lays them out
         # (typesize 1, 128 KiB blocks); the payload is the oracle's greedy LZ4 writer
@@ -74,7 +90,7 @@ def run_format(fmt, args, dev, rank, world):
     d_desc = to_device_bytes(descs, dev)
     stream = torch.cuda.current_stream()
 
-    comp = "lz4" if fmt == "LZ4" else "zlib"
+    comp = {"LZ4": "lz4", "ZSTD": "zstd"}.get(fmt, "zlib")
 
     def step():
         eng.decode(d_src, d_desc, d_dst, d_st, compressor=comp, shuffle=1, itemsize=4, stream=stream)
@@ -547,6 +563,7 @@ def main():
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     ap.add_argument("--lz4", type=int, default=1, help="also measure Blosc-lz4 1 MiB chunks (N=1)")
     ap.add_argument("--cfg1", type=int, default=1, help="also measure configs[0] uncompressed read selection (N=1)")
+    ap.add_argument("--zstd", type=int, default=1, help="also measure Blosc-zstd 1 MiB chunks (N=1; needs the image's libblosc)")
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
     ap.add_argument("--cfg4", type=int, default=-1,
                     help="configs[3] sharded decode+select+RCCL gather (default: on when N > 1)")
@@ -619,6 +636,18 @@ def main():
         del r3
     if world == 1 and args.e2e:
         out["e2e_pcie"] = run_e2e(r1, args, dev)
+    if world == 1 and args.zstd:
+        try:
+            zu = args.unique
+            args.unique = min(args.unique, 256)
+            r4 = run_format("ZSTD", args, dev, rank, world)
+            args.unique = zu
+            out["zstd"] = {"value": round(r4["dec_bytes"] * args.steps / r4["elapsed_s"] / 1e9, 2), "unit": "GB/s",
+                           "format": "Blosc-zstd frames from libblosc 1.21 (level 5, typesize 1)",
+                           "compressed_bytes_per_gpu": r4["comp_bytes"], "zstd_kernel_ms": round(r4["kernel_ms"], 3)}
+            del r4
+        except Exception as e:   # corpus writer unavailable: the headline stands
+            out["zstd"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     if world == 1 and args.cfg1:
         out["cfg1"] = run_cfg1(args, dev)
     if world == 1 and args.cfg3:

@@ -41,14 +41,14 @@ extern "C" {
 #define HSDS_ERR_DATA -2        /* corrupt deflate data, bad adler32, bad header  */
 #define HSDS_ERR_TRUNC -3       /* stream ends before its end-of-stream marker    */
 #define HSDS_ERR_SIZE -4        /* decoded size differs from the expected size    */
-#define HSDS_ERR_UNSUPPORTED -5 /* zstd/snappy Blosc codec, bitshuffle, rank > 8  */
+#define HSDS_ERR_UNSUPPORTED -5 /* snappy Blosc codec, bitshuffle, rank > 8 ...  */
 #define HSDS_ERR_ARG -6         /* invalid argument                               */
 #define HSDS_ERR_DEVICE -7      /* HIP runtime failure                            */
 
 /* compressor codes (storUtil._uncompress compressor argument) */
 #define HSDS_COMP_NONE 0        /* None / "scaleoffset"                           */
 #define HSDS_COMP_ZLIB 1        /* "gzip" / "deflate" / "zlib"                    */
-#define HSDS_COMP_OTHER 2       /* lz4 / lz4hc / blosclz / ...: Blosc frames only  */
+#define HSDS_COMP_OTHER 2       /* lz4 / lz4hc / blosclz / zstd: Blosc frames only */
 
 /* Blosc inner codec of the write path (storUtil._compress cname) */
 #define HSDS_CNAME_ZLIB 0       /* "gzip" / "deflate" / "zlib": Blosc codec 3      */
