@@ -287,6 +287,40 @@ HZ_HD int huf_stream(const Tables& t, const In& in, uint32_t at, uint32_t n, hz_
   return b.pos == 0 ? 0 : -1;
 }
 
+// n bytes from s to d with d <= s (possibly overlapping): 16 loads issued together,
+// then 16 stores, so a copy costs one memory latency per 16 bytes, not per byte
+HZ_HD void copy_fwd(hz_gu8* d, hz_gu8* s, uint32_t n) {
+  uint32_t i = 0;
+  for (; i + 16u <= n; i += 16u) {
+    uint8_t v[16];
+    HZ_UNROLL
+    for (int k = 0; k < 16; k++) v[k] = s[i + k];
+    HZ_UNROLL
+    for (int k = 0; k < 16; k++) d[i + k] = v[k];
+  }
+  for (; i < n; i++) d[i] = s[i];
+}
+// match of ml bytes at op, distance off: byte i comes from op - off + (i mod off),
+// which is already final, so the loads of a 16-byte step are independent
+HZ_HD void copy_match(hz_gu8* dst, uint32_t op, uint32_t off, uint32_t ml) {
+  const uint32_t src = op - off;
+  uint32_t i = 0, r = 0;                      // r = i mod off
+  for (; i + 16u <= ml; i += 16u) {
+    uint8_t v[16];
+    HZ_UNROLL
+    for (int k = 0; k < 16; k++) {
+      v[k] = dst[src + r];
+      r = r + 1u == off ? 0u : r + 1u;
+    }
+    HZ_UNROLL
+    for (int k = 0; k < 16; k++) dst[op + i + k] = v[k];
+  }
+  for (; i < ml; i++) {
+    dst[op + i] = dst[src + r];
+    r = r + 1u == off ? 0u : r + 1u;
+  }
+}
+
 // one compressed block at input [at, at + n); output from op; returns the new op or < 0
 HZ_HD int64_t block(Tables& t, const In& in, uint32_t at, uint32_t n, hz_gu8* dst, uint32_t op, uint32_t cap) {
   if (n < 1) return E_DATA;
@@ -398,17 +432,17 @@ HZ_HD int64_t block(Tables& t, const In& in, uint32_t at, uint32_t n, hz_gu8* ds
       // the block must still fit: then the copies never reach the unread literals
       // at the end of the span
       if ((uint64_t)op + ml + (rsz - lp) > cap) return E_SIZE;
-      for (uint32_t i = 0; i < ll; i++) dst[op + i] = lit[lp + i];     // forward: op <= lbase + lp
+      copy_fwd(dst + op, lit + lp, ll);          // forward: op <= lbase + lp
       op += ll; lp += ll;
       if (off == 0 || off > op) return E_DATA;
-      for (uint32_t i = 0; i < ml; i++) dst[op + i] = dst[op + i - (uint32_t)off];
+      copy_match(dst, op, (uint32_t)off, ml);
       op += ml;
     }
     if (b.pos != 0) return E_DATA;
   }
   const uint32_t rest = rsz - lp;
   if ((uint64_t)op + rest > cap) return E_SIZE;
-  for (uint32_t i = 0; i < rest; i++) dst[op + i] = lit[lp + i];
+  copy_fwd(dst + op, lit + lp, rest);
   return (int64_t)op + rest;
 }
 
