@@ -8,7 +8,7 @@
 //   inflate_kernel      persistent waves pull stream items from a device counter;
 //                       one wavefront decodes one zlib stream (inflate_wave.h)
 //   lz_kernel           the same for LZ4 / BloscLZ Blosc splits (lz_wave.h)
-//   zstd_kernel         zstd Blosc splits, one lane per split (zstd_lane.h)
+//   zstd_kernel         zstd Blosc splits, one wavefront per split (zstd_wave.h)
 //   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
 //   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
 //                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
@@ -31,7 +31,7 @@
 #include "deflate_wave.h"
 #include "lz_wave.h"
 #include "lz4_enc.h"
-#include "zstd_lane.h"
+#include "zstd_wave.h"
 
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -335,25 +335,49 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, 
 }
 
 // -------------------------------------------------------------------------
-// zstd splits (zstd_lane.h): one LANE per split; each lane owns a decode-table slot
-// in global scratch and pulls items from its own counter until the batch is done
+// zstd splits (zstd_wave.h): persistent 64-thread workgroups, one split per wave
+// (tables and the sequence window in LDS, all lanes resolving the output)
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) zstd_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) zstd_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
                                                   int64_t nchunks, uint32_t* __restrict__ counter,
                                                   int32_t* __restrict__ status,
-                                                  const uint32_t* __restrict__ kind_counts, uint8_t* scratch) {
+                                                  const uint32_t* __restrict__ kind_counts) {
+  __shared__ zw::Shared ls;
   if (kind_counts[2] == 0) return;
   const uint32_t total = offs[nchunks];
-  zs::Tables& t = *(zs::Tables*)(scratch + ((size_t)blockIdx.x * 64 + threadIdx.x) * zs::ZTAB_BYTES);
+  const int lane = threadIdx.x;
+#ifdef HZ_PROFILE
+  HzProf prof_;
+  for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
+  prof_.last = __builtin_amdgcn_s_memtime();
+  prof_.cur = 0;
+  HzProf* prof = &prof_;
+#else
+  HzProf* prof = nullptr;
+#endif
   for (;;) {
-    const uint32_t item = atomicAdd(counter, 1u);
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(counter, 1u);
+    item = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(item, 0, 64));
     if (item >= total) break;
     const int64_t ci = item_chunk(offs, nchunks, item);
     const Item it = slots[ci * KSLOTS + (item - offs[ci])];
-    if ((it.kind & 0xff) != ITEM_ZSTD) continue;
-    const int st = zs::frame(t, (const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len);
-    if (st != HSDS_OK) atomicMin(&status[it.chunk], st);
+    if ((zw::uni(it.kind) & 0xff) != ITEM_ZSTD) continue;
+    // the frame walk is uniform: keep its operands in scalar registers
+    const uint64_t src = ((uint64_t)zw::uni((uint32_t)(it.src >> 32)) << 32) | zw::uni((uint32_t)it.src);
+    const uint64_t dst = ((uint64_t)zw::uni((uint32_t)(it.dst >> 32)) << 32) | zw::uni((uint32_t)it.dst);
+    const int st = zw::frame(ls, (const uint8_t*)src, zw::uni(it.src_len), (uint8_t*)dst, zw::uni(it.dst_len), prof);
+    if (lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
+    __syncthreads();
   }
+#ifdef HZ_PROFILE
+  {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    prof_.acc[prof_.cur] += now - prof_.last;
+    if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&hz_prof[i], (unsigned long long)prof_.acc[i]);
+  }
+#endif
+  (void)prof;
 }
 
 // -------------------------------------------------------------------------
@@ -971,6 +995,7 @@ struct hsds_engine {
   int num_cus;
   int inflate_blocks_per_cu;   // occupancy of inflate_kernel (LDS-bound)
   int lz_blocks_per_cu;        // occupancy of lz_kernel
+  int zstd_blocks_per_cu;      // occupancy of zstd_kernel
   hz::Tune tune;
   // workspace (grown on demand)
   uint8_t* ws = nullptr;
@@ -992,8 +1017,6 @@ struct hsds_engine {
   size_t ews_bytes = 0;
   uint8_t* escr = nullptr;
   size_t escr_bytes = 0;
-  uint8_t* zscr = nullptr;       // zstd decode tables: one slot per lane of zstd_kernel
-  size_t zscr_bytes = 0;
   hipEvent_t ev2, ev3;
   int ev_enc_valid = 0;
 };
@@ -1047,6 +1070,9 @@ int hsds_engine_create(int device, hsds_engine** out) {
   int olz = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olz, lz_kernel, 64, 0) != hipSuccess || olz < 1) olz = 8;
   e->lz_blocks_per_cu = olz;
+  int ozs = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&ozs, zstd_kernel, 64, 0) != hipSuccess || ozs < 1) ozs = 8;
+  e->zstd_blocks_per_cu = ozs;
   int o1 = 0, o2 = 0, o3 = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, parse_kernel, 64, 0) != hipSuccess || o1 < 1) o1 = 2;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, huff_kernel, 64, 0) != hipSuccess || o2 < 1) o2 = 4;
@@ -1085,7 +1111,6 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (e->h_dev_dst) hipFree(e->h_dev_dst);
   if (e->ews) hipFree(e->ews);
   if (e->escr) hipFree(e->escr);
-  if (e->zscr) hipFree(e->zscr);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
   hipEventDestroy(e->ev2);
@@ -1134,7 +1159,6 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   // the destination buffer, so it spans the destination extent
   if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
   if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
-  if (grow((void**)&e->zscr, &e->zscr_bytes, (size_t)e->num_cus * 64 * zs::ZTAB_BYTES)) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
   hipLaunchKernelGGL(frame_walk_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
@@ -1152,8 +1176,11 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   if (lgrid < 1) lgrid = 1;
   hipLaunchKernelGGL(lz_kernel, dim3((unsigned)lgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 3, d_status,
                      ctr + 4);
-  hipLaunchKernelGGL(zstd_kernel, dim3((unsigned)e->num_cus), dim3(64), 0, st, slots, offs, nchunks, ctr + 7, d_status,
-                     ctr + 4, e->zscr);
+  int64_t zgrid = (int64_t)e->num_cus * e->zstd_blocks_per_cu;
+  if (zgrid > nchunks * 16) zgrid = nchunks * 16;
+  if (zgrid < 1) zgrid = 1;
+  hipLaunchKernelGGL(zstd_kernel, dim3((unsigned)zgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 7, d_status,
+                     ctr + 4);
   hipEventRecord(e->ev1, st);
   e->ev_valid = 1;
   hipLaunchKernelGGL(unshuffle_kernel, dim3(2048), dim3(256), 0, st, meta, list, ctr + 1, d_status);

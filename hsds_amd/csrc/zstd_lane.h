@@ -160,25 +160,39 @@ HZ_HD int16_t def_norm(uint32_t which, uint32_t s) {
   }
   return s == 0 ? 1 : s == 1 ? 4 : s == 2 ? 3 : s < 9 ? 2 : s < 46 ? 1 : -1;
 }
-HZ_HD uint32_t ll_base(uint32_t c) {
-  if (c < 16) return c;
-  const uint32_t v[20] = {16, 18, 20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
-  return v[c - 16];
-}
+// code -> baseline / extra bits (RFC 8878 3.1.1.3.2.1.1), from packed immediates: a
+// local table would be read from memory on every sequence
 HZ_HD uint32_t ll_bits(uint32_t c) {
   if (c < 16) return 0;
-  const uint8_t v[20] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-  return v[c - 16];
+  if (c >= 25) return c - 19;                                   // 25: 6 bits ... 35: 16 bits
+  return (uint32_t)((0x433221111ull >> (4 * (c - 16))) & 15u);   // 16..24: 1 1 1 1 2 2 3 3 4
 }
-HZ_HD uint32_t ml_base(uint32_t c) {
-  if (c < 32) return c + 3;
-  const uint32_t v[21] = {35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
-  return v[c - 32];
+HZ_HD uint32_t ll_base(uint32_t c) {
+  if (c < 16) return c;
+  if (c >= 25) return 1u << (c - 19);                           // 64, 128, ... 65536
+  // 16..24: 16 18 20 22 24 28 32 40 48, 6 bits each
+  const uint64_t v = 16ull | 18ull << 6 | 20ull << 12 | 22ull << 18 | 24ull << 24 | 28ull << 30 | 32ull << 36 |
+                     40ull << 42 | 48ull << 48;
+  return (uint32_t)((v >> (6 * (c - 16))) & 63u);
 }
 HZ_HD uint32_t ml_bits(uint32_t c) {
   if (c < 32) return 0;
-  const uint8_t v[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-  return v[c - 32];
+  if (c >= 43) return c - 36;                                   // 43: 7 bits ... 52: 16 bits
+  // 32..42: 1 1 1 1 2 2 3 3 4 4 5, 3 bits each
+  const uint64_t v = 1ull | 1ull << 3 | 1ull << 6 | 1ull << 9 | 2ull << 12 | 2ull << 15 | 3ull << 18 | 3ull << 21 |
+                     4ull << 24 | 4ull << 27 | 5ull << 30;
+  return (uint32_t)((v >> (3 * (c - 32))) & 7u);
+}
+HZ_HD uint32_t ml_base(uint32_t c) {
+  if (c < 32) return c + 3;
+  if (c >= 43) return (1u << (c - 36)) + 3u;                    // 131, 259, ... 65539
+  // 32..42: 35 37 39 41 43 47 51 59 67 | 83 99, 7 bits each
+  if (c < 41) {
+    const uint64_t v = 35ull | 37ull << 7 | 39ull << 14 | 41ull << 21 | 43ull << 28 | 47ull << 35 | 51ull << 42 |
+                       59ull << 49 | 67ull << 56;
+    return (uint32_t)((v >> (7 * (c - 32))) & 127u);
+  }
+  return c == 41 ? 83u : 99u;
 }
 
 // LL / OF / ML table: mode 0 predefined, 1 RLE, 2 FSE description, 3 repeat
@@ -274,17 +288,42 @@ HZ_HD int64_t huf_tree(Tables& t, const In& in, uint32_t at, uint32_t n) {
   return used;
 }
 
+// one Huffman literal stream (backward bitstream of n bytes at `at`) -> cnt symbols.
+// The bits come through a 64-bit register window refilled with two aligned dword
+// loads, so a refill costs one memory latency per ~4 symbols.
 HZ_HD int huf_stream(const Tables& t, const In& in, uint32_t at, uint32_t n, hz_gu8* out, uint32_t cnt) {
-  Bits b;
-  if (bits_init(b, in, at, n)) return -1;
-  for (uint32_t i = 0; i < cnt; i++) {
-    const int64_t save = b.pos;
-    const uint32_t peek = bits_read(b, t.huf_bits);
+  if (n == 0 || at + n > in.n) return -1;
+  const uint32_t last = b8(in, at + n - 1);
+  if (!last) return -1;
+  const uint32_t a = (uint32_t)(((uintptr_t)in.p + at) & 3u);
+  hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, in.p + at - a);     // stream byte i is base[a + i]
+  int64_t pos = 8 * (int64_t)(n - 1) + hib(last);          // bits left
+  int64_t wlo = 0;                                         // window holds stream bits [wlo, wlo + 64)
+  bool loaded = false, at_start = false;                   // at_start: the window reaches bit 0
+  uint64_t w = 0;
+  const uint32_t hb = t.huf_bits;
+  const uint64_t mask = (1ull << hb) - 1ull;
+  uint32_t i = 0;
+  for (; i < cnt; i++) {
+    const int64_t np = pos - (int64_t)hb;
+    if (!loaded || (np < wlo && !at_start)) {
+      // window [wl, wl + 64) with wl dword-aligned in base coordinates, wl <= np
+      int64_t wl = pos - 64 + 8 * (int64_t)a;                // in base bit coordinates
+      wl = wl < 0 ? 0 : ((wl + 31) & ~(int64_t)31);
+      const uint32_t k = (uint32_t)(wl >> 5);
+      w = (uint64_t)hz::load_word(base, k, a, a + n) | ((uint64_t)hz::load_word(base, k + 1u, a, a + n) << 32);
+      wlo = wl - 8 * (int64_t)a;                             // stream bit of w's bit 0 (may be < 0)
+      loaded = true;
+      at_start = wl == 0;
+    }
+    uint32_t peek;
+    if (np >= wlo) peek = (uint32_t)((w >> (np - wlo)) & mask);
+    else peek = (uint32_t)((w << (wlo - np)) & mask);      // bits below the stream start read as 0
     const Huf e = t.huf[peek];
-    b.pos = save - e.nb;
+    pos -= e.nb;
     out[i] = e.sym;
   }
-  return b.pos == 0 ? 0 : -1;
+  return pos == 0 ? 0 : -1;
 }
 
 // n bytes from s to d with d <= s (possibly overlapping): 16 loads issued together,

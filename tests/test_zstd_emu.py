@@ -19,19 +19,25 @@ SRC = os.path.join(ROOT, "tests", "emu", "zstd_emu.cpp")
 
 @pytest.fixture(scope="module")
 def emu():
-    hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("zstd_lane.h", "inflate_wave.h")]
+    hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("zstd_lane.h", "zstd_wave.h", "inflate_wave.h")]
     if not os.path.exists(EMU) or os.path.getmtime(EMU) < max(os.path.getmtime(p) for p in [SRC] + hdrs):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", EMU, SRC])
     L = ctypes.CDLL(EMU)
     L.emu_zstd_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+    L.emu_zstd_frame_wave.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
     return L
+
+
+WAVE = [False]
 
 
 def split(L, comp, n):
     src = np.frombuffer(comp, np.uint8).copy() if comp else np.zeros(1, np.uint8)
-    dst = np.zeros(max(n, 1), np.uint8)
-    r = L.emu_zstd_frame(src.ctypes.data, len(comp), dst.ctypes.data, n)
-    return r, dst[:n].tobytes()
+    dst = np.zeros(max(n, 1) + 3, np.uint8)
+    o = 1 if WAVE[0] else 0                   # the wave decoder also at an odd destination
+    fn = L.emu_zstd_frame_wave if WAVE[0] else L.emu_zstd_frame
+    r = fn(src.ctypes.data, len(comp), dst.ctypes.data + o, n)
+    return r, dst[o:o + n].tobytes()
 
 
 def frame_decode(L, f, oracle_lib=None):
@@ -74,7 +80,10 @@ def frame_decode(L, f, oracle_lib=None):
     return bytes(out)
 
 
-def test_zstd_reference_goldens(emu, golden2, oracle_lib):
+@pytest.mark.parametrize("wave", [False, True])
+def test_zstd_reference_goldens(emu, golden2, oracle_lib, wave):
+    """the lane decoder (zstd_lane.h) and the wavefront decoder (zstd_wave.h)"""
+    WAVE[0] = wave
     meta, arrs = golden2
     checked = 0
     for c in meta["cases"]:
@@ -89,3 +98,20 @@ def test_zstd_reference_goldens(emu, golden2, oracle_lib):
         assert hashlib.sha256(got).hexdigest() == c["out_sha256"], c["name"]
         checked += 1
     assert checked >= 35
+
+
+@pytest.mark.parametrize("wave", [False, True])
+def test_zstd_bench_corpus(emu, wave):
+    """libblosc 1.21 zstd frames of the bench corpus (128 KiB blocks with ~37K sequences
+    each, repeat offsets, multi-window decodes): decoded bytes equal the raw chunk"""
+    if not os.path.exists("/opt/conda/lib/libblosc.so.1"):
+        pytest.skip("the image's libblosc is absent")
+    import sys
+    sys.path.insert(0, ROOT)
+    from bench import make_corpus
+    WAVE[0] = wave
+    raw, blobs = make_corpus("ZSTD", 2, 20261016, 2)
+    for r, b in zip(raw, blobs):
+        got = frame_decode(emu, bytes(np.asarray(b, np.uint8)))
+        assert not isinstance(got, int), got
+        assert got == np.ascontiguousarray(r).view(np.uint8).tobytes()

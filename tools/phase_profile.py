@@ -24,6 +24,7 @@ NAMES = ["other", "blk-stage", "hdr-lens", "tables", "win-stage", "A", "A'", "re
 
 
 LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
+ZSTD_NAMES = ["other", "literals", "seq-decode", "resolve"]
 
 
 def run(fmt, n, unique, tune=None):
@@ -37,7 +38,7 @@ def run(fmt, n, unique, tune=None):
     d_src = torch.from_numpy(src).to(dev)
     d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
-    comp = "lz4" if fmt == "LZ4" else "zlib"
+    comp = {"LZ4": "lz4", "ZSTD": "zstd"}.get(fmt, "zlib")
     eng.decode(d_src, descs, d_dst, d_st, compressor=comp, shuffle=1, itemsize=4)
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
@@ -53,12 +54,14 @@ def run(fmt, n, unique, tune=None):
     streams = n * 4
     for i in range(16):
         if buf[i]:
-            print(f"   {(LZ_NAMES if fmt == 'LZ4' else NAMES)[i]:10s} {100.0*buf[i]/tot:6.2f}%   {buf[i]/streams/1e3:9.1f} kcyc/stream")
+            print(f"   {(LZ_NAMES if fmt == 'LZ4' else ZSTD_NAMES if fmt == 'ZSTD' else NAMES)[i]:10s} {100.0*buf[i]/tot:6.2f}%   {buf[i]/streams/1e3:9.1f} kcyc/stream")
 
 
 if __name__ == "__main__":
     n1 = int(os.environ.get("HZ_PROF_N1", "1024"))
     run("F1", n1, 256)
     run("F2", int(os.environ.get("HZ_PROF_N2", "256")), 128)
+    if os.environ.get("HZ_PROF_ZSTD", "0") == "1":
+        run("ZSTD", int(os.environ.get("HZ_PROF_NZS", "512")), 128)
     if os.environ.get("HZ_PROF_LZ", "1") == "1":
         run("LZ4", int(os.environ.get("HZ_PROF_NLZ", "1024")), 256)
