@@ -19,7 +19,11 @@
  *   - the other Blosc inner codecs the reference writes with cname = the dataset's
  *     compressor (storUtil.py:255-262): LZ4 block decode (lz4 1.9.x) and BloscLZ
  *     (c-blosc 1.21), restated from their published formats (orc_lz4_decode,
- *     orc_blosclz_decode).  zstd and snappy stay unsupported.
+ *     orc_blosclz_decode), and zstd (orc_zstd_decode); snappy stays unsupported.
+ *   - _unshuffle / _shuffle codec 2 (bitshuffle+LZ4 behind HSDS's 12-byte header,
+ *     storUtil.py:103-131,144-174): orc_bitshuffle_decode / orc_bitshuffle_encode.
+ *     bitshuffle 0.5.2 (requirements.txt:11) is absent; its bit transposition is
+ *     pinned by tests/golden/bitshuffle_cases (imagecodecs' bitshuffle 0.3.5 core).
  *
  * Parity pinning: tests/test_oracle_golden.py checks every function here against the
  * golden vectors in tests/golden/ that were produced by the reference's own
@@ -954,3 +958,112 @@ void orc_encode_batch(int op, const uint8_t *const *src, const int64_t *srclen, 
   orc_batch_t b = {op, src, srclen, dst, dstcap, status, n, 0, doshuffle, typesize, clevel, 0};
   run_batch(&b, nthreads);
 }
+
+
+/* ---- bitshuffle + LZ4 (shuffle = 2) ------------------------------------------------
+ * HSDS frame (storUtil._shuffle, storUtil.py:103-131): u64 BE chunk bytes, u32 BE
+ * block_size * itemsize, then bitshuffle.compress_lz4: per block of block_size
+ * elements a u32 BE LZ4 block size and the LZ4 block of the block's bit transposition
+ * (bshuf_trans_bit_elem); a last block of the remaining elements rounded down to a
+ * multiple of 8; the n % 8 leftover elements raw.  Bit transposition of n elements
+ * (n % 8 == 0) of es bytes: row r = 8 j + k holds bit k of byte j of every element,
+ * element i at bit i % 8 of row byte i / 8.
+ */
+#define BSHUF_ERR ORC_ERR_DATA
+
+static int64_t bshuf_default_block(int64_t es) {     /* bshuf_default_block_size */
+  int64_t bs = (8192 / es) / 8 * 8;
+  return bs < 128 ? 128 : bs;
+}
+
+static void bshuf_trans(const uint8_t *in, uint8_t *out, int64_t n, int64_t es) {
+  const int64_t row = n / 8;
+  memset(out, 0, (size_t)(n * es));
+  for (int64_t i = 0; i < n; i++)
+    for (int64_t j = 0; j < es; j++) {
+      const uint8_t b = in[i * es + j];
+      for (int k = 0; k < 8; k++)
+        out[(j * 8 + k) * row + i / 8] |= (uint8_t)(((b >> k) & 1) << (i % 8));
+    }
+}
+
+static void bshuf_untrans(const uint8_t *in, uint8_t *out, int64_t n, int64_t es) {
+  const int64_t row = n / 8;
+  for (int64_t i = 0; i < n; i++)
+    for (int64_t j = 0; j < es; j++) {
+      uint8_t b = 0;
+      for (int k = 0; k < 8; k++) b |= (uint8_t)(((in[(j * 8 + k) * row + i / 8] >> (i % 8)) & 1) << k);
+      out[i * es + j] = b;
+    }
+}
+
+static uint32_t rd32be(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+/* storUtil._unshuffle(codec=2) (storUtil.py:144-174) + bitshuffle.decompress_lz4:
+ * returns chunk_bytes or an error (each error is HTTPInternalServerError there). */
+int64_t orc_bitshuffle_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64_t chunk_bytes, int64_t es) {
+  if (srclen < 12 || es < 1 || chunk_bytes < 0 || chunk_bytes % es) return ORC_ERR_FRAME;    /* :148-152 */
+  uint64_t total = 0;
+  for (int i = 0; i < 8; i++) total = total << 8 | src[i];
+  if (total != (uint64_t)chunk_bytes) return ORC_ERR_SIZE;                                 /* :160-164 */
+  int64_t bs = (int64_t)rd32be(src + 8) / es;                                              /* :167 */
+  if (bs == 0) bs = bshuf_default_block(es);
+  if (bs % 8) return ORC_ERR_FRAME;                           /* bshuf: block size not a multiple of 8 */
+  const int64_t n = chunk_bytes / es;
+  uint8_t *tmp = (uint8_t *)malloc((size_t)(bs * es) + 1);
+  int64_t p = 12, e = 0;
+  int64_t rc = chunk_bytes;
+  while (e + 8 <= n && rc >= 0) {
+    int64_t cnt = n - e >= bs ? bs : (n - e) / 8 * 8;
+    if (p + 4 > srclen) { rc = ORC_ERR_TRUNC; break; }
+    const int64_t nb = (int64_t)rd32be(src + p);
+    p += 4;
+    if (nb > srclen - p) { rc = ORC_ERR_TRUNC; break; }
+    const int64_t r = orc_lz4_decode(src + p, nb, tmp, cnt * es);
+    if (r != cnt * es) { rc = r < 0 ? r : ORC_ERR_SIZE; break; }
+    bshuf_untrans(tmp, dst + e * es, cnt, es);
+    p += nb;
+    e += cnt;
+  }
+  free(tmp);
+  if (rc < 0) return rc;
+  const int64_t left = (n - e) * es;                          /* n % 8 elements, raw */
+  if (p + left > srclen) return ORC_ERR_TRUNC;
+  memcpy(dst + e * es, src + p, (size_t)left);
+  p += left;
+  if (p != srclen) return ORC_ERR_SIZE;                       /* decompress_lz4: consumed != input */
+  return chunk_bytes;
+}
+
+/* storUtil._shuffle(codec=2) with the oracle's greedy LZ4 writer (the LZ4 bytes differ
+ * from liblz4's; any LZ4 decoder reads both).  Returns the frame size or an error. */
+int64_t orc_bitshuffle_encode(const uint8_t *src, int64_t nbytes, int64_t es, int64_t block, uint8_t *dst,
+                              int64_t cap) {
+  if (es < 1 || nbytes % es || block < 0 || block % 8 || cap < 12) return ORC_ERR_FRAME;
+  const int64_t bs = block ? block : bshuf_default_block(es), n = nbytes / es;
+  for (int i = 0; i < 8; i++) dst[i] = (uint8_t)((uint64_t)nbytes >> (56 - 8 * i));
+  const uint32_t bn = (uint32_t)(block * es);
+  dst[8] = (uint8_t)(bn >> 24); dst[9] = (uint8_t)(bn >> 16); dst[10] = (uint8_t)(bn >> 8); dst[11] = (uint8_t)bn;
+  uint8_t *tmp = (uint8_t *)malloc((size_t)(bs * es) + 1);
+  int64_t p = 12, e = 0, rc = 0;
+  while (e + 8 <= n) {
+    const int64_t cnt = n - e >= bs ? bs : (n - e) / 8 * 8;
+    bshuf_trans(src + e * es, tmp, cnt, es);
+    if (p + 4 > cap) { rc = ORC_ERR_SIZE; break; }
+    const int64_t c = orc_lz4_encode(tmp, cnt * es, dst + p + 4, cap - p - 4);
+    if (c < 0) { rc = c; break; }
+    dst[p] = (uint8_t)(c >> 24); dst[p + 1] = (uint8_t)(c >> 16); dst[p + 2] = (uint8_t)(c >> 8); dst[p + 3] = (uint8_t)c;
+    p += 4 + c;
+    e += cnt;
+  }
+  free(tmp);
+  if (rc < 0) return rc;
+  const int64_t left = (n - e) * es;
+  if (p + left > cap) return ORC_ERR_SIZE;
+  memcpy(dst + p, src + e * es, (size_t)left);
+  return p + left;
+}
+
+/* the bare transposition (tests) */
+void orc_bshuf_trans(const uint8_t *in, uint8_t *out, int64_t n, int64_t es) { bshuf_trans(in, out, n, es); }
+void orc_bshuf_untrans(const uint8_t *in, uint8_t *out, int64_t n, int64_t es) { bshuf_untrans(in, out, n, es); }

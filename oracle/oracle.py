@@ -70,6 +70,12 @@ def lib():
         L.orc_unshuffle.argtypes = [P, I64, I, P]
         L.orc_adler32.argtypes = [P, I64]
         L.orc_adler32.restype = ctypes.c_uint32
+        L.orc_bitshuffle_decode.argtypes = [P, I64, P, I64, I64]
+        L.orc_bitshuffle_decode.restype = I64
+        L.orc_bitshuffle_encode.argtypes = [P, I64, I64, I64, P, I64]
+        L.orc_bitshuffle_encode.restype = I64
+        L.orc_bshuf_trans.argtypes = [P, P, I64, I64]
+        L.orc_bshuf_untrans.argtypes = [P, P, I64, I64]
         L.orc_uncompress_batch.argtypes = [P, P, P, P, I64, I, I, I, I, P]
         L.orc_encode_batch.argtypes = [I, P, P, P, P, I64, I, I, I, I, P]
         _lib = L
@@ -259,3 +265,33 @@ def select_scatter(arr, slices, data):
     """np_arr[data_sel] = chunk_arr (chunk_crawl.py:418) / chunkWriteSelection copy."""
     arr[tuple(slices)] = data
     return arr
+
+
+# ---- bitshuffle + LZ4 (shuffle = 2; storUtil.py:103-131,144-174) ----
+
+def bitshuffle_decode(data, chunk_bytes, itemsize):
+    """storUtil._unshuffle(codec=2): the chunk bytes, or a negative status"""
+    s = _u8(data)
+    if s.size == 0:
+        s = np.zeros(1, np.uint8)[:0]
+    out = np.empty(max(chunk_bytes, 1), np.uint8)
+    r = lib().orc_bitshuffle_decode(s.ctypes.data, s.size, out.ctypes.data, chunk_bytes, itemsize)
+    return r if r < 0 else out[:chunk_bytes].tobytes()
+
+
+def bitshuffle_encode(data, itemsize, block=2048):
+    """storUtil._shuffle(codec=2) with block = config bit_shuffle_default_blocksize"""
+    s = _u8(data)
+    cap = s.size + s.size // 8 + 4 * (s.size // max(block * itemsize, 8) + 2) + 64
+    out = np.empty(cap, np.uint8)
+    n = lib().orc_bitshuffle_encode(s.ctypes.data, s.size, itemsize, block, out.ctypes.data, cap)
+    if n < 0:
+        raise ValueError(f"bitshuffle encode failed: {n}")
+    return out[:n].tobytes()
+
+
+def bshuf_trans(data, itemsize):
+    s = _u8(data)
+    out = np.empty(s.size, np.uint8)
+    lib().orc_bshuf_trans(s.ctypes.data, out.ctypes.data, s.size // itemsize, itemsize)
+    return out.tobytes()

@@ -32,6 +32,16 @@ def golden2():
 
 
 @pytest.fixture(scope="session")
+def bshuf_golden():
+    """bitshuffle+LZ4 HSDS frames (tests/golden/make_bitshuffle_golden.py)"""
+    import json
+    import numpy as np
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "bitshuffle_cases.json")))
+    arrs = np.load(os.path.join(ROOT, "tests", "golden", "bitshuffle_cases.npz"))
+    return d, arrs
+
+
+@pytest.fixture(scope="session")
 def selection_golden():
     import json
     return json.load(open(os.path.join(ROOT, "tests", "golden", "selection_cases.json")))
