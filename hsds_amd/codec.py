@@ -7,11 +7,13 @@ Same names, argument meaning and error behaviour as the reference:
     storUtil.py:203-204) or inflates a zlib stream (storUtil.py:209-220) and
     byte-unshuffles it (storUtil.py:225-226).  Any codec failure raises
     HTTPInternalServerError, an unknown shuffle code raises ValueError.
-  * `_shuffle` / `_unshuffle` codec 1 = numcodecs.Shuffle(itemsize) (storUtil.py:94-143).
+  * `_shuffle` / `_unshuffle` codec 1 = numcodecs.Shuffle(itemsize) (storUtil.py:94-143);
+    `_unshuffle` codec 2 = bitshuffle+LZ4 behind HSDS's 12-byte header
+    (storUtil.py:144-174), decoded by bshuf_kernel.
 
 All byte work runs on the MI355X through the C ABI (include/hsds_amd.h); there is
-no CPU fallback.  Bitshuffle (codec 2) and Blosc inner codecs other than zlib are
-outside this engine's scope and raise.
+no CPU fallback.  The bitshuffle writer (`_shuffle` codec 2), the zstd writer and the
+snappy codec raise NotImplementedError.
 """
 import numpy as np
 
@@ -74,7 +76,10 @@ def _shuffle(codec, data, chunk_shape=None, dtype=None):
 
 
 def _unshuffle(codec, data, dtype=None, chunk_shape=None):
-    """storUtil._unshuffle (storUtil.py:136): codec 1 = byte unshuffle."""
+    """storUtil._unshuffle (storUtil.py:136): codec 1 = byte unshuffle, codec 2 =
+    bitshuffle+LZ4 (storUtil.py:144-174: a short buffer, a header whose chunk bytes
+    differ from prod(chunk_shape) * itemsize, and any decode failure raise
+    HTTPInternalServerError)."""
     if codec == BYTE_SHUFFLE:
         src = _as_bytes(data)
         out = np.empty(src.size, np.uint8)
@@ -84,7 +89,19 @@ def _unshuffle(codec, data, dtype=None, chunk_shape=None):
             raise nat.NativeError(rc, "hsds_unshuffle")
         return out.tobytes()
     if codec == BIT_SHUFFLE:
-        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+        itemsize = _itemsize(dtype)
+        chunk_size = int(np.prod(chunk_shape)) * itemsize      # TypeError without a shape, as there
+        src = _as_bytes(data)
+        if src.size < 12:
+            raise HTTPInternalServerError()
+        out = np.empty(max(chunk_size, 1), np.uint8)
+        n = nat.lib().hsds_uncompress(nat.engine().h, src.ctypes.data, src.size, nat.COMP_NONE, BIT_SHUFFLE,
+                                      itemsize, out.ctypes.data, chunk_size)
+        if n < 0:
+            if n in (nat.ERR_ARG, nat.ERR_DEVICE):
+                raise nat.NativeError(n, "hsds_uncompress")
+            raise HTTPInternalServerError()
+        return out[:n].tobytes()
     raise ValueError()
 
 
@@ -105,7 +122,11 @@ def _uncompress(data, compressor=None, shuffle=0, level=None, dtype=None, chunk_
     if comp == nat.COMP_NONE and not shuffle:
         return bytes(src)
     if shuffle == BIT_SHUFFLE:
-        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+        # the outer codec first (its output is the bitshuffle object), then _unshuffle
+        # codec 2 (storUtil.py:189-227)
+        if comp != nat.COMP_NONE:
+            data = _uncompress(data, compressor, 0, level, dtype, None)
+        return _unshuffle(BIT_SHUFFLE, data, dtype=dtype, chunk_shape=chunk_shape)
     if comp != nat.COMP_NONE and _blosc_nbytes(src) is not None and (src[2] >> 5) not in (0, 1, 3, 4):
         # snappy inner codec: not built into the numcodecs the reference pins either
         raise NotImplementedError(f"Blosc inner codec {int(src[2] >> 5)} (snappy) is outside the hsds_amd engine scope")

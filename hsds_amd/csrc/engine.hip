@@ -9,6 +9,8 @@
 //                       one wavefront decodes one zlib stream (inflate_wave.h)
 //   lz_kernel           the same for LZ4 / BloscLZ Blosc splits (lz_wave.h)
 //   zstd_kernel         zstd Blosc splits, one wavefront per split (zstd_wave.h)
+//   bshuf_kernel        bitshuffle+LZ4 chunks (shuffle = 2), one wavefront per chunk
+//                       (bshuf.h)
 //   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
 //   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
 //                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
@@ -32,6 +34,7 @@
 #include "lz_wave.h"
 #include "lz4_enc.h"
 #include "zstd_wave.h"
+#include "bshuf.h"
 
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -378,6 +381,34 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) zs
   }
 #endif
   (void)prof;
+}
+
+// -------------------------------------------------------------------------
+// bitshuffle+LZ4 chunks (storUtil._unshuffle codec 2, storUtil.py:144-174): persistent
+// 64-thread workgroups take one chunk at a time (bshuf.h); the LZ4 blocks are staged in
+// `stg` at the chunk's destination offsets, then un-transposed into dst.
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) bshuf_kernel(const uint8_t* __restrict__ src,
+                                                   const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
+                                                   uint8_t* __restrict__ dst, uint8_t* __restrict__ stg,
+                                                   int32_t* __restrict__ status, uint32_t* __restrict__ counter,
+                                                   int itemsize) {
+  __shared__ bs::Shared sh;
+  const int lane = threadIdx.x;
+  for (;;) {
+    uint32_t ci = 0;
+    if (lane == 0) ci = atomicAdd(counter, 1u);
+    ci = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(ci, 0, 64));
+    if ((int64_t)ci >= nchunks) break;
+    const hsds_chunk_desc d = chunks[ci];
+    int st;
+    if (d.src_len > 0xffffffffull || d.dst_len > 0xffffffffull) st = HSDS_ERR_SIZE;
+    else
+      st = bs::chunk(sh, src + d.src_off, (uint32_t)d.src_len, dst + d.dst_off, stg + d.dst_off, (uint32_t)d.dst_len,
+                     (uint32_t)itemsize);
+    if (lane == 0) status[ci] = st;
+    __syncthreads();
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -995,6 +1026,7 @@ struct hsds_engine {
   int num_cus;
   int inflate_blocks_per_cu;   // occupancy of inflate_kernel (LDS-bound)
   int lz_blocks_per_cu;        // occupancy of lz_kernel
+  int bshuf_blocks_per_cu;     // occupancy of bshuf_kernel
   int zstd_blocks_per_cu;      // occupancy of zstd_kernel
   hz::Tune tune;
   // workspace (grown on demand)
@@ -1070,6 +1102,9 @@ int hsds_engine_create(int device, hsds_engine** out) {
   int olz = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olz, lz_kernel, 64, 0) != hipSuccess || olz < 1) olz = 8;
   e->lz_blocks_per_cu = olz;
+  int obs = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&obs, bshuf_kernel, 64, 0) != hipSuccess || obs < 1) obs = 8;
+  e->bshuf_blocks_per_cu = obs;
   int ozs = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&ozs, zstd_kernel, 64, 0) != hipSuccess || ozs < 1) ozs = 8;
   e->zstd_blocks_per_cu = ozs;
@@ -1138,6 +1173,22 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   if (nchunks > (int64_t)(1u << 24)) return HSDS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (shuffle == HSDS_SHUFFLE_BIT && compressor == HSDS_COMP_NONE) {
+    // bitshuffle+LZ4 objects as stored (no outer compressor): bshuf_kernel alone
+    if (inexact) return HSDS_ERR_UNSUPPORTED;       // _unshuffle needs the chunk shape
+    if (grow((void**)&e->ws, &e->ws_bytes, 256)) return HSDS_ERR_DEVICE;
+    if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
+    uint32_t* ctr = (uint32_t*)e->ws;
+    if (hipMemsetAsync(ctr, 0, 4, st) != hipSuccess) return HSDS_ERR_DEVICE;
+    int64_t grid = (int64_t)e->num_cus * e->bshuf_blocks_per_cu;
+    if (grid > nchunks) grid = nchunks;
+    hipEventRecord(e->ev0, st);
+    hipLaunchKernelGGL(bshuf_kernel, dim3((unsigned)grid), dim3(64), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
+                       (uint8_t*)d_dst, e->tmp, d_status, ctr, itemsize);
+    hipEventRecord(e->ev1, st);
+    e->ev_valid = 1;
+    return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+  }
   // workspace layout
   const size_t sz_slots = (size_t)nchunks * KSLOTS * sizeof(Item);
   const size_t sz_counts = ((size_t)nchunks * 4 + 255) & ~(size_t)255;

@@ -59,7 +59,7 @@ extern "C" {
 /* shuffle codes (storUtil.BYTE_SHUFFLE / BIT_SHUFFLE) */
 #define HSDS_SHUFFLE_NONE 0
 #define HSDS_SHUFFLE_BYTE 1
-#define HSDS_SHUFFLE_BIT 2      /* not supported (bitshuffle+LZ4)                 */
+#define HSDS_SHUFFLE_BIT 2      /* bitshuffle+LZ4 objects (decode, no outer codec) */
 
 #define HSDS_MAX_RANK 8
 
@@ -116,7 +116,12 @@ int hsds_set_tuning(hsds_engine* e, uint32_t seg_bits, uint32_t warmup_bits, uin
  * stream is inflated (compressor == HSDS_COMP_ZLIB) and then byte-unshuffled
  * with `itemsize` when shuffle == HSDS_SHUFFLE_BYTE.  dst_extent = bytes spanned by
  * d_dst (max dst_off + dst_len); the engine keeps a staging buffer of that size
- * for chunks that must be unshuffled after inflate. */
+ * for chunks that must be unshuffled after inflate.
+ * shuffle == HSDS_SHUFFLE_BIT with compressor == HSDS_COMP_NONE decodes the
+ * bitshuffle+LZ4 objects of storUtil._shuffle(codec=2) (12-byte header, replaces
+ * storUtil._unshuffle codec 2, storUtil.py:144-174; dst_len = the chunk bytes the
+ * header must state).  With an outer compressor, decode with HSDS_SHUFFLE_NONE first
+ * and then run this on its outputs (per-chunk status HSDS_ERR_UNSUPPORTED otherwise). */
 int hsds_decode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks,
                       int64_t nchunks, void* d_dst, uint64_t dst_extent, int32_t* d_status,
                       int compressor, int shuffle, int itemsize, void* stream);
