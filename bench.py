@@ -60,6 +60,11 @@ def make_corpus(fmt, n_unique, base_seed, threads):
             return out[:k].copy()
         with ThreadPoolExecutor(threads) as ex:
             blobs = list(ex.map(enc, raw))
+    elif fmt == "BSHUF":
+        # bitshuffle+LZ4 objects as _shuffle(codec=2) writes them for an f32 chunk
+        # (HSDS default block 2048 elements, 12-byte header); oracle LZ4 writer
+        with ThreadPoolExecutor(threads) as ex:
+            blobs = [np.frombuffer(b, np.uint8) for b in ex.map(lambda r: orc.bitshuffle_encode(r, 4, 2048), raw)]
     elif fmt == "LZ4":
         # Blosc-lz4 frames as _compress(compressor="lz4", level=5) lays them out
         # (typesize 1, 128 KiB blocks); the payload is the oracle's greedy LZ4 writer
@@ -90,10 +95,11 @@ def run_format(fmt, args, dev, rank, world):
     d_desc = to_device_bytes(descs, dev)
     stream = torch.cuda.current_stream()
 
-    comp = {"LZ4": "lz4", "ZSTD": "zstd"}.get(fmt, "zlib")
+    comp = {"LZ4": "lz4", "ZSTD": "zstd", "BSHUF": None}.get(fmt, "zlib")
+    shuffle = 2 if fmt == "BSHUF" else 1
 
     def step():
-        eng.decode(d_src, d_desc, d_dst, d_st, compressor=comp, shuffle=1, itemsize=4, stream=stream)
+        eng.decode(d_src, d_desc, d_dst, d_st, compressor=comp, shuffle=shuffle, itemsize=4, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -549,6 +555,22 @@ def cpu_baseline(blobs, seconds, threads, compressor="zlib"):
     return done * CHUNK_BYTES / el / 1e9, done
 
 
+def cpu_baseline_bshuf(blobs, seconds, threads):
+    """Oracle bitshuffle+LZ4 decode (storUtil._unshuffle codec 2 restated) on the box's
+    host cores, one chunk per task, bounded to about `seconds` of wall time."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as orc
+    done = 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < seconds:
+            for r in ex.map(lambda b: orc.bitshuffle_decode(b, CHUNK_BYTES, 4), blobs):
+                assert not isinstance(r, int)
+            done += len(blobs)
+    el = time.perf_counter() - t0
+    return done * CHUNK_BYTES / el / 1e9, done
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -562,6 +584,7 @@ def main():
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     ap.add_argument("--lz4", type=int, default=1, help="also measure Blosc-lz4 1 MiB chunks (N=1)")
+    ap.add_argument("--bshuf", type=int, default=1, help="also measure bitshuffle+LZ4 1 MiB f32 chunks (N=1)")
     ap.add_argument("--cfg1", type=int, default=1, help="also measure configs[0] uncompressed read selection (N=1)")
     ap.add_argument("--zstd", type=int, default=1, help="also measure Blosc-zstd 1 MiB chunks (N=1; needs the image's libblosc)")
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
@@ -648,6 +671,21 @@ def main():
             del r4
         except Exception as e:   # corpus writer unavailable: the headline stands
             out["zstd"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+    if world == 1 and args.bshuf:
+        bu = args.unique
+        args.unique = min(args.unique, 256)
+        r5 = run_format("BSHUF", args, dev, rank, world)
+        args.unique = bu
+        out["bshuf"] = {"value": round(r5["dec_bytes"] * args.steps / r5["elapsed_s"] / 1e9, 2), "unit": "GB/s",
+                        "format": "bitshuffle+LZ4 objects (shuffle=2, f32, 2048-element blocks, 12-byte header)",
+                        "compressed_bytes_per_gpu": r5["comp_bytes"], "bshuf_kernel_ms": round(r5["kernel_ms"], 3)}
+        if args.cpu_seconds > 0:
+            threads = min(16, os.cpu_count() or 1)
+            v, n = cpu_baseline_bshuf(r5["blobs"][:64], min(args.cpu_seconds, 4.0), threads)
+            out["bshuf"]["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+                                            "sample": f"{n} x 1 MiB bitshuffle+LZ4 chunk decodes, oracle, "
+                                                      f"{threads} threads"}
+        del r5
     if world == 1 and args.cfg1:
         out["cfg1"] = run_cfg1(args, dev)
     if world == 1 and args.cfg3:
