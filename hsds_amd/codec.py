@@ -9,11 +9,11 @@ Same names, argument meaning and error behaviour as the reference:
     HTTPInternalServerError, an unknown shuffle code raises ValueError.
   * `_shuffle` / `_unshuffle` codec 1 = numcodecs.Shuffle(itemsize) (storUtil.py:94-143);
     `_unshuffle` codec 2 = bitshuffle+LZ4 behind HSDS's 12-byte header
-    (storUtil.py:144-174), decoded by bshuf_kernel.
+    (storUtil.py:144-174), decoded by bshuf_kernel; `_shuffle` codec 2 writes it
+    (storUtil.py:103-131) through the bitshuffle encode kernels.
 
 All byte work runs on the MI355X through the C ABI (include/hsds_amd.h); there is
-no CPU fallback.  The bitshuffle writer (`_shuffle` codec 2), the zstd writer and the
-snappy codec raise NotImplementedError.
+no CPU fallback.  The zstd writer and the snappy codec raise NotImplementedError.
 """
 import numpy as np
 
@@ -27,6 +27,8 @@ except Exception:  # pragma: no cover - aiohttp is in the image
 
 BYTE_SHUFFLE = 1
 BIT_SHUFFLE = 2
+# config bit_shuffle_default_blocksize (storUtil.py:110), elements per bitshuffle block
+BIT_SHUFFLE_BLOCK = 2048
 
 
 def getCompressors():
@@ -71,7 +73,24 @@ def _shuffle(codec, data, chunk_shape=None, dtype=None):
             raise nat.NativeError(rc, "hsds_shuffle")
         return out.tobytes()
     if codec == BIT_SHUFFLE:
-        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+        # bitshuffle.compress_lz4 of data.reshape(chunk_shape) behind the 12-byte header
+        # (storUtil.py:103-131); the reshape's ValueError on a size mismatch is kept
+        itemsize = dtype.itemsize if isinstance(dtype, np.dtype) else np.dtype(dtype).itemsize \
+            if dtype is not None else None.itemsize        # AttributeError without a dtype, as there
+        chunk_size = int(np.prod(chunk_shape)) * itemsize
+        src = _as_bytes(data)
+        if src.size != chunk_size or src.size % itemsize:
+            raise ValueError(f"cannot reshape array of size {src.size // max(itemsize, 1)} into shape {chunk_shape}")
+        block = BIT_SHUFFLE_BLOCK
+        cap = int(nat.lib().hsds_bitshuffle_bound(src.size, itemsize, block))
+        if cap < 0:
+            raise nat.NativeError(cap, "hsds_bitshuffle_bound")
+        out = np.empty(cap, np.uint8)
+        n = nat.lib().hsds_bitshuffle_compress(nat.engine().h, src.ctypes.data, src.size, itemsize, block,
+                                               out.ctypes.data, cap)
+        if n < 0:
+            raise nat.NativeError(n, "hsds_bitshuffle_compress")
+        return out[:n].tobytes()
     raise ValueError()
 
 
@@ -170,15 +189,25 @@ def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape
     storUtil.py:255-257; lz4 and lz4hc carry LZ4 blocks, blosclz BloscLZ), typesize 1 because the
     reference always hands Blosc a bytes object, and the byte-shuffle flag from
     `shuffle`.  Differences from the reference, by design:
-      * bitshuffle (shuffle=2) and the zstd encoder are outside this engine
-        and raise NotImplementedError (the reference would encode them with c-blosc);
+      * the zstd encoder is outside this engine and raises NotImplementedError
+        (the reference would encode it with c-blosc);
+      * bitshuffle (shuffle=2) objects carry the GPU LZ4 writer's blocks, not liblz4's
+        (any valid block: bitshuffle.decompress_lz4 reads both);
       * an encoder failure raises instead of silently storing the raw bytes
         (storUtil.py:266-279 logs and returns `data`, which its own reader then
         rejects: SURVEY.md section 8b)."""
     if not compressor and shuffle != BIT_SHUFFLE:
         return data
     if shuffle == BIT_SHUFFLE:
-        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+        # bitshuffle first, then Blosc without its own shuffle (storUtil.py:243-251); a
+        # bitshuffle failure is logged there and the bytes go on unshuffled
+        try:
+            data = _shuffle(BIT_SHUFFLE, data, dtype=dtype, chunk_shape=chunk_shape)
+        except (ValueError, TypeError, AttributeError):
+            pass
+        shuffle = 0
+        if not compressor or compressor == "scaleoffset":
+            return data
     if shuffle not in (0, BYTE_SHUFFLE):
         raise ValueError()
     if not compressor or compressor == "scaleoffset":

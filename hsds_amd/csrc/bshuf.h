@@ -81,6 +81,32 @@ inline void untrans_block(hz_gcu8* in, hz_gu8* out, uint32_t cnt, uint32_t es) {
   }
 }
 
+// Forward bit transposition (the write path, storUtil._shuffle codec 2 ->
+// bshuf_trans_bit_elem) of elements 8 q .. 8 q + 7 of a block of cnt elements
+// (cnt % 8 == 0, row = cnt / 8): blk points at the block's first element, out at its
+// transposed copy.  Row byte q of rows 8 j .. 8 j + 7 comes from byte j of the 8
+// elements, through the same 8x8 bit transpose the decoder inverts with.
+HZ_HD void trans_group(hz_gcu8* blk, hz_gu8* out, uint32_t q, uint32_t row, uint32_t es) {
+  hz_gcu8* e = blk + (uint64_t)q * 8u * es;
+  if (es == 4u && !(((uintptr_t)e) & 3u)) {
+    uint32_t w[8];
+    for (uint32_t m = 0; m < 8u; m++) w[m] = *(const hz_gu32*)(e + 4u * m);
+    for (uint32_t j = 0; j < 4u; j++) {
+      uint64_t x = 0;
+      for (uint32_t m = 0; m < 8u; m++) x |= (uint64_t)((w[m] >> (8u * j)) & 0xffu) << (8u * m);
+      const uint64_t y = t8x8(x);                        // byte k: bit k of byte j of each element
+      for (uint32_t k = 0; k < 8u; k++) out[(uint64_t)(j * 8u + k) * row + q] = (uint8_t)(y >> (8u * k));
+    }
+    return;
+  }
+  for (uint32_t j = 0; j < es; j++) {
+    uint64_t x = 0;
+    for (uint32_t m = 0; m < 8u; m++) x |= (uint64_t)e[m * es + j] << (8u * m);
+    const uint64_t y = t8x8(x);
+    for (uint32_t k = 0; k < 8u; k++) out[(uint64_t)(j * 8u + k) * row + q] = (uint8_t)(y >> (8u * k));
+  }
+}
+
 HZ_HD uint32_t be32(hz_gcu8* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
 struct Shared {

@@ -709,9 +709,10 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
                                                    const uint32_t* __restrict__ segoffs, int64_t nchunks,
                                                    uint32_t* __restrict__ counter, hd::SegParse* __restrict__ sp,
                                                    SegMeta* __restrict__ meta, uint16_t* __restrict__ tok,
-                                                   uint32_t* __restrict__ adler, uint32_t seg_cap, int level) {
+                                                   uint32_t* __restrict__ adler, uint32_t seg_cap, int level,
+                                                   uint32_t ks, uint32_t item_cap) {
   __shared__ hd::ParseShared sh;
-  const uint32_t total = offs[nchunks];
+  const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   const int lane = threadIdx.x;
   const hd::Tune tune = hd::tune_for_level(level);
 #ifdef HZ_PROFILE
@@ -729,7 +730,8 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
     item = __shfl(item, 0, 64);
     if (item >= total) break;
     const int64_t ci = item_chunk(offs, nchunks, item);
-    const uint32_t slot = (uint32_t)(ci * KSLOTS + (item - offs[ci]));
+    // ks: slots per chunk (Blosc splits), or 0 for the compact layout (slot = item)
+    const uint32_t slot = ks ? (uint32_t)(ci * ks + (item - offs[ci])) : item;
     const EncItem it = slots[slot];
     const uint32_t g0 = segoffs[ci] + it.seg0;
     const uint32_t nseg = hd::nsegments(it.len);
@@ -931,11 +933,12 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
                                                        const hsds_chunk_desc* __restrict__ chunks, uint8_t* dst_base,
                                                        const EncGeom* __restrict__ geom,
                                                        const ItemOut* __restrict__ iout,
-                                                       const int32_t* __restrict__ status, int write, int blosclz) {
-  const uint32_t total = offs[nchunks];
+                                                       const int32_t* __restrict__ status, int write, int blosclz,
+                                                       uint32_t ks, uint32_t item_cap) {
+  const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
     const int64_t ci = item_chunk(offs, nchunks, item);
-    const uint32_t slot = (uint32_t)(ci * KSLOTS + (item - offs[ci]));
+    const uint32_t slot = ks ? (uint32_t)(ci * ks + (item - offs[ci])) : item;
     const EncItem it = slots[slot];
     const uint32_t g0 = segoffs[ci] + it.seg0;
     if (g0 + hd::nsegments(it.len) > seg_cap) continue;   // the layout phase fails the chunk
@@ -1014,6 +1017,129 @@ __global__ void __launch_bounds__(256) raw_copy_kernel(const uint8_t* __restrict
   const ItemOut* io = iout + ci * KSLOTS;
   for (uint32_t k = 0; k < cnt; k++)
     if (io[k].raw) wg_copy(out + io[k].pos, (const uint8_t*)it[k].src, it[k].len, it[k].ts, it[k].neb, it[k].off);
+}
+
+// -------------------------------------------------------------------------
+// bitshuffle+LZ4 write path (storUtil._shuffle codec 2, storUtil.py:103-131 ->
+// bitshuffle.compress_lz4): plan -> scan -> fill (one LZ4 item per block, compact slot
+// layout) -> forward bit transposition into a staging copy -> parse -> LZ4 size pass ->
+// layout (12-byte header, u32 BE block sizes, raw n % 8 leftover) -> LZ4 write pass.
+// EncGeom reuse: nbytes = chunk bytes, bs = block elements, nblocks = full blocks,
+// ts = itemsize, flags = elements of the last (partial) block.
+// -------------------------------------------------------------------------
+constexpr int BSHUF_PARSE_LEVEL = 1;   // one hash candidate per position, as LZ4_compress_default
+
+__global__ void bs_plan_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
+                               uint32_t* __restrict__ counts, uint32_t* __restrict__ segcnt,
+                               EncGeom* __restrict__ geom, int32_t* __restrict__ status, uint32_t es,
+                               uint32_t block, uint64_t src_extent) {
+  const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const hsds_chunk_desc c = chunks[ci];
+  const uint64_t n = c.src_len;
+  const uint32_t bsz = block ? block : bs::default_block(es);
+  EncGeom g = {n, bsz, 0, 0, es, 0};
+  int st = HSDS_OK;
+  uint32_t cnt = 0, nseg = 0;
+  if (n % es || c.src_off > src_extent || n > src_extent - c.src_off || n >= (1ull << 31) - 64 || c.dst_len < 12) {
+    st = HSDS_ERR_ARG;
+  } else {
+    const uint32_t nel = (uint32_t)(n / es);
+    const uint32_t nfull = nel / bsz;
+    const uint32_t last = (nel - nfull * bsz) / 8u * 8u;
+    g.nblocks = nfull;
+    g.flags = last;
+    cnt = nfull + (last ? 1u : 0u);
+    nseg = nfull * hd::nsegments(bsz * es) + (last ? hd::nsegments(last * es) : 0u);
+  }
+  counts[ci] = cnt;
+  segcnt[ci] = nseg;
+  status[ci] = st;
+  geom[ci] = g;
+}
+
+// one thread per chunk: the chunk's LZ4 items at slots[offs[ci] ..] (those below
+// slot_cap; a chunk that crosses it fails)
+__global__ void bs_fill_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
+                               const uint32_t* __restrict__ offs, const EncGeom* __restrict__ geom,
+                               EncItem* __restrict__ slots, int32_t* __restrict__ status, const uint8_t* stg,
+                               uint32_t slot_cap) {
+  const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const EncGeom g = geom[ci];
+  const uint32_t o0 = offs[ci], o1 = offs[ci + 1];
+  if (o1 > slot_cap && status[ci] == HSDS_OK) status[ci] = HSDS_ERR_UNSUPPORTED;
+  const uint64_t bbytes = g.bs * g.ts;
+  const uint32_t segs_full = hd::nsegments((uint32_t)bbytes);
+  for (uint32_t k = 0; k < o1 - o0 && o0 + k < slot_cap; k++) {
+    EncItem it;
+    it.src = (uint64_t)(stg + chunks[ci].src_off + k * bbytes);
+    it.len = k < g.nblocks ? (uint32_t)bbytes : g.flags * g.ts;
+    it.off = 0;
+    it.ts = 1;
+    it.neb = 0;
+    it.chunk = (uint32_t)ci;
+    it.seg0 = k * segs_full;
+    it.pad[0] = it.pad[1] = 0;
+    slots[o0 + k] = it;
+  }
+}
+
+// forward bit transposition of every block: work item = 8 elements (one row byte q)
+__global__ void __launch_bounds__(256) bs_trans_kernel(const uint8_t* __restrict__ src,
+                                                       const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
+                                                       const EncGeom* __restrict__ geom,
+                                                       const int32_t* __restrict__ status, uint8_t* __restrict__ stg) {
+  for (int64_t ci = blockIdx.y; ci < nchunks; ci += gridDim.y) {
+    if (status[ci] != HSDS_OK) continue;
+    const EncGeom g = geom[ci];
+    const uint32_t bsz = (uint32_t)g.bs, es = g.ts;
+    const uint32_t nq = (g.nblocks * bsz + g.flags) / 8u;
+    const uint64_t base = chunks[ci].src_off;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+      const uint32_t e0 = q * 8u, b = e0 / bsz;
+      const uint32_t cnt = b < g.nblocks ? bsz : g.flags;
+      const uint64_t boff = base + (uint64_t)b * bsz * es;
+      bs::trans_group(HZ_GLOBAL(hz_gcu8*, src + boff), HZ_GLOBAL(hz_gu8*, stg + boff), (e0 - b * bsz) / 8u, cnt / 8u,
+                      es);
+    }
+  }
+}
+
+// one thread per chunk: LZ4 block sizes -> frame positions, header, u32 BE sizes, raw
+// leftover elements, frame size (or HSDS_ERR_SIZE when it exceeds dst_len)
+__global__ void bs_layout_kernel(const uint8_t* __restrict__ src, const hsds_chunk_desc* __restrict__ chunks,
+                                 int64_t nchunks, uint8_t* __restrict__ dst_base, const uint32_t* __restrict__ offs,
+                                 const uint32_t* __restrict__ segoffs, const EncGeom* __restrict__ geom,
+                                 const uint32_t* __restrict__ lzsize, ItemOut* __restrict__ iout,
+                                 int64_t* __restrict__ sizes, int32_t* __restrict__ status, uint32_t hdr_block,
+                                 uint32_t seg_cap) {
+  const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  sizes[ci] = 0;
+  if (status[ci] != HSDS_OK) return;
+  if (segoffs[ci + 1] > seg_cap) { status[ci] = HSDS_ERR_UNSUPPORTED; return; }
+  const hsds_chunk_desc c = chunks[ci];
+  const EncGeom g = geom[ci];
+  const uint32_t o0 = offs[ci], o1 = offs[ci + 1];
+  uint64_t pos = 12;
+  for (uint32_t k = o0; k < o1; k++) {
+    iout[k] = ItemOut{(uint32_t)(pos + 4), 0u};
+    pos += 4 + (uint64_t)lzsize[k];
+  }
+  const uint64_t done = ((uint64_t)g.nblocks * g.bs + g.flags) * g.ts;
+  const uint64_t left = g.nbytes - done;
+  const uint64_t total = pos + left;
+  if (total > c.dst_len || total > 0xffffffffull) { status[ci] = HSDS_ERR_SIZE; return; }
+  uint8_t* out = dst_base + c.dst_off;
+  for (int i = 0; i < 8; i++) out[i] = (uint8_t)(g.nbytes >> (56 - 8 * i));        // storUtil.py:127
+  for (int i = 0; i < 4; i++) out[8 + i] = (uint8_t)(hdr_block >> (24 - 8 * i));    // storUtil.py:128
+  for (uint32_t k = o0; k < o1; k++) {
+    const uint32_t p = iout[k].pos - 4, v = lzsize[k];
+    out[p] = (uint8_t)(v >> 24); out[p + 1] = (uint8_t)(v >> 16); out[p + 2] = (uint8_t)(v >> 8); out[p + 3] = (uint8_t)v;
+  }
+  for (uint64_t i = 0; i < left; i++) out[pos + i] = src[c.src_off + done + i];
+  sizes[ci] = (int64_t)total;
 }
 
 }  // namespace
@@ -1444,7 +1570,7 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   };
   hipEventRecord(e->ev2, st);
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, nchunks * KSLOTS)), dim3(64), 0, st, slots,
-                     offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, clevel);
+                     offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, clevel, (uint32_t)KSLOTS, 0xffffffffu);
   if (cname == HSDS_CNAME_ZLIB) {
     hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 1, sp, meta, sc, seg_cap, clevel);
@@ -1456,12 +1582,12 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
     const unsigned lgrid = grid_for(16, nchunks * KSLOTS);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                        seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0,
-                       (int)(cname == HSDS_CNAME_BLOSCLZ));
+                       (int)(cname == HSDS_CNAME_BLOSCLZ), (uint32_t)KSLOTS, 0xffffffffu);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
                        segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)lzsize);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                        seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 1,
-                       (int)(cname == HSDS_CNAME_BLOSCLZ));
+                       (int)(cname == HSDS_CNAME_BLOSCLZ), (uint32_t)KSLOTS, 0xffffffffu);
   }
   hipLaunchKernelGGL(raw_copy_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
                      nchunks, (uint8_t*)d_dst, slots, counts, geom, iout, d_status);
@@ -1507,6 +1633,129 @@ int64_t hsds_compress_codec(hsds_engine* e, const void* src, int64_t n, int clev
   if (status) return status;
   if (hipMemcpy(&size, dsize, 8, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
   if (size < 16 || size > cap) return HSDS_ERR_SIZE;
+  if (hipMemcpy(dst, e->h_dev_dst, (size_t)size, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  return size;
+}
+
+// ---- bitshuffle+LZ4 encode (storUtil._shuffle codec 2) ---------------------------
+static uint32_t host_bshuf_default_block(uint32_t es) {   // bs::default_block on the host
+  const uint32_t b = (8192u / es) / 8u * 8u;
+  return b < 128u ? 128u : b;
+}
+
+int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src_extent,
+                                 const hsds_chunk_desc* d_chunks, int64_t nchunks, void* d_dst, uint64_t dst_extent,
+                                 int64_t* d_sizes, int32_t* d_status, int itemsize, int block, void* stream) {
+  if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
+  if (itemsize < 1 || itemsize > 4096 || block < 0 || block % 8) return HSDS_ERR_ARG;
+  if (nchunks == 0) return HSDS_OK;
+  if (nchunks > (int64_t)(1u << 22)) return HSDS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  const uint32_t es = (uint32_t)itemsize;
+  const uint64_t bsz = block ? (uint64_t)block : host_bshuf_default_block(es);
+  // every block but a chunk's last is bsz elements: slots and segments bounded by the source extent
+  const uint64_t slot_cap64 = src_extent / (bsz * es) + (uint64_t)nchunks + 64;
+  const uint64_t seg_cap64 = src_extent / hd::SEG + slot_cap64 + 64;
+  if (seg_cap64 > 0xffffffffull || (uint64_t)block * es > 0xffffffffull) return HSDS_ERR_ARG;
+  const uint32_t slot_cap = (uint32_t)slot_cap64, seg_cap = (uint32_t)seg_cap64;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t sz_slots = al((size_t)slot_cap * sizeof(EncItem));
+  const size_t sz_iout = al((size_t)slot_cap * sizeof(ItemOut));
+  const size_t sz_lzsize = al((size_t)slot_cap * 4);
+  const size_t sz_counts = al((size_t)nchunks * 4);
+  const size_t sz_offs = al((size_t)(nchunks + 1) * 4);
+  const size_t sz_geom = al((size_t)nchunks * sizeof(EncGeom));
+  const size_t sz_sp = al((size_t)seg_cap * sizeof(hd::SegParse));
+  const size_t sz_meta = al((size_t)seg_cap * sizeof(SegMeta));
+  const size_t sz_adler = al((size_t)slot_cap * 4);
+  const size_t need = sz_slots + sz_iout + sz_lzsize + 2 * sz_counts + 2 * sz_offs + sz_geom + sz_sp + sz_meta +
+                      sz_adler + 256;
+  if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
+  uint8_t* w = e->ews;
+  EncItem* slots = (EncItem*)w; w += sz_slots;
+  ItemOut* iout = (ItemOut*)w; w += sz_iout;
+  uint32_t* lzsize = (uint32_t*)w; w += sz_lzsize;
+  uint32_t* counts = (uint32_t*)w; w += sz_counts;
+  uint32_t* segcnt = (uint32_t*)w; w += sz_counts;
+  uint32_t* offs = (uint32_t*)w; w += sz_offs;
+  uint32_t* segoffs = (uint32_t*)w; w += sz_offs;
+  EncGeom* geom = (EncGeom*)w; w += sz_geom;
+  hd::SegParse* sp = (hd::SegParse*)w; w += sz_sp;
+  SegMeta* meta = (SegMeta*)w; w += sz_meta;
+  uint32_t* adler = (uint32_t*)w; w += sz_adler;
+  uint32_t* ctr = (uint32_t*)w;
+  if (grow((void**)&e->escr, &e->escr_bytes, (size_t)seg_cap * hd::SEG_TOK * 2 + 256)) return HSDS_ERR_DEVICE;
+  uint16_t* tok = (uint16_t*)e->escr;
+  if (grow((void**)&e->tmp, &e->tmp_bytes, src_extent ? src_extent : 1)) return HSDS_ERR_DEVICE;
+  uint8_t* stg = e->tmp;
+  if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  const int tpb = 256;
+  const int nb = (int)((nchunks + tpb - 1) / tpb);
+  hipEventRecord(e->ev2, st);
+  hipLaunchKernelGGL(bs_plan_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, counts, segcnt, geom, d_status,
+                     es, (uint32_t)block, src_extent);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, segcnt, segoffs, nchunks);
+  hipLaunchKernelGGL(bs_fill_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, offs, geom, slots, d_status, stg,
+                     slot_cap);
+  const unsigned gy = (unsigned)(nchunks < 65535 ? nchunks : 65535);
+  hipLaunchKernelGGL(bs_trans_kernel, dim3(16, gy), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, geom,
+                     d_status, stg);
+  auto grid_for = [&](int per_cu, int64_t cap) {
+    int64_t g = (int64_t)e->num_cus * per_cu;
+    if (g > cap) g = cap;
+    return (unsigned)(g < 1 ? 1 : g);
+  };
+  hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, slot_cap)), dim3(64), 0, st, slots, offs,
+                     segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, BSHUF_PARSE_LEVEL, 0u, slot_cap);
+  const unsigned lgrid = grid_for(16, slot_cap);
+  hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
+                     seg_cap, BSHUF_PARSE_LEVEL, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0, 0, 0u, slot_cap);
+  hipLaunchKernelGGL(bs_layout_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
+                     (uint8_t*)d_dst, offs, segoffs, geom, lzsize, iout, d_sizes, d_status,
+                     (uint32_t)((uint64_t)block * es), seg_cap);
+  hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
+                     seg_cap, BSHUF_PARSE_LEVEL, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 1, 0, 0u, slot_cap);
+  hipEventRecord(e->ev3, st);
+  e->ev_enc_valid = 1;
+  return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+// frame bound: header, a u32 size and an LZ4 worst case (n + n / 255 + 16) per block, leftover
+int64_t hsds_bitshuffle_bound(int64_t n, int itemsize, int block) {
+  if (n < 0 || itemsize < 1 || block < 0 || block % 8) return HSDS_ERR_ARG;
+  const int64_t bb = (block ? (int64_t)block : (int64_t)host_bshuf_default_block((uint32_t)itemsize)) * itemsize;
+  const int64_t nblk = n / bb + 1;
+  return 12 + n + nblk * (4 + 16) + n / 255 + 16;
+}
+
+int64_t hsds_bitshuffle_compress(hsds_engine* e, const void* src, int64_t n, int itemsize, int block, void* dst,
+                                 int64_t cap) {
+  const int64_t bound = hsds_bitshuffle_bound(n, itemsize, block);
+  if (!e || bound < 0 || (n && !src) || !dst || cap < 12) return HSDS_ERR_ARG;
+  if (n % itemsize) return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  const size_t desc_off = ((size_t)n + 255) & ~(size_t)255;
+  const size_t stat_off = ((size_t)bound + 255) & ~(size_t)255;
+  if (grow((void**)&e->h_dev_src, &e->h_dev_src_bytes, desc_off + sizeof(hsds_chunk_desc))) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->h_dev_dst, &e->h_dev_dst_bytes, stat_off + 64)) return HSDS_ERR_DEVICE;
+  hsds_chunk_desc c = {0, (uint64_t)n, 0, (uint64_t)bound};
+  hsds_chunk_desc* dd = (hsds_chunk_desc*)(e->h_dev_src + desc_off);
+  int64_t* dsize = (int64_t*)(e->h_dev_dst + stat_off);
+  int32_t* dstat = (int32_t*)(e->h_dev_dst + stat_off + 16);
+  if (n && hipMemcpy(e->h_dev_src, src, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (hipMemcpy(dd, &c, sizeof(c), hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
+  int r = hsds_encode_bitshuffle_batch(e, e->h_dev_src, (uint64_t)n, dd, 1, e->h_dev_dst, (uint64_t)bound, dsize,
+                                       dstat, itemsize, block, nullptr);
+  if (r) return r;
+  int32_t status = 0;
+  int64_t size = 0;
+  if (hipMemcpy(&status, dstat, 4, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (status) return status;
+  if (hipMemcpy(&size, dsize, 8, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (size < 12) return HSDS_ERR_SIZE;
+  if (size > cap) return HSDS_ERR_SIZE;
   if (hipMemcpy(dst, e->h_dev_dst, (size_t)size, hipMemcpyDeviceToHost) != hipSuccess) return HSDS_ERR_DEVICE;
   return size;
 }

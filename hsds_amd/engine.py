@@ -95,6 +95,25 @@ class ChunkEngine:
             raise nat.NativeError(rc, "hsds_encode_batch_codec")
         return chunk_descs
 
+    def encode_bitshuffle(self, src, chunk_descs, dst, sizes, status, itemsize, block=2048, stream=None):
+        """Asynchronously write bitshuffle+LZ4 objects (storUtil._shuffle codec 2,
+        storUtil.py:103-131) for the chunks `chunk_descs` at dst_off in `dst` (dst_len =
+        capacity, >= nat.lib().hsds_bitshuffle_bound(src_len, itemsize, block)).  `block`
+        is the bitshuffle block in elements (HSDS config bit_shuffle_default_blocksize,
+        2048)."""
+        if isinstance(chunk_descs, np.ndarray):
+            n = chunk_descs.size
+            chunk_descs = to_device_bytes(chunk_descs, self.device)
+        else:
+            n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
+        rc = nat.lib().hsds_encode_bitshuffle_batch(self.eng.h, _ptr(src), src.numel() * src.element_size(),
+                                                    _ptr(chunk_descs), n, _ptr(dst),
+                                                    dst.numel() * dst.element_size(), _ptr(sizes), _ptr(status),
+                                                    int(itemsize), int(block), _stream_handle(stream))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_encode_bitshuffle_batch")
+        return chunk_descs
+
     def last_deflate_ms(self):
         return self.eng.last_deflate_ms()
 

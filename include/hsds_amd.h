@@ -20,6 +20,9 @@
  *                           write_s3_obj (hsds/datanode_lib.py:126-311), batched over many dirty chunks
  *   hsds_encode_batch_codec / hsds_compress_codec
  *                        <- the same with Blosc(cname = "lz4" / "lz4hc" / "blosclz") (storUtil.py:255-262)
+ *   hsds_encode_bitshuffle_batch / hsds_bitshuffle_compress / hsds_bitshuffle_bound
+ *                        <- storUtil.py:94-131 _shuffle(codec=2, ...) (bitshuffle.compress_lz4 behind
+ *                           the 12-byte header), reached from _compress(shuffle=2) (storUtil.py:243-251)
  *
  * Threading: an engine is bound to one device and may be used from one host thread
  * at a time (HSDS data nodes are single-threaded asyncio processes).  All *_batch
@@ -185,6 +188,26 @@ int64_t hsds_compress(hsds_engine* e, const void* src, int64_t n, int clevel, in
 /* ... and for any HSDS_CNAME_* */
 int64_t hsds_compress_codec(hsds_engine* e, const void* src, int64_t n, int clevel, int shuffle, int typesize,
                             int cname, void* dst, int64_t cap);
+
+/* Batched bitshuffle+LZ4 objects (storUtil._shuffle codec 2, storUtil.py:103-131):
+ * chunk k (src_len bytes of itemsize-byte elements) becomes u64 BE src_len, u32 BE
+ * block * itemsize (0 when block == 0: the bitshuffle default block), then per block
+ * of `block` elements (0: bshuf_default_block_size) a u32 BE size and the LZ4 block of
+ * the block's bit transposition, a last block of the remaining elements rounded down
+ * to a multiple of 8, and the n % 8 leftover elements raw.  LZ4 bytes come from the
+ * GPU writer (any valid block; they decode through bitshuffle.decompress_lz4).
+ * src_extent = bytes spanned by d_src (bounds the per-block work items); dst_len
+ * should be >= hsds_bitshuffle_bound(src_len, ...), else the chunk may fail with
+ * HSDS_ERR_SIZE.  Frame sizes to d_sizes[k], statuses to d_status[k]. */
+int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src_extent,
+                                 const hsds_chunk_desc* d_chunks, int64_t nchunks, void* d_dst, uint64_t dst_extent,
+                                 int64_t* d_sizes, int32_t* d_status, int itemsize, int block, void* stream);
+/* Worst-case object size for n bytes (LZ4 bound per block + headers). */
+int64_t hsds_bitshuffle_bound(int64_t n, int itemsize, int block);
+/* Host-buffer single object (storUtil._shuffle(2, data, chunk_shape, dtype)).
+ * Returns the object size (<= cap) or a negative HSDS_ERR_*. */
+int64_t hsds_bitshuffle_compress(hsds_engine* e, const void* src, int64_t n, int itemsize, int block, void* dst,
+                                 int64_t cap);
 
 /* Device time (ms) of the deflate kernel of the most recent hsds_encode_batch. */
 int hsds_last_deflate_ms(hsds_engine* e, float* ms);

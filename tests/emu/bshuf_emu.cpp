@@ -17,3 +17,8 @@ extern "C" int emu_bshuf_chunk(const uint8_t* src, uint32_t n, uint8_t* dst, uin
 extern "C" void emu_bshuf_untrans(const uint8_t* in, uint8_t* out, uint32_t cnt, uint32_t es) {
   bs::untrans_block(in, out, cnt, es);
 }
+
+// the forward transposition of the write path (cnt % 8 == 0): every row byte q
+extern "C" void emu_bshuf_trans(const uint8_t* in, uint8_t* out, uint32_t cnt, uint32_t es) {
+  for (uint32_t q = 0; q < cnt / 8u; q++) bs::trans_group(in, out, q, cnt / 8u, es);
+}

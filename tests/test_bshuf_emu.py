@@ -24,6 +24,7 @@ def emu():
     L = ctypes.CDLL(EMU)
     L.emu_bshuf_chunk.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
     L.emu_bshuf_untrans.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    L.emu_bshuf_trans.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
     return L
 
 
@@ -69,3 +70,29 @@ def test_bshuf_oracle_frames(emu, oracle_lib):
         for bad in (blob[:-1], blob + b"\0"):
             assert decode(emu, bad, len(raw), es)[0] < 0
             assert isinstance(oracle_lib.bitshuffle_decode(bad, len(raw), es), int)
+
+
+@pytest.mark.parametrize("es", [1, 2, 3, 4, 5, 8, 16, 32])
+@pytest.mark.parametrize("cnt", [8, 64, 2048])
+def test_forward_transposition_matches_oracle(emu, es, cnt):
+    """bs::trans_group (the write path's transposition) equals the oracle's
+    bshuf_trans_bit_elem restatement, and untrans_block inverts it."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(es * 1000 + cnt)
+    for kind in ("random", "smooth"):
+        if kind == "random":
+            x = rng.integers(0, 256, cnt * es, dtype=np.uint8)
+        else:
+            x = np.frombuffer(np.round(np.cumsum(rng.normal(size=cnt * es // 4 + 1)), 2).astype("<f4").tobytes(),
+                              np.uint8)[:cnt * es].copy()
+        # aligned and unaligned element bases (the f32 fast path needs 4-byte alignment)
+        for off in (0, 1):
+            buf = np.zeros(cnt * es + 8, np.uint8)
+            buf[off:off + cnt * es] = x
+            out = np.zeros(cnt * es, np.uint8)
+            emu.emu_bshuf_trans(buf.ctypes.data + off, out.ctypes.data, cnt, es)
+            ref = np.frombuffer(orc.bshuf_trans(x.tobytes(), es), np.uint8)
+            assert out.tobytes() == ref.tobytes()
+            back = np.zeros(cnt * es, np.uint8)
+            emu.emu_bshuf_untrans(out.ctypes.data, back.ctypes.data, cnt, es)
+            assert back.tobytes() == x.tobytes()

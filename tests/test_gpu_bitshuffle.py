@@ -123,3 +123,158 @@ def test_full_size_chunks(oracle_lib, torch_dev):
     for i in range(64):
         o = int(descs[i]["dst_off"])
         assert h[o:o + (1 << 20)].tobytes() == raws[i], i
+
+
+# ---- write path: storUtil._shuffle codec 2 (storUtil.py:103-131) -----------------------
+
+def _walk(frame, nbytes, es):
+    """(header, [decoded LZ4 blocks], leftover bytes) of a bitshuffle+LZ4 object, the
+    blocks decoded by the oracle's LZ4 decoder."""
+    from oracle import oracle as orc
+    b = bytes(frame)
+    hdr = b[:12]
+    bs = int.from_bytes(b[8:12], "big") // es
+    if bs == 0:
+        bs = max(128, (8192 // es) // 8 * 8)
+    n, e, p, blocks = nbytes // es, 0, 12, []
+    while e + 8 <= n:
+        cnt = bs if n - e >= bs else (n - e) // 8 * 8
+        nb = int.from_bytes(b[p:p + 4], "big")
+        blk = orc.lz4_decode(b[p + 4:p + 4 + nb], cnt * es)
+        assert not isinstance(blk, int), blk
+        blocks.append(bytes(blk))
+        p += 4 + nb
+        e += cnt
+    left = b[p:]
+    assert len(left) == (n - e) * es
+    return hdr, blocks, left
+
+
+def test_shuffle_codec2_matches_reference_goldens(bshuf_golden, torch_dev):
+    """codec._shuffle(2, raw) against the frames the reference's libraries wrote for the
+    same raw bytes: identical header, block count, decoded (bit-transposed) block bytes
+    and raw leftover; the LZ4 bytes themselves may differ (any valid block)."""
+    from hsds_amd import codec
+    meta, arrs = bshuf_golden
+    n_checked = 0
+    for c in meta["cases"]:
+        if c["status"] != "ok" or c["block"] != 2048:
+            continue
+        raw = arrs[c["name"] + "__raw"].tobytes()
+        gold = arrs[c["name"] + "__in"].tobytes()
+        dt = _dtype(c)
+        shape = (c["nbytes"] // c["itemsize"],)
+        got = codec._shuffle(2, raw, chunk_shape=shape, dtype=dt)
+        assert _walk(got, c["nbytes"], c["itemsize"]) == _walk(gold, c["nbytes"], c["itemsize"]), c["name"]
+        assert codec._unshuffle(2, got, dtype=dt, chunk_shape=shape) == raw
+        n_checked += 1
+    assert n_checked >= 5
+
+
+def _bshuf_batch(eng, torch, dev, chunks, es, block, src_pad=0, caps=None):
+    from hsds_amd import _native as nat
+    from hsds_amd.engine import CHUNK_DESC_DTYPE
+    descs = np.zeros(len(chunks), CHUNK_DESC_DTYPE)
+    srcb, off = [], 0
+    for i, c in enumerate(chunks):
+        off += src_pad
+        srcb.append((off, c))
+        off += len(c)
+    src = np.zeros(max(off, 1), np.uint8)
+    doff = 0
+    for i, (o, c) in enumerate(srcb):
+        src[o:o + len(c)] = np.frombuffer(c, np.uint8)
+        cap = int(nat.lib().hsds_bitshuffle_bound(max(len(c) // es * es, 0), es, block)) if caps is None else caps[i]
+        descs[i] = (o, len(c), doff, cap)
+        doff += (cap + 3) // 4 * 4
+    d_src = torch.from_numpy(src).to(dev)
+    d_dst = torch.zeros(max(doff, 1), dtype=torch.uint8, device=dev)
+    sizes = torch.zeros(len(chunks), dtype=torch.int64, device=dev)
+    status = torch.full((len(chunks),), 99, dtype=torch.int32, device=dev)
+    eng.encode_bitshuffle(d_src, descs, d_dst, sizes, status, itemsize=es, block=block)
+    torch.cuda.synchronize()
+    host = d_dst.cpu().numpy()
+    st = status.cpu().numpy()
+    sz = sizes.cpu().numpy()
+    return [host[int(d["dst_off"]):int(d["dst_off"]) + int(s)].tobytes() for d, s in zip(descs, sz)], st, descs
+
+
+@pytest.mark.parametrize("es,block", [(4, 2048), (1, 2048), (2, 256), (8, 64), (3, 128), (4, 0), (16, 16)])
+def test_encode_batch_roundtrip_oracle(torch_dev, es, block):
+    """Mixed batch at unaligned source offsets: every object decodes through the oracle
+    (orc_bitshuffle_decode, pinned by the reference goldens) and bshuf_kernel to the
+    input; headers carry the chunk bytes and block * itemsize as storUtil.py:127-128."""
+    import torch
+    from hsds_amd.engine import ChunkEngine as Engine
+    from oracle import oracle as orc
+    eng = Engine(0)
+    rng = np.random.default_rng(es * 7 + block)
+    chunks = []
+    for nel in (0, 5, 8, 1003, 4096, 65536 + 13, 262144):
+        kind = len(chunks) % 3
+        if kind == 0:
+            sm = (np.cumsum(rng.normal(size=max(nel, 1))) * 100).astype("<i8").view(np.uint8)
+            x = np.resize(sm, nel * es).astype(np.uint8)
+        elif kind == 1:
+            x = rng.integers(0, 256, nel * es, dtype=np.uint8)
+        else:
+            x = np.zeros(nel * es, np.uint8)
+        chunks.append(x.tobytes())
+    frames, st, _ = _bshuf_batch(eng, torch, torch_dev, chunks, es, block, src_pad=3)
+    assert (st == 0).all(), st
+    for raw, fr in zip(chunks, frames):
+        assert int.from_bytes(fr[:8], "big") == len(raw)
+        assert int.from_bytes(fr[8:12], "big") == block * es
+        back = orc.bitshuffle_decode(fr, len(raw), es)
+        assert not isinstance(back, int), back
+        assert bytes(back) == raw
+        bs = block or max(128, (8192 // es) // 8 * 8)
+        if len(raw) >= bs * es:
+            hdr, blocks, left = _walk(fr, len(raw), es)
+            assert blocks[0] == orc.bshuf_trans(raw[:bs * es], es)
+    # and through the GPU decoder
+    from hsds_amd import codec
+    for raw, fr in zip(chunks, frames):
+        dt = np.dtype("V%d" % es)
+        assert codec._unshuffle(2, fr, dtype=dt, chunk_shape=(len(raw) // es,)) == raw
+
+
+def test_encode_batch_statuses(torch_dev):
+    """A capacity below the object size fails that chunk alone (HSDS_ERR_SIZE); a length
+    that is not a whole number of elements is an argument error."""
+    import torch
+    from hsds_amd import _native as nat
+    from hsds_amd.engine import ChunkEngine as Engine
+    from oracle import oracle as orc
+    eng = Engine(0)
+    rng = np.random.default_rng(5)
+    good = rng.integers(0, 256, 40000, dtype=np.uint8).tobytes()
+    frames, st, descs = _bshuf_batch(eng, torch, torch_dev, [good, good[:4003], good], 4, 2048,
+                                     caps=[30000, 8000, 40011])
+    assert st[0] == nat.ERR_SIZE and st[2] == nat.ERR_SIZE
+    assert st[1] == nat.ERR_ARG
+    frames, st, _ = _bshuf_batch(eng, torch, torch_dev, [good, good[:4000]], 4, 2048)
+    assert (st == 0).all()
+    assert bytes(orc.bitshuffle_decode(frames[1], 4000, 4)) == good[:4000]
+
+
+def test_compress_shuffle2(torch_dev):
+    """_compress(shuffle=2) (storUtil.py:238-281): the bitshuffle object alone without a
+    compressor, wrapped in a Blosc frame (shuffle off) with one; _uncompress reads both
+    back.  A shape that does not match the bytes leaves them unshuffled, as there."""
+    from hsds_amd import codec
+    from oracle import oracle as orc
+    rng = np.random.default_rng(11)
+    arr = np.round(np.cumsum(rng.normal(size=(64, 1024)), axis=1), 2).astype("<f4")
+    raw = arr.tobytes()
+    dt = arr.dtype
+    obj = codec._compress(raw, compressor=None, shuffle=2, dtype=dt, chunk_shape=arr.shape)
+    assert len(obj) < len(raw)
+    assert bytes(orc.bitshuffle_decode(obj, len(raw), 4)) == raw
+    assert codec._uncompress(obj, compressor=None, shuffle=2, dtype=dt, chunk_shape=arr.shape) == raw
+    for comp in ("gzip", "lz4"):
+        fr = codec._compress(raw, compressor=comp, level=5, shuffle=2, dtype=dt, chunk_shape=arr.shape)
+        assert fr[3] == 1 and not (fr[2] & 0x01)          # Blosc typesize 1, no byte shuffle
+        assert bytes(orc.bitshuffle_decode(orc.blosc_decode(fr, len(obj) + 64), len(raw), 4)) == raw
+        assert codec._uncompress(fr, compressor=comp, shuffle=2, dtype=dt, chunk_shape=arr.shape) == raw
+    assert codec._compress(raw, compressor=None, shuffle=2, dtype=dt, chunk_shape=(3, 3)) == raw
