@@ -444,6 +444,54 @@ def run_cfg5(args, dev, rank=0):
                          "ms_per_step": round(el4 * 1e3, 3), "compressed_bytes": comp4,
                          "encode_ms": round(eng.last_deflate_ms(), 3),
                          "format": "Blosc-lz4 frames (typesize 1, c-blosc lz4 blocksize), parse tokens -> LZ4 blocks"}
+    # the same scatter + encode for a bitshuffle dataset (storUtil._shuffle codec 2:
+    # bitshuffle+LZ4 objects, f32, 2048-element blocks, no outer compressor)
+    from hsds_amd import _native as nat
+    bound = int(nat.lib().hsds_bitshuffle_bound(cbytes, 4, 2048))
+    bdescs, _, bext = encode_descs([cbytes] * n, overhead=bound - cbytes)
+    d_bdesc = to_device_bytes(bdescs, dev)
+    del frames
+    frames = torch.empty(bext, dtype=torch.uint8, device=dev)
+
+    def step_bshuf():
+        eng.copy(slab_u8, chunks, d_cd, stream=stream)
+        eng.encode_bitshuffle(chunks, d_bdesc, frames, sizes, st, itemsize=4, block=2048, stream=stream)
+
+    step_bshuf()
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0, "bitshuffle encode status errors"
+    for k in (0, n // 3, n - 1):
+        o = int(bdescs[k]["dst_off"])
+        fr = frames[o:o + int(sizes[k])].cpu().numpy().tobytes()
+        back = orc.bitshuffle_decode(fr, cbytes, 4)
+        assert not isinstance(back, int) and bytes(back) == chunks[k * cbytes:(k + 1) * cbytes].cpu().numpy().tobytes(), \
+            f"bitshuffle chunk {k}"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_bshuf()
+    torch.cuda.synchronize()
+    elb = (time.perf_counter() - t0) / args.steps
+    compb = int(sizes.sum())
+    out["bshuf_encode"] = {"value": round(slab_bytes / elb / 1e9, 2), "unit": "GB/s slab (scatter + encode)",
+                           "ms_per_step": round(elb * 1e3, 3), "compressed_bytes": compb,
+                           "encode_ms": round(eng.last_deflate_ms(), 3),
+                           "algorithmic_GBps": round((slab_bytes + compb) / (eng.last_deflate_ms() / 1e3) / 1e9, 2),
+                           "format": "bitshuffle+LZ4 objects (f32, 2048-element blocks, 12-byte header)"}
+    if args.cpu_seconds > 0 and rank == 0:
+        from concurrent.futures import ThreadPoolExecutor
+        threads = min(16, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        done = 0
+        with ThreadPoolExecutor(threads) as ex:
+            while time.perf_counter() - t1 < min(args.cpu_seconds / 4, 3.0):
+                for r in ex.map(lambda x: orc.bitshuffle_encode(x, 4, 2048), samp):
+                    assert len(r) > 12
+                done += len(samp)
+        cel = time.perf_counter() - t1
+        out["bshuf_encode"]["cpu_baseline"] = {
+            "value": round(done * cbytes / cel / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{done} x 1 MiB bitshuffle+LZ4 encodes (oracle transposition + greedy LZ4)"}
     if args.cpu_seconds > 0 and rank == 0:
         threads = min(16, os.cpu_count() or 1)
         t1 = time.perf_counter()

@@ -28,7 +28,7 @@ from operator import attrgetter
 import numpy as np
 
 from . import _native as nat
-from .codec import HTTPInternalServerError
+from .codec import BIT_SHUFFLE_BLOCK, HTTPInternalServerError
 
 # HDF5 file chunk location (rangegetUtil.py:9): index = hyper-chunk index tuple,
 # offset / length = byte range in the HDF5 file
@@ -359,6 +359,13 @@ class ChunkRead:
         self.chunk_id, self.key, self.offset, self.length = chunk_id, key, offset, length
 
 
+def _check_decodable(comp, shuffle):
+    """Bitshuffle objects inside an outer Blosc frame decode one at a time through
+    codec._uncompress; the batched reader takes bare bitshuffle+LZ4 objects only."""
+    if shuffle == 2 and comp != nat.COMP_NONE:
+        raise NotImplementedError("batched read of bitshuffle objects under an outer compressor")
+
+
 def _filter_args(filter_ops, dtype):
     """(compressor code, shuffle, itemsize) for hsds_decode_batch from getFilterOps."""
     if not filter_ops:
@@ -367,8 +374,6 @@ def _filter_args(filter_ops, dtype):
     code = nat.COMP_NONE if not comp or comp == "scaleoffset" else \
         nat.COMP_ZLIB if comp in ("gzip", "deflate", "zlib") else nat.COMP_OTHER
     shuffle = int(filter_ops.get("shuffle") or 0)
-    if shuffle == 2:
-        raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
     dt = filter_ops.get("dtype", dtype)
     return code, shuffle, np.dtype(dt if dt is not None else dtype).itemsize
 
@@ -463,6 +468,7 @@ class ChunkReader:
         if not pieces:
             return []
         comp, shuffle, isz = _filter_args(filter_ops, (filter_ops or {}).get("dtype", np.uint8))
+        _check_decodable(comp, shuffle)
         src, descs, ext = pack_chunks(pieces, [int(h5_size)] * len(pieces))
         dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
         status = torch.full((len(pieces),), 99, dtype=torch.int32, device=self.device)
@@ -540,6 +546,7 @@ class ChunkReader:
         # ONE decode batch into a contiguous buffer (plain objects and HDF5 chunks)
         dec = [j for j in jobs if j[1] in ("plain", "h5")]
         if dec:
+            _check_decodable(comp, shuffle)
             sizes = [chunk_size if kind == "plain" else h5_size for _, kind, _, _ in dec]
             src, descs, ext = pack_chunks([blobs[bi] for _, _, bi, _ in dec], sizes)
             d_src = torch.from_numpy(src).to(self.device)
@@ -734,7 +741,8 @@ class ChunkStore:
         """s3sync for every dirty chunk (datanode_lib.py:1186-1318, 126-311): ONE
         hsds_encode_batch_codec straight from the HBM cache slots (storUtil._compress's
         Blosc frames with the dataset's codec (zlib, lz4, lz4hc), level and shuffle flag; no compressor
-        -> the raw bytes, putStorBytes semantics), one device-to-host copy of the
+        -> the raw bytes, putStorBytes semantics; a bitshuffle dataset first goes through ONE
+        hsds_encode_bitshuffle_batch, storUtil.py:243-251), one device-to-host copy of the
         frames, `put(key, bytes)` per chunk, then clearDirty.  `keys` maps chunk id ->
         storage key (default: hsds_amd.partition.getS3Key).  Returns the flushed ids."""
         import torch
@@ -750,26 +758,52 @@ class ChunkStore:
             comp = None
         if comp and nat.cname_code(comp) is None:
             raise NotImplementedError(f"Blosc codec {comp!r} has no encoder in the hsds_amd engine")
-        if (filter_ops or {}).get("shuffle") == 2:
-            raise NotImplementedError("bitshuffle+LZ4 is outside the hsds_amd engine scope")
+        bitshuffle = (filter_ops or {}).get("shuffle") == 2
+        src, src_nodes_off = abase, [n.off for n in nodes]
+        src_lens = [n.nbytes for n in nodes]
+        if bitshuffle:
+            # _compress(shuffle=2): bitshuffle+LZ4 objects first (storUtil.py:243-251), in
+            # ONE hsds_encode_bitshuffle_batch from the cache slots; Blosc (shuffle off)
+            # wraps them when the dataset also has a compressor
+            dt = np.dtype(filter_ops.get("dtype") or np.uint8)
+            bounds = [int(nat.lib().hsds_bitshuffle_bound(L, dt.itemsize, BIT_SHUFFLE_BLOCK)) for L in src_lens]
+            bdescs, _, bext = encode_descs(src_lens, overhead=0)
+            for d, n, b in zip(bdescs, nodes, bounds):
+                d["src_off"] = n.off
+                d["dst_len"] = b
+            bdescs["dst_off"] = np.concatenate([[0], np.cumsum([(b + 255) // 256 * 256 for b in bounds])[:-1]])
+            bext = int(sum((b + 255) // 256 * 256 for b in bounds))
+            bframes = torch.empty(max(bext, 1), dtype=torch.uint8, device=abase.device)
+            bsizes = torch.zeros(len(ids), dtype=torch.int64, device=abase.device)
+            bstatus = torch.full((len(ids),), 99, dtype=torch.int32, device=abase.device)
+            self.reader.eng.encode_bitshuffle(abase, bdescs, bframes, bsizes, bstatus, itemsize=dt.itemsize,
+                                              block=BIT_SHUFFLE_BLOCK)
+            if (bstatus.cpu().numpy() != 0).any():
+                raise HTTPInternalServerError()
+            src, src_nodes_off = bframes, [int(d["dst_off"]) for d in bdescs]
+            src_lens = [int(x) for x in bsizes.cpu().numpy()]
+            if not comp:
+                host = bframes.cpu().numpy()
+                blobs = [host[o:o + L].tobytes() for o, L in zip(src_nodes_off, src_lens)]
         if comp:
             level = filter_ops.get("level", 5)
             level = 5 if level is None else int(level)
-            descs, _, dext = encode_descs([n.nbytes for n in nodes])
-            for d, n in zip(descs, nodes):
-                d["src_off"] = n.off
+            descs, _, dext = encode_descs(src_lens)
+            for d, o in zip(descs, src_nodes_off):
+                d["src_off"] = o
             frames = torch.empty(max(dext, 1), dtype=torch.uint8, device=abase.device)
             sizes = torch.zeros(len(ids), dtype=torch.int64, device=abase.device)
             status = torch.full((len(ids),), 99, dtype=torch.int32, device=abase.device)
-            self.reader.eng.encode(abase, descs, frames, sizes, status, clevel=level,
-                                   shuffle=int(filter_ops.get("shuffle") or 0), typesize=1, compressor=comp)
+            self.reader.eng.encode(src, descs, frames, sizes, status, clevel=level,
+                                   shuffle=0 if bitshuffle else int(filter_ops.get("shuffle") or 0), typesize=1,
+                                   compressor=comp)
             st = status.cpu().numpy()
             if (st != 0).any():
                 raise HTTPInternalServerError()
             host = frames.cpu().numpy()
             sz = sizes.cpu().numpy()
             blobs = [host[int(d["dst_off"]):int(d["dst_off"]) + int(s)].tobytes() for d, s in zip(descs, sz)]
-        else:
+        elif not bitshuffle:
             blobs = [self.cache.node_bytes(k).cpu().numpy().tobytes() for k in ids]
         for k, b in zip(ids, blobs):
             put(keys[k] if keys else getS3Key(k), b)

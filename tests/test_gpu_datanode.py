@@ -266,3 +266,52 @@ def test_put_and_flush_lz4_dataset(dev, oracle_lib):
         if cid in ids:
             want[sel] = d
         assert r.cpu().numpy().tobytes() == want.tobytes(), cid
+
+
+@pytest.mark.parametrize("with_deflate", [False, True])
+def test_put_and_flush_bitshuffle_dataset(dev, oracle_lib, with_deflate):
+    """A bitshuffle dataset (getFilterOps -> shuffle 2): PUT_Chunk into fill-initialised
+    chunks, flush through ONE bitshuffle encode batch (and the Blosc zlib wrap when the
+    dataset also has deflate, storUtil.py:243-262); the objects decode through the
+    oracle, bare objects read back through the batched GPU reader, wrapped ones
+    through codec._uncompress."""
+    from hsds_amd import codec
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    from hsds_amd.filters import getFilterOps
+    orc = oracle_lib
+    dims = (64, 200)
+    dt = np.dtype("<f4")
+    filters = [{"class": "H5Z_FILTER_BITSHUFFLE", "id": 32008, "name": "bitshuffle"}]
+    if with_deflate:
+        filters.append({"class": "H5Z_FILTER_DEFLATE", "id": 1, "level": 4})
+    ops = getFilterOps({"filter_map": {}}, "d-b", filters, dtype=dt, chunk_shape=dims)
+    assert ops["shuffle"] == 2
+    rng = np.random.default_rng(21)
+    cs = ChunkStore(lambda k, o, n: None, mem_target=1 << 24, device=dev)
+    sel = (slice(0, 64), slice(3, 200, 2))
+    writes, truth = [], {}
+    for i in range(3):
+        d = np.round(np.cumsum(rng.normal(size=(64, len(range(3, 200, 2)))), axis=1), 2).astype(dt)
+        writes.append((ChunkRead(f"c-b_{i}_0", f"k{i}"), sel, d))
+        w = np.zeros(dims, dt)
+        w[sel] = d
+        truth[f"c-b_{i}_0"] = w
+    cs.put_selections(writes, dt, dims, filter_ops=ops)
+    flushed = {}
+    keys = {f"c-b_{i}_0": f"k{i}" for i in range(3)}
+    ids = cs.flush(lambda k, b: flushed.__setitem__(k, b), filter_ops=ops, keys=keys)
+    assert sorted(ids) == sorted(keys)
+    for cid in ids:
+        f = flushed[keys[cid]]
+        want = truth[cid].tobytes()
+        obj = orc.blosc_decode(f, len(f) * 64) if with_deflate else f
+        if with_deflate:
+            assert f[2] >> 5 == 3 and not (f[2] & 1)        # Blosc zlib, shuffle off
+        assert bytes(orc.bitshuffle_decode(obj, len(want), 4)) == want, cid
+        assert codec._uncompress(f, compressor=ops.get("compressor"), shuffle=2, dtype=dt,
+                                 chunk_shape=dims) == want
+    if not with_deflate:
+        cs2 = ChunkStore(lambda k, o, n: flushed.get(k), mem_target=1 << 24, device=dev)
+        res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in sorted(keys)], dt, dims, filter_ops=ops)
+        for cid, r in zip(sorted(keys), res):
+            assert r.cpu().numpy().tobytes() == truth[cid].tobytes(), cid

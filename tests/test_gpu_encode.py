@@ -94,8 +94,11 @@ def test_compress_passthrough_and_errors(dev):
     data = b"abc" * 100
     assert codec._compress(data) is data                 # no compressor: unchanged (storUtil.py:239-241)
     assert codec._compress(data, compressor=None, shuffle=1) is data
-    with pytest.raises(NotImplementedError):
-        codec._compress(data, compressor="zlib", shuffle=2)
+    # shuffle=2 without a dtype: _shuffle fails, the reference logs it and Blosc-encodes
+    # the bytes unshuffled (storUtil.py:243-251)
+    fr = codec._compress(data, compressor="zlib", shuffle=2)
+    assert fr[2] >> 5 == 3 and not (fr[2] & 1)
+    assert codec._uncompress(fr, compressor="zlib") == data
     with pytest.raises(NotImplementedError):
         codec._compress(data, compressor="zstd")
 
