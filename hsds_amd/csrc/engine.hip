@@ -935,6 +935,9 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
                                                        const ItemOut* __restrict__ iout,
                                                        const int32_t* __restrict__ status, int write, int blosclz,
                                                        uint32_t ks, uint32_t item_cap) {
+  __shared__ lze::CopyList cl;
+  if (threadIdx.x == 0) cl.n = 0;
+  __syncthreads();
   const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
     const int64_t ci = item_chunk(offs, nchunks, item);
@@ -951,7 +954,7 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
       if (status[ci] != HSDS_OK || geom[ci].memcpyed || iout[slot].raw) continue;
       uint8_t* o = dst_base + chunks[ci].dst_off + iout[slot].pos;
       if (blosclz) lze::blosclz_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, o, 1);
-      else lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, o, 1);
+      else lze::lz4_block_wave(sp + g0, tok + (size_t)g0 * hd::SEG_TOK, job, o, 1, &cl);
     }
   }
 }
@@ -1154,6 +1157,7 @@ struct hsds_engine {
   int lz_blocks_per_cu;        // occupancy of lz_kernel
   int bshuf_blocks_per_cu;     // occupancy of bshuf_kernel
   int zstd_blocks_per_cu;      // occupancy of zstd_kernel
+  int lz4w_blocks_per_cu = 16; // occupancy of lz4_block_kernel (LZ4 / BloscLZ writer)
   hz::Tune tune;
   // workspace (grown on demand)
   uint8_t* ws = nullptr;
@@ -1234,6 +1238,9 @@ int hsds_engine_create(int device, hsds_engine** out) {
   int ozs = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&ozs, zstd_kernel, 64, 0) != hipSuccess || ozs < 1) ozs = 8;
   e->zstd_blocks_per_cu = ozs;
+  int olw = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olw, lz4_block_kernel, 64, 0) != hipSuccess || olw < 1) olw = 16;
+  e->lz4w_blocks_per_cu = olw;
   int o1 = 0, o2 = 0, o3 = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, parse_kernel, 64, 0) != hipSuccess || o1 < 1) o1 = 2;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, huff_kernel, 64, 0) != hipSuccess || o2 < 1) o2 = 4;
@@ -1579,7 +1586,7 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
     hipLaunchKernelGGL(emit_kernel, dim3(grid_for(e->emit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 2, so, sc, sp, tok, slots, (uint32_t*)d_dst, seg_cap, clevel);
   } else {
-    const unsigned lgrid = grid_for(16, nchunks * KSLOTS);
+    const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, nchunks * KSLOTS);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                        seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0,
                        (int)(cname == HSDS_CNAME_BLOSCLZ), (uint32_t)KSLOTS, 0xffffffffu);
@@ -1709,7 +1716,7 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
   };
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, slot_cap)), dim3(64), 0, st, slots, offs,
                      segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, BSHUF_PARSE_LEVEL, 0u, slot_cap);
-  const unsigned lgrid = grid_for(16, slot_cap);
+  const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, slot_cap);
   hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                      seg_cap, BSHUF_PARSE_LEVEL, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0, 0, 0u, slot_cap);
   hipLaunchKernelGGL(bs_layout_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,

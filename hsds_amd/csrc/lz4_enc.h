@@ -56,15 +56,66 @@ HZ_HD uint32_t in_byte(InRd& in, uint32_t pos) {
   return in.ts > 1u ? (uint32_t)in.blk[hd::shuffled_src_index(in.off + pos, in.ts, in.neb)] : lz::rd_byte(in.r, pos);
 }
 
+// Literal runs of RUN_MIN bytes or more are not copied by the lane that owns their
+// sequence (a run can span many lanes' token ranges, up to a whole incompressible
+// block): the lane reserves the bytes and lists the run; the whole wave then copies
+// the listed runs (flush_runs), 64 bytes per instruction.
+constexpr uint32_t RUN_MIN = 64;
+constexpr uint32_t RUN_CAP = 136;        // > SEG / RUN_MIN + carried run + final run
+struct CopyRun {
+  hz_gu8* dst;
+  uint32_t src, len;
+};
+struct CopyList {
+  uint32_t n;
+  CopyRun r[RUN_CAP];
+};
+HZ_HD bool defer_run(CopyList* cl, hz_gu8* dst, uint32_t src, uint32_t len) {
+  if (!cl) return false;
+#if HZ_GPU
+  const uint32_t k = atomicAdd(&cl->n, 1u);
+#else
+  const uint32_t k = cl->n++;
+#endif
+  if (k >= RUN_CAP) return false;        // list full: the lane copies the run itself
+  cl->r[k].dst = dst;
+  cl->r[k].src = src;
+  cl->r[k].len = len;
+  return true;
+}
+#if HZ_GPU
+__device__
+#else
+static
+#endif
+inline void flush_runs(CopyList* cl, const hd::EncJob& job) {
+  WAVE_SYNC();
+  const uint32_t nr = cl->n < RUN_CAP ? cl->n : RUN_CAP;
+  hz_gcu8* s = HZ_GLOBAL(hz_gcu8*, job.src);
+  for (uint32_t k = 0; k < nr; k++) {
+    hz_gu8* const d = cl->r[k].dst;
+    const uint32_t src = cl->r[k].src, len = cl->r[k].len;
+    LANE_LOOP {
+      for (uint32_t i = (uint32_t)lane; i < len; i += 64u)
+        d[i] = job.ts > 1u ? s[hd::shuffled_src_index(job.off + src + i, job.ts, job.neb)] : s[src + i];
+    }
+  }
+  WAVE_SYNC();
+  LANE_LOOP { if (lane == 0) cl->n = 0; }
+  WAVE_SYNC();
+}
+
 // one sequence: literals [l0, l1), then a match (ml >= 4) of distance dist; ml == 0:
 // the final literals-only sequence
-HZ_HD void sequence(Out& o, InRd& in, uint32_t l0, uint32_t l1, uint32_t dist, uint32_t ml) {
+HZ_HD void sequence(Out& o, InRd& in, uint32_t l0, uint32_t l1, uint32_t dist, uint32_t ml,
+                    CopyList* cl = nullptr) {
   const uint32_t ll = l1 - l0;
   const uint32_t mc = ml ? (ml - 4u < 15u ? ml - 4u : 15u) : 0u;
   put(o, ((ll < 15u ? ll : 15u) << 4) | mc);
   if (ll >= 15u) put_len(o, ll - 15u);
   if (o.write) {
-    for (uint32_t p = l0; p < l1; p++) put(o, in_byte(in, p));
+    if (ll >= RUN_MIN && defer_run(cl, o.p + o.n, l0, ll)) o.n += ll;
+    else for (uint32_t p = l0; p < l1; p++) put(o, in_byte(in, p));
   } else {
     o.n += ll;
   }
@@ -80,31 +131,41 @@ HZ_HD uint32_t ext_len(uint32_t v) { return v >= 15u ? (v - 15u) / 255u + 1u : 0
 HZ_HD uint32_t seq_size(uint32_t run, uint32_t ml) { return 1u + ext_len(run) + run + (ml ? 2u + ext_len(ml - 4u) : 0u); }
 
 // Walk lane `lane`'s parse tokens of one segment (input from p0): f(pos, len, dist)
-// for every match of the parse, in order.
+// for every match of the parse, in order.  Token slots 2k, 2k+1 share the word
+// (k * WAVE + lane); TB words are loaded per batch (independent loads in flight
+// instead of one dependent load per token pair) and shifted through wv[0].
 template <class F>
 HZ_HD void lane_tokens(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, F&& f) {
-  uint32_t pos = p0, pend = 0;
-  bool have = false;
-  for (uint32_t s = 0; s < ns; s++) {
-    uint32_t t;
-    if (!have) {
-      const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)hd::tslot(s, lane) * 2u);
-      t = pr & 0xffffu; pend = pr >> 16; have = true;
-    } else {
-      t = pend; have = false;
+  constexpr uint32_t TB = 8;
+  hz_gcu32* gw = (hz_gcu32*)gtok;
+  const uint32_t nw = (ns + 1u) >> 1;
+  uint32_t pos = p0, tl = 0;
+  bool want_dist = false;
+  for (uint32_t w0 = 0; w0 < nw; w0 += TB) {
+    uint32_t wv[TB];
+#pragma unroll
+    for (uint32_t i = 0; i < TB; i++)
+      wv[i] = w0 + i < nw ? gw[(size_t)(w0 + i) * (uint32_t)hd::WAVE + (uint32_t)lane] : 0u;
+    const uint32_t cnt = nw - w0 < TB ? nw - w0 : TB;
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t word = wv[0];
+#pragma unroll
+      for (uint32_t i = 0; i + 1 < TB; i++) wv[i] = wv[i + 1];
+      const uint32_t s = 2u * (w0 + k);
+      for (uint32_t h = 0; h < 2u && s + h < ns; h++) {
+        const uint32_t t = h ? word >> 16 : word & 0xffffu;
+        if (want_dist) {
+          f(pos, tl, t + 1u);
+          pos += tl;
+          want_dist = false;
+        } else if (t & 0x8000u) {
+          tl = (t & 0x7fffu) + 3u;
+          want_dist = true;
+        } else {
+          pos++;
+        }
+      }
     }
-    if (!(t & 0x8000u)) { pos++; continue; }
-    uint32_t dv;
-    s++;
-    if (!have) {
-      const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)hd::tslot(s, lane) * 2u);
-      dv = pr & 0xffffu; pend = pr >> 16; have = true;
-    } else {
-      dv = pend; have = false;
-    }
-    const uint32_t len = (t & 0x7fffu) + 3u;
-    f(pos, len, dv + 1u);
-    pos += len;
   }
 }
 
@@ -126,7 +187,7 @@ HZ_HD void lane_matches(hz_gcu8* gtok, uint32_t ns, int lane, uint32_t p0, uint3
 // output offsets from a prefix sum.  write == 0: returns the block size; write == 1:
 // writes the block to out (and returns the size).
 HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const hd::EncJob& job, uint8_t* out,
-                              int write) {
+                              int write, CopyList* cl = nullptr) {
   const uint32_t n = job.len;
   const uint32_t nseg = hd::nsegments(n);
   uint32_t carry = 0;      // literals pending from earlier segments
@@ -198,12 +259,13 @@ HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const
           in_init(in, job);
           uint32_t lit0 = s0 + a0 - LV(cin);
           lane_matches(gtok, sp[sg].nslot[lane], lane, s0 + a0, n, [&](uint32_t pos, uint32_t ml, uint32_t dist) {
-            sequence(o, in, lit0, pos, dist, ml);
+            sequence(o, in, lit0, pos, dist, ml, cl);
             lit0 = pos + ml;
           });
         }
       }
       WAVE_SYNC();
+      if (cl) flush_runs(cl, job);
     }
     carry = seg_carry;
     base += seg_total;
@@ -215,9 +277,10 @@ HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const
         Out o = {HZ_GLOBAL(hz_gu8*, out + base), 0u, 1};
         InRd in;
         in_init(in, job);
-        sequence(o, in, n - carry, n, 0u, 0u);
+        sequence(o, in, n - carry, n, 0u, 0u, cl);
       }
     }
+    if (cl) flush_runs(cl, job);
   }
   return base + seq_size(carry, 0u);
 }

@@ -82,7 +82,9 @@ extern "C" int64_t emu_lz4_block(const uint8_t* src, uint32_t n, uint8_t* dst, u
   free(ps);
   const uint32_t sz = lze::lz4_block_wave(sp.data(), tok.data(), job, nullptr, 0);
   if (sz > cap) return -1;
-  const uint32_t sz2 = lze::lz4_block_wave(sp.data(), tok.data(), job, dst, 1);
+  lze::CopyList* cl = (lze::CopyList*)calloc(1, sizeof(lze::CopyList));   // the kernel's LDS run list
+  const uint32_t sz2 = lze::lz4_block_wave(sp.data(), tok.data(), job, dst, 1, cl);
+  free(cl);
   return sz2 == sz ? (int64_t)sz : -2;
 }
 
