@@ -359,11 +359,37 @@ class ChunkRead:
         self.chunk_id, self.key, self.offset, self.length = chunk_id, key, offset, length
 
 
-def _check_decodable(comp, shuffle):
-    """Bitshuffle objects inside an outer Blosc frame decode one at a time through
-    codec._uncompress; the batched reader takes bare bitshuffle+LZ4 objects only."""
-    if shuffle == 2 and comp != nat.COMP_NONE:
-        raise NotImplementedError("batched read of bitshuffle objects under an outer compressor")
+def _decode_batch(eng, d_src, descs, dbuf, status, comp, shuffle, isz, blobs):
+    """hsds_decode_batch for one batch.  Bitshuffle objects under an outer compressor
+    (what _compress(shuffle=2) stores when the dataset also has one, storUtil.py:243-262)
+    take two launches on the same stream, as _uncompress does (storUtil.py:189-227):
+    the outer Blosc frames into a staging buffer sized by their headers' nbytes, then
+    the bitshuffle objects from there into `dbuf`.  A status from the first stage wins."""
+    import torch
+    if not (shuffle == 2 and comp != nat.COMP_NONE):
+        eng.decode(d_src, descs, dbuf, status, compressor=_comp_name(comp), shuffle=shuffle, itemsize=isz)
+        return
+    from .codec import _as_bytes, _blosc_nbytes
+    from .engine import CHUNK_DESC_DTYPE
+    inner = []
+    for b in blobs:
+        nb = _blosc_nbytes(_as_bytes(b)) if len(b) else None
+        if nb is None:
+            # a bare zlib stream has no recorded inner size: codec._uncompress reads it
+            raise NotImplementedError("batched read of a non-Blosc outer stream around bitshuffle objects")
+        inner.append(nb)
+    d1 = np.zeros(len(blobs), CHUNK_DESC_DTYPE)
+    d2 = np.zeros(len(blobs), CHUNK_DESC_DTYPE)
+    off = 0
+    for k, nb in enumerate(inner):
+        d1[k] = (descs[k]["src_off"], descs[k]["src_len"], off, nb)
+        d2[k] = (off, nb, descs[k]["dst_off"], descs[k]["dst_len"])
+        off += (nb + 255) // 256 * 256
+    ibuf = torch.empty(max(off, 1), dtype=torch.uint8, device=dbuf.device)
+    st1 = torch.full_like(status, 99)
+    eng.decode(d_src, d1, ibuf, st1, compressor=_comp_name(comp), shuffle=0, itemsize=1)
+    eng.decode(ibuf, d2, dbuf, status, compressor=None, shuffle=2, itemsize=isz)
+    torch.where(st1 != nat.OK, st1, status, out=status)
 
 
 def _filter_args(filter_ops, dtype):
@@ -468,12 +494,11 @@ class ChunkReader:
         if not pieces:
             return []
         comp, shuffle, isz = _filter_args(filter_ops, (filter_ops or {}).get("dtype", np.uint8))
-        _check_decodable(comp, shuffle)
         src, descs, ext = pack_chunks(pieces, [int(h5_size)] * len(pieces))
         dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
         status = torch.full((len(pieces),), 99, dtype=torch.int32, device=self.device)
-        self.eng.decode(torch.from_numpy(src).to(self.device), descs, dbuf, status, compressor=_comp_name(comp),
-                        shuffle=shuffle, itemsize=isz)
+        _decode_batch(self.eng, torch.from_numpy(src).to(self.device), descs, dbuf, status, comp, shuffle, isz,
+                      pieces)
         self.stats["decode_calls"] += 1
         st = status.cpu().numpy()
         host = dbuf.cpu().numpy()
@@ -546,13 +571,12 @@ class ChunkReader:
         # ONE decode batch into a contiguous buffer (plain objects and HDF5 chunks)
         dec = [j for j in jobs if j[1] in ("plain", "h5")]
         if dec:
-            _check_decodable(comp, shuffle)
             sizes = [chunk_size if kind == "plain" else h5_size for _, kind, _, _ in dec]
             src, descs, ext = pack_chunks([blobs[bi] for _, _, bi, _ in dec], sizes)
             d_src = torch.from_numpy(src).to(self.device)
             dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
             status = torch.full((len(dec),), 99, dtype=torch.int32, device=self.device)
-            self.eng.decode(d_src, descs, dbuf, status, compressor=_comp_name(comp), shuffle=shuffle, itemsize=isz)
+            _decode_batch(self.eng, d_src, descs, dbuf, status, comp, shuffle, isz, [blobs[bi] for _, _, bi, _ in dec])
             self.stats["decode_calls"] += 1
             self.stats["objects"] += sum(1 for _, k, _, _ in dec if k == "plain")
             self.stats["h5_chunks"] += sum(1 for _, k, _, _ in dec if k == "h5")

@@ -310,8 +310,17 @@ def test_put_and_flush_bitshuffle_dataset(dev, oracle_lib, with_deflate):
         assert bytes(orc.bitshuffle_decode(obj, len(want), 4)) == want, cid
         assert codec._uncompress(f, compressor=ops.get("compressor"), shuffle=2, dtype=dt,
                                  chunk_shape=dims) == want
-    if not with_deflate:
-        cs2 = ChunkStore(lambda k, o, n: flushed.get(k), mem_target=1 << 24, device=dev)
-        res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in sorted(keys)], dt, dims, filter_ops=ops)
-        for cid, r in zip(sorted(keys), res):
-            assert r.cpu().numpy().tobytes() == truth[cid].tobytes(), cid
+    # batched read-back: one bitshuffle decode launch, or two (outer Blosc, then
+    # bitshuffle) when the dataset also has deflate; a corrupted object fails alone
+    store = dict(flushed)
+    bad = bytearray(store["k1"])
+    bad[len(bad) // 2] ^= 0xFF
+    bad[-3] ^= 0x5A
+    store["k1"] = bytes(bad)
+    cs2 = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in sorted(keys)], dt, dims, filter_ops=ops)
+    for cid, r in zip(sorted(keys), res):
+        if keys[cid] == "k1":
+            assert isinstance(r, Exception) or r.cpu().numpy().tobytes() != truth[cid].tobytes()
+            continue
+        assert r.cpu().numpy().tobytes() == truth[cid].tobytes(), cid
