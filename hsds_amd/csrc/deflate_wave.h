@@ -67,12 +67,15 @@ struct Tune {
   uint32_t nice;     // stop searching at this match length
   uint32_t too_far;  // length-3 matches farther than this are not taken (zlib TOO_FAR)
   uint32_t stored;   // 1: level 0, stored blocks only
+  uint32_t fast_head; // 1: no exact chains (LZ4 items): prev[p] = the hash head of the
+                      // previous 64-position step, head[h] = any position of this step
 };
 
 HZ_HD Tune tune_for_level(int level) {
   Tune t;
   t.too_far = 4096;
   t.stored = level <= 0 ? 1u : 0u;
+  t.fast_head = 0;
   switch (level) {
     case 1: t.chain = 1; t.nice = 8; break;
     case 2: t.chain = 2; t.nice = 16; break;
@@ -354,7 +357,33 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     WAVE_SYNC();
 
     const uint32_t lo_pos = s0 > WIN ? s0 - WIN : 0u;   // farthest match source
-    if (!tune.stored) {
+    if (!tune.stored && tune.fast_head) {
+      // ---- approximate chains: every candidate is still an earlier position with the
+      // same hash, so any parse over them is valid; only match quality can differ ----
+      HZ_T(2);
+      for (uint32_t g = s0; g < s1; g += WAVE) {
+        LANE_VAR(uint32_t, hh);
+        LANE_VAR(uint32_t, hp);
+        LANE_VAR(uint32_t, hn);
+        LANE_LOOP {
+          const uint32_t p = g + (uint32_t)lane;
+          LV(hh) = KEY_NONE;
+          if (p < s1 && p + 2u < n) LV(hh) = hash3(rd32(sh, p));
+        }
+        HD_NEIGHBOURS(hp, hn, hh);
+        LANE_LOOP {
+          // the position just before, when it has the same hash (runs), else the head
+          const uint32_t p = g + (uint32_t)lane;
+          if (LV(hh) != KEY_NONE)
+            sh.prev[p - s0] = LV(hp) == LV(hh) ? (uint16_t)((p - 1u) & 0xffffu) : sh.head[LV(hh)];
+        }
+        WAVE_SYNC();
+        LANE_LOOP {
+          if (LV(hh) != KEY_NONE) sh.head[LV(hh)] = (uint16_t)((g + (uint32_t)lane) & 0xffffu);
+        }
+        WAVE_SYNC();
+      }
+    } else if (!tune.stored) {
       // ---- exact hash chains, 64 positions per step ----
       HZ_T(2);
       for (uint32_t g = s0; g < s1; g += WAVE) {

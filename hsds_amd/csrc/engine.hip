@@ -703,6 +703,8 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
 }
 
 
+constexpr int PARSE_FAST = 100;        // parse_kernel level offset: approximate chains (LZ4 items)
+
 // P: persistent waves, one zlib stream each
 __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ slots,
                                                    const uint32_t* __restrict__ offs,
@@ -714,7 +716,12 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
   __shared__ hd::ParseShared sh;
   const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   const int lane = threadIdx.x;
-  const hd::Tune tune = hd::tune_for_level(level);
+  // level > PARSE_FAST: the LZ4-only approximate-chain parse at level - PARSE_FAST
+  hd::Tune tune = hd::tune_for_level(level > PARSE_FAST ? level - PARSE_FAST : level);
+  if (level > PARSE_FAST) {
+    tune.fast_head = 1;
+    level -= PARSE_FAST;
+  }
 #ifdef HZ_PROFILE
   HzProf prof_;
   for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
@@ -1715,7 +1722,8 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
     return (unsigned)(g < 1 ? 1 : g);
   };
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, slot_cap)), dim3(64), 0, st, slots, offs,
-                     segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, BSHUF_PARSE_LEVEL, 0u, slot_cap);
+                     segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, PARSE_FAST + BSHUF_PARSE_LEVEL, 0u,
+                     slot_cap);
   const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, slot_cap);
   hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                      seg_cap, BSHUF_PARSE_LEVEL, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0, 0, 0u, slot_cap);

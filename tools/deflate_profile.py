@@ -33,12 +33,23 @@ def main():
     sizes = torch.zeros(n, dtype=torch.int64, device=dev)
     st = torch.zeros(n, dtype=torch.int32, device=dev)
     eng = ChunkEngine(0)
-    eng.encode(data, descs, frames, sizes, st, clevel=4)
+    if os.environ.get("HZ_PROF_BSHUF", "0") == "1":
+        # bitshuffle+LZ4 objects: parse level 1 over 8 KiB transposed blocks
+        bound = int(L.hsds_bitshuffle_bound(1 << 20, 4, 2048))
+        descs, _, dext = encode_descs([1 << 20] * n, overhead=bound - (1 << 20))
+        frames = torch.empty(dext, dtype=torch.uint8, device=dev)
+
+        def enc():
+            eng.encode_bitshuffle(data, descs, frames, sizes, st, itemsize=4, block=2048)
+    else:
+        def enc():
+            eng.encode(data, descs, frames, sizes, st, clevel=4)
+    enc()
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
     L.hsds_debug_profile(buf, 1)
     t = time.perf_counter()
-    eng.encode(data, descs, frames, sizes, st, clevel=4)
+    enc()
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     L.hsds_debug_profile(buf, 1)
