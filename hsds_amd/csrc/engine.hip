@@ -1584,7 +1584,11 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   };
   hipEventRecord(e->ev2, st);
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, nchunks * KSLOTS)), dim3(64), 0, st, slots,
-                     offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, clevel, (uint32_t)KSLOTS, 0xffffffffu);
+                     offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap,
+                     // lz4 (the speed codec) parses with approximate chains; zlib, lz4hc and
+                     // blosclz keep the exact chains
+                     cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, (uint32_t)KSLOTS,
+                     0xffffffffu);
   if (cname == HSDS_CNAME_ZLIB) {
     hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 1, sp, meta, sc, seg_cap, clevel);
