@@ -36,6 +36,9 @@
 #include "zstd_wave.h"
 #include "bshuf.h"
 
+#ifndef HZ_ZSTD_WPE
+#define HZ_ZSTD_WPE 3      // zstd_kernel waves per SIMD the compiler must allow (VGPR budget)
+#endif
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
 namespace {
@@ -341,7 +344,7 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, 
 // zstd splits (zstd_wave.h): persistent 64-thread workgroups, one split per wave
 // (tables and the sequence window in LDS, all lanes resolving the output)
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) zstd_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ_ZSTD_WPE))) zstd_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
                                                   int64_t nchunks, uint32_t* __restrict__ counter,
                                                   int32_t* __restrict__ status,
                                                   const uint32_t* __restrict__ kind_counts) {
