@@ -140,8 +140,8 @@ class Engine:
         except Exception:
             pass
 
-    def set_tuning(self, seg_bits=288, warmup_bits=384, cont_bits=192, rounds=4):
-        rc = lib().hsds_set_tuning(self.h, seg_bits, warmup_bits, cont_bits, rounds)
+    def set_tuning(self, seg_over16=1, warmup_bits=384, rounds=4):
+        rc = lib().hsds_set_tuning(self.h, seg_over16, warmup_bits, 0, rounds)
         if rc != OK:
             raise NativeError(rc, "hsds_set_tuning")
 

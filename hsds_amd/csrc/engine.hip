@@ -30,6 +30,7 @@
 
 #include "../../include/hsds_amd.h"
 #include "inflate_wave.h"
+#include "inflate2.h"
 #include "deflate_wave.h"
 #include "lz_wave.h"
 #include "lz4_enc.h"
@@ -43,14 +44,16 @@
 
 namespace {
 
-constexpr int KSLOTS = 256;          // max deflate streams / raw splits per chunk
-constexpr int INFLATE_WAVES_PER_CU = 8;   // LDS-bound: sizeof(hz::Shared) <= 20 KiB
-static_assert(sizeof(hz::Shared) * INFLATE_WAVES_PER_CU <= 160 * 1024, "inflate LDS block too large");
+constexpr int KSLOTS = 256;          // encode: max zlib streams per chunk (enc_plan_kernel)
 
 // ITEM_LZ4 / ITEM_BLOSCLZ: Blosc splits of the byte-LZ77 codecs (lz_wave.h)
-enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_ZSTD = 4, ITEM_INEXACT = 0x100 };
+enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_ZSTD = 4, ITEM_INEXACT = 0x100,
+                  ITEM_PLANE = 1u << 24 };
 
-struct Item {          // 32 bytes
+// decode work item (32 bytes): one zlib stream / raw span / LZ split.  kind word: bits 0-7
+// decoder, bit 8 inexact size, bits 16-23 byte-unshuffle element size n (<= 1: none), bit 24
+// plane split (the item is plane j, bits 25-29, of a Blosc block whose base is `dst`)
+struct Item {
   uint64_t src;
   uint64_t dst;
   uint32_t src_len;
@@ -59,10 +62,10 @@ struct Item {          // 32 bytes
   uint32_t kind;
 };
 
-struct ChunkMeta {     // post-decode unshuffle work for one chunk
+struct ChunkMeta {     // post-decode unshuffle of LZ / zstd Blosc blocks staged in tmp
   uint64_t tmp;        // staged (shuffled) bytes
   uint64_t dst;
-  uint32_t mode;       // 0 none, 1 Blosc blocks (ts, bs), 2 whole chunk (itemsize)
+  uint32_t mode;       // 0 none, 1 Blosc blocks (ts, bs)
   uint32_t ts;
   uint32_t bs;
   uint32_t nbytes;
@@ -73,14 +76,26 @@ __device__ __forceinline__ uint32_t rd32le(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// output map of an item (hz2::Perm): F2 chunks and Blosc shuffled blocks land unshuffled
+__device__ __forceinline__ hz2::Perm item_perm(const Item& it) {
+  const uint32_t n = (it.kind >> 16) & 0xffu;
+  if (n <= 1u) return hz2::perm_make(1u, 1u, 0u);
+  if (it.kind & ITEM_PLANE) return hz2::perm_make(n, it.dst_len, ((it.kind >> 25) & 31u) * it.dst_len);
+  return hz2::perm_make(n, it.dst_len / n, 0u);
+}
+
 // -------------------------------------------------------------------------
-// frame walk: one thread per chunk.  Restates c-blosc 1.21 blosc_decompress
-// frame rules (see oracle/oracle.c orc_blosc_decode) and storUtil._uncompress's
-// dispatch.  Items go to slot range [chunk*KSLOTS, chunk*KSLOTS + count).
+// frame walk: one thread per chunk.  Restates c-blosc 1.21 blosc_decompress frame rules
+// (oracle/oracle.c orc_blosc_decode) and storUtil._uncompress's dispatch
+// (storUtil.py:182-235).  The walk runs twice: once to count the chunk's items, then -- after
+// one atomic allocation from the batch's item pool -- to write them, so a chunk may have any
+// number of Blosc splits (pool capacity: 8 per chunk + 1 per 2 KiB of destination).
+// zlib streams and raw spans carry their unshuffle map (item_perm); LZ / zstd splits of a
+// shuffled frame are staged in tmp and unshuffled by unshuffle_kernel.
 // -------------------------------------------------------------------------
 __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
-                                  int64_t nchunks, uint8_t* dst_base, uint8_t* tmp_base, Item* __restrict__ slots,
-                                  uint32_t* __restrict__ counts, ChunkMeta* __restrict__ meta,
+                                  int64_t nchunks, uint8_t* dst_base, uint8_t* tmp_base, Item* __restrict__ pool,
+                                  uint32_t pool_cap, uint32_t* __restrict__ pool_ctr, ChunkMeta* __restrict__ meta,
                                   uint32_t* __restrict__ meta_list, uint32_t* __restrict__ meta_count,
                                   uint32_t* __restrict__ kind_counts, int32_t* __restrict__ status,
                                   int compressor, int shuffle, int itemsize, int inexact) {
@@ -90,94 +105,110 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
   const uint8_t* s = src_base + c.src_off;
   const uint64_t L = c.src_len, n = c.dst_len;
   uint8_t* out = dst_base + c.dst_off;
-  uint8_t* tmp = tmp_base + c.dst_off;
-  Item* slot = slots + ci * KSLOTS;
+  uint8_t* tmp = tmp_base ? tmp_base + c.dst_off : nullptr;
   int st = HSDS_OK;
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, base = 0, nlz = 0, nzs = 0;
+  Item* slot = nullptr;
   ChunkMeta m = {0, (uint64_t)out, 0, 0, 0, (uint32_t)n};
-  auto emit = [&](uint32_t kind, const uint8_t* sp, uint64_t sl, uint8_t* dp, uint64_t dl) {
-    if (cnt >= (uint32_t)KSLOTS) { st = HSDS_ERR_UNSUPPORTED; return; }
-    Item it;
-    it.src = (uint64_t)sp; it.dst = (uint64_t)dp; it.src_len = (uint32_t)sl; it.dst_len = (uint32_t)dl;
-    it.chunk = (uint32_t)ci; it.kind = kind;
-    slot[cnt++] = it;
-  };
-  if (L >= (1ull << 28) || n >= (1ull << 31)) {
-    st = HSDS_ERR_UNSUPPORTED;
-  } else if (compressor == HSDS_COMP_NONE) {
-    if (L != n) st = HSDS_ERR_SIZE;
-    else if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
-    else if (shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1) {
-      if (n % (uint64_t)itemsize) st = HSDS_ERR_ARG;
-      else { emit(ITEM_RAW, s, L, tmp, n); m.mode = 2; m.tmp = (uint64_t)tmp; m.ts = (uint32_t)itemsize; }
-    } else emit(ITEM_RAW, s, L, out, n);
-  } else if (L >= 4 && rd8(s) <= 2 && rd8(s + 3) > 0) {
-    // ---- Blosc1 frame (shuffle filter handled in-frame: storUtil.py:203-204) ----
-    if (L < 16) st = HSDS_ERR_FRAME;
-    else {
-      const uint32_t ver = rd8(s), verlz = rd8(s + 1), flags = rd8(s + 2), ts = rd8(s + 3);
-      const uint32_t codec = (flags >> 5) & 7;   // 0 blosclz, 1 lz4/lz4hc, 2 snappy, 3 zlib, 4 zstd
-      const uint32_t kind = codec == 3 ? ITEM_ZLIB : codec == 1 ? ITEM_LZ4 : codec == 4 ? ITEM_ZSTD : ITEM_BLOSCLZ;
-      const uint64_t nbytes = rd32le(s + 4), bs = rd32le(s + 8), cbytes = rd32le(s + 12);
-      if (ver != 2 || cbytes > L || cbytes < 16) st = HSDS_ERR_FRAME;
-      else if (nbytes != n) st = HSDS_ERR_SIZE;
-      else if (flags & 0x02) {
-        if (nbytes + 16 > cbytes) st = HSDS_ERR_FRAME;
-        else emit(ITEM_RAW, s + 16, nbytes, out, nbytes);
-      } else if (codec != 3 && codec != 1 && codec != 0 && codec != 4) st = HSDS_ERR_UNSUPPORTED;   // snappy
-      else if (verlz != 1) st = HSDS_ERR_FRAME;
-      else if (flags & 0x04) st = HSDS_ERR_UNSUPPORTED;
-      else if (nbytes > 0) {
-        if (bs == 0 || bs > nbytes) st = HSDS_ERR_FRAME;
-        else {
-          const uint64_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
-          const uint64_t hdr = 16 + 4 * nblocks;
-          const int doshuffle = (flags & 0x01) && ts > 1;
-          uint8_t* target = doshuffle ? tmp : out;
-          if (hdr > cbytes) st = HSDS_ERR_FRAME;
-          for (uint64_t b = 0; b < nblocks && st == HSDS_OK; b++) {
-            const int isleft = (b == nblocks - 1) && leftover;
-            const uint64_t bsz = isleft ? leftover : bs;
-            const uint32_t nspl = (!(flags & 0x10) && ts <= 16 && bs / ts >= 128 && !isleft) ? ts : 1;
-            const uint64_t neblock = bsz / nspl;
-            int64_t p = (int32_t)rd32le(s + 16 + 4 * b);
-            if (p < (int64_t)hdr || p >= (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
-            for (uint32_t j = 0; j < nspl; j++) {
-              if (p + 4 > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
-              const int64_t cs = (int32_t)rd32le(s + p);
-              p += 4;
-              if (cs < 0 || p + cs > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
-              emit((uint64_t)cs == neblock ? ITEM_RAW : kind, s + p, (uint64_t)cs,
-                   target + b * bs + j * neblock, neblock);
-              if (st != HSDS_OK) break;
-              p += cs;
+  for (int pass = 0; pass < 2; pass++) {
+    cnt = 0; nlz = 0; nzs = 0;
+    m.mode = 0;
+    auto emit = [&](uint32_t kind, const uint8_t* sp, uint64_t sl, uint8_t* dp, uint64_t dl) {
+      if (pass == 1) {
+        Item it;
+        it.src = (uint64_t)sp; it.dst = (uint64_t)dp; it.src_len = (uint32_t)sl; it.dst_len = (uint32_t)dl;
+        it.chunk = (uint32_t)ci; it.kind = kind;
+        slot[cnt] = it;
+      }
+      cnt++;
+      nlz += (kind & 0xff) == ITEM_LZ4 || (kind & 0xff) == ITEM_BLOSCLZ;
+      nzs += (kind & 0xff) == ITEM_ZSTD;
+    };
+    const uint32_t shuf_n = (shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1) ? ((uint32_t)itemsize << 16) : 0u;
+    if (L >= (1ull << 28) || n >= (1ull << 31)) {
+      st = HSDS_ERR_UNSUPPORTED;
+    } else if (compressor == HSDS_COMP_NONE) {
+      if (L != n) st = HSDS_ERR_SIZE;
+      else if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
+      else if (shuf_n && (n % (uint64_t)itemsize)) st = HSDS_ERR_ARG;
+      else if (shuf_n && itemsize > 255) st = HSDS_ERR_UNSUPPORTED;
+      else emit(ITEM_RAW | shuf_n, s, L, out, n);
+    } else if (L >= 4 && rd8(s) <= 2 && rd8(s + 3) > 0) {
+      // ---- Blosc1 frame (shuffle filter handled in-frame: storUtil.py:203-204) ----
+      if (L < 16) st = HSDS_ERR_FRAME;
+      else {
+        const uint32_t ver = rd8(s), verlz = rd8(s + 1), flags = rd8(s + 2), ts = rd8(s + 3);
+        const uint32_t codec = (flags >> 5) & 7;   // 0 blosclz, 1 lz4/lz4hc, 2 snappy, 3 zlib, 4 zstd
+        const uint32_t kind = codec == 3 ? ITEM_ZLIB : codec == 1 ? ITEM_LZ4 : codec == 4 ? ITEM_ZSTD : ITEM_BLOSCLZ;
+        const uint64_t nbytes = rd32le(s + 4), bs = rd32le(s + 8), cbytes = rd32le(s + 12);
+        if (ver != 2 || cbytes > L || cbytes < 16) st = HSDS_ERR_FRAME;
+        else if (nbytes != n) st = HSDS_ERR_SIZE;
+        else if (flags & 0x02) {
+          if (nbytes + 16 > cbytes) st = HSDS_ERR_FRAME;
+          else emit(ITEM_RAW, s + 16, nbytes, out, nbytes);
+        } else if (codec != 3 && codec != 1 && codec != 0 && codec != 4) st = HSDS_ERR_UNSUPPORTED;   // snappy
+        else if (verlz != 1) st = HSDS_ERR_FRAME;
+        else if (flags & 0x04) st = HSDS_ERR_UNSUPPORTED;
+        else if (nbytes > 0) {
+          if (bs == 0 || bs > nbytes) st = HSDS_ERR_FRAME;
+          else {
+            const uint64_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
+            const uint64_t hdr = 16 + 4 * nblocks;
+            const int doshuffle = (flags & 0x01) && ts > 1;
+            // zlib streams / raw splits land unshuffled through their output map; the LZ
+            // decoders write plain bytes, so their shuffled frames go through tmp
+            const int staged = doshuffle && kind != ITEM_ZLIB;
+            if (staged && !tmp) st = HSDS_ERR_UNSUPPORTED;
+            uint8_t* target = staged ? tmp : out;
+            if (hdr > cbytes) st = HSDS_ERR_FRAME;
+            for (uint64_t b = 0; b < nblocks && st == HSDS_OK; b++) {
+              const int isleft = (b == nblocks - 1) && leftover;
+              const uint64_t bsz = isleft ? leftover : bs;
+              const uint32_t nspl = (!(flags & 0x10) && ts <= 16 && bs / ts >= 128 && !isleft) ? ts : 1;
+              const uint64_t neblock = bsz / nspl;
+              int64_t p = (int32_t)rd32le(s + 16 + 4 * b);
+              if (p < (int64_t)hdr || p >= (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
+              for (uint32_t j = 0; j < nspl; j++) {
+                if (p + 4 > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
+                const int64_t cs = (int32_t)rd32le(s + p);
+                p += 4;
+                if (cs < 0 || p + cs > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
+                const uint32_t k = (uint64_t)cs == neblock ? ITEM_RAW : kind;
+                if (doshuffle && !staged) {
+                  // plane split j of the block (nspl == ts), or the whole shuffled block
+                  const uint32_t pm = (ts << 16) | (nspl > 1 ? ITEM_PLANE | (j << 25) : 0u);
+                  emit(k | pm, s + p, (uint64_t)cs, out + b * bs, neblock);
+                } else {
+                  emit(k, s + p, (uint64_t)cs, target + b * bs + j * neblock, neblock);
+                }
+                p += cs;
+              }
             }
+            if (staged) { m.mode = 1; m.tmp = (uint64_t)tmp; m.ts = ts; m.bs = (uint32_t)bs; }
           }
-          if (doshuffle) { m.mode = 1; m.tmp = (uint64_t)tmp; m.ts = ts; m.bs = (uint32_t)bs; }
         }
       }
+    } else if (compressor == HSDS_COMP_ZLIB) {
+      if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
+      else if (shuf_n && (n % (uint64_t)itemsize)) st = HSDS_ERR_ARG;
+      else if (shuf_n && itemsize > 255) st = HSDS_ERR_UNSUPPORTED;
+      else emit((inexact && !shuf_n ? (ITEM_ZLIB | ITEM_INEXACT) : ITEM_ZLIB) | shuf_n, s, L, out, n);
+    } else {
+      st = HSDS_ERR_UNSUPPORTED;
     }
-  } else if (compressor == HSDS_COMP_ZLIB) {
-    if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
-    else if (shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1) {
-      if (n % (uint64_t)itemsize) st = HSDS_ERR_ARG;
-      else { emit(ITEM_ZLIB, s, L, tmp, n); m.mode = 2; m.tmp = (uint64_t)tmp; m.ts = (uint32_t)itemsize; }
-    } else emit(inexact ? (ITEM_ZLIB | ITEM_INEXACT) : ITEM_ZLIB, s, L, out, n);
-  } else {
-    st = HSDS_ERR_UNSUPPORTED;
+    if (st != HSDS_OK) { cnt = 0; m.mode = 0; break; }
+    if (pass == 0) {
+      if (cnt == 0) break;
+      base = atomicAdd(pool_ctr, cnt);
+      if (base + cnt > pool_cap || base + cnt < base) { st = HSDS_ERR_UNSUPPORTED; cnt = 0; m.mode = 0; break; }
+      slot = pool + base;
+    }
   }
-  if (st != HSDS_OK) { cnt = 0; m.mode = 0; }
-  // items per decoder (kind_counts[0]: LZ splits for lz_kernel, [1]: the rest for
-  // inflate_kernel), so that a kernel with nothing to do exits at once
-  uint32_t nlz = 0, nzs = 0;
-  for (uint32_t k = 0; k < cnt; k++) {
-    nlz += (slot[k].kind & 0xff) == ITEM_LZ4 || (slot[k].kind & 0xff) == ITEM_BLOSCLZ;
-    nzs += (slot[k].kind & 0xff) == ITEM_ZSTD;
-  }
-  if (nlz) atomicAdd(&kind_counts[0], nlz);
-  if (cnt - nlz - nzs) atomicAdd(&kind_counts[1], cnt - nlz - nzs);
-  if (nzs) atomicAdd(&kind_counts[2], nzs);
-  counts[ci] = cnt;
+  // items per decoder (kind_counts[0]: LZ splits for lz_kernel, [1]: zlib + raw for
+  // inflate2_kernel, [2]: zstd), so that a kernel with nothing to do exits at once
+  if (nlz && cnt) atomicAdd(&kind_counts[0], nlz);
+  if (cnt - nlz - nzs && cnt) atomicAdd(&kind_counts[1], cnt - nlz - nzs);
+  if (nzs && cnt) atomicAdd(&kind_counts[2], nzs);
   status[ci] = st;
   meta[ci] = m;
   if (m.mode) {
@@ -186,7 +217,7 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
   }
 }
 
-// item index -> (chunk, slot) by binary search over the exclusive item offsets
+// item index -> (chunk, slot) by binary search over the exclusive item offsets (encode side)
 __device__ __forceinline__ int64_t item_chunk(const uint32_t* offs, int64_t nchunks, uint32_t item) {
   int64_t lo = 0, hi = nchunks - 1;
   while (lo < hi) {
@@ -222,17 +253,34 @@ __global__ void scan_kernel(const uint32_t* __restrict__ counts, uint32_t* __res
 }
 
 // -------------------------------------------------------------------------
-// inflate: persistent 64-thread workgroups; each pulls stream items from a
-// device counter until the batch total (offs[nchunks]) is exhausted.
+// inflate: persistent 64-thread workgroups; each pulls items from the pool until the
+// pool's fill count is reached.  zlib streams go to hz2::inflate_stream (inflate2.h) with
+// the wave's own match ring (rings + blockIdx.x * RING_BYTES); raw spans are copied.
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
-                                                     int64_t nchunks, uint32_t* __restrict__ counter,
-                                                     int32_t* __restrict__ status, uint32_t* __restrict__ sizes,
-                                                     const uint32_t* __restrict__ kind_counts, hz::Tune tune) {
-  __shared__ hz::Shared sh;
-  if (kind_counts[1] == 0) return;   // only LZ splits in this batch (lz_kernel)
-  const uint32_t total = offs[nchunks];
+__device__ __forceinline__ void raw_copy(const Item& it, int lane) {
+  const uint8_t* sp = (const uint8_t*)it.src;
+  uint8_t* dp = (uint8_t*)it.dst;
+  const uint32_t len = it.dst_len;
+  const hz2::Perm P = item_perm(it);
+  if (P.n == 1u && !(((uintptr_t)sp | (uintptr_t)dp) & 15u)) {
+    const uint32_t n16 = len >> 4;
+    for (uint32_t i = lane; i < n16; i += 64) ((uint4*)dp)[i] = ((const uint4*)sp)[i];
+    for (uint32_t i = (n16 << 4) + lane; i < len; i += 64) dp[i] = sp[i];
+  } else {
+    for (uint32_t i = lane; i < len; i += 64) dp[hz2::perm_at(P, i)] = sp[i];
+  }
+}
+
+__global__ void __launch_bounds__(64) inflate2_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+                                                      uint32_t* __restrict__ counter, int32_t* __restrict__ status,
+                                                      uint32_t* __restrict__ sizes,
+                                                      const uint32_t* __restrict__ kind_counts, hz2::Tune tune,
+                                                      uint8_t* __restrict__ rings) {
+  __shared__ hz2::Shared sh;
+  if (kind_counts[1] == 0) return;   // only LZ / zstd splits in this batch
+  const uint32_t total = *pool_ctr;
   const int lane = threadIdx.x;
+  uint8_t* ring = rings + (size_t)blockIdx.x * hz2::RING_BYTES;
 #ifdef HZ_PROFILE
   HzProf prof_;
   for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
@@ -245,27 +293,21 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
   for (;;) {
     uint32_t item = 0;
     if (lane == 0) item = atomicAdd(counter, 1u);
-    item = __shfl(item, 0, 64);
+    item = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(item, 0, 64));
     if (item >= total) break;
-    // chunk of this item: largest c with offs[c] <= item
-    int64_t lo = 0, hi = nchunks - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi + 1) >> 1;
-      if (offs[mid] <= item) lo = mid; else hi = mid - 1;
-    }
-    const Item it = slots[lo * KSLOTS + (item - offs[lo])];
+    const Item it = pool[item];
+    const uint32_t kind = it.kind & 0xff;
     int st;
-    if ((it.kind & 0xff) == ITEM_RAW) {
-      const uint8_t* sp = (const uint8_t*)it.src;
-      uint8_t* dp = (uint8_t*)it.dst;
-      for (uint32_t i = lane; i < it.dst_len; i += 64) dp[i] = sp[i];
+    if (kind == ITEM_RAW) {
+      raw_copy(it, lane);
       st = HSDS_OK;
-    } else if ((it.kind & 0xff) == ITEM_LZ4 || (it.kind & 0xff) == ITEM_BLOSCLZ || (it.kind & 0xff) == ITEM_ZSTD) {
-      continue;                        // lz_kernel's / zstd_kernel's item
+    } else if (kind == ITEM_ZLIB) {
+      hz2::Job job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
+                      (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr,
+                      item_perm(it)};
+      st = hz2::inflate_stream<hz2::Stats>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
     } else {
-      hz::StreamJob job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
-                           (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr};
-      st = hz::inflate_stream<hz::Stats>(sh, job, tune, (hz::Stats*)nullptr, prof);
+      continue;                        // lz_kernel's / zstd_kernel's item
     }
     if (lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
     __syncthreads();
@@ -285,13 +327,13 @@ __global__ void __launch_bounds__(64) inflate_kernel(const Item* __restrict__ sl
 // item table as inflate_kernel; a wave takes lz::GROUP consecutive items at a time
 // and decodes the LZ ones among them together (one split per header-walking lane).
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
-                                                int64_t nchunks, uint32_t* __restrict__ counter,
+__global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+                                                uint32_t* __restrict__ counter,
                                                 int32_t* __restrict__ status,
                                                 const uint32_t* __restrict__ kind_counts) {
   __shared__ lz::Shared ls;
   if (kind_counts[0] == 0) return;
-  const uint32_t total = offs[nchunks];
+  const uint32_t total = *pool_ctr;
   const int lane = threadIdx.x;
 #ifdef HZ_PROFILE
   HzProf prof_;
@@ -311,12 +353,7 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, 
     lz::LaneJob j = {nullptr, nullptr, 0u, 0u, 0u, 0u};
     uint32_t chunk = 0;
     if (lane < lz::GROUP && item < total) {
-      int64_t lo = 0, hi = nchunks - 1;
-      while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (offs[mid] <= item) lo = mid; else hi = mid - 1;
-      }
-      const Item it = slots[lo * KSLOTS + (item - offs[lo])];
+      const Item it = pool[item];
       const uint32_t kind = it.kind & 0xff;
       if (kind == ITEM_LZ4 || kind == ITEM_BLOSCLZ) {
         j = {(const uint8_t*)it.src, (uint8_t*)it.dst, it.src_len, it.dst_len,
@@ -344,13 +381,13 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ slots, 
 // zstd splits (zstd_wave.h): persistent 64-thread workgroups, one split per wave
 // (tables and the sequence window in LDS, all lanes resolving the output)
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ_ZSTD_WPE))) zstd_kernel(const Item* __restrict__ slots, const uint32_t* __restrict__ offs,
-                                                  int64_t nchunks, uint32_t* __restrict__ counter,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ_ZSTD_WPE))) zstd_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+                                                  uint32_t* __restrict__ counter,
                                                   int32_t* __restrict__ status,
                                                   const uint32_t* __restrict__ kind_counts) {
   __shared__ zw::Shared ls;
   if (kind_counts[2] == 0) return;
-  const uint32_t total = offs[nchunks];
+  const uint32_t total = *pool_ctr;
   const int lane = threadIdx.x;
 #ifdef HZ_PROFILE
   HzProf prof_;
@@ -366,8 +403,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ_ZSTD
     if (lane == 0) item = atomicAdd(counter, 1u);
     item = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(item, 0, 64));
     if (item >= total) break;
-    const int64_t ci = item_chunk(offs, nchunks, item);
-    const Item it = slots[ci * KSLOTS + (item - offs[ci])];
+    const Item it = pool[item];
     if ((zw::uni(it.kind) & 0xff) != ITEM_ZSTD) continue;
     // the frame walk is uniform: keep its operands in scalar registers
     const uint64_t src = ((uint64_t)zw::uni((uint32_t)(it.src >> 32)) << 32) | zw::uni((uint32_t)it.src);
@@ -488,13 +524,9 @@ __global__ void __launch_bounds__(256) unshuffle_kernel(const ChunkMeta* __restr
     const ChunkMeta m = meta[ci];
     const uint8_t* in = (const uint8_t*)m.tmp;
     uint8_t* out = (uint8_t*)m.dst;
-    if (m.mode == 2) {
-      shuffle_span<true>(in, out, m.nbytes, m.ts, threadIdx.x, blockDim.x);
-    } else {
-      for (uint64_t b0 = 0; b0 < m.nbytes; b0 += m.bs) {
-        const uint64_t bsz = m.nbytes - b0 < m.bs ? m.nbytes - b0 : m.bs;
-        shuffle_span<true>(in + b0, out + b0, bsz, m.ts, threadIdx.x, blockDim.x);
-      }
+    for (uint64_t b0 = 0; b0 < m.nbytes; b0 += m.bs) {
+      const uint64_t bsz = m.nbytes - b0 < m.bs ? m.nbytes - b0 : m.bs;
+      shuffle_span<true>(in + b0, out + b0, bsz, m.ts, threadIdx.x, blockDim.x);
     }
   }
 }
@@ -1163,15 +1195,17 @@ __global__ void bs_layout_kernel(const uint8_t* __restrict__ src, const hsds_chu
 struct hsds_engine {
   int device;
   int num_cus;
-  int inflate_blocks_per_cu;   // occupancy of inflate_kernel (LDS-bound)
+  int inflate_blocks_per_cu;   // occupancy of inflate2_kernel
   int lz_blocks_per_cu;        // occupancy of lz_kernel
   int bshuf_blocks_per_cu;     // occupancy of bshuf_kernel
   int zstd_blocks_per_cu;      // occupancy of zstd_kernel
   int lz4w_blocks_per_cu = 16; // occupancy of lz4_block_kernel (LZ4 / BloscLZ writer)
-  hz::Tune tune;
+  hz2::Tune tune;
   // workspace (grown on demand)
   uint8_t* ws = nullptr;
   size_t ws_bytes = 0;
+  uint8_t* rings = nullptr;    // inflate2 match rings, one per resident wave
+  size_t rings_bytes = 0;
   uint8_t* tmp = nullptr;
   size_t tmp_bytes = 0;
   // host staging for the single-chunk host API
@@ -1231,8 +1265,8 @@ int hsds_engine_create(int device, hsds_engine** out) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
   e->num_cus = prop.multiProcessorCount;
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, inflate_kernel, 64, 0) != hipSuccess || occ < 1)
-    occ = INFLATE_WAVES_PER_CU;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, inflate2_kernel, 64, 0) != hipSuccess || occ < 1)
+    occ = 8;
   // development override (A/B experiments): fewer resident inflate wavefronts per CU
   if (const char* ev = getenv("HSDS_INFLATE_WAVES")) {
     const int v = atoi(ev);
@@ -1258,19 +1292,15 @@ int hsds_engine_create(int device, hsds_engine** out) {
   e->parse_blocks_per_cu = o1;
   e->huff_blocks_per_cu = o2;
   e->emit_blocks_per_cu = o3;
-  e->tune.L0 = hz::LMAX;
-  // A/B on MI355X (tools/ab_tune.sh): warm-up 96 -> 384 bits and a fill target of
-  // 12/16 slots cut the repair rounds: F1 +8 %, F2 +21 % over (96, 11/16)
+  // warm-up 384 bits, segments sized to 1 + 1/16 of the previous block, 4 repair rounds
   e->tune.W = 384;
-  e->tune.adapt = 12;
-  e->tune.C = 192;
   e->tune.max_rounds = 4;
-  // development override (A/B experiments): "L0,W,adapt,C,rounds", validated like hsds_set_tuning
+  e->tune.over16 = 1;
+  // development override (A/B experiments): "W,rounds,over16"
   if (const char* ev = getenv("HSDS_INFLATE_TUNE")) {
-    unsigned l0, w, ad, c; int rd;
-    if (sscanf(ev, "%u,%u,%u,%u,%d", &l0, &w, &ad, &c, &rd) == 5 && l0 >= (unsigned)hz::LMIN &&
-        w <= (unsigned)hz::WMAX && c <= (unsigned)hz::CMAX && ad <= 16 && rd >= 0 && rd <= 64) {
-      e->tune.L0 = l0 < (unsigned)hz::LMAX ? l0 : (unsigned)hz::LMAX; e->tune.W = w; e->tune.adapt = ad; e->tune.C = c; e->tune.max_rounds = rd;
+    unsigned w, ov; int rd;
+    if (sscanf(ev, "%u,%d,%u", &w, &rd, &ov) == 3 && w <= 4096u && rd >= 0 && rd <= 64 && ov <= 16u) {
+      e->tune.W = w; e->tune.max_rounds = rd; e->tune.over16 = ov;
       fprintf(stderr, "hsds_amd: inflate tune override %s\n", ev);
     }
   }
@@ -1284,6 +1314,7 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (!e) return;
   hipSetDevice(e->device);
   if (e->ws) hipFree(e->ws);
+  if (e->rings) hipFree(e->rings);
   if (e->tmp) hipFree(e->tmp);
   if (e->h_dev_src) hipFree(e->h_dev_src);
   if (e->h_dev_dst) hipFree(e->h_dev_dst);
@@ -1296,13 +1327,12 @@ void hsds_engine_destroy(hsds_engine* e) {
   delete e;
 }
 
-int hsds_set_tuning(hsds_engine* e, uint32_t seg_bits, uint32_t warmup_bits, uint32_t cont_bits, int32_t rounds) {
+int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t unused, int32_t rounds) {
+  (void)unused;
   if (!e) return HSDS_ERR_ARG;
-  if (seg_bits < (uint32_t)hz::LMIN || seg_bits > (uint32_t)hz::LMAX) return HSDS_ERR_ARG;
-  if (warmup_bits > (uint32_t)hz::WMAX || cont_bits > (uint32_t)hz::CMAX || rounds < 0 || rounds > 64) return HSDS_ERR_ARG;
-  e->tune.L0 = seg_bits;
+  if (seg_over16 > 16u || warmup_bits > 4096u || rounds < 0 || rounds > 64) return HSDS_ERR_ARG;
+  e->tune.over16 = seg_over16;
   e->tune.W = warmup_bits;
-  e->tune.C = cont_bits;
   e->tune.max_rounds = rounds;
   return HSDS_OK;
 }
@@ -1332,52 +1362,54 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
     e->ev_valid = 1;
     return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
   }
-  // workspace layout
-  const size_t sz_slots = (size_t)nchunks * KSLOTS * sizeof(Item);
-  const size_t sz_counts = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
-  const size_t sz_offs = ((size_t)(nchunks + 1) * 4 + 255) & ~(size_t)255;
-  const size_t sz_meta = (size_t)nchunks * sizeof(ChunkMeta);
+  // workspace: the item pool (8 per chunk + 1 per 2 KiB of destination: any c-blosc frame
+  // fits, whatever its number of splits), chunk meta and the unshuffle list
+  const uint64_t cap64 = (uint64_t)nchunks * 8u + dst_extent / 2048u + 64u;
+  const uint32_t pool_cap = cap64 > 0xffffffffull ? 0xffffffffu : (uint32_t)cap64;
+  const size_t sz_pool = ((size_t)pool_cap * sizeof(Item) + 255) & ~(size_t)255;
+  const size_t sz_meta = ((size_t)nchunks * sizeof(ChunkMeta) + 255) & ~(size_t)255;
   const size_t sz_list = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
-  const size_t need = sz_slots + sz_counts + sz_offs + sz_meta + sz_list + 256;
+  const size_t need = sz_pool + sz_meta + sz_list + 256;
   if (grow((void**)&e->ws, &e->ws_bytes, need)) return HSDS_ERR_DEVICE;
   uint8_t* w = e->ws;
-  Item* slots = (Item*)w; w += sz_slots;
-  uint32_t* counts = (uint32_t*)w; w += sz_counts;
-  uint32_t* offs = (uint32_t*)w; w += sz_offs;
+  Item* pool = (Item*)w; w += sz_pool;
   ChunkMeta* meta = (ChunkMeta*)w; w += sz_meta;
   uint32_t* list = (uint32_t*)w; w += sz_list;
   // [0] inflate item counter, [1] meta list count, [2] inexact size, [3] LZ item counter,
-  // [4] LZ items, [5] other items, [6] zstd items, [7] zstd item counter
+  // [4] LZ items, [5] zlib + raw items, [6] zstd items, [7] zstd item counter, [8] pool fill
   uint32_t* ctr = (uint32_t*)w;
-  // staging for shuffled outputs (F2 chunks, Blosc typesize > 1): same offsets as
-  // the destination buffer, so it spans the destination extent
-  if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
-  if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  // staging for LZ / zstd Blosc frames with typesize > 1 (zlib and raw items land unshuffled
+  // through their output map): only batches of a non-zlib codec can have them
+  uint8_t* tmp = nullptr;
+  if (compressor == HSDS_COMP_OTHER) {
+    if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
+    tmp = e->tmp;
+  }
+  // one match ring per resident inflate wave
+  int64_t grid = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
+  if (grid > nchunks * 64) grid = nchunks * 64;
+  if (grid < 1) grid = 1;
+  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * hz2::RING_BYTES)) return HSDS_ERR_DEVICE;
+  if (hipMemsetAsync(ctr, 0, 64, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
   hipLaunchKernelGGL(frame_walk_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
-                     (uint8_t*)d_dst, e->tmp, slots, counts, meta, list, ctr + 1, ctr + 4, d_status, compressor,
-                     shuffle, itemsize, inexact);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
-  int64_t grid = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
-  if (grid > nchunks * 4) grid = nchunks * 4;
-  if (grid < 1) grid = 1;
+                     (uint8_t*)d_dst, tmp, pool, pool_cap, ctr + 8, meta, list, ctr + 1, ctr + 4, d_status,
+                     compressor, shuffle, itemsize, inexact);
   hipEventRecord(e->ev0, st);
-  hipLaunchKernelGGL(inflate_kernel, dim3((unsigned)grid), dim3(64), 0, st, slots, offs, nchunks, ctr, d_status,
-                     ctr + 2, ctr + 4, e->tune);
+  hipLaunchKernelGGL(inflate2_kernel, dim3((unsigned)grid), dim3(64), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
+                     ctr + 4, e->tune, e->rings);
   int64_t lgrid = (int64_t)e->num_cus * e->lz_blocks_per_cu;
-  if (lgrid > (nchunks * KSLOTS + lz::GROUP - 1) / lz::GROUP) lgrid = (nchunks * KSLOTS + lz::GROUP - 1) / lz::GROUP;
+  if (lgrid > (nchunks * 64 + lz::GROUP - 1) / lz::GROUP) lgrid = (nchunks * 64 + lz::GROUP - 1) / lz::GROUP;
   if (lgrid < 1) lgrid = 1;
-  hipLaunchKernelGGL(lz_kernel, dim3((unsigned)lgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 3, d_status,
-                     ctr + 4);
+  hipLaunchKernelGGL(lz_kernel, dim3((unsigned)lgrid), dim3(64), 0, st, pool, ctr + 8, ctr + 3, d_status, ctr + 4);
   int64_t zgrid = (int64_t)e->num_cus * e->zstd_blocks_per_cu;
   if (zgrid > nchunks * 16) zgrid = nchunks * 16;
   if (zgrid < 1) zgrid = 1;
-  hipLaunchKernelGGL(zstd_kernel, dim3((unsigned)zgrid), dim3(64), 0, st, slots, offs, nchunks, ctr + 7, d_status,
-                     ctr + 4);
+  hipLaunchKernelGGL(zstd_kernel, dim3((unsigned)zgrid), dim3(64), 0, st, pool, ctr + 8, ctr + 7, d_status, ctr + 4);
   hipEventRecord(e->ev1, st);
   e->ev_valid = 1;
-  hipLaunchKernelGGL(unshuffle_kernel, dim3(2048), dim3(256), 0, st, meta, list, ctr + 1, d_status);
+  if (tmp) hipLaunchKernelGGL(unshuffle_kernel, dim3(2048), dim3(256), 0, st, meta, list, ctr + 1, d_status);
   if (hipGetLastError() != hipSuccess) return HSDS_ERR_DEVICE;
   if (inexact_size) *inexact_size = ctr + 2;
   return HSDS_OK;

@@ -1,0 +1,868 @@
+// inflate2.h -- two-pass, long-segment zlib (RFC 1950/1951) decoder, one wavefront per stream.
+//
+// Replaces, for the HSDS data-node hot path, the zlib inflate that the reference reaches
+// through storUtil._uncompress (hsds/util/storUtil.py:209-220, CPython zlib.decompress) and
+// through c-blosc's zlib_wrap_decompress for every Blosc split (storUtil.py:195-208).  Output
+// is bit-identical to libz; corrupt / truncated streams and adler32 mismatches fail (the
+// reference's HTTPInternalServerError).
+//
+// Design (DESIGN.md "Inflate"): a Huffman block is cut into 64 segments of L bits, L sized
+// from the previous block so that one window covers the whole block (L is thousands of
+// bits, not hundreds).  Per window:
+//   A   lane i decodes from W bits before its segment (warm-up: Huffman codes
+//       self-synchronise) to the first token start at or past the next segment, recording
+//       its first K token starts with the output / match counts reached there;
+//   A'  lane i keeps decoding into segment i+1 until it lands on one of lane i+1's recorded
+//       starts ("sync": from there both decodes coincide) -- no token storage at all;
+//   R   a lane its predecessor never met is re-decoded from the predecessor's exit;
+//   P   wave prefix sums of the synced output / match counts give every lane its output
+//       offset and its slot in the wave's match ring;
+//   E   every valid lane decodes its exact range again: literal bytes go straight to their
+//       final address in dst, matches (pos, len, dist) to the match ring in HBM;
+//   M   the ring is resolved in batches of 64 matches: bytes a batch's match copies either
+//       lie before the batch (final) or inside an earlier match of the batch (one LDS owner
+//       map hop each), so all 64 lanes copy at once.
+// The output address of stream byte x goes through an optional byte-unshuffle permutation
+// (HDF5 shuffle of F2 chunks, Blosc typesize > 1 blocks), so unshuffle costs nothing extra.
+// adler32 is accumulated as per-lane (sum b, sum pos*b) pairs by the emit and resolve steps.
+//
+// SINGLE SOURCE for the HIP kernel and the CPU emulation (tests/emu/inflate2_emu.cpp), like
+// inflate_wave.h whose helpers (table build, LUT format, load_word) it reuses.
+#pragma once
+#include "inflate_wave.h"
+
+namespace hz2 {
+
+using hz::WAVE;
+using hz::LL_ROOT;
+using hz::D_ROOT;
+using hz::LL_SUB;
+using hz::D_SUB;
+using hz::ST_OK;
+using hz::ST_DATA;
+using hz::ST_TRUNC;
+using hz::ST_SIZE;
+using hz::T_EOB;
+using hz::T_ERR;
+using hz::T_MATCH;
+using hz::ADLER_MOD;
+
+#ifndef HZ2_K
+#define HZ2_K 16
+#endif
+constexpr int K = HZ2_K;                  // recorded token starts per lane
+constexpr uint32_t LMIN = 64;
+constexpr uint32_t LMAX = 1u << 16;       // segment bits (lane output stays well inside u32)
+constexpr uint32_t MCAP_LANE = 256;       // matches per lane per window (ring bound)
+constexpr uint32_t RING = MCAP_LANE * WAVE;   // match ring entries per wave
+constexpr uint32_t RING_BYTES = RING * 8u;
+constexpr uint32_t SPAN = 2048;           // resolve batch: output bytes covered by the source map
+constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
+static_assert(MPL == 4, "sel4 selects among four per-lane matches");
+constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
+#ifndef HZ2_RG
+#define HZ2_RG 8
+#endif
+constexpr uint32_t RG = HZ2_RG;           // resolve: source bytes a lane loads before it stores
+constexpr uint32_t SYNC_NONE = 0xfeu;     // predecessor ended (EOB / ERR / CUT): lane beyond the window
+constexpr uint32_t SYNC_FAIL = 0xffu;     // predecessor never met this lane's recorded path
+constexpr uint32_t END_NONE = 0, END_EOB = 1, END_ERR = 2, END_CUT = 3;
+
+// record: bits 0-10 token start relative to the segment, 11-23 output bytes, 24-28 matches
+// (cumulative from the lane's first record; K tokens of <= 48 bits / <= 258 bytes fit)
+HZ_HD uint32_t rec_pack(uint32_t rel, uint32_t o, uint32_t m) { return rel | (o << 11) | (m << 24); }
+HZ_HD uint32_t rec_rel(uint32_t r) { return r & 0x7ffu; }
+HZ_HD uint32_t rec_out(uint32_t r) { return (r >> 11) & 0x1fffu; }
+HZ_HD uint32_t rec_mat(uint32_t r) { return r >> 24; }
+
+struct Shared {
+  uint16_t lut_ll[(1 << LL_ROOT) + LL_SUB];
+  uint16_t lut_d[(1 << D_ROOT) + D_SUB];
+  uint16_t tb_first[16];
+  uint16_t tb_offs[17];
+  uint16_t tb_next[16];
+  union {
+    struct {                      // Huffman table build scratch (dead while windows run)
+      uint16_t sorted_ll[288];
+      uint16_t sorted_d[32];
+      uint16_t cnt_ll[16];
+      uint16_t cnt_d[16];
+      uint16_t cnt_cl[16];
+      uint16_t sorted_cl[20];
+      uint8_t lens[320 + 32];
+    };
+    uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
+    uint16_t smap[SPAN];          // phase M: batch byte -> distance to its source (0: literal)
+  };
+  uint32_t syncw[WAVE];           // record index where the predecessor met this lane / SYNC_*
+  uint32_t endp[WAVE];            // lane's exclusive end (token boundary)
+  uint32_t nrec[WAVE];
+  int32_t u_status;
+  uint32_t u_pos;
+  uint32_t u_nlen, u_ndist;
+};
+
+struct Tune {
+  uint32_t W;          // warm-up bits before a segment
+  int max_rounds;      // repair rounds per window
+  uint32_t over16;     // segment over-provisioning against the previous block size, in 16ths
+};
+
+// Output address map: stream byte x -> dst offset.  n == 1: x + x0.  Otherwise the HDF5 /
+// Blosc byte unshuffle of a span of N elements of n bytes (`body` = N * n; tail bytes stay),
+// evaluated at X = x0 + x (x0 places a Blosc plane split inside its block).
+struct Perm {
+  uint32_t n, N, body, magic, x0;
+};
+
+HZ_HD uint32_t umulhi32(uint32_t a, uint32_t b) {
+#if HZ_GPU
+  return __umulhi(a, b);
+#else
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+HZ_HD uint32_t perm_at(const Perm& p, uint32_t x) {
+  const uint32_t X = x + p.x0;
+  if (p.n == 1u || X >= p.body) return X;
+  uint32_t q = umulhi32(X, p.magic);     // X / N or one more
+  uint32_t r = X - q * p.N;
+  if ((int32_t)r < 0) { q--; r += p.N; }
+  return r * p.n + q;
+}
+
+HZ_HD Perm perm_make(uint32_t n, uint32_t N, uint32_t x0) {
+  Perm p;
+  p.n = n < 1u ? 1u : n;
+  p.N = N < 1u ? 1u : N;
+  p.body = p.n == 1u ? 0u : p.N * p.n;
+  p.magic = p.N <= 1u ? 0xffffffffu : (uint32_t)(((1ull << 32) + p.N - 1u) / p.N);
+  p.x0 = x0;
+  return p;
+}
+
+// ---- bit reader straight from the stream in global memory --------------------------------
+// Words move through a 4-word shift register q (q0 next) refilled from the quad f, which was
+// loaded when the previous quad became current: a quad load has a whole quad of tokens
+// (~10) to arrive before the rotation that consumes it, and loads are unconditional (the
+// address is clamped to the stream's last quad) so the load writes f directly.  bb holds
+// `avail` (>= 32 after a fill) bits from bit position `pos` (relative to the 16-byte aligned
+// stream base).  Bits past the stream end are whatever the clamped loads return: the decode
+// of the true path never reads them (a token reaching past the end ends the window beyond
+// limit_bits, which fails as truncated); speculative lanes may.
+struct GRd {
+  uint64_t bb;
+  uint32_t avail;
+  uint32_t pos;
+  uint32_t qa;         // dword index of the quad after q (= the quad in f)
+  uint32_t qn;         // words left in q
+  uint32_t q0, q1, q2, q3;
+  uint32_t f0, f1, f2, f3;
+};
+
+struct Src {
+  hz_gcu8* base;       // 16-byte aligned base
+  uint32_t lo, hi;     // valid byte range relative to base
+  uint32_t last;       // dword index of the last quad holding stream bytes
+};
+
+HZ_HD uint32_t gword(const Src& s, uint32_t k) { return hz::load_word(s.base, k, s.lo, s.hi); }
+
+// quad qa (clamped to the stream's last quad: an aligned 16-byte block holding a stream
+// byte never crosses a page, so the load is always safe)
+HZ_HD void g_quad(const Src& s, uint32_t qa, uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3) {
+  const uint32_t b0 = (qa < s.last ? qa : s.last) * 4u;
+#if HZ_GPU
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+  const u32x4 v = *(gu32x4*)(s.base + b0);
+  a0 = v.x; a1 = v.y; a2 = v.z; a3 = v.w;
+#else
+  uint8_t t[16] = {0};
+  for (uint32_t i = 0; i < 16u && b0 + i < s.hi; i++) t[i] = s.base[b0 + i];
+  memcpy(&a0, t, 4); memcpy(&a1, t + 4, 4); memcpy(&a2, t + 8, 4); memcpy(&a3, t + 12, 4);
+#endif
+}
+
+HZ_HD uint32_t g_take(const Src& s, GRd& r) {
+  const uint32_t w = r.q0;
+  r.q0 = r.q1; r.q1 = r.q2; r.q2 = r.q3;
+  if (--r.qn == 0u) {
+    r.q0 = r.f0; r.q1 = r.f1; r.q2 = r.f2; r.q3 = r.f3;
+    r.qn = 4u;
+    r.qa += 4u;
+    g_quad(s, r.qa, r.f0, r.f1, r.f2, r.f3);
+  }
+  return w;
+}
+
+HZ_HD void g_init(const Src& s, GRd& r, uint32_t p) {
+  const uint32_t k = p >> 5, qa = k & ~3u, qi = k & 3u;
+  uint32_t a0, a1, a2, a3;
+  g_quad(s, qa, a0, a1, a2, a3);
+  // shift register starts at word qi of the quad
+  r.q0 = qi == 0u ? a0 : qi == 1u ? a1 : qi == 2u ? a2 : a3;
+  r.q1 = qi == 0u ? a1 : qi == 1u ? a2 : a3;
+  r.q2 = qi == 0u ? a2 : a3;
+  r.q3 = a3;
+  r.qn = 4u - qi;
+  r.qa = qa + 4u;
+  g_quad(s, r.qa, r.f0, r.f1, r.f2, r.f3);
+  const uint32_t sh = p & 31u;
+  const uint32_t w0 = g_take(s, r);
+  const uint32_t w1 = g_take(s, r);
+  r.bb = (((uint64_t)w1 << 32) | w0) >> sh;
+  r.avail = 64u - sh;
+  r.pos = p;
+}
+
+HZ_HD void g_fill(const Src& s, GRd& r) {
+  if (r.avail < 32u) {
+    r.bb |= (uint64_t)g_take(s, r) << r.avail;
+    r.avail += 32u;
+  }
+}
+
+HZ_HD void g_drop(GRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n; }
+
+HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
+  uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
+  if (!(e & 15u)) e = sh->lut_ll[(1u << LL_ROOT) + ((e >> 4) & 511u) + ((uint32_t)(bits >> LL_ROOT) & hz::bmask(e >> 13))];
+  return e;
+}
+HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
+  uint32_t e = sh->lut_d[bits & ((1u << D_ROOT) - 1)];
+  if (!(e & 15u)) e = sh->lut_d[(1u << D_ROOT) + ((e >> 4) & 511u) + ((uint32_t)(bits >> D_ROOT) & hz::bmask(e >> 13))];
+  return e;
+}
+
+// one token at r.pos (hz::next_token over the global reader): literal byte, T_EOB, T_ERR, or
+// T_MATCH | len << 16 | (dist - 1).  Invalid codes advance by their table length.
+HZ_HD uint32_t next_token(const Shared* sh, const Src& s, GRd& r) {
+  g_fill(s, r);
+  const uint32_t e = lookup_ll(sh, r.bb);
+  const uint32_t nb = e & 15u, p = e >> 4;
+  const uint32_t q = p - 257u;
+  const int islen = q < 29u;
+  const uint32_t xb = (islen && q >= 8u && q < 28u) ? (q - 4u) >> 2 : 0u;
+  const uint32_t base = q < 8u ? q + 3u : q == 28u ? 258u : ((4u | (q & 3u)) << xb) + 3u;
+  const uint32_t len = base + ((uint32_t)(r.bb >> nb) & hz::bmask(xb));
+  g_drop(r, nb + xb);
+  uint32_t tok = p <= 256u ? p : T_ERR;
+  if (islen) {
+    g_fill(s, r);
+    const uint32_t ed = lookup_d(sh, r.bb);
+    const uint32_t nd = ed & 15u, d = ed >> 4;
+    const int ok = d < 30u;
+    const uint32_t xd = (ok && d >= 2u) ? (d - 2u) >> 1 : 0u;
+    const uint32_t dist = (d < 4u ? d + 1u : ((2u | (d & 1u)) << xd) + 1u) + ((uint32_t)(r.bb >> nd) & hz::bmask(xd));
+    g_drop(r, ok ? nd + xd : nd);
+    tok = ok ? (T_MATCH | (len << 16) | (dist - 1u)) : T_ERR;
+  }
+  return tok;
+}
+
+// a[u] for a register array and a runtime u < MPL (no dynamic register indexing)
+HZ_HD uint32_t sel4(const uint32_t* a, uint32_t u) { return u == 0u ? a[0] : u == 1u ? a[1] : u == 2u ? a[2] : a[3]; }
+
+HZ_HD uint32_t tok_len(uint32_t t) { return (t & T_MATCH) ? ((t >> 16) & 0x1ffu) : 1u; }
+
+struct Job {
+  const uint8_t* src;   // stream bytes (any alignment)
+  uint32_t src_len;
+  uint8_t* dst;         // base of the permuted output span
+  uint32_t dst_len;     // expected stream output (exact) or capacity (exact == 0)
+  uint32_t exact;
+  uint32_t* out_len;    // optional decoded length
+  Perm perm;
+};
+
+struct Stats {
+  uint64_t windows, blocks, stored, tokens, matches, lanes_valid, repairs, repair_lanes, cuts, batches, hops;
+  uint64_t steps_a, steps_e, extra_windows;
+};
+
+}  // namespace hz2
+
+#if HZ_GPU
+namespace hz2 {
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wave_excl_scan(v, (int)threadIdx.x); }
+}  // namespace hz2
+// value of lane-variable v in lane i (uniform i); LANE_ARR: a per-lane array
+#define LV_AT(v, i) ((uint32_t)__shfl((int)(v), (int)(i), 64))
+#define LANE_ARR(T, name, n) T name[n]
+#define LVA_AT(arr, u, i) ((uint32_t)__shfl((int)hz2::sel4(arr, u), (int)(i), 64))
+#else
+#define LV_AT(v, i) ((v)[i])
+#define LANE_ARR(T, name, n) T name[64][n]
+#define LVA_AT(arr, u, i) ((arr)[i][u])
+#endif
+
+namespace hz2 {
+
+template <class StatsT>
+#if HZ_GPU
+__device__ __forceinline__
+#else
+static
+#endif
+int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_base, StatsT* stats, HzProf* prof = nullptr) {
+  (void)prof;
+  const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 15u);
+  const Src S = {HZ_GLOBAL(hz_gcu8*, job.src - a), a, a + job.src_len, ((a + job.src_len - 1u) >> 2) & ~3u};
+  const uint32_t limit_bits = S.hi * 8u;
+  const uint32_t dst_len = job.dst_len;
+  hz_gu8* const dst = HZ_GLOBAL(hz_gu8*, job.dst);
+  hz_gu32* const ring = HZ_GLOBAL(hz_gu32*, ring_base);
+  const Perm P = job.perm;
+
+  LANE_VAR(uint32_t, s1);     // adler32 partial sums of the bytes this lane wrote: sum b, sum pos*b
+  LANE_VAR(uint32_t, s2);
+  LANE_LOOP { LV(s1) = 0; LV(s2) = 0; }
+
+  // ---- zlib header (RFC 1950) ----
+  if (job.src_len < 2) return ST_TRUNC;
+  {
+    GRd r;
+    g_init(S, r, S.lo * 8u);
+    const uint64_t two = r.bb;
+    const uint32_t cmf = (uint32_t)(two & 0xffu), flg = (uint32_t)((two >> 8) & 0xffu);
+    if ((cmf & 0x0f) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0) return ST_DATA;
+    if (flg & 0x20) return ST_DATA;   // preset dictionary: Z_NEED_DICT
+  }
+  uint32_t pos = S.lo * 8u + 16u;
+  uint32_t out = 0;
+  uint32_t prev_block_bits = 0;
+
+  for (;;) {  // ---- deflate blocks ----
+    HZ_T(1);
+    if (pos + 3u > limit_bits) return ST_TRUNC;
+    uint32_t h3;
+    {
+      GRd r;
+      g_init(S, r, pos);
+      h3 = (uint32_t)(r.bb & 7u);
+    }
+    const uint32_t block_start = pos;
+    pos += 3;
+    const uint32_t bfinal = h3 & 1u, btype = h3 >> 1;
+    if (stats) stats->blocks++;
+    if (btype == 3) return ST_DATA;
+    if (btype == 0) {
+      // ---- stored block: copied through the output map ----
+      pos = (pos + 7u) & ~7u;
+      if (pos + 32u > limit_bits) return ST_TRUNC;
+      GRd r;
+      g_init(S, r, pos);
+      const uint32_t ln = (uint32_t)(r.bb & 0xffffffffu);
+      const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
+      if ((len ^ 0xffffu) != nlen) return ST_DATA;
+      pos += 32u;
+      if (pos + len * 8u > limit_bits) return ST_TRUNC;
+      if (out + len > dst_len) return ST_SIZE;
+      const uint32_t sb = pos >> 3;
+      LANE_LOOP {
+        uint32_t a1 = LV(s1), a2 = LV(s2);
+        for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
+          const uint32_t b = S.base[sb + i];
+          dst[perm_at(P, out + i)] = (uint8_t)b;
+          a1 += b;
+          a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
+        }
+        LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
+      }
+      out += len;
+      pos += len * 8u;
+      if (stats) stats->stored++;
+      WAVE_SYNC_GLOBAL();
+      if (bfinal) break;
+      continue;
+    }
+    // ---- Huffman code lengths ----
+    uint32_t nlen = 288, ndist = 32;
+    if (btype == 1) {
+      LANE_LOOP {
+        for (int q = lane; q < 320; q += 64) sh.lens[q] = q >= 288 ? 5 : q < 144 ? 8 : q < 256 ? 9 : q < 280 ? 7 : 8;
+      }
+      WAVE_SYNC();
+    } else {
+      // dynamic header (RFC 1951 3.2.7), decoded serially by lane 0
+      LANE_LOOP {
+        if (lane == 0) {
+          int st = ST_OK;
+          GRd r;
+          g_init(S, r, pos);
+          g_fill(S, r);
+          const uint32_t hlit = (uint32_t)(r.bb & 31u) + 257u, hdist = (uint32_t)((r.bb >> 5) & 31u) + 1u;
+          const uint32_t hclen = (uint32_t)((r.bb >> 10) & 15u) + 4u;
+          g_drop(r, 14);
+          if (hlit > 286 || hdist > 30) st = ST_DATA;
+          uint16_t* cl = sh.sorted_cl;
+          for (int i = 0; i < 19; i++) cl[i] = 0;
+          for (uint32_t i = 0; i < hclen; i++) {
+            g_fill(S, r);
+            cl[hz::cl_order(i)] = (uint16_t)(r.bb & 7u);
+            g_drop(r, 3);
+          }
+          uint16_t* cnt = sh.cnt_cl;
+          for (int l = 0; l < 16; l++) cnt[l] = 0;
+          for (int i = 0; i < 19; i++) cnt[cl[i]]++;
+          cnt[0] = 0;
+          int left = 1, maxl = 0;
+          for (int l = 1; l <= 7; l++) {
+            left <<= 1; left -= cnt[l];
+            if (cnt[l]) maxl = l;
+            if (left < 0) st = ST_DATA;
+          }
+          if (left > 0 || maxl == 0) st = ST_DATA;   // code-length code must be complete
+          uint16_t* clut = sh.lut_d;                   // 7-bit LUT (sym | len << 8), rebuilt below
+          if (st == ST_OK) {
+            uint16_t* next = sh.tb_next;                 // next code per length (LDS: no scratch)
+            uint32_t code = 0;
+            for (int l = 1; l <= 7; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; next[l] = (uint16_t)code; }
+            for (int i = 0; i < 19; i++) {
+              const uint32_t l = cl[i];
+              if (!l) continue;
+              const uint32_t rc = hz::rev_bits(next[l]++, (int)l);
+              for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint16_t)(i | (l << 8));
+            }
+          }
+          const uint32_t total = hlit + hdist;
+          uint32_t n = 0;
+          while (st == ST_OK && n < total) {
+            if (r.pos > limit_bits + 64u) { st = ST_TRUNC; break; }
+            g_fill(S, r);
+            const uint32_t e = clut[r.bb & 127u];
+            const uint32_t sym = e & 0xffu, l = e >> 8;
+            g_drop(r, l);
+            if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
+            uint32_t rep, val = 0;
+            if (sym == 16) {
+              if (n == 0) { st = ST_DATA; break; }
+              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(r.bb & 3u); g_drop(r, 2);
+            } else if (sym == 17) { rep = 3 + (uint32_t)(r.bb & 7u); g_drop(r, 3); }
+            else { rep = 11 + (uint32_t)(r.bb & 127u); g_drop(r, 7); }
+            if (n + rep > total) { st = ST_DATA; break; }
+            for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
+          }
+          if (st == ST_OK && r.pos > limit_bits) st = ST_TRUNC;
+          if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;   // missing end-of-block code
+          if (st == ST_OK) {
+            for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
+            for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
+            for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
+          }
+          sh.u_status = st;
+          sh.u_pos = r.pos;
+          sh.u_nlen = hlit;
+          sh.u_ndist = hdist;
+        }
+      }
+      WAVE_SYNC();
+      const int hst = sh.u_status;
+      if (hst != ST_OK) return hst;
+      pos = sh.u_pos;
+      nlen = sh.u_nlen;
+      ndist = sh.u_ndist;
+    }
+    HZ_T(2);
+    {
+      int bst = ST_OK;
+      hz::TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB};
+      HZ_BUILD_TABLE(sh, tll, bst);
+      if (bst != ST_OK) return bst;
+      hz::TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB};
+      HZ_BUILD_TABLE(sh, td, bst);
+      if (bst != ST_OK) return bst;
+    }
+    WAVE_SYNC();
+
+    // ---- windows over the Huffman block ----
+    // expected block size: the previous block's (zlib closes blocks at a fixed symbol count),
+    // else up to 200 kbit; over-provisioned so that one window usually reaches the EOB
+    uint32_t est = prev_block_bits ? prev_block_bits : 200000u;
+    {
+      const uint32_t rem = limit_bits > pos ? limit_bits - pos : 0u;
+      if (est > rem + 64u) est = rem + 64u;
+    }
+    est += (uint32_t)(((uint64_t)est * tune.over16) >> 4);
+    int first_window = 1;
+    for (;;) {
+      if (stats) { stats->windows++; if (!first_window) stats->extra_windows++; }
+      const uint32_t ws = pos;
+      uint32_t L = (est + 63u) >> 6;
+      L = L < LMIN ? LMIN : L > LMAX ? LMAX : L;
+      const uint32_t W = tune.W;
+
+      HZ_T(3);
+      // -------- phase A: warm-up + own segment, first K token starts recorded --------
+      LANE_VAR(GRd, rd);
+      LANE_VAR(uint32_t, co);      // output bytes since the first record
+      LANE_VAR(uint32_t, cm);      // matches since the first record
+      LANE_VAR(uint32_t, ek);      // END_*
+      LANE_VAR(uint32_t, ea);      // position after the EOB token
+      LANE_LOOP {
+        const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
+        const uint32_t p0 = (lane > 0 && ss - ws > W) ? ss - W : ws;
+        GRd r;
+        g_init(S, r, p0);
+        uint32_t steps = 0;
+        while (r.pos < ss) { (void)next_token(&sh, S, r); steps++; }
+        uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0;
+        while (r.pos < se) {
+          if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
+          const uint32_t tp = r.pos;
+          const uint32_t t = next_token(&sh, S, r);
+          steps++;
+          if (t == T_EOB || t == T_ERR) { e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; break; }
+          if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
+          o += tok_len(t);
+          m += (t & T_MATCH) ? 1u : 0u;
+        }
+        sh.nrec[lane] = nr;
+        sh.syncw[lane] = lane == 0 ? 0u : SYNC_NONE;
+        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;
+        if (stats) stats->steps_a += steps;
+      }
+      WAVE_SYNC();
+
+      HZ_T(4);
+      // -------- phase A': continuation until lane+1's recorded path is met --------
+      // (a lane that ended leaves its successor at SYNC_NONE)
+#define HZ2_CONTINUE(lane_)                                                                      \
+      do {                                                                                       \
+        GRd r = LV(rd);                                                                          \
+        uint32_t o = LV(co), m = LV(cm), e = LV(ek), after = LV(ea);                             \
+        uint32_t res = SYNC_NONE;                                                                \
+        if (e == END_NONE && (lane_) < 63) {                                                     \
+          const uint32_t base = ws + (uint32_t)((lane_) + 1) * L;                                \
+          const uint32_t nrn = sh.nrec[(lane_) + 1];                                             \
+          uint32_t k = 0;                                                                        \
+          res = SYNC_FAIL;                                                                       \
+          for (;;) {                                                                             \
+            const uint32_t rel = r.pos - base;                                                   \
+            while (k < nrn && hz2::rec_rel(sh.rec[k][(lane_) + 1]) < rel) k++;                   \
+            if (k >= nrn) break;                                                                 \
+            if (hz2::rec_rel(sh.rec[k][(lane_) + 1]) == rel) { res = k; break; }                 \
+            const uint32_t tp = r.pos;                                                           \
+            const uint32_t t = hz2::next_token(&sh, S, r);                                       \
+            if (t == T_EOB || t == T_ERR) {                                                      \
+              e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; res = SYNC_NONE; break; \
+            }                                                                                    \
+            if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; res = SYNC_NONE; break; } \
+            o += hz2::tok_len(t);                                                                \
+            m += (t & T_MATCH) ? 1u : 0u;                                                        \
+          }                                                                                      \
+        }                                                                                        \
+        if ((lane_) < 63) sh.syncw[(lane_) + 1] = res;                                           \
+        sh.endp[lane_] = r.pos;                                                                  \
+        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;                          \
+      } while (0)
+      LANE_LOOP { HZ2_CONTINUE(lane); }
+      WAVE_SYNC();
+
+      HZ_T(5);
+      // -------- repair rounds --------
+      // a lane whose predecessor exists but never met its path re-runs A + A' from the
+      // predecessor's exit (a token boundary), recording its new path; its successor's sync
+      // is recomputed.  Adjacent lanes are never redone in the same round.
+      for (int round = 0; round < tune.max_rounds; round++) {
+        const uint64_t redo_m = WAVE_BALLOT(lane > 0 && sh.syncw[lane] == SYNC_FAIL && sh.syncw[lane - 1] < (uint32_t)K);
+        if (!redo_m) break;
+        if (stats) { stats->repairs++; stats->repair_lanes += hz::popc64(redo_m); }
+        LANE_LOOP {
+          if ((redo_m >> lane) & 1ull) {
+            const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
+            GRd r;
+            g_init(S, r, sh.endp[lane - 1]);
+            uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0;
+            while (r.pos < se || nr == 0) {
+              if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
+              const uint32_t tp = r.pos;
+              const uint32_t t = next_token(&sh, S, r);
+              if (t == T_EOB || t == T_ERR) { e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; break; }
+              if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
+              o += tok_len(t);
+              m += (t & T_MATCH) ? 1u : 0u;
+            }
+            sh.nrec[lane] = nr;
+            sh.syncw[lane] = 0;                       // its path starts at record 0
+            LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;
+          }
+        }
+        WAVE_SYNC();
+        LANE_LOOP {
+          if ((redo_m >> lane) & 1ull) HZ2_CONTINUE(lane);
+        }
+        WAVE_SYNC();
+      }
+#undef HZ2_CONTINUE
+
+      HZ_T(6);
+      // -------- validity, window end, prefix sums --------
+      // lane i is valid when every lane before it is and lane i-1 met its path
+      uint32_t V = 1;
+      {
+        const uint64_t okm = WAVE_BALLOT(lane == 0 || sh.syncw[lane] < (uint32_t)K);
+        while (V < 64u && ((okm >> V) & 1ull)) V++;
+      }
+      LANE_VAR(uint32_t, wout);
+      LANE_VAR(uint32_t, wmat);
+      LANE_VAR(uint32_t, sbit);    // exact start bit of the lane's range
+      LANE_LOOP {
+        uint32_t wo = 0, wm = 0, sb = 0;
+        if ((uint32_t)lane < V) {
+          const uint32_t k = sh.syncw[lane];
+          const uint32_t rc = sh.rec[k][lane];
+          wo = LV(co) - rec_out(rc);
+          wm = LV(cm) - rec_mat(rc);
+          sb = ws + (uint32_t)lane * L + rec_rel(rc);
+        }
+        LV(wout) = wo; LV(wmat) = wm; LV(sbit) = sb;
+      }
+      // the first valid lane that ended (EOB / ERR / CUT) closes the window
+      int end_lane = -1;
+      {
+        const uint64_t em = WAVE_BALLOT((uint32_t)lane < V && LV(ek) != END_NONE);
+        if (em) end_lane = (int)__builtin_ctzll(em);
+      }
+      if (end_lane >= 0) V = (uint32_t)end_lane + 1u;
+      if (stats) stats->lanes_valid += V;
+      uint32_t end_kind = END_NONE, npos = 0;
+      LANE_LOOP {
+        if ((uint32_t)lane >= V) { LV(wout) = 0; LV(wmat) = 0; }
+        if (lane == (end_lane >= 0 ? end_lane : (int)V - 1)) {
+          sh.u_status = (int32_t)LV(ek);
+          sh.u_pos = LV(ek) == END_EOB ? LV(ea) : sh.endp[lane];
+          sh.u_nlen = sh.endp[lane];
+        }
+      }
+      WAVE_SYNC();
+      end_kind = (uint32_t)sh.u_status;
+      npos = sh.u_pos;
+      if (end_kind == END_ERR) {
+        // the first invalid code on the true path: a stream that ran out of input is
+        // truncated, anything else is corrupt
+        return sh.u_nlen + 64u > limit_bits ? ST_TRUNC : ST_DATA;
+      }
+      LANE_VAR(uint32_t, obase);
+      LANE_VAR(uint32_t, mbase);
+      uint32_t wtotal = 0, mtotal = 0;
+#if HZ_GPU
+      obase = wave_excl_scan32(wout);
+      mbase = wave_excl_scan32(wmat);
+      wtotal = hz::wave_sum(wout);
+      mtotal = hz::wave_sum(wmat);
+#else
+      for (int lane = 0; lane < 64; lane++) { obase[lane] = wtotal; mbase[lane] = mtotal; wtotal += wout[lane]; mtotal += wmat[lane]; }
+#endif
+      if (stats) stats->matches += mtotal;
+      if (out + wtotal > dst_len) return ST_SIZE;
+      if (npos > limit_bits) return ST_TRUNC;
+
+      HZ_T(7);
+      // -------- phase E: exact decode of every valid range; literals to dst, matches to the ring --------
+      LANE_VAR(int, lerr);
+      LANE_LOOP {
+        int err = 0;
+        uint32_t steps = 0;
+        if ((uint32_t)lane < V) {
+          GRd r;
+          g_init(S, r, LV(sbit));
+          const uint32_t stop = sh.endp[lane];
+          uint32_t o = out + LV(obase), mi = LV(mbase);
+          uint32_t a1 = 0;
+          uint64_t a2 = 0;
+          while (r.pos < stop) {
+            const uint32_t t = next_token(&sh, S, r);
+            steps++;
+            if (!(t & T_MATCH)) {
+              dst[perm_at(P, o)] = (uint8_t)t;
+              a1 += t;
+              a2 += (uint64_t)o * t;
+              o++;
+            } else {
+              const uint32_t ln = (t >> 16) & 0x1ffu, d = (t & 0x7fffu) + 1u;
+              if (d > o) { err = 1; break; }
+              ring[2u * mi] = o;
+              ring[2u * mi + 1u] = (ln << 16) | (d - 1u);
+              mi++;
+              o += ln;
+            }
+          }
+          LV(s1) = (LV(s1) + a1 % ADLER_MOD) % ADLER_MOD;
+          LV(s2) = (uint32_t)((LV(s2) + a2 % ADLER_MOD) % ADLER_MOD);
+        }
+        LV(lerr) = err;
+        if (stats) stats->steps_e += steps;
+      }
+      if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
+      WAVE_SYNC_GLOBAL();
+
+      HZ_T(8);
+      // -------- phase M: resolve the window's matches, 64 at a time --------
+      // match bytes' adler sums: a1 < 2^32 and a2 < 2^64 for any window (< 2^24 bytes)
+      LANE_VAR(uint32_t, ra1);
+      LANE_VAR(uint64_t, ra2);
+      LANE_LOOP { LV(ra1) = 0; LV(ra2) = 0; }
+      // batch = the next <= 256 matches whose output span [F, F + span) fits the source map;
+      // lane l holds matches b0 + l + 64 u (u < MPL: coalesced record loads); the next
+      // batch's records are loaded while this one resolves.
+      //   1. every match byte x gets smap[x - F] = distance to its source (periodic
+      //      extension of an overlapping copy), literal bytes 0;
+      //   2. all lanes walk the span byte-strided, follow smap while the source is inside
+      //      the batch and not a literal, load the byte (before the batch: final; a literal:
+      //      written by E) and store it.
+      LANE_ARR(uint32_t, ro, MPL);
+      LANE_ARR(uint32_t, rw, MPL);
+      LANE_LOOP {
+HZ_UNROLL
+        for (uint32_t u = 0; u < MPL; u++) {
+          const uint32_t j = (uint32_t)lane + 64u * u;
+          LV(ro)[u] = j < mtotal ? ring[2u * j] : 0xffffffffu;
+          LV(rw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
+        }
+      }
+      for (uint32_t b0 = 0; b0 < mtotal;) {
+        if (stats) stats->batches++;
+        const uint32_t F = LVA_AT(ro, 0, 0);
+        uint32_t nb = 0, open_ = 1;
+HZ_UNROLL
+        for (uint32_t u = 0; u < MPL; u++) {
+          const uint64_t fit = WAVE_BALLOT(LV(ro)[u] != 0xffffffffu && LV(ro)[u] + (LV(rw)[u] >> 16) - F <= SPAN);
+          const uint32_t k = ~fit ? (uint32_t)__builtin_ctzll(~fit) : 64u;   // leading fitting matches
+          nb += open_ ? k : 0u;
+          open_ = open_ && k == 64u;
+        }
+        const uint32_t last_o = LVA_AT(ro, (nb - 1u) >> 6, (nb - 1u) & 63u);
+        const uint32_t last_w = LVA_AT(rw, (nb - 1u) >> 6, (nb - 1u) & 63u);
+        const uint32_t span = last_o + (last_w >> 16) - F;
+        LANE_LOOP {
+          for (uint32_t q = (uint32_t)lane * 2u; q < span; q += 128u) *(uint32_t*)&sh.smap[q] = 0u;
+        }
+        WAVE_SYNC();
+        LANE_LOOP {
+HZ_UNROLL
+          for (uint32_t u = 0; u < MPL; u++) {
+            if ((uint32_t)lane + 64u * u < nb) {
+              const uint32_t o0 = LV(ro)[u] - F, ln = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
+              // byte t copies o - d + (t mod d): distance d + d * floor(t / d)
+              uint32_t dist = d, jj = 0;
+              for (uint32_t t = 0; t < ln; t++) {
+                sh.smap[o0 + t] = (uint16_t)dist;
+                if (++jj == d) { jj = 0; dist += d; }
+              }
+            }
+          }
+        }
+        WAVE_SYNC();
+        // prefetch the next batch's records
+        LANE_ARR(uint32_t, no, MPL);
+        LANE_ARR(uint32_t, nw, MPL);
+        LANE_LOOP {
+HZ_UNROLL
+          for (uint32_t u = 0; u < MPL; u++) {
+            const uint32_t j = b0 + nb + (uint32_t)lane + 64u * u;
+            LV(no)[u] = j < mtotal ? ring[2u * j] : 0xffffffffu;
+            LV(nw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
+          }
+        }
+        LANE_LOOP {
+          uint32_t a1 = LV(ra1);
+          uint64_t a2 = LV(ra2);
+          for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
+            uint32_t src[RG];
+HZ_UNROLL
+            for (uint32_t i = 0; i < RG; i++) {
+              const uint32_t q = h0 + (uint32_t)lane + 64u * i;
+              uint32_t y = 0xffffffffu;
+              if (q < span) {
+                const uint32_t dq = sh.smap[q];
+                if (dq) {
+                  y = F + q - dq;
+                  uint32_t hops = 0;
+                  while (y >= F) {            // inside the batch: follow an earlier match byte
+                    const uint32_t d2 = sh.smap[y - F];
+                    if (!d2) break;
+                    y -= d2;
+                    hops++;
+                  }
+                  if (stats) stats->hops += hops;
+                }
+              }
+              src[i] = y;
+            }
+            uint32_t bv[RG];
+HZ_UNROLL
+            for (uint32_t i = 0; i < RG; i++) bv[i] = src[i] != 0xffffffffu ? (uint32_t)dst[perm_at(P, src[i])] : 0u;
+HZ_UNROLL
+            for (uint32_t i = 0; i < RG; i++) {
+              if (src[i] != 0xffffffffu) {
+                const uint32_t x = F + h0 + (uint32_t)lane + 64u * i;
+                dst[perm_at(P, x)] = (uint8_t)bv[i];
+                a1 += bv[i];
+                a2 += (uint64_t)x * bv[i];
+              }
+            }
+          }
+          LV(ra1) = a1;
+          LV(ra2) = a2;
+        }
+        WAVE_SYNC_GLOBAL();
+        LANE_LOOP {
+HZ_UNROLL
+          for (uint32_t u = 0; u < MPL; u++) { LV(ro)[u] = LV(no)[u]; LV(rw)[u] = LV(nw)[u]; }
+        }
+        b0 += nb;
+      }
+      LANE_LOOP {
+        LV(s1) = (LV(s1) + LV(ra1) % ADLER_MOD) % ADLER_MOD;
+        LV(s2) = (uint32_t)((LV(s2) + LV(ra2) % ADLER_MOD) % ADLER_MOD);
+      }
+
+      HZ_T(10);
+      out += wtotal;
+      pos = npos;
+      first_window = 0;
+      if (end_kind == END_EOB) break;
+      // the block goes on: the rest is estimated from what is left of the estimate
+      const uint32_t used = npos - ws;
+      est = est > used ? est - used : 0u;
+      const uint32_t floor_est = ((npos - block_start) >> 3) + 64u * LMIN;
+      est = est < floor_est ? floor_est : est;
+      {
+        const uint32_t rem = limit_bits > pos ? limit_bits - pos : 0u;
+        if (est > rem + 64u) est = rem + 64u;
+      }
+    }
+    prev_block_bits = pos - block_start;
+    if (bfinal) break;
+  }
+  // ---- trailer: adler32 (big-endian) after byte alignment ----
+  HZ_T(9);
+  pos = (pos + 7u) & ~7u;
+  if (pos + 32u > limit_bits) return ST_TRUNC;
+  uint32_t t32;
+  {
+    GRd r;
+    g_init(S, r, pos);
+    t32 = (uint32_t)(r.bb & 0xffffffffu);
+  }
+  const uint32_t want = (t32 >> 24) | ((t32 >> 8) & 0xff00u) | ((t32 << 8) & 0xff0000u) | (t32 << 24);
+  uint64_t S1 = 0, S2 = 0;
+#if HZ_GPU
+  S1 = hz::wave_sum64((uint64_t)s1);
+  S2 = hz::wave_sum64((uint64_t)s2);
+#else
+  for (int lane = 0; lane < 64; lane++) { S1 += s1[lane]; S2 += s2[lane]; }
+#endif
+  const uint32_t A = (uint32_t)((1u + S1) % ADLER_MOD);
+  const uint32_t B = (uint32_t)(((uint64_t)(out % ADLER_MOD) * A + ADLER_MOD - (S2 % ADLER_MOD)) % ADLER_MOD);
+  if (((B << 16) | A) != want) return ST_DATA;
+  if (job.exact && out != dst_len) return ST_SIZE;
+  if (job.out_len) *job.out_len = out;
+  return ST_OK;
+}
+
+}  // namespace hz2

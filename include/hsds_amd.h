@@ -105,9 +105,11 @@ void hsds_engine_destroy(hsds_engine* e);
 const char* hsds_version(void);
 const char* hsds_strerror(int status);
 
-/* Tuning of the inflate kernel (segment bits, warm-up bits, continuation bits,
- * repair rounds).  Defaults are set by hsds_engine_create. */
-int hsds_set_tuning(hsds_engine* e, uint32_t seg_bits, uint32_t warmup_bits, uint32_t cont_bits,
+/* Tuning of the inflate kernel: segment over-provisioning against the previous
+ * deflate block in 16ths (0..16), warm-up bits before a segment (0..4096), an unused
+ * argument (0), repair rounds per window (0..64).  Any setting decodes the same bytes;
+ * it only moves work between the phases.  Defaults are set by hsds_engine_create. */
+int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t unused,
                     int32_t repair_rounds);
 
 /* ---- decode -------------------------------------------------------------- */

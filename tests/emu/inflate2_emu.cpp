@@ -1,0 +1,29 @@
+// CPU emulation driver for hsds_amd/csrc/inflate2.h (TEST INFRASTRUCTURE ONLY).
+// Runs the single-source two-pass wave decoder with LANE_LOOP iterating the 64 lanes in
+// order, so its orchestration (segments, sync, repairs, emit, match-ring resolve, fused
+// unshuffle) is checked against libz on CPU.  Never used by the product.
+#include <stdlib.h>
+#include "../../hsds_amd/csrc/inflate2.h"
+
+// perm_n > 1: the output is written through the byte-unshuffle map of perm_n-byte elements
+// (dst holds the unshuffled bytes), as the engine does for F2 chunks.
+extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,
+                            int max_rounds, uint32_t over16, uint32_t perm_n, uint64_t* stats_out) {
+  hz2::Shared* sh = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
+  uint8_t* ring = (uint8_t*)malloc(hz2::RING_BYTES);
+  hz2::Stats st = {};
+  const uint32_t n = perm_n < 1 ? 1 : perm_n;
+  hz2::Job job = {src, src_len, dst, dst_len, 1u, nullptr, hz2::perm_make(n, dst_len / n, 0)};
+  hz2::Tune tune = {W, max_rounds, over16};
+  int r = hz2::inflate_stream<hz2::Stats>(*sh, job, tune, ring, &st);
+  if (stats_out) {
+    const uint64_t v[] = {st.windows, st.blocks, st.stored, st.tokens, st.matches, st.lanes_valid, st.repairs,
+                          st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows};
+    for (int i = 0; i < 14; i++) stats_out[i] = v[i];
+  }
+  free(ring);
+  free(sh);
+  return r;
+}
+
+extern "C" int emu2_shared_bytes() { return (int)sizeof(hz2::Shared); }
