@@ -271,7 +271,7 @@ __device__ __forceinline__ void raw_copy(const Item& it, int lane) {
   }
 }
 
-__global__ void __launch_bounds__(64) inflate2_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) inflate2_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
                                                       uint32_t* __restrict__ counter, int32_t* __restrict__ status,
                                                       uint32_t* __restrict__ sizes,
                                                       const uint32_t* __restrict__ kind_counts, hz2::Tune tune,
@@ -305,7 +305,8 @@ __global__ void __launch_bounds__(64) inflate2_kernel(const Item* __restrict__ p
       hz2::Job job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
                       (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr,
                       item_perm(it)};
-      st = hz2::inflate_stream<hz2::Stats>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
+      if (job.perm.n > 1u) st = hz2::inflate_stream<hz2::Stats, true>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
+      else st = hz2::inflate_stream<hz2::Stats, false>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
     } else {
       continue;                        // lz_kernel's / zstd_kernel's item
     }

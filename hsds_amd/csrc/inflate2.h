@@ -56,14 +56,18 @@ constexpr uint32_t LMAX = 1u << 16;       // segment bits (lane output stays wel
 constexpr uint32_t MCAP_LANE = 256;       // matches per lane per window (ring bound)
 constexpr uint32_t RING = MCAP_LANE * WAVE;   // match ring entries per wave
 constexpr uint32_t RING_BYTES = RING * 8u;
-constexpr uint32_t SPAN = 2048;           // resolve batch: output bytes covered by the source map
+constexpr uint32_t SPAN = 1536;           // resolve batch: output bytes covered by the source map
 constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
 static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 #ifndef HZ2_RG
 #define HZ2_RG 8
 #endif
-constexpr uint32_t RG = HZ2_RG;           // resolve: source bytes a lane loads before it stores
+constexpr uint32_t RG = HZ2_RG;           // resolve (unshuffled output): bytes a lane loads before it stores
+#ifndef HZ2_DW
+#define HZ2_DW 2
+#endif
+constexpr uint32_t DW = HZ2_DW;           // resolve (plain output): dwords a lane loads before it stores
 constexpr uint32_t SYNC_NONE = 0xfeu;     // predecessor ended (EOB / ERR / CUT): lane beyond the window
 constexpr uint32_t SYNC_FAIL = 0xffu;     // predecessor never met this lane's recorded path
 constexpr uint32_t END_NONE = 0, END_EOB = 1, END_ERR = 2, END_CUT = 3;
@@ -92,7 +96,10 @@ struct Shared {
       uint8_t lens[320 + 32];
     };
     uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
-    uint16_t smap[SPAN];          // phase M: batch byte -> distance to its source (0: literal)
+    struct {                      // phase M
+      uint16_t smap[SPAN];        // batch byte -> distance to its source (0: literal)
+      uint32_t sbuf[SPAN / 4 + 2];   // plain output: the batch's aligned dwords, patched in LDS
+    };
   };
   uint32_t syncw[WAVE];           // record index where the predecessor met this lane / SYNC_*
   uint32_t endp[WAVE];            // lane's exclusive end (token boundary)
@@ -301,7 +308,9 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
 
 namespace hz2 {
 
-template <class StatsT>
+// PERM: the job's output map is an unshuffle (F2 chunks, shuffled Blosc blocks); otherwise
+// stream byte x is dst[x] and the resolve stores whole aligned dwords
+template <class StatsT, bool PERM>
 #if HZ_GPU
 __device__ __forceinline__
 #else
@@ -366,7 +375,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         uint32_t a1 = LV(s1), a2 = LV(s2);
         for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
           const uint32_t b = S.base[sb + i];
-          dst[perm_at(P, out + i)] = (uint8_t)b;
+          dst[PERM ? perm_at(P, out + i) : out + i] = (uint8_t)b;
           a1 += b;
           a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
         }
@@ -678,7 +687,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             const uint32_t t = next_token(&sh, S, r);
             steps++;
             if (!(t & T_MATCH)) {
-              dst[perm_at(P, o)] = (uint8_t)t;
+              dst[PERM ? perm_at(P, o) : o] = (uint8_t)t;
               a1 += t;
               a2 += (uint64_t)o * t;
               o++;
@@ -768,46 +777,118 @@ HZ_UNROLL
             LV(nw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
           }
         }
-        LANE_LOOP {
-          uint32_t a1 = LV(ra1);
-          uint64_t a2 = LV(ra2);
-          for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
-            uint32_t src[RG];
+        if (PERM) {
+          // unshuffled output: byte-strided over the span
+          LANE_LOOP {
+            uint32_t a1 = LV(ra1);
+            uint64_t a2 = LV(ra2);
+            for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
+              uint32_t src[RG];
 HZ_UNROLL
-            for (uint32_t i = 0; i < RG; i++) {
-              const uint32_t q = h0 + (uint32_t)lane + 64u * i;
-              uint32_t y = 0xffffffffu;
-              if (q < span) {
-                const uint32_t dq = sh.smap[q];
-                if (dq) {
-                  y = F + q - dq;
-                  uint32_t hops = 0;
-                  while (y >= F) {            // inside the batch: follow an earlier match byte
-                    const uint32_t d2 = sh.smap[y - F];
-                    if (!d2) break;
-                    y -= d2;
-                    hops++;
+              for (uint32_t i = 0; i < RG; i++) {
+                const uint32_t q = h0 + (uint32_t)lane + 64u * i;
+                uint32_t y = 0xffffffffu;
+                if (q < span) {
+                  const uint32_t dq = sh.smap[q];
+                  if (dq) {
+                    y = F + q - dq;
+                    while (y >= F) {            // inside the batch: follow an earlier match byte
+                      const uint32_t d2 = sh.smap[y - F];
+                      if (!d2) break;
+                      y -= d2;
+                      if (stats) stats->hops++;
+                    }
                   }
-                  if (stats) stats->hops += hops;
+                }
+                src[i] = y;
+              }
+              uint32_t bv[RG];
+HZ_UNROLL
+              for (uint32_t i = 0; i < RG; i++) bv[i] = src[i] != 0xffffffffu ? (uint32_t)dst[perm_at(P, src[i])] : 0u;
+HZ_UNROLL
+              for (uint32_t i = 0; i < RG; i++) {
+                if (src[i] != 0xffffffffu) {
+                  const uint32_t x = F + h0 + (uint32_t)lane + 64u * i;
+                  dst[perm_at(P, x)] = (uint8_t)bv[i];
+                  a1 += bv[i];
+                  a2 += (uint64_t)x * bv[i];
                 }
               }
-              src[i] = y;
             }
-            uint32_t bv[RG];
-HZ_UNROLL
-            for (uint32_t i = 0; i < RG; i++) bv[i] = src[i] != 0xffffffffu ? (uint32_t)dst[perm_at(P, src[i])] : 0u;
-HZ_UNROLL
-            for (uint32_t i = 0; i < RG; i++) {
-              if (src[i] != 0xffffffffu) {
-                const uint32_t x = F + h0 + (uint32_t)lane + 64u * i;
-                dst[perm_at(P, x)] = (uint8_t)bv[i];
-                a1 += bv[i];
-                a2 += (uint64_t)x * bv[i];
-              }
+            LV(ra1) = a1;
+            LV(ra2) = a2;
+          }
+        } else {
+          // plain output: the aligned dwords covering the span are loaded (coalesced) into
+          // LDS, every match byte's source is gathered into them (a source before the batch
+          // from dst, a literal of the batch from LDS), and the dwords are stored back
+          // (coalesced) -- one load round trip and one store drain per batch.  Dwords
+          // reaching outside the stream's output store their match bytes one by one.
+          const uint32_t mis = (uint32_t)((uintptr_t)(job.dst + F) & 3u);
+          const uint32_t xa = F - mis;                           // stream position of dword 0
+          const uint32_t ndw = (span + mis + 3u) >> 2;
+          LANE_LOOP {
+            for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
+              const uint32_t x0 = xa + 4u * k;
+              sh.sbuf[k] = (x0 + 4u <= dst_len && (int32_t)x0 >= 0) ? *(hz_gu32*)(dst + x0) : 0u;
             }
           }
-          LV(ra1) = a1;
-          LV(ra2) = a2;
+          WAVE_SYNC();
+          LANE_LOOP {
+            uint32_t a1 = LV(ra1);
+            uint64_t a2 = LV(ra2);
+            for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
+              uint32_t src[RG];
+HZ_UNROLL
+              for (uint32_t i = 0; i < RG; i++) {
+                const uint32_t q = h0 + (uint32_t)lane + 64u * i;
+                uint32_t y = 0xffffffffu;
+                if (q < span) {
+                  const uint32_t dq = sh.smap[q];
+                  if (dq) {
+                    y = F + q - dq;
+                    while (y >= F) {
+                      const uint32_t d2 = sh.smap[y - F];
+                      if (!d2) break;
+                      y -= d2;
+                      if (stats) stats->hops++;
+                    }
+                  }
+                }
+                src[i] = y;
+              }
+              uint32_t bv[RG];
+HZ_UNROLL
+              for (uint32_t i = 0; i < RG; i++) {
+                const uint32_t y = src[i];
+                bv[i] = 0u;
+                if (y != 0xffffffffu) {
+                  if (y >= F) { const uint32_t by = y - xa; bv[i] = (sh.sbuf[by >> 2] >> (8u * (by & 3u))) & 0xffu; }
+                  else bv[i] = dst[y];
+                }
+              }
+HZ_UNROLL
+              for (uint32_t i = 0; i < RG; i++) {
+                if (src[i] != 0xffffffffu) {
+                  const uint32_t q = h0 + (uint32_t)lane + 64u * i, x = F + q, bx = x - xa;
+                  ((uint8_t*)sh.sbuf)[bx] = (uint8_t)bv[i];
+                  a1 += bv[i];
+                  a2 += (uint64_t)x * bv[i];
+                  const uint32_t x0 = xa + (bx & ~3u);               // its dword, as in the stores below
+                  if (!(x0 + 4u <= dst_len && (int32_t)x0 >= 0)) dst[x] = (uint8_t)bv[i];
+                }
+              }
+            }
+            LV(ra1) = a1;
+            LV(ra2) = a2;
+          }
+          WAVE_SYNC();
+          LANE_LOOP {
+            for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
+              const uint32_t x0 = xa + 4u * k;
+              if (x0 + 4u <= dst_len && (int32_t)x0 >= 0) *(hz_gu32*)(dst + x0) = sh.sbuf[k];
+            }
+          }
         }
         WAVE_SYNC_GLOBAL();
         LANE_LOOP {

@@ -7,15 +7,18 @@
 
 // perm_n > 1: the output is written through the byte-unshuffle map of perm_n-byte elements
 // (dst holds the unshuffled bytes), as the engine does for F2 chunks.
+// dst_off: the stream's output starts dst_off bytes into dst (dst has dst_len + dst_off + 8
+// bytes; the bytes around the output must stay untouched)
 extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,
-                            int max_rounds, uint32_t over16, uint32_t perm_n, uint64_t* stats_out) {
+                            int max_rounds, uint32_t over16, uint32_t perm_n, uint32_t dst_off, uint64_t* stats_out) {
   hz2::Shared* sh = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
   uint8_t* ring = (uint8_t*)malloc(hz2::RING_BYTES);
   hz2::Stats st = {};
   const uint32_t n = perm_n < 1 ? 1 : perm_n;
-  hz2::Job job = {src, src_len, dst, dst_len, 1u, nullptr, hz2::perm_make(n, dst_len / n, 0)};
+  hz2::Job job = {src, src_len, dst + dst_off, dst_len, 1u, nullptr, hz2::perm_make(n, dst_len / n, 0)};
   hz2::Tune tune = {W, max_rounds, over16};
-  int r = hz2::inflate_stream<hz2::Stats>(*sh, job, tune, ring, &st);
+  int r = n > 1 ? hz2::inflate_stream<hz2::Stats, true>(*sh, job, tune, ring, &st)
+                : hz2::inflate_stream<hz2::Stats, false>(*sh, job, tune, ring, &st);
   if (stats_out) {
     const uint64_t v[] = {st.windows, st.blocks, st.stored, st.tokens, st.matches, st.lanes_valid, st.repairs,
                           st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows};

@@ -24,18 +24,21 @@ def emu():
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", EMU, SRC])
     L = ctypes.CDLL(EMU)
     L.emu_inflate2.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-                               ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+                               ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
     return L
 
 
-def run(L, comp, n, W=384, rounds=4, over16=1, perm_n=1):
+def run(L, comp, n, W=384, rounds=4, over16=1, perm_n=1, dst_off=0):
     src = np.frombuffer(comp, np.uint8).copy()
     if src.size == 0:
         src = np.zeros(1, np.uint8)
-    dst = np.zeros(max(n, 1), np.uint8)
+    guard = 0xA5
+    dst = np.full(max(n, 1) + dst_off + 8, guard, np.uint8)
     st = np.zeros(len(STATS), np.uint64)
-    r = L.emu_inflate2(src.ctypes.data, len(comp), dst.ctypes.data, n, W, rounds, over16, perm_n, st.ctypes.data)
-    return r, dst[:n].tobytes(), dict(zip(STATS, st.tolist()))
+    r = L.emu_inflate2(src.ctypes.data, len(comp), dst.ctypes.data, n, W, rounds, over16, perm_n, dst_off,
+                       st.ctypes.data)
+    assert (dst[:dst_off] == guard).all() and (dst[dst_off + n:] == guard).all(), "write outside the output"
+    return r, dst[dst_off:dst_off + n].tobytes(), dict(zip(STATS, st.tolist()))
 
 
 def corpus():
@@ -190,6 +193,21 @@ def test_deep_codes_use_second_level_tables(emu):
         comp = zlib.compress(data, level)
         r, out, _ = run(emu, comp, len(data))
         assert r == 0 and out == data, (level, r)
+
+
+@pytest.mark.parametrize("off", [1, 2, 3, 5])
+def test_unaligned_output(emu, off):
+    """the resolve's dword path at every output alignment (the first / last dwords of the
+    stream reach outside it and must be written bytewise), plain and unshuffled output"""
+    for name in ("smooth_f32", "text", "runs", "zeros"):
+        data = corpus()[name][:50001]
+        c = zlib.compress(data, 6)
+        r, out, _ = run(emu, c, len(data), dst_off=off)
+        assert r == 0 and out == data, (name, off)
+    data = corpus()["int16"][:40000]
+    shuffled = np.frombuffer(data, np.uint8).reshape(-1, 2).T.copy().tobytes()
+    r, out, _ = run(emu, zlib.compress(shuffled, 4), len(data), perm_n=2, dst_off=off)
+    assert r == 0 and out == data
 
 
 def test_long_overlapping_matches_and_far_distances(emu):
