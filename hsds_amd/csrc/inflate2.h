@@ -79,7 +79,7 @@ HZ_HD uint32_t rec_rel(uint32_t r) { return r & 0x7ffu; }
 HZ_HD uint32_t rec_out(uint32_t r) { return (r >> 11) & 0x1fffu; }
 HZ_HD uint32_t rec_mat(uint32_t r) { return r >> 24; }
 
-struct Shared {
+struct alignas(16) Shared {
   uint16_t lut_ll[(1 << LL_ROOT) + LL_SUB];
   uint16_t lut_d[(1 << D_ROOT) + D_SUB];
   uint16_t tb_first[16];
@@ -96,6 +96,7 @@ struct Shared {
       uint8_t lens[320 + 32];
     };
     uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
+    alignas(16) uint8_t ostage[WAVE][32];   // phase E (plain output): each lane's current 32-byte output window
     struct {                      // phase M
       uint16_t smap[SPAN];        // batch byte -> distance to its source (0: literal)
       uint32_t sbuf[SPAN / 4 + 2];   // plain output: the batch's aligned dwords, patched in LDS
@@ -324,6 +325,12 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
   const uint32_t dst_len = job.dst_len;
   hz_gu8* const dst = HZ_GLOBAL(hz_gu8*, job.dst);
   hz_gu32* const ring = HZ_GLOBAL(hz_gu32*, ring_base);
+#if HZ_GPU
+  typedef __attribute__((address_space(1))) uint64_t hz_gu64;
+#else
+  typedef uint64_t hz_gu64;
+#endif
+  hz_gu64* const ring64 = HZ_GLOBAL(hz_gu64*, ring_base);
   const Perm P = job.perm;
 
   LANE_VAR(uint32_t, s1);     // adler32 partial sums of the bytes this lane wrote: sum b, sum pos*b
@@ -672,6 +679,11 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
 
       HZ_T(7);
       // -------- phase E: exact decode of every valid range; literals to dst, matches to the ring --------
+      // Stores are the cost here (every store is a separate memory request): matches go to
+      // the ring in 16-byte pairs, and on plain output each lane's literals are gathered in
+      // its 32-byte LDS window and written as two 16-byte stores (match bytes in between get
+      // stale bytes that phase M overwrites); windows that reach outside the lane's own range
+      // write their literals byte by byte.
       LANE_VAR(int, lerr);
       LANE_LOOP {
         int err = 0;
@@ -680,26 +692,82 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           GRd r;
           g_init(S, r, LV(sbit));
           const uint32_t stop = sh.endp[lane];
-          uint32_t o = out + LV(obase), mi = LV(mbase);
+          const uint32_t lo_x = out + LV(obase), hi_x = lo_x + LV(wout);
+          uint32_t o = lo_x, mi = LV(mbase);
           uint32_t a1 = 0;
           uint64_t a2 = 0;
+          uint64_t pend = 0;
+          uint32_t haspend = 0;
+          const uint32_t A = (uint32_t)((uintptr_t)job.dst & 31u);
+          uint32_t cw = 0xffffffffu, msk = 0;
+          auto flush = [&]() {
+            if (!msk) return;
+            const uint32_t wx = (cw << 5) - A;          // stream position of the window's byte 0
+            if ((int32_t)wx >= (int32_t)lo_x && wx + 32u <= hi_x) {
+#if HZ_GPU
+              typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+              typedef __attribute__((address_space(1))) u32x4 gu32x4;
+              const u32x4 v0 = *(const u32x4*)&sh.ostage[lane][0];
+              const u32x4 v1 = *(const u32x4*)&sh.ostage[lane][16];
+              *(gu32x4*)(dst + wx) = v0;
+              *(gu32x4*)(dst + wx + 16u) = v1;
+#else
+              memcpy(dst + wx, &sh.ostage[lane][0], 32);
+#endif
+            } else {
+              for (uint32_t m = msk; m; m &= m - 1u) {
+                const uint32_t b = (uint32_t)__builtin_ctz(m);
+                dst[wx + b] = sh.ostage[lane][b];
+              }
+            }
+          };
           while (r.pos < stop) {
             const uint32_t t = next_token(&sh, S, r);
             steps++;
             if (!(t & T_MATCH)) {
-              dst[PERM ? perm_at(P, o) : o] = (uint8_t)t;
+#ifndef HZ2_EXP_NOSTORE
+              if (PERM) {
+                dst[perm_at(P, o)] = (uint8_t)t;
+              } else {
+                const uint32_t ax = A + o, w = ax >> 5;
+                if (w != cw) { flush(); cw = w; msk = 0; }
+                sh.ostage[lane][ax & 31u] = (uint8_t)t;
+                msk |= 1u << (ax & 31u);
+              }
+#endif
               a1 += t;
               a2 += (uint64_t)o * t;
               o++;
             } else {
               const uint32_t ln = (t >> 16) & 0x1ffu, d = (t & 0x7fffu) + 1u;
               if (d > o) { err = 1; break; }
-              ring[2u * mi] = o;
-              ring[2u * mi + 1u] = (ln << 16) | (d - 1u);
+              const uint64_t rv = (uint64_t)o | ((uint64_t)((ln << 16) | (d - 1u)) << 32);
+#ifndef HZ2_EXP_NOSTORE
+              if (haspend) {                           // records mi-1 (even) and mi: one 16-byte store
+#if HZ_GPU
+                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                typedef __attribute__((address_space(1))) u64x2 gu64x2;
+                u64x2 v;
+                v.x = pend; v.y = rv;
+                *(gu64x2*)(ring64 + mi - 1u) = v;
+#else
+                ring64[mi - 1u] = pend; ring64[mi] = rv;
+#endif
+                haspend = 0;
+              } else if (!(mi & 1u)) {
+                pend = rv; haspend = 1;
+              } else {
+                ring64[mi] = rv;
+              }
+#endif
               mi++;
               o += ln;
             }
           }
+#ifndef HZ2_EXP_NOSTORE
+          if (haspend) ring64[mi - 1u] = pend;
+          if (!PERM) flush();
+#endif
           LV(s1) = (LV(s1) + a1 % ADLER_MOD) % ADLER_MOD;
           LV(s2) = (uint32_t)((LV(s2) + a2 % ADLER_MOD) % ADLER_MOD);
         }
@@ -733,7 +801,11 @@ HZ_UNROLL
           LV(rw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
         }
       }
+#ifdef HZ2_EXP_NOM
+      for (uint32_t b0 = 0; b0 < 0u;) {
+#else
       for (uint32_t b0 = 0; b0 < mtotal;) {
+#endif
         if (stats) stats->batches++;
         const uint32_t F = LVA_AT(ro, 0, 0);
         uint32_t nb = 0, open_ = 1;
