@@ -91,6 +91,7 @@ def lib():
         "hsds_encode_bitshuffle_batch": (I, [P, P, U64, P, I64, P, U64, P, P, I, I, P]),
         "hsds_bitshuffle_bound": (I64, [I64, I, I]),
         "hsds_bitshuffle_compress": (I64, [P, P, I64, I, I, P, I64]),
+        "hsds_partition_ids": (I, [ctypes.c_char_p, I, P, I64, I, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

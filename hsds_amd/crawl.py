@@ -1,4 +1,5 @@
-"""Chunk-sharded hyperslab read across the GPUs of one node.
+"""Chunk-sharded hyperslab read and write across the GPUs of one node (SURVEY.md section 8e,
+cfg3 / cfg4 reads, cfg5 writes).
 
 Reference flow (one HTTP request per chunk): the SN crawler fans a selection out to the
 data nodes by `getObjPartition(chunk_id, dn_count)` (hsds/chunk_crawl.py:362-418,
@@ -19,6 +20,14 @@ selection, world), so no metadata is exchanged: each rank
 and the root scatters every piece into the slab with one more hsds_copy_batch launch.
 Missing chunks (no stored object) are decoded as fill-value chunks, which leaves the
 slab exactly as the reference leaves it (prefilled, chunk_crawl.py:362-366).
+
+The write is the mirror (PUT_Value -> _doHyperslabWrite -> write_chunk_hyperslab ->
+PUT_Chunk -> save_chunk -> s3sync, chunk_sn.py:555-646, chunk_crawl.py:75-150,
+chunk_dn.py:41-314, datanode_lib.py:1186-1318): the root gathers every chunk's piece of
+the request array, arr[data_sel], into per-owner packed buffers (one copy launch), sends
+each owner its buffer (one point-to-point message per rank), and every rank applies its
+pieces to its chunks through its HBM chunk store (read-modify-write with chunk_init,
+compare, conditional copy, dirty marking) and encodes its dirty chunks locally on flush.
 """
 from dataclasses import dataclass
 
@@ -43,11 +52,45 @@ def _align(n, a):
     return (n + a - 1) // a * a
 
 
-class SelectionPlan:
-    """Per-chunk read plan of a hyperslab selection sharded over `world` ranks.
+def _dim_pieces(s, c):
+    """One dimension of a hyperslab over chunks of extent c, vectorized: arrays of chunk
+    index, chunk-relative start, count and slab start for every chunk the slice touches, in
+    getChunkIds order (chunkUtil.py:459-582), with getChunkSelection's start snapped onto
+    the step lattice and getChunkCoverage / getDataCoverage's slices (chunkUtil.py:608-790)."""
+    start, stop, step = int(s.start), int(s.stop), int(s.step or 1)
+    if stop <= start:
+        z = np.zeros(0, np.int64)
+        return z, z, z, z
+    if step > c:
+        pts = np.arange(start, stop, step, dtype=np.int64)
+        idx = pts // c
+        return idx, pts - idx * c, np.ones_like(idx), (pts - start) // step
+    last = sel.slice_stop(slice(start, stop, step))
+    idx = np.arange(start // c, -(-last // c), dtype=np.int64)
+    lo = idx * c
+    first = np.where(start >= lo, start, start + (-(-(lo - start) // step)) * step)
+    end = np.minimum(stop, lo + c)
+    count = np.where(end > first, -(-(end - first) // step), 0)
+    return idx, first - lo, count, (first - start) // step
 
-    `selection` is a tuple of slices (getSelectionList output).  Point (coordinate)
-    selections are not hyperslabs and are outside the distributed path."""
+
+def _c_strides(shape, itemsize):
+    st = [itemsize] * len(shape)
+    for d in range(len(shape) - 2, -1, -1):
+        st[d] = st[d + 1] * int(shape[d + 1])
+    return np.array(st, np.int64)
+
+
+class SelectionPlan:
+    """Per-chunk plan of a hyperslab selection sharded over `world` ranks, computed with
+    numpy over the per-dimension chunk grids (O(#chunks) array work, no Python loop per
+    chunk) and the batched md5 partition of the C ABI (hsds_partition_ids).
+
+    Read side (SN read, chunk_crawl.py:395-418): decoded chunk -> packed piece
+    (pack_descs) -> slab (place_descs).  Write side (SN write, chunk_crawl.py:118-135, and
+    PUT_Chunk, chunk_dn.py:284-302): slab -> packed piece (gather_descs) -> chunk
+    (apply_descs).  `selection` is a tuple of slices (getSelectionList output).  Point
+    (coordinate) selections are not hyperslabs and are outside the distributed path."""
 
     ALIGN = 16
 
@@ -59,73 +102,168 @@ class SelectionPlan:
             raise NotImplementedError("coordinate selections are outside the distributed hyperslab path")
         if len(self.selection) != len(self.dims) or len(self.layout) != len(self.dims):
             raise ValueError("selection / layout rank does not match dataset rank")
+        self.dset_id = dset_id
         self.dtype = np.dtype(dtype)
         self.itemsize = self.dtype.itemsize
         self.world = int(world)
+        self.rank = len(self.dims)
         self.slab_shape = tuple(sel.getSelectionShape(self.selection))
         self.slab_nbytes = int(np.prod(self.slab_shape, dtype=np.int64)) * self.itemsize
         self.chunk_nbytes = int(np.prod(self.layout, dtype=np.int64)) * self.itemsize
-        part = partition or (lambda cid: getObjPartition(cid, self.world))
-        self.pieces = []
-        for cid in sel.getChunkIds(dset_id, self.selection, self.layout):
-            csel = sel.getChunkSelection(cid, self.selection, self.layout)
-            if csel is None:
-                continue
-            shape = tuple(sel.getSelectionShape(csel))
-            n = int(np.prod(shape, dtype=np.int64)) * self.itemsize
-            if n == 0:
-                continue
-            self.pieces.append(Piece(cid, part(cid), tuple(sel.getChunkCoverage(cid, self.selection, self.layout)),
-                                     tuple(sel.getDataCoverage(cid, self.selection, self.layout)), shape, n))
-        self.by_rank = [[] for _ in range(self.world)]
-        for i, p in enumerate(self.pieces):
-            self.by_rank[p.owner].append(i)
+        self.steps = np.array([int(s.step or 1) for s in self.selection], np.int64)
+        if not dset_id.startswith("d-"):
+            raise ValueError(f"Bad Request: invalid dset id: {dset_id}")
+        self.prefix = "c-" + dset_id[2:] + "_"
+        per_dim = [_dim_pieces(s, c) for s, c in zip(self.selection, self.layout)]
+        R = self.rank
+        grids = [np.meshgrid(*[pd[k] for pd in per_dim], indexing="ij") for k in range(4)]
+        idx, cst, cnt, dst = (np.stack([g.reshape(-1) for g in gk], axis=1) if R else np.zeros((1, 0), np.int64)
+                              for gk in grids)
+        keep = (cnt > 0).all(axis=1)
+        self.idx, self.cstart, self.count, self.dstart = idx[keep], cst[keep], cnt[keep], dst[keep]
+        n = len(self.idx)
+        self.nbytes = np.prod(self.count, axis=1) * self.itemsize if n else np.zeros(0, np.int64)
+        if partition is not None:
+            self.owner = np.array([partition(self._cid(i)) for i in range(n)], np.int32)
+        elif self.world == 1:
+            self.owner = np.zeros(n, np.int32)
+        else:
+            self.owner = partition_ids(self.prefix, self.idx, self.world)
+        self.by_rank = [np.nonzero(self.owner == r)[0] for r in range(self.world)]
+        sizes = (self.nbytes + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.off = np.zeros(n, np.int64)
         self.rank_bytes = []
         for r in range(self.world):
-            off = 0
-            for i in self.by_rank[r]:
-                self.pieces[i].off = off
-                off += _align(self.pieces[i].nbytes, self.ALIGN)
-            self.rank_bytes.append(off)
+            ir = self.by_rank[r]
+            if len(ir):
+                cs = np.cumsum(sizes[ir])
+                self.off[ir] = cs - sizes[ir]
+                self.rank_bytes.append(int(cs[-1]))
+            else:
+                self.rank_bytes.append(0)
         self.rank_base = np.concatenate([[0], np.cumsum(self.rank_bytes)]).astype(np.int64)
         self.gathered_nbytes = int(self.rank_base[-1])
+        self._pieces = None
+
+    def _cid(self, i):
+        return self.prefix + "_".join(str(int(v)) for v in self.idx[i])
+
+    @property
+    def pieces(self):
+        """Piece records (built on first use; the plan itself is arrays)."""
+        if self._pieces is None:
+            out = []
+            for i in range(len(self.idx)):
+                cs = tuple(slice(int(a), int(a) + (int(c) - 1) * int(t) + 1, int(t))
+                           for a, c, t in zip(self.cstart[i], self.count[i], self.steps))
+                ds = tuple(slice(int(a), int(a) + int(c), 1) for a, c in zip(self.dstart[i], self.count[i]))
+                out.append(Piece(self._cid(i), int(self.owner[i]), cs, ds, tuple(int(c) for c in self.count[i]),
+                                 int(self.nbytes[i]), int(self.off[i])))
+            self._pieces = out
+        return self._pieces
 
     def chunk_ids(self, rank):
-        """Chunk ids this rank decodes, in packing order."""
-        return [self.pieces[i].chunk_id for i in self.by_rank[rank]]
+        """Chunk ids this rank decodes (or writes), in packing order."""
+        return [self._cid(i) for i in self.by_rank[rank]]
 
     def selected_bytes(self, rank=None):
-        idx = range(len(self.pieces)) if rank is None else self.by_rank[rank]
-        return sum(self.pieces[i].nbytes for i in idx)
+        return int(self.nbytes.sum() if rank is None else self.nbytes[self.by_rank[rank]].sum())
+
+    # -- copy descriptors (COPY_DESC_DTYPE records, one per piece) --
+    def _descs(self, ii, chunk_side, chunk_base, packed_base, to_chunk):
+        """Descriptors between each piece's chunk-side region (chunk arrays at
+        chunk_base[k], or the slab when chunk_side is False) and its packed bytes."""
+        from .engine import COPY_DESC_DTYPE
+        n, R = len(ii), self.rank
+        if n == 0:
+            return np.zeros((0, 27), np.int64)
+        # the 216-byte record as 27 int64 words: src_off, dst_off, src_stride[8],
+        # dst_stride[8], count[8], rank | itemsize << 32
+        m = np.zeros((n, 27), np.int64)
+        cnt = self.count[ii]
+        # packed piece: C-contiguous array of its selection shape
+        pst = np.empty((n, R), np.int64)
+        pst[:, R - 1] = self.itemsize
+        for d in range(R - 2, -1, -1):
+            pst[:, d] = pst[:, d + 1] * cnt[:, d + 1]
+        if chunk_side:
+            cs = _c_strides(self.layout, self.itemsize)
+            off = np.asarray(chunk_base, np.int64) + self.cstart[ii] @ cs
+            st = cs * self.steps
+        else:
+            ss = _c_strides(self.slab_shape, self.itemsize)
+            off = int(chunk_base) + self.dstart[ii] @ ss
+            st = ss
+        poff = np.asarray(packed_base, np.int64) + self.off[ii]
+        if to_chunk:
+            m[:, 0], m[:, 1] = poff, off
+            m[:, 2:2 + R], m[:, 10:10 + R] = pst, st
+        else:
+            m[:, 0], m[:, 1] = off, poff
+            m[:, 2:2 + R], m[:, 10:10 + R] = st, pst
+        m[:, 18:18 + R] = cnt
+        m[:, 26] = R | (self.itemsize << 32)
+        return m
 
     def pack_descs(self, rank, chunk_offsets, packed_base=0):
-        """Copy descriptors: decoded chunk k (C-order `layout` array at byte offset
-        chunk_offsets[k] of the decode buffer) -> its piece in the packed buffer."""
-        idx = self.by_rank[rank]
-        if len(chunk_offsets) != len(idx):
+        """Read: decoded chunk k (C-order `layout` array at byte offset chunk_offsets[k]
+        of the decode buffer) -> its piece in the rank's packed buffer."""
+        ii = self.by_rank[rank]
+        if len(chunk_offsets) != len(ii):
             raise ValueError("one decoded chunk offset per owned piece expected")
-        recs = [sel.copy_desc(self.layout, p.chunk_slices, p.shape, sel._contig_slices(p.shape), self.itemsize,
-                              src_base=int(o), dst_base=packed_base + p.off)
-                for p, o in ((self.pieces[i], o) for i, o in zip(idx, chunk_offsets))]
-        return _cat(recs)
+        return _recs(self._descs(ii, True, chunk_offsets, packed_base, False))
 
     def place_descs(self, ranks=None):
-        """Copy descriptors: gathered buffer (rank r's packed bytes at rank_base[r]) ->
-        slab[data_slices]."""
-        recs = []
-        for r in (range(self.world) if ranks is None else ranks):
-            for i in self.by_rank[r]:
-                p = self.pieces[i]
-                recs.append(sel.copy_desc(p.shape, sel._contig_slices(p.shape), self.slab_shape, p.data_slices,
-                                          self.itemsize, src_base=int(self.rank_base[r]) + p.off))
-        return _cat(recs)
+        """Read: gathered buffer (rank r's packed bytes at rank_base[r]) -> slab[data_slices]."""
+        rs = range(self.world) if ranks is None else ranks
+        return _cat([self._descs(self.by_rank[r], False, 0, self.rank_base[r], True) for r in rs])
+
+    def gather_descs(self, ranks=None, slab_base=0):
+        """Write: slab[data_slices] (the request's array, C order, at slab_base) -> each
+        piece in the scattered buffer (rank r's pieces at rank_base[r]): arr[data_sel] of
+        write_chunk_hyperslab (chunk_crawl.py:135)."""
+        rs = range(self.world) if ranks is None else ranks
+        return _cat([self._descs(self.by_rank[r], False, slab_base, self.rank_base[r], False) for r in rs])
+
+    def apply_descs(self, rank, chunk_offsets, packed_base=0, broadcast=False):
+        """Write: the rank's packed piece k -> chunk k (at chunk_offsets[k]) [chunk_sel]:
+        chunkWriteSelection's copy (chunkUtil.py:983-986).  broadcast: every element of
+        every piece reads the one value at packed_base (element_count == 1,
+        chunk_crawl.py:118-133, chunk_dn.py:292-297)."""
+        ii = self.by_rank[rank]
+        if len(chunk_offsets) != len(ii):
+            raise ValueError("one chunk offset per owned piece expected")
+        m = self._descs(ii, True, chunk_offsets, packed_base, True)
+        if broadcast:
+            m[:, 0] = packed_base
+            m[:, 2:10] = 0
+        return _recs(m)
 
 
-def _cat(recs):
+def partition_ids(prefix, idx, world):
+    """getObjPartition of every chunk id prefix + '_'.join(idx[i]) (C ABI, batched md5)."""
+    import ctypes
+    from . import _native as nat
+    idx = np.ascontiguousarray(idx, np.int64)
+    n = len(idx)
+    owner = np.zeros(n, np.int32)
+    if n:
+        rc = nat.lib().hsds_partition_ids(prefix.encode(), idx.shape[1], idx.ctypes.data, n, int(world),
+                                          owner.ctypes.data)
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_partition_ids")
+    return owner
+
+
+def _recs(m):
+    """int64 (n, 27) matrix -> COPY_DESC_DTYPE records (a view, no copy)."""
     from .engine import COPY_DESC_DTYPE
-    if not recs:
-        return np.zeros(0, COPY_DESC_DTYPE)
-    return np.concatenate(recs)
+    return np.ascontiguousarray(m).view(COPY_DESC_DTYPE).reshape(len(m))
+
+
+def _cat(mats):
+    mats = [m for m in mats if len(m)]
+    return _recs(np.concatenate(mats) if mats else np.zeros((0, 27), np.int64))
 
 
 def exchange(packed, plan, rank, root=0, group=None, gathered=None):
@@ -261,3 +399,137 @@ class ShardedReader:
         if len(plan.pieces):
             self.eng.copy(got, slab, st["d_place"])
         return slab
+
+
+def broadcast_write(arr, selection):
+    """write_chunk_hyperslab's broadcast test (chunk_crawl.py:118-135): a one-element
+    request array and no step > 1 in the selection -> the value is sent to every chunk
+    with element_count = 1.  A one-element array with a stepped selection that has more
+    than one element cannot be indexed by data_sel there either (the reference fails)."""
+    n = int(np.prod(np.shape(arr)))
+    if n != 1:
+        return False
+    if any((s.step or 1) > 1 for s in selection):
+        if int(np.prod(sel.getSelectionShape(selection))) != 1:
+            raise ValueError("one-element write with a stepped selection: no broadcast")
+        return False
+    return True
+
+
+class ShardedWriter:
+    """GPU write of a hyperslab: gather per-owner pieces on the root -> scatter -> apply
+    (RMW in each rank's HBM chunk store) -> flush (local encode).
+
+    `store` is this rank's hsds_amd.datanode.ChunkStore (its chunks are the ones the md5
+    rule assigns to it, like a DN's)."""
+
+    def __init__(self, plan, rank, store, root=0, group=None):
+        import torch
+        from .engine import ChunkEngine
+        self.plan, self.rank, self.store, self.root, self.group = plan, rank, store, root, group
+        self.device = store.cache.arena.buf.device
+        self.eng = ChunkEngine(self.device.index)
+        self.torch = torch
+
+    def scatter(self, arr=None, broadcast=False):
+        """Root: `arr` is the request array (numpy or a uint8 / typed device tensor, C order,
+        selection shape; one element when broadcasting).  Returns this rank's packed pieces
+        (uint8 device tensor; the single value when broadcasting)."""
+        torch = self.torch
+        plan = self.plan
+        if broadcast:
+            val = np.zeros(1, plan.dtype)
+            if self.rank == self.root:
+                val[...] = np.asarray(arr).reshape(-1)[0] if not isinstance(arr, torch.Tensor) else \
+                    arr.reshape(-1).view(torch.uint8)[:plan.itemsize].cpu().numpy().view(plan.dtype)[0]
+            t = torch.from_numpy(val.view(np.uint8).copy()).to(self.device)
+            if plan.world > 1:
+                import torch.distributed as dist
+                dist.broadcast(t, self.root, group=self.group)
+            return t
+        if self.rank == self.root:
+            if isinstance(arr, torch.Tensor):
+                d_arr = arr.reshape(-1).view(torch.uint8) if arr.dtype != torch.uint8 else arr.reshape(-1)
+                if d_arr.device != self.device:
+                    d_arr = d_arr.to(self.device)
+            else:
+                a = np.ascontiguousarray(arr, dtype=plan.dtype)
+                if tuple(a.shape) != tuple(plan.slab_shape):
+                    raise ValueError(f"request array shape {a.shape} != selection shape {plan.slab_shape}")
+                d_arr = torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(self.device)
+            if d_arr.numel() != plan.slab_nbytes:
+                raise ValueError("request array size does not match the selection")
+            scattered = torch.empty(max(plan.gathered_nbytes, 1), dtype=torch.uint8, device=self.device)
+            if len(plan.idx):
+                self.eng.copy(d_arr, scattered, plan.gather_descs())
+        else:
+            scattered = None
+        if plan.world == 1:
+            return scattered
+        return scatter_exchange(scattered, plan, self.rank, self.root, self.group, self.device)
+
+    def apply(self, packed, filter_ops=None, fill_value=None, write_zero_chunks=False, broadcast=False):
+        """PUT_Chunk for every piece this rank owns; returns {chunk_id: dirty}."""
+        from .datanode import ChunkRead
+        from .partition import getS3Key
+        plan = self.plan
+        ids = plan.chunk_ids(self.rank)
+        if not ids:
+            return {}
+        reads = [ChunkRead(c, getS3Key(c)) for c in ids]
+
+        def make(offs):
+            # `packed` starts at this rank's first piece (the root's is a view at its rank_base)
+            return plan.apply_descs(self.rank, offs, packed_base=0, broadcast=broadcast)
+        dirty = self.store.put_pieces(reads, packed, make, plan.dtype, plan.layout, filter_ops=filter_ops,
+                                      fill_value=fill_value, write_zero_chunks=write_zero_chunks)
+        return dict(zip(ids, dirty))
+
+    def write(self, arr=None, filter_ops=None, fill_value=None, write_zero_chunks=False):
+        """scatter + apply; `arr` matters on the root only."""
+        bc = False
+        if self.rank == self.root:
+            bc = broadcast_write(arr, self.plan.selection) if arr is not None and not \
+                isinstance(arr, self.torch.Tensor) else False
+        if self.plan.world > 1:
+            import torch.distributed as dist
+            flag = self.torch.tensor([1 if bc else 0], dtype=self.torch.int32, device=self.device)
+            dist.broadcast(flag, self.root, group=self.group)
+            bc = bool(flag.item())
+        packed = self.scatter(arr, broadcast=bc)
+        return self.apply(packed, filter_ops=filter_ops, fill_value=fill_value, write_zero_chunks=write_zero_chunks,
+                          broadcast=bc)
+
+    def flush(self, put, filter_ops=None):
+        """s3sync of this rank's dirty chunks (local encode, ChunkStore.flush)."""
+        return self.store.flush(put, filter_ops=filter_ops)
+
+
+def scatter_exchange(scattered, plan, rank, root=0, group=None, device=None):
+    """Root -> every rank: rank r receives plan.rank_bytes[r] bytes (its pieces, the root's
+    scattered[rank_base[r]:...]).  One point-to-point message per rank (RCCL over xGMI on
+    GPUs, gloo on CPU).  Returns this rank's packed tensor."""
+    import torch
+    import torch.distributed as dist
+    nb = plan.rank_bytes[rank]
+    if rank == root:
+        peers = [r for r in range(plan.world) if r != root and plan.rank_bytes[r]]
+        parts = {r: scattered[int(plan.rank_base[r]):int(plan.rank_base[r]) + plan.rank_bytes[r]] for r in peers}
+        if dist.get_backend(group) == "nccl" and peers:
+            for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, parts[r], r, group=group) for r in peers]):
+                q.wait()
+        else:
+            reqs = [dist.isend(parts[r], r, group=group) for r in peers]
+            for q in reqs:
+                q.wait()
+        b = int(plan.rank_base[root])
+        return scattered[b:b + max(nb, 1)]
+    dev = device if device is not None else torch.device("cpu")
+    out = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+    if nb:
+        if dist.get_backend(group) == "nccl":
+            for q in dist.batch_isend_irecv([dist.P2POp(dist.irecv, out[:nb], root, group=group)]):
+                q.wait()
+        else:
+            dist.recv(out[:nb], root, group=group)
+    return out

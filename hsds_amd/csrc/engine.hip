@@ -28,6 +28,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <thread>
+#include <vector>
+
 #include "../../include/hsds_amd.h"
 #include "inflate_wave.h"
 #include "inflate2.h"
@@ -561,6 +564,7 @@ __device__ __forceinline__ void region_offsets(const hsds_copy_desc& d, int64_t 
 }
 
 __device__ __forceinline__ void copy_elem(const uint8_t* s, uint8_t* d, int itemsize) {
+  if (itemsize == 16 && !(((uintptr_t)s | (uintptr_t)d) & 15)) { *(uint4*)d = *(const uint4*)s; return; }
   if (itemsize == 4 && !(((uintptr_t)s | (uintptr_t)d) & 3)) { *(uint32_t*)d = *(const uint32_t*)s; return; }
   if (itemsize == 8 && !(((uintptr_t)s | (uintptr_t)d) & 7)) { *(uint64_t*)d = *(const uint64_t*)s; return; }
   if (itemsize == 2 && !(((uintptr_t)s | (uintptr_t)d) & 1)) { *(uint16_t*)d = *(const uint16_t*)s; return; }
@@ -1239,6 +1243,63 @@ static int grow(void** p, size_t* have, size_t need) {
   return 0;
 }
 
+// ---- host: MD5 (RFC 1321) for the chunk -> GPU partition rule (idUtil.getIdHash) ----
+namespace {
+struct Md5 {
+  uint32_t a, b, c, d;
+};
+inline uint32_t rotl32(uint32_t x, int c) { return (x << c) | (x >> (32 - c)); }
+void md5_block(Md5& h, const uint8_t* p) {
+  static const uint32_t K[64] = {
+      0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+      0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+      0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+      0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+      0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+      0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+      0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+      0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+  static const int R[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
+                            5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20,
+                            4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
+                            6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+  uint32_t m[16];
+  for (int i = 0; i < 16; i++) m[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) |
+                                      ((uint32_t)p[4 * i + 2] << 16) | ((uint32_t)p[4 * i + 3] << 24);
+  uint32_t a = h.a, b = h.b, c = h.c, d = h.d;
+  for (int i = 0; i < 64; i++) {
+    uint32_t f;
+    int g;
+    if (i < 16) { f = (b & c) | (~b & d); g = i; }
+    else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
+    else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
+    else { f = c ^ (b | ~d); g = (7 * i) & 15; }
+    const uint32_t t = d;
+    d = c; c = b;
+    b = b + rotl32(a + f + K[i] + m[g], R[i]);
+    a = t;
+  }
+  h.a += a; h.b += b; h.c += c; h.d += d;
+}
+// first 20 bits of md5(msg) (the 5 hex digits of getIdHash)
+uint32_t md5_prefix20(const uint8_t* msg, size_t n) {
+  Md5 h = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476};
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) md5_block(h, msg + i);
+  uint8_t tail[128] = {0};
+  const size_t r = n - i;
+  memcpy(tail, msg + i, r);
+  tail[r] = 0x80;
+  const size_t tl = r + 9 <= 64 ? 64 : 128;
+  const uint64_t bits = (uint64_t)n * 8u;
+  for (int k = 0; k < 8; k++) tail[tl - 8 + k] = (uint8_t)(bits >> (8 * k));
+  md5_block(h, tail);
+  if (tl == 128) md5_block(h, tail + 64);
+  const uint32_t b0 = h.a & 0xff, b1 = (h.a >> 8) & 0xff, b2 = (h.a >> 16) & 0xff;
+  return (b0 << 12) | (b1 << 4) | (b2 >> 4);
+}
+}  // namespace
+
 extern "C" {
 
 const char* hsds_version(void) { return HSDS_VERSION; }
@@ -1435,6 +1496,38 @@ int hsds_debug_profile(unsigned long long* out16, int reset) {
   (void)out16; (void)reset;
   return HSDS_ERR_UNSUPPORTED;
 #endif
+}
+
+int hsds_partition_ids(const char* prefix, int rank, const int64_t* idx, int64_t n, int world, int32_t* owner) {
+  if (!prefix || rank < 1 || rank > 32 || n < 0 || world < 1 || (n && (!idx || !owner))) return HSDS_ERR_ARG;
+  const size_t pl = strlen(prefix);
+  if (pl > 256) return HSDS_ERR_ARG;
+  for (int64_t i = 0; i < n * rank; i++)
+    if (idx[i] < 0) return HSDS_ERR_ARG;
+  auto work = [=](int64_t i0, int64_t i1) {
+    char buf[256 + 32 * 21];
+    memcpy(buf, prefix, pl);
+    for (int64_t i = i0; i < i1; i++) {
+      size_t len = pl;
+      for (int d = 0; d < rank; d++) {
+        int64_t v = idx[i * rank + d];
+        if (d) buf[len++] = '_';
+        char tmp[21];
+        int k = 0;
+        do { tmp[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+        while (k) buf[len++] = tmp[--k];
+      }
+      owner[i] = (int32_t)(md5_prefix20((const uint8_t*)buf, len) % (uint32_t)world);
+    }
+  };
+  // one host thread per 4096 ids, at most 8
+  int nt = (int)((n + 4095) / 4096);
+  if (nt > 8) nt = 8;
+  if (nt <= 1) { work(0, n); return HSDS_OK; }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+  for (auto& x : th) x.join();
+  return HSDS_OK;
 }
 
 int hsds_last_inflate_ms(hsds_engine* e, float* ms) {

@@ -682,16 +682,46 @@ class ChunkStore:
         if todo:
             res = self.reader.read(todo, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
                                    layout_class=layout_class, hyper_dims=hyper_dims)
+            init = [r.chunk_id for r, v in zip(todo, res) if isinstance(v, HTTPNotFound) and chunk_init]
+            if init:
+                self._fill_new(init, dtype, chunk_dims, fill_value)
             for r, v in zip(todo, res):
                 if isinstance(v, HTTPNotFound) and chunk_init:
-                    arr = np.full(chunk_dims, fill_value, dtype=dtype) if fill_value is not None \
-                        else np.zeros(chunk_dims, dtype=dtype)
-                    self.cache[r.chunk_id] = arr
                     v = self.cache[r.chunk_id]
                 elif isinstance(v, HTTPNotFound):
                     v = None                               # 404: no chunk
                 out[r.chunk_id] = v
         return [out[r.chunk_id] for r in reads]
+
+    def _fill_new(self, keys, dtype, chunk_dims, fill_value):
+        """get_chunk's chunk_init for missing objects (datanode_lib.py:1132-1138): a cache
+        slot per key holding the fill value (or zeros) over the full layout dims -- ONE
+        broadcast copy launch from a one-element device buffer, not one upload per chunk."""
+        import torch
+        from .engine import COPY_DESC_DTYPE
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(chunk_dims, dtype=np.int64)) * dtype.itemsize
+        one = np.zeros(1, dtype)
+        if fill_value is not None:
+            one[...] = fill_value
+        pat = one.view(np.uint8)
+        # widest pattern that tiles the chunk: 16 bytes when the element size divides it
+        unit = 16 if (16 % dtype.itemsize == 0 and nbytes % 16 == 0) else dtype.itemsize
+        pat = np.tile(pat, unit // dtype.itemsize) if unit != dtype.itemsize else pat
+        abase = self.cache.arena.buf
+        d_pat = torch.from_numpy(np.ascontiguousarray(pat).copy()).to(abase.device)
+        recs = np.zeros(len(keys), COPY_DESC_DTYPE)
+        for k, key in enumerate(keys):
+            slot = self.cache.reserve(key, chunk_dims, dtype)
+            if slot is None:
+                raise MemoryError("chunk cache full of dirty chunks")
+            recs[k]["dst_off"] = slot.data_ptr() - abase.data_ptr()
+        recs["src_off"] = 0
+        recs["dst_stride"][:, 0] = unit
+        recs["count"][:, 0] = nbytes // unit
+        recs["rank"] = 1
+        recs["itemsize"] = unit
+        self.reader.eng.copy(d_pat, abase, recs)
 
     # ---- write side (PUT_Chunk -> save_chunk -> s3sync / write_s3_obj) ------------
     def put_selections(self, writes, dtype, chunk_dims, filter_ops=None, fill_value=None, write_zero_chunks=False):
@@ -722,6 +752,9 @@ class ChunkStore:
         reads = [w[0] for w in writes]
         arrs = self.get_chunks(reads, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
                                chunk_init=True)
+        for v in arrs:
+            if isinstance(v, Exception):
+                raise v                      # the read's own error (get_chunk's 500 surfaces from PUT_Chunk)
         # pin the target slots while the update runs
         for r in reads:
             n = self.cache._lru.get(r.chunk_id)
@@ -760,6 +793,81 @@ class ChunkStore:
             out.append(bool(d))
         del arrs
         return out
+
+    def put_pieces(self, reads, d_data, make_descs, dtype, chunk_dims, filter_ops=None, fill_value=None,
+                   write_zero_chunks=False):
+        """PUT_Chunk for many chunks with the request data already in HBM (the sharded
+        write path, crawl.ShardedWriter).  `reads` are the target chunks (distinct ids),
+        `make_descs(slot_offsets)` returns the copy records d_data -> cache arena for
+        those slots (SelectionPlan.apply_descs).  The chunks are read with chunk_init
+        (RMW of an existing object, else the fill value: chunk_dn.py:174-190), then ONE
+        compare launch (chunkWriteSelection's no-change test, chunkUtil.py:983) and ONE
+        conditional copy launch update them; changed chunks (all with write_zero_chunks,
+        chunk_dn.py:306) are marked dirty (save_chunk).  Returns the dirty flag per read."""
+        import torch
+        from .selection import _kind
+        dtype = np.dtype(dtype)
+        chunk_dims = tuple(int(c) for c in chunk_dims)
+        if len({r.chunk_id for r in reads}) != len(reads):
+            raise ValueError("put_pieces takes each chunk once")
+        arrs = self.get_chunks(reads, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
+                               chunk_init=True)
+        for v in arrs:
+            if isinstance(v, Exception):
+                raise v                      # the read's own error (a 500 from get_chunk)
+        for r in reads:
+            n = self.cache._lru.get(r.chunk_id)
+            if n is None:
+                raise MemoryError("chunk cache cannot hold the write batch")
+            n.pinned = True
+        try:
+            abase = self.cache.arena.buf
+            offs = [self.cache._lru[r.chunk_id].off for r in reads]
+            dd = make_descs(offs)
+            differs = torch.zeros(max(len(reads), 1), dtype=torch.int32, device=abase.device)
+            if len(dd):
+                d_desc = self.reader.eng.compare(d_data, abase, dd, _kind(dtype), differs)
+                self.reader.eng.copy(d_data, abase, d_desc, flags=differs)
+            dirty = differs[:len(reads)].cpu().numpy().astype(bool)
+        finally:
+            for r in reads:
+                self.cache.unpin(r.chunk_id)
+        out = []
+        for r, d in zip(reads, dirty):
+            if d or write_zero_chunks:
+                self.cache.setDirty(r.chunk_id)
+            out.append(bool(d))
+        del arrs
+        return out
+
+    def encode_dirty(self, filter_ops, stream=None):
+        """The device half of flush for a dataset with a Blosc compressor (no bitshuffle):
+        ONE asynchronous hsds_encode_batch_codec of every dirty chunk straight from its cache
+        slot.  Returns (ids, frames, descs, sizes, status) -- device tensors, nothing copied
+        to the host, chunks still dirty (flush() finishes the s3sync)."""
+        import torch
+        from .engine import encode_descs
+        comp = (filter_ops or {}).get("compressor")
+        if not comp or comp == "scaleoffset" or (filter_ops or {}).get("shuffle") == 2:
+            raise ValueError("encode_dirty covers Blosc-compressed datasets without bitshuffle")
+        if nat.cname_code(comp) is None:
+            raise NotImplementedError(f"Blosc codec {comp!r} has no encoder in the hsds_amd engine")
+        ids = [k for k in list(self.cache._lru) if self.cache.isDirty(k)]
+        abase = self.cache.arena.buf
+        nodes = [self.cache._lru[k] for k in ids]
+        descs, _, dext = encode_descs([n.nbytes for n in nodes])
+        if len(ids):
+            descs["src_off"] = [n.off for n in nodes]
+        level = filter_ops.get("level", 5)
+        level = 5 if level is None else int(level)
+        frames = torch.empty(max(dext, 1), dtype=torch.uint8, device=abase.device)
+        sizes = torch.zeros(max(len(ids), 1), dtype=torch.int64, device=abase.device)
+        status = torch.full((max(len(ids), 1),), 99, dtype=torch.int32, device=abase.device)
+        if ids:
+            self.reader.eng.encode(abase, descs, frames, sizes, status, clevel=level,
+                                   shuffle=int(filter_ops.get("shuffle") or 0), typesize=1, compressor=comp,
+                                   stream=stream)
+        return ids, frames, descs, sizes, status
 
     def flush(self, put, filter_ops=None, keys=None):
         """s3sync for every dirty chunk (datanode_lib.py:1186-1318, 126-311): ONE

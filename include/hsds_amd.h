@@ -112,6 +112,13 @@ const char* hsds_strerror(int status);
 int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t unused,
                     int32_t repair_rounds);
 
+/* ---- partition ------------------------------------------------------------- */
+/* getObjPartition (hsds/util/idUtil.py:61-66, 481-486) for a batch of chunk ids of one
+ * dataset: owner[i] = int(md5(prefix + "i0_i1_..")[:5], 16) % world, where row i of the
+ * n x rank index array idx holds the chunk index (chunkUtil.getChunkId,
+ * chunkUtil.py:353-371: prefix = "c-<dset uuid>_").  Host-only; no engine needed. */
+int hsds_partition_ids(const char* prefix, int rank, const int64_t* idx, int64_t n, int world, int32_t* owner);
+
 /* ---- decode -------------------------------------------------------------- */
 /* Batched, device-resident decode.  d_src, d_chunks, d_dst, d_status are device
  * pointers; decoded chunk k is written to d_dst + d_chunks[k].dst_off and its
