@@ -88,7 +88,7 @@ def lib():
         "hsds_compress": (I64, [P, P, I64, I, I, I, P, I64]),
         "hsds_compress_codec": (I64, [P, P, I64, I, I, I, I, P, I64]),
         "hsds_last_deflate_ms": (I, [P, ctypes.POINTER(ctypes.c_float)]),
-        "hsds_encode_bitshuffle_batch": (I, [P, P, U64, P, I64, P, U64, P, P, I, I, P]),
+        "hsds_encode_bitshuffle_batch": (I, [P, P, U64, U64, P, I64, P, U64, P, P, I, I, P]),
         "hsds_bitshuffle_bound": (I64, [I64, I, I]),
         "hsds_bitshuffle_compress": (I64, [P, P, I64, I, I, P, I64]),
         "hsds_partition_ids": (I, [ctypes.c_char_p, I, P, I64, I, P]),

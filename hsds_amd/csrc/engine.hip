@@ -1079,6 +1079,32 @@ __global__ void __launch_bounds__(256) raw_copy_kernel(const uint8_t* __restrict
 // -------------------------------------------------------------------------
 constexpr int BSHUF_PARSE_LEVEL = 1;   // one hash candidate per position, as LZ4_compress_default
 
+// compact staging: exclusive prefix of the chunks' 16-byte aligned source lengths (one
+// workgroup of 1024), soffs[n] = total
+__global__ void stage_scan_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t n, uint64_t* __restrict__ soffs) {
+  __shared__ uint64_t part[1024];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const uint64_t v = i < n ? ((chunks[i].src_len + 15) & ~15ull) : 0ull;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const uint64_t y = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0ull;
+      __syncthreads();
+      part[threadIdx.x] += y;
+      __syncthreads();
+    }
+    if (i < n) soffs[i] = carry + part[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) soffs[n] = carry;
+}
+
 __global__ void bs_plan_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
                                uint32_t* __restrict__ counts, uint32_t* __restrict__ segcnt,
                                EncGeom* __restrict__ geom, int32_t* __restrict__ status, uint32_t es,
@@ -1113,17 +1139,18 @@ __global__ void bs_plan_kernel(const hsds_chunk_desc* __restrict__ chunks, int64
 __global__ void bs_fill_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
                                const uint32_t* __restrict__ offs, const EncGeom* __restrict__ geom,
                                EncItem* __restrict__ slots, int32_t* __restrict__ status, const uint8_t* stg,
-                               uint32_t slot_cap) {
+                               uint32_t slot_cap, const uint64_t* __restrict__ soffs, uint64_t stg_bytes) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
   const EncGeom g = geom[ci];
   const uint32_t o0 = offs[ci], o1 = offs[ci + 1];
   if (o1 > slot_cap && status[ci] == HSDS_OK) status[ci] = HSDS_ERR_UNSUPPORTED;
+  if (soffs[ci] + chunks[ci].src_len > stg_bytes && status[ci] == HSDS_OK) status[ci] = HSDS_ERR_ARG;
   const uint64_t bbytes = g.bs * g.ts;
   const uint32_t segs_full = hd::nsegments((uint32_t)bbytes);
   for (uint32_t k = 0; k < o1 - o0 && o0 + k < slot_cap; k++) {
     EncItem it;
-    it.src = (uint64_t)(stg + chunks[ci].src_off + k * bbytes);
+    it.src = (uint64_t)(stg + soffs[ci] + k * bbytes);
     it.len = k < g.nblocks ? (uint32_t)bbytes : g.flags * g.ts;
     it.off = 0;
     it.ts = 1;
@@ -1139,19 +1166,20 @@ __global__ void bs_fill_kernel(const hsds_chunk_desc* __restrict__ chunks, int64
 __global__ void __launch_bounds__(256) bs_trans_kernel(const uint8_t* __restrict__ src,
                                                        const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
                                                        const EncGeom* __restrict__ geom,
-                                                       const int32_t* __restrict__ status, uint8_t* __restrict__ stg) {
+                                                       const int32_t* __restrict__ status, uint8_t* __restrict__ stg,
+                                                       const uint64_t* __restrict__ soffs) {
   for (int64_t ci = blockIdx.y; ci < nchunks; ci += gridDim.y) {
     if (status[ci] != HSDS_OK) continue;
     const EncGeom g = geom[ci];
     const uint32_t bsz = (uint32_t)g.bs, es = g.ts;
     const uint32_t nq = (g.nblocks * bsz + g.flags) / 8u;
-    const uint64_t base = chunks[ci].src_off;
+    const uint64_t base = chunks[ci].src_off, sbase = soffs[ci];
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
       const uint32_t e0 = q * 8u, b = e0 / bsz;
       const uint32_t cnt = b < g.nblocks ? bsz : g.flags;
-      const uint64_t boff = base + (uint64_t)b * bsz * es;
-      bs::trans_group(HZ_GLOBAL(hz_gcu8*, src + boff), HZ_GLOBAL(hz_gu8*, stg + boff), (e0 - b * bsz) / 8u, cnt / 8u,
-                      es);
+      const uint64_t boff = (uint64_t)b * bsz * es;
+      bs::trans_group(HZ_GLOBAL(hz_gcu8*, src + base + boff), HZ_GLOBAL(hz_gu8*, stg + sbase + boff),
+                      (e0 - b * bsz) / 8u, cnt / 8u, es);
     }
   }
 }
@@ -1790,7 +1818,7 @@ static uint32_t host_bshuf_default_block(uint32_t es) {   // bs::default_block o
   return b < 128u ? 128u : b;
 }
 
-int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src_extent,
+int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src_extent, uint64_t src_bytes,
                                  const hsds_chunk_desc* d_chunks, int64_t nchunks, void* d_dst, uint64_t dst_extent,
                                  int64_t* d_sizes, int32_t* d_status, int itemsize, int block, void* stream) {
   if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
@@ -1801,9 +1829,13 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
   const uint32_t es = (uint32_t)itemsize;
   const uint64_t bsz = block ? (uint64_t)block : host_bshuf_default_block(es);
-  // every block but a chunk's last is bsz elements: slots and segments bounded by the source extent
-  const uint64_t slot_cap64 = src_extent / (bsz * es) + (uint64_t)nchunks + 64;
-  const uint64_t seg_cap64 = src_extent / hd::SEG + slot_cap64 + 64;
+  // work areas and the transposition staging are sized by the batch's own bytes (sum of
+  // src_len, 16-byte aligned per chunk: the staging holds the chunks back to back), not by
+  // the extent of the buffer they sit in (a flush from a large cache arena)
+  const uint64_t sb = src_bytes ? src_bytes + 16u * (uint64_t)nchunks : src_extent + 16u * (uint64_t)nchunks;
+  // every block but a chunk's last is bsz elements: slots and segments bounded by sb
+  const uint64_t slot_cap64 = sb / (bsz * es) + (uint64_t)nchunks + 64;
+  const uint64_t seg_cap64 = sb / hd::SEG + slot_cap64 + 64;
   if (seg_cap64 > 0xffffffffull || (uint64_t)block * es > 0xffffffffull) return HSDS_ERR_ARG;
   const uint32_t slot_cap = (uint32_t)slot_cap64, seg_cap = (uint32_t)seg_cap64;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1816,8 +1848,9 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
   const size_t sz_sp = al((size_t)seg_cap * sizeof(hd::SegParse));
   const size_t sz_meta = al((size_t)seg_cap * sizeof(SegMeta));
   const size_t sz_adler = al((size_t)slot_cap * 4);
+  const size_t sz_soffs = al((size_t)(nchunks + 1) * 8);
   const size_t need = sz_slots + sz_iout + sz_lzsize + 2 * sz_counts + 2 * sz_offs + sz_geom + sz_sp + sz_meta +
-                      sz_adler + 256;
+                      sz_adler + sz_soffs + 256;
   if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
   uint8_t* w = e->ews;
   EncItem* slots = (EncItem*)w; w += sz_slots;
@@ -1831,10 +1864,11 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
   hd::SegParse* sp = (hd::SegParse*)w; w += sz_sp;
   SegMeta* meta = (SegMeta*)w; w += sz_meta;
   uint32_t* adler = (uint32_t*)w; w += sz_adler;
+  uint64_t* soffs = (uint64_t*)w; w += sz_soffs;
   uint32_t* ctr = (uint32_t*)w;
   if (grow((void**)&e->escr, &e->escr_bytes, (size_t)seg_cap * hd::SEG_TOK * 2 + 256)) return HSDS_ERR_DEVICE;
   uint16_t* tok = (uint16_t*)e->escr;
-  if (grow((void**)&e->tmp, &e->tmp_bytes, src_extent ? src_extent : 1)) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->tmp, &e->tmp_bytes, sb ? sb : 1)) return HSDS_ERR_DEVICE;
   uint8_t* stg = e->tmp;
   if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
@@ -1844,11 +1878,12 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
                      es, (uint32_t)block, src_extent);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, segcnt, segoffs, nchunks);
+  hipLaunchKernelGGL(stage_scan_kernel, dim3(1), dim3(1024), 0, st, d_chunks, nchunks, soffs);
   hipLaunchKernelGGL(bs_fill_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, offs, geom, slots, d_status, stg,
-                     slot_cap);
+                     slot_cap, soffs, sb);
   const unsigned gy = (unsigned)(nchunks < 65535 ? nchunks : 65535);
   hipLaunchKernelGGL(bs_trans_kernel, dim3(16, gy), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, geom,
-                     d_status, stg);
+                     d_status, stg, soffs);
   auto grid_for = [&](int per_cu, int64_t cap) {
     int64_t g = (int64_t)e->num_cus * per_cu;
     if (g > cap) g = cap;
@@ -1894,7 +1929,7 @@ int64_t hsds_bitshuffle_compress(hsds_engine* e, const void* src, int64_t n, int
   int32_t* dstat = (int32_t*)(e->h_dev_dst + stat_off + 16);
   if (n && hipMemcpy(e->h_dev_src, src, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
   if (hipMemcpy(dd, &c, sizeof(c), hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
-  int r = hsds_encode_bitshuffle_batch(e, e->h_dev_src, (uint64_t)n, dd, 1, e->h_dev_dst, (uint64_t)bound, dsize,
+  int r = hsds_encode_bitshuffle_batch(e, e->h_dev_src, (uint64_t)n, (uint64_t)n, dd, 1, e->h_dev_dst, (uint64_t)bound, dsize,
                                        dstat, itemsize, block, nullptr);
   if (r) return r;
   int32_t status = 0;

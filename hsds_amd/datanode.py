@@ -364,32 +364,74 @@ def _decode_batch(eng, d_src, descs, dbuf, status, comp, shuffle, isz, blobs):
     (what _compress(shuffle=2) stores when the dataset also has one, storUtil.py:243-262)
     take two launches on the same stream, as _uncompress does (storUtil.py:189-227):
     the outer Blosc frames into a staging buffer sized by their headers' nbytes, then
-    the bitshuffle objects from there into `dbuf`.  A status from the first stage wins."""
+    the bitshuffle objects from there into `dbuf`.  A status from the first stage wins.
+
+    Each object is judged alone, as the reference's per-chunk _uncompress is: a blob that
+    is not a Blosc frame goes through zlib.decompress semantics when the compressor is
+    zlib (codec._uncompress on the engine, storUtil.py:206-217) and otherwise fails that
+    chunk only (storUtil.py:218-221); a header whose nbytes exceeds the largest
+    bitshuffle object the chunk can have (hsds_bitshuffle_bound at the smallest block)
+    fails that chunk instead of sizing the staging buffer."""
     import torch
     if not (shuffle == 2 and comp != nat.COMP_NONE):
         eng.decode(d_src, descs, dbuf, status, compressor=_comp_name(comp), shuffle=shuffle, itemsize=isz)
         return
-    from .codec import _as_bytes, _blosc_nbytes
+    from .codec import HTTPInternalServerError as _Err500, _as_bytes, _blosc_nbytes, _uncompress
     from .engine import CHUNK_DESC_DTYPE
-    inner = []
-    for b in blobs:
+    n = len(blobs)
+    pre = np.zeros(n, np.int32)                # per-chunk failures found on the host
+    inner, host_inner = [0] * n, {}
+    for k, b in enumerate(blobs):
+        cap = int(nat.lib().hsds_bitshuffle_bound(int(descs[k]["dst_len"]), isz, 8))
         nb = _blosc_nbytes(_as_bytes(b)) if len(b) else None
         if nb is None:
-            # a bare zlib stream has no recorded inner size: codec._uncompress reads it
-            raise NotImplementedError("batched read of a non-Blosc outer stream around bitshuffle objects")
-        inner.append(nb)
-    d1 = np.zeros(len(blobs), CHUNK_DESC_DTYPE)
-    d2 = np.zeros(len(blobs), CHUNK_DESC_DTYPE)
-    off = 0
-    for k, nb in enumerate(inner):
-        d1[k] = (descs[k]["src_off"], descs[k]["src_len"], off, nb)
-        d2[k] = (off, nb, descs[k]["dst_off"], descs[k]["dst_len"])
-        off += (nb + 255) // 256 * 256
+            if comp != nat.COMP_ZLIB:
+                pre[k] = nat.ERR_FRAME
+                continue
+            try:
+                raw = _uncompress(bytes(b), "zlib", 0)
+            except _Err500:
+                pre[k] = nat.ERR_DATA
+                continue
+            if len(raw) > cap:
+                pre[k] = nat.ERR_DATA
+                continue
+            host_inner[k] = raw
+            inner[k] = len(raw)
+        elif nb > cap:
+            pre[k] = nat.ERR_DATA
+        else:
+            inner[k] = nb
+    ok = np.flatnonzero(pre == 0)
+    blosc = np.array([k for k in ok if k not in host_inner], np.int64)
+    off, ioff = 0, np.zeros(n, np.int64)
+    for k in ok:
+        ioff[k] = off
+        off += (inner[k] + 255) // 256 * 256
     ibuf = torch.empty(max(off, 1), dtype=torch.uint8, device=dbuf.device)
-    st1 = torch.full_like(status, 99)
-    eng.decode(d_src, d1, ibuf, st1, compressor=_comp_name(comp), shuffle=0, itemsize=1)
-    eng.decode(ibuf, d2, dbuf, status, compressor=None, shuffle=2, itemsize=isz)
+    st1 = torch.zeros_like(status)
+    if blosc.size:
+        d1 = np.zeros(blosc.size, CHUNK_DESC_DTYPE)
+        for j, k in enumerate(blosc):
+            d1[j] = (descs[k]["src_off"], descs[k]["src_len"], ioff[k], inner[k])
+        s1 = torch.full((blosc.size,), 99, dtype=status.dtype, device=status.device)
+        eng.decode(d_src, d1, ibuf, s1, compressor=_comp_name(comp), shuffle=0, itemsize=1)
+        st1[torch.from_numpy(blosc).to(status.device)] = s1
+    for k, raw in host_inner.items():
+        if raw:
+            ibuf[int(ioff[k]):int(ioff[k]) + len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8) \
+                .to(ibuf.device, non_blocking=False)
+    if ok.size:
+        d2 = np.zeros(ok.size, CHUNK_DESC_DTYPE)
+        for j, k in enumerate(ok):
+            d2[j] = (ioff[k], inner[k], descs[k]["dst_off"], descs[k]["dst_len"])
+        s2 = torch.full((ok.size,), 99, dtype=status.dtype, device=status.device)
+        eng.decode(ibuf, d2, dbuf, s2, compressor=None, shuffle=2, itemsize=isz)
+        status[torch.from_numpy(ok).to(status.device)] = s2
     torch.where(st1 != nat.OK, st1, status, out=status)
+    if (pre != 0).any():
+        bad = np.flatnonzero(pre != 0)
+        status[torch.from_numpy(bad).to(status.device)] = torch.from_numpy(pre[bad]).to(status.device)
 
 
 def _filter_args(filter_ops, dtype):

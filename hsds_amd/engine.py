@@ -95,19 +95,23 @@ class ChunkEngine:
             raise nat.NativeError(rc, "hsds_encode_batch_codec")
         return chunk_descs
 
-    def encode_bitshuffle(self, src, chunk_descs, dst, sizes, status, itemsize, block=2048, stream=None):
+    def encode_bitshuffle(self, src, chunk_descs, dst, sizes, status, itemsize, block=2048, stream=None,
+                          src_bytes=None):
         """Asynchronously write bitshuffle+LZ4 objects (storUtil._shuffle codec 2,
         storUtil.py:103-131) for the chunks `chunk_descs` at dst_off in `dst` (dst_len =
         capacity, >= nat.lib().hsds_bitshuffle_bound(src_len, itemsize, block)).  `block`
         is the bitshuffle block in elements (HSDS config bit_shuffle_default_blocksize,
-        2048)."""
+        2048).  The engine's scratch is sized by `src_bytes` (the batch's total src_len,
+        taken from host descriptors when not given), not by the extent of `src`."""
         if isinstance(chunk_descs, np.ndarray):
             n = chunk_descs.size
+            if src_bytes is None:
+                src_bytes = int(chunk_descs["src_len"].sum()) if n else 0
             chunk_descs = to_device_bytes(chunk_descs, self.device)
         else:
             n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
         rc = nat.lib().hsds_encode_bitshuffle_batch(self.eng.h, _ptr(src), src.numel() * src.element_size(),
-                                                    _ptr(chunk_descs), n, _ptr(dst),
+                                                    int(src_bytes or 0), _ptr(chunk_descs), n, _ptr(dst),
                                                     dst.numel() * dst.element_size(), _ptr(sizes), _ptr(status),
                                                     int(itemsize), int(block), _stream_handle(stream))
         if rc != nat.OK:

@@ -205,10 +205,14 @@ int64_t hsds_compress_codec(hsds_engine* e, const void* src, int64_t n, int clev
  * the block's bit transposition, a last block of the remaining elements rounded down
  * to a multiple of 8, and the n % 8 leftover elements raw.  LZ4 bytes come from the
  * GPU writer (any valid block; they decode through bitshuffle.decompress_lz4).
- * src_extent = bytes spanned by d_src (bounds the per-block work items); dst_len
+ * src_extent = bytes spanned by d_src (descriptor bounds check); src_bytes = sum of
+ * the batch's src_len (0: use src_extent): the engine's scratch (block work items,
+ * LZ4 token segments, the transposition staging, which holds the chunks back to
+ * back) is sized by it, so a flush of a few chunks from a large arena stays small;
+ * a batch whose src_len sum exceeds src_bytes fails with HSDS_ERR_ARG.  dst_len
  * should be >= hsds_bitshuffle_bound(src_len, ...), else the chunk may fail with
  * HSDS_ERR_SIZE.  Frame sizes to d_sizes[k], statuses to d_status[k]. */
-int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src_extent,
+int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src_extent, uint64_t src_bytes,
                                  const hsds_chunk_desc* d_chunks, int64_t nchunks, void* d_dst, uint64_t dst_extent,
                                  int64_t* d_sizes, int32_t* d_status, int itemsize, int block, void* stream);
 /* Worst-case object size for n bytes (LZ4 bound per block + headers). */

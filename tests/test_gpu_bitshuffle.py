@@ -278,3 +278,45 @@ def test_compress_shuffle2(torch_dev):
         assert bytes(orc.bitshuffle_decode(orc.blosc_decode(fr, len(obj) + 64), len(raw), 4)) == raw
         assert codec._uncompress(fr, compressor=comp, shuffle=2, dtype=dt, chunk_shape=arr.shape) == raw
     assert codec._compress(raw, compressor=None, shuffle=2, dtype=dt, chunk_shape=(3, 3)) == raw
+
+
+def test_encode_scratch_sized_by_batch_not_arena(torch_dev):
+    """A flush of two dirty chunks out of a 1 GiB cache arena: the engine's scratch (block
+    work items, LZ4 token segments, transposition staging) follows the batch's bytes, so
+    the device memory it takes stays a few MiB; objects still decode through the oracle."""
+    import torch
+    from hsds_amd import _native as nat
+    from hsds_amd.engine import CHUNK_DESC_DTYPE, ChunkEngine as Engine
+    from oracle import oracle as orc
+    arena = torch.zeros(1 << 30, dtype=torch.uint8, device=torch_dev)
+    rng = np.random.default_rng(11)
+    raws = [(np.cumsum(rng.normal(size=65536)) * 10).astype("<f4").tobytes(), rng.bytes(4 * 3001)]
+    offs = [(1 << 30) - (3 << 20), (1 << 29) + 4096]
+    for o, r in zip(offs, raws):
+        arena[o:o + len(r)] = torch.from_numpy(np.frombuffer(r, np.uint8).copy()).to(torch_dev)
+    descs = np.zeros(2, CHUNK_DESC_DTYPE)
+    doff = 0
+    for i, (o, r) in enumerate(zip(offs, raws)):
+        cap = int(nat.lib().hsds_bitshuffle_bound(len(r), 4, 2048))
+        descs[i] = (o, len(r), doff, cap)
+        doff += (cap + 255) // 256 * 256
+    dst = torch.zeros(doff, dtype=torch.uint8, device=torch_dev)
+    sizes = torch.zeros(2, dtype=torch.int64, device=torch_dev)
+    status = torch.full((2,), 99, dtype=torch.int32, device=torch_dev)
+    torch.cuda.synchronize()
+    eng = Engine(0)
+    free0 = torch.cuda.mem_get_info()[0]
+    eng.encode_bitshuffle(arena, descs, dst, sizes, status, itemsize=4, block=2048)
+    torch.cuda.synchronize()
+    used = free0 - torch.cuda.mem_get_info()[0]
+    assert used < (96 << 20), used
+    assert (status.cpu().numpy() == 0).all()
+    host, sz = dst.cpu().numpy(), sizes.cpu().numpy()
+    for d, s, r in zip(descs, sz, raws):
+        fr = host[int(d["dst_off"]):int(d["dst_off"]) + int(s)].tobytes()
+        assert bytes(orc.bitshuffle_decode(fr, len(r), 4)) == r
+    # descriptors whose src_len sum exceeds the declared src_bytes fail as an argument error
+    status.fill_(99)
+    eng.encode_bitshuffle(arena, descs, dst, sizes, status, itemsize=4, block=2048, src_bytes=1024)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() != 0).any()

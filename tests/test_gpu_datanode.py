@@ -314,13 +314,55 @@ def test_put_and_flush_bitshuffle_dataset(dev, oracle_lib, with_deflate):
     # bitshuffle) when the dataset also has deflate; a corrupted object fails alone
     store = dict(flushed)
     bad = bytearray(store["k1"])
-    bad[len(bad) // 2] ^= 0xFF
-    bad[-3] ^= 0x5A
+    if with_deflate:
+        bad[4:8] = (0x7FFFFFF0).to_bytes(4, "little")   # Blosc nbytes past any chunk's object
+    else:
+        bad[12:16] = (0x7FFFFF00).to_bytes(4, "big")    # first LZ4 block size past the object
     store["k1"] = bytes(bad)
     cs2 = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
     res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in sorted(keys)], dt, dims, filter_ops=ops)
     for cid, r in zip(sorted(keys), res):
         if keys[cid] == "k1":
-            assert isinstance(r, Exception) or r.cpu().numpy().tobytes() != truth[cid].tobytes()
+            assert isinstance(r, codec.HTTPInternalServerError), r
             continue
         assert r.cpu().numpy().tobytes() == truth[cid].tobytes(), cid
+
+
+def test_bitshuffle_deflate_batch_fails_per_chunk(dev, oracle_lib):
+    """bitshuffle + deflate dataset read in one batch with objects the reference judges one
+    by one (storUtil._uncompress, storUtil.py:189-227): Blosc-wrapped (decoded), a bare
+    zlib stream around the bitshuffle object (zlib.decompress path, decoded), a zero-filled
+    short read (storUtil.py:480-485), a truncated frame and a frame with an oversized
+    nbytes (500 for that chunk only)."""
+    import torch
+    from hsds_amd import codec
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    from hsds_amd.filters import getFilterOps
+    orc = oracle_lib
+    dims, dt = (32, 100), np.dtype("<i4")
+    filters = [{"class": "H5Z_FILTER_BITSHUFFLE", "id": 32008, "name": "bitshuffle"},
+               {"class": "H5Z_FILTER_DEFLATE", "id": 1, "level": 4}]
+    ops = getFilterOps({"filter_map": {}}, "d-c", filters, dtype=dt, chunk_shape=dims)
+    rng = np.random.default_rng(4)
+    truth, store = {}, {}
+    for i in range(6):
+        a = (np.cumsum(rng.integers(-50, 50, size=dims), axis=1)).astype(dt)
+        truth[f"k{i}"] = a.tobytes()
+        obj = codec._compress(a.tobytes(), compressor=None, shuffle=2, dtype=dt, chunk_shape=dims)
+        store[f"k{i}"] = codec._compress(obj, compressor="deflate", level=4) if i != 1 else zlib.compress(obj, 6)
+        assert bytes(orc.bitshuffle_decode(obj, a.nbytes, 4)) == a.tobytes()
+    store["k2"] = store["k2"][:len(store["k2"]) // 2]                # truncated Blosc frame
+    big = bytearray(store["k3"])
+    big[4:8] = (0xFFFFFF00).to_bytes(4, "little")                     # nbytes ~4 GiB
+    store["k3"] = bytes(big)
+    reads = [ChunkRead(f"c-c_{i}", f"k{i}") for i in range(6)]
+    reads[4] = ChunkRead("c-c_4", "k4", offset=0, length=len(store["k4"]) + 10)   # short read: zeros
+    fetch = lambda k, o, n: store.get(k) if not n else store[k][o:o + n]
+    cs = ChunkStore(fetch, mem_target=1 << 24, device=dev)
+    res = cs.get_chunks(reads, dt, dims, filter_ops=ops)
+    torch.cuda.synchronize()
+    for i, r in enumerate(res):
+        if i in (2, 3, 4):
+            assert isinstance(r, codec.HTTPInternalServerError), (i, r)
+        else:
+            assert r.cpu().numpy().tobytes() == truth[f"k{i}"], i
