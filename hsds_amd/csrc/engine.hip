@@ -47,7 +47,6 @@
 
 namespace {
 
-constexpr int KSLOTS = 256;          // encode: max zlib streams per chunk (enc_plan_kernel)
 
 // ITEM_LZ4 / ITEM_BLOSCLZ: Blosc splits of the byte-LZ77 codecs (lz_wave.h)
 enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_ZSTD = 4, ITEM_INEXACT = 0x100,
@@ -686,12 +685,18 @@ __device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint6
   return bs;
 }
 
+// two passes over the same split walk: fill = 0 counts every chunk's splits (and zlib
+// segments) and its geometry; after the prefix sums, fill = 1 writes the splits compactly
+// at offs[ci] (no per-chunk split cap: a chunk whose splits pass item_cap fails alone)
 __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
                                 int64_t nchunks, EncItem* __restrict__ slots, uint32_t* __restrict__ counts,
                                 uint32_t* __restrict__ segcnt, EncGeom* __restrict__ geom,
-                                int32_t* __restrict__ status, int clevel, int shuffle, int typesize, int cname) {
+                                int32_t* __restrict__ status, int clevel, int shuffle, int typesize, int cname,
+                                const uint32_t* __restrict__ offs, uint32_t item_cap, int fill) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
+  if (fill && status[ci] != HSDS_OK) return;
+  const uint64_t base_slot = fill ? offs[ci] : 0;
   const hsds_chunk_desc c = chunks[ci];
   const uint32_t ts = typesize < 1 || typesize > 255 ? 1u : (uint32_t)typesize;
   const uint64_t nbytes = c.src_len;
@@ -719,7 +724,8 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
         const uint32_t nspl = (!(g.flags & 0x10) && !isleft) ? ts : 1u;
         const uint64_t neblock = bsz / nspl;
         for (uint32_t j = 0; j < nspl; j++) {
-          if (cnt >= (uint32_t)KSLOTS) { st = HSDS_ERR_UNSUPPORTED; break; }
+          if (cnt == 0xffffffffu) { st = HSDS_ERR_UNSUPPORTED; break; }
+          if (!fill) { cnt++; nseg += hd::nsegments((uint32_t)neblock); continue; }
           EncItem it;
           it.src = (uint64_t)(csrc + b * bs + (doshuffle ? 0 : j * neblock));
           it.len = (uint32_t)neblock;
@@ -729,11 +735,18 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
           it.chunk = (uint32_t)ci;
           it.seg0 = nseg;
           it.pad[0] = it.pad[1] = 0;
-          slots[ci * KSLOTS + cnt++] = it;
+          if (base_slot + cnt < item_cap) slots[base_slot + cnt] = it;
+          cnt++;
           nseg += hd::nsegments((uint32_t)neblock);
         }
       }
     }
+  }
+  if (fill) {
+    // splits past the slot capacity: the chunk fails (its in-capacity splits stay valid
+    // work items; layout and the raw copies skip a failed chunk)
+    if (base_slot + cnt > item_cap) status[ci] = HSDS_ERR_UNSUPPORTED;
+    return;
   }
   if (st != HSDS_OK) { cnt = 0; nseg = 0; }
   counts[ci] = cnt;
@@ -827,6 +840,7 @@ __global__ void __launch_bounds__(64) huff_kernel(const uint32_t* __restrict__ s
 // -> block bit positions, frame header, bstarts, split length prefixes, zlib headers
 __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks, uint8_t* dst_base,
                               const EncItem* __restrict__ slots, const uint32_t* __restrict__ counts,
+                              const uint32_t* __restrict__ offs,
                               const uint32_t* __restrict__ segoffs, EncGeom* __restrict__ geom,
                               const hd::SegCode* __restrict__ sc, const uint32_t* __restrict__ adler,
                               ItemOut* __restrict__ iout, hd::SegOut* __restrict__ so, int64_t* __restrict__ sizes,
@@ -842,8 +856,9 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
   if (g1 > seg_cap) { status[ci] = HSDS_ERR_UNSUPPORTED; sizes[ci] = HSDS_ERR_UNSUPPORTED; return; }
   const hsds_chunk_desc c = chunks[ci];
   EncGeom g = geom[ci];
-  const EncItem* it = slots + ci * KSLOTS;
-  ItemOut* io = iout + ci * KSLOTS;
+  const uint32_t i0 = offs[ci];
+  const EncItem* it = slots + i0;
+  ItemOut* io = iout + i0;
   uint8_t* out = dst_base + c.dst_off;
   const uint64_t maxbytes = g.nbytes + 16;
   uint32_t memcpyed = g.memcpyed;
@@ -862,7 +877,7 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
         maxout = (int64_t)maxbytes - (int64_t)nt;
         if (maxout <= 0) { memcpyed = 1; break; }
       }
-      int64_t cb = lzsize ? (int64_t)lzsize[ci * KSLOTS + k]
+      int64_t cb = lzsize ? (int64_t)lzsize[i0 + k]
                           : (int64_t)hd::stream_layout(sc + g0 + it[k].seg0, it[k].len, nullptr);
       if (cb > maxout) cb = 0;                     // compress2 / LZ4_compress would not fit
       uint32_t israw = 0;
@@ -900,10 +915,10 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
         if (last) end = ((bpos + 7u) & ~7ull) + 32u;
         hd::SegOut& o = so[g0 + it[kk].seg0 + s];
         o.bitpos = base + start;
-        o.item = (uint32_t)(ci * KSLOTS + kk);
+        o.item = i0 + kk;
         o.seg = s;
         o.flags = 1u | (last ? 2u : 0u);
-        o.adler = adler[ci * KSLOTS + kk];
+        o.adler = adler[i0 + kk];
         dw[(base + start) >> 5] = 0;
         dw[(base + end - 1) >> 5] = 0;
       }
@@ -928,7 +943,7 @@ __global__ void layout_kernel(const hsds_chunk_desc* __restrict__ chunks, int64_
       for (uint32_t j = 0; j < nspl; j++, kk++) {
         const uint32_t p = io[kk].pos;
         const uint32_t cs = io[kk].raw ? it[kk].len
-                            : lzsize ? lzsize[ci * KSLOTS + kk]
+                            : lzsize ? lzsize[i0 + kk]
                                      : (uint32_t)hd::stream_layout(sc + g0 + it[kk].seg0, it[kk].len, nullptr);
         for (int i = 0; i < 4; i++) out[p - 4 + i] = (uint8_t)(cs >> (8 * i));
         if (!io[kk].raw && !lzsize) {
@@ -1050,6 +1065,7 @@ __global__ void __launch_bounds__(256) raw_copy_kernel(const uint8_t* __restrict
                                                        const hsds_chunk_desc* __restrict__ chunks, int64_t nchunks,
                                                        uint8_t* dst_base, const EncItem* __restrict__ slots,
                                                        const uint32_t* __restrict__ counts,
+                                                       const uint32_t* __restrict__ offs,
                                                        const EncGeom* __restrict__ geom,
                                                        const ItemOut* __restrict__ iout,
                                                        const int32_t* __restrict__ status) {
@@ -1063,8 +1079,8 @@ __global__ void __launch_bounds__(256) raw_copy_kernel(const uint8_t* __restrict
     return;
   }
   const uint32_t cnt = counts[ci];
-  const EncItem* it = slots + ci * KSLOTS;
-  const ItemOut* io = iout + ci * KSLOTS;
+  const EncItem* it = slots + offs[ci];
+  const ItemOut* io = iout + offs[ci];
   for (uint32_t k = 0; k < cnt; k++)
     if (io[k].raw) wg_copy(out + io[k].pos, (const uint8_t*)it[k].src, it[k].len, it[k].ts, it[k].neb, it[k].off);
 }
@@ -1254,6 +1270,8 @@ struct hsds_engine {
   int emit_blocks_per_cu = 1;
   uint8_t* ews = nullptr;
   size_t ews_bytes = 0;
+  uint8_t* ecw = nullptr;      // encode: per-chunk plan arrays
+  size_t ecw_bytes = 0;
   uint8_t* escr = nullptr;
   size_t escr_bytes = 0;
   hipEvent_t ev2, ev3;
@@ -1409,6 +1427,7 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (e->h_dev_src) hipFree(e->h_dev_src);
   if (e->h_dev_dst) hipFree(e->h_dev_dst);
   if (e->ews) hipFree(e->ews);
+  if (e->ecw) hipFree(e->ecw);
   if (e->escr) hipFree(e->escr);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
@@ -1688,84 +1707,94 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   if (nchunks > (int64_t)(1u << 22)) return HSDS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
-  // segment capacity: every byte of every chunk at most once per SEG, plus the
-  // partial last segment of up to 16 streams per chunk (chunks beyond it fail)
-  const uint64_t seg_cap64 = dst_extent / hd::SEG + (uint64_t)nchunks * 16 + 64;
-  if (seg_cap64 > 0xffffffffull) return HSDS_ERR_ARG;
-  const uint32_t seg_cap = (uint32_t)seg_cap64;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t ns = (size_t)nchunks * KSLOTS;
-  const size_t sz_slots = al(ns * sizeof(EncItem));
-  const size_t sz_adler = al(ns * 4);
-  const size_t sz_iout = al(ns * sizeof(ItemOut));
+  // per-chunk plan arrays (own buffer: they survive the resize of the split / segment area)
   const size_t sz_counts = al((size_t)nchunks * 4);
   const size_t sz_offs = al((size_t)(nchunks + 1) * 4);
   const size_t sz_geom = al((size_t)nchunks * sizeof(EncGeom));
-  const size_t sz_sp = al((size_t)seg_cap * sizeof(hd::SegParse));
-  const size_t sz_sc = al((size_t)seg_cap * sizeof(hd::SegCode));
-  const size_t sz_so = al((size_t)seg_cap * sizeof(hd::SegOut));
-  const size_t sz_meta = al((size_t)seg_cap * sizeof(SegMeta));
-  const size_t sz_lzsize = al(ns * 4);
-  const size_t need = sz_slots + sz_adler + sz_iout + 2 * sz_counts + 2 * sz_offs + sz_geom + sz_sp + sz_sc + sz_so +
-                      sz_meta + sz_lzsize + 256;
-  if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
-  uint8_t* w = e->ews;
-  EncItem* slots = (EncItem*)w; w += sz_slots;
-  uint32_t* adler = (uint32_t*)w; w += sz_adler;
-  ItemOut* iout = (ItemOut*)w; w += sz_iout;
+  if (grow((void**)&e->ecw, &e->ecw_bytes, 2 * sz_counts + 2 * sz_offs + sz_geom + 256)) return HSDS_ERR_DEVICE;
+  uint8_t* w = e->ecw;
   uint32_t* counts = (uint32_t*)w; w += sz_counts;
   uint32_t* segcnt = (uint32_t*)w; w += sz_counts;
   uint32_t* offs = (uint32_t*)w; w += sz_offs;
   uint32_t* segoffs = (uint32_t*)w; w += sz_offs;
   EncGeom* geom = (EncGeom*)w; w += sz_geom;
+  uint32_t* ctr = (uint32_t*)w;    // [0] parse items, [1] huffman segments, [2] emit segments
+  if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
+  const int tpb = 256;
+  const int nb = (int)((nchunks + tpb - 1) / tpb);
+  // pass 1: every chunk's split and segment counts (no per-chunk split cap), prefix sums,
+  // then the exact totals to the host: the split / segment work areas (about 24 KB of
+  // parse state + tokens per 8 KiB segment) are sized by the batch, not by a worst case
+  hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
+                     (EncItem*)nullptr, counts, segcnt, geom, d_status, clevel, shuffle, typesize, cname,
+                     (const uint32_t*)nullptr, 0u, 0);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, segcnt, segoffs, nchunks);
+  uint32_t tot[2] = {0, 0};
+  if (hipMemcpyAsync(&tot[0], offs + nchunks, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(&tot[1], segoffs + nchunks, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return HSDS_ERR_DEVICE;
+  const uint32_t item_cap = tot[0] + 1, seg_cap = tot[1] + 1;
+  const size_t ns = (size_t)item_cap;
+  const size_t sz_slots = al(ns * sizeof(EncItem));
+  const size_t sz_adler = al(ns * 4);
+  const size_t sz_iout = al(ns * sizeof(ItemOut));
+  const size_t sz_sp = al((size_t)seg_cap * sizeof(hd::SegParse));
+  const size_t sz_sc = al((size_t)seg_cap * sizeof(hd::SegCode));
+  const size_t sz_so = al((size_t)seg_cap * sizeof(hd::SegOut));
+  const size_t sz_meta = al((size_t)seg_cap * sizeof(SegMeta));
+  const size_t sz_lzsize = al(ns * 4);
+  const size_t need = sz_slots + sz_adler + sz_iout + sz_sp + sz_sc + sz_so + sz_meta + sz_lzsize + 256;
+  if (grow((void**)&e->ews, &e->ews_bytes, need)) return HSDS_ERR_DEVICE;
+  w = e->ews;
+  EncItem* slots = (EncItem*)w; w += sz_slots;
+  uint32_t* adler = (uint32_t*)w; w += sz_adler;
+  ItemOut* iout = (ItemOut*)w; w += sz_iout;
   hd::SegParse* sp = (hd::SegParse*)w; w += sz_sp;
   hd::SegCode* sc = (hd::SegCode*)w; w += sz_sc;
   hd::SegOut* so = (hd::SegOut*)w; w += sz_so;
   SegMeta* meta = (SegMeta*)w; w += sz_meta;
   uint32_t* lzsize = (uint32_t*)w; w += sz_lzsize;
-  uint32_t* ctr = (uint32_t*)w;    // [0] parse items, [1] huffman segments, [2] emit segments
   // token slots: SEG_TOK per segment
   if (grow((void**)&e->escr, &e->escr_bytes, (size_t)seg_cap * hd::SEG_TOK * 2 + 256)) return HSDS_ERR_DEVICE;
   uint16_t* tok = (uint16_t*)e->escr;
-  if (hipMemsetAsync(ctr, 0, 32, st) != hipSuccess) return HSDS_ERR_DEVICE;
-  const int tpb = 256;
-  const int nb = (int)((nchunks + tpb - 1) / tpb);
+  // pass 2: the splits, compact at offs[ci]
   hipLaunchKernelGGL(enc_plan_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks, slots,
-                     counts, segcnt, geom, d_status, clevel, shuffle, typesize, cname);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, counts, offs, nchunks);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, segcnt, segoffs, nchunks);
+                     counts, segcnt, geom, d_status, clevel, shuffle, typesize, cname, (const uint32_t*)offs,
+                     item_cap, 1);
   auto grid_for = [&](int per_cu, int64_t cap) {
     int64_t g = (int64_t)e->num_cus * per_cu;
     if (g > cap) g = cap;
     return (unsigned)(g < 1 ? 1 : g);
   };
   hipEventRecord(e->ev2, st);
-  hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, nchunks * KSLOTS)), dim3(64), 0, st, slots,
+  hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, item_cap)), dim3(64), 0, st, slots,
                      offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap,
                      // lz4 (the speed codec) parses with approximate chains; zlib, lz4hc and
                      // blosclz keep the exact chains
-                     cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, (uint32_t)KSLOTS,
-                     0xffffffffu);
+                     cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, 0u, item_cap);
   if (cname == HSDS_CNAME_ZLIB) {
     hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 1, sp, meta, sc, seg_cap, clevel);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
-                       segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)nullptr);
+                       offs, segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)nullptr);
     hipLaunchKernelGGL(emit_kernel, dim3(grid_for(e->emit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 2, so, sc, sp, tok, slots, (uint32_t*)d_dst, seg_cap, clevel);
   } else {
-    const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, nchunks * KSLOTS);
+    const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, item_cap);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                        seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0,
-                       (int)(cname == HSDS_CNAME_BLOSCLZ), (uint32_t)KSLOTS, 0xffffffffu);
+                       (int)(cname == HSDS_CNAME_BLOSCLZ), 0u, item_cap);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
-                       segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)lzsize);
+                       offs, segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)lzsize);
     hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                        seg_cap, clevel, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 1,
-                       (int)(cname == HSDS_CNAME_BLOSCLZ), (uint32_t)KSLOTS, 0xffffffffu);
+                       (int)(cname == HSDS_CNAME_BLOSCLZ), 0u, item_cap);
   }
   hipLaunchKernelGGL(raw_copy_kernel, dim3((unsigned)nchunks), dim3(256), 0, st, (const uint8_t*)d_src, d_chunks,
-                     nchunks, (uint8_t*)d_dst, slots, counts, geom, iout, d_status);
+                     nchunks, (uint8_t*)d_dst, slots, counts, offs, geom, iout, d_status);
   hipEventRecord(e->ev3, st);
   e->ev_enc_valid = 1;
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;

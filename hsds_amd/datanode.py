@@ -768,7 +768,8 @@ class ChunkStore:
     # ---- write side (PUT_Chunk -> save_chunk -> s3sync / write_s3_obj) ------------
     def put_selections(self, writes, dtype, chunk_dims, filter_ops=None, fill_value=None, write_zero_chunks=False):
         """PUT_Chunk for many chunks at once (chunk_dn.py:55-314).  `writes` is a list
-        of (ChunkRead, slices, data) with data a host ndarray of the selection shape.
+        of (ChunkRead, slices, data) with data a host ndarray of the selection shape
+        (a compound field subset, PUT_Chunk's `fields`, updates those fields only).
         Every target chunk is fetched (get_chunk with chunk_init: missing chunks start
         from the fill value), then ONE compare launch (chunkWriteSelection's
         ndarray_compare, chunkUtil.py:983) and ONE conditional copy launch update the
@@ -776,8 +777,7 @@ class ChunkStore:
         chunk_dn.py:306) are marked dirty for the next flush (save_chunk,
         datanode_lib.py:1145-1183).  Returns one is_dirty flag per write."""
         import torch
-        from .engine import COPY_DESC_DTYPE
-        from .selection import _contig_slices, _kind, copy_desc
+        from .selection import _write_data, apply_writes, write_selection_descs
         dtype = np.dtype(dtype)
         chunk_dims = tuple(int(c) for c in chunk_dims)
         # requests are applied in order: writes to the same chunk go to later rounds
@@ -805,13 +805,13 @@ class ChunkStore:
             n.pinned = True
         try:
             abase = self.cache.arena.buf
-            data_parts, descs, offs = [], [], 0
-            for (r, slices, data) in writes:
-                data = np.ascontiguousarray(data, dtype=dtype)
+            data_parts, items, offs = [], [], 0
+            for wi, (r, slices, data) in enumerate(writes):
+                data = _write_data(dtype, data)      # a field subset: PUT_Chunk `fields` (chunk_dn.py:112-140)
                 slot = self.cache.node_bytes(r.chunk_id)
                 slot_off = slot.data_ptr() - abase.data_ptr()
-                descs.append(copy_desc(data.shape, _contig_slices(data.shape), chunk_dims, tuple(slices),
-                                       dtype.itemsize, src_base=offs, dst_base=slot_off))
+                items.append((wi, write_selection_descs(chunk_dims, dtype, tuple(slices), data.shape, data.dtype,
+                                                        data_base=offs, chunk_base=slot_off)))
                 data_parts.append(data.view(np.uint8).reshape(-1))
                 offs += (data.nbytes + 255) // 256 * 256
             host = np.zeros(max(offs, 1), np.uint8)
@@ -820,10 +820,7 @@ class ChunkStore:
                 host[o:o + part.size] = part
                 o += (part.size + 255) // 256 * 256
             d_data = torch.from_numpy(host).to(abase.device)
-            dd = np.concatenate(descs) if descs else np.zeros(0, COPY_DESC_DTYPE)
-            differs = torch.zeros(max(len(writes), 1), dtype=torch.int32, device=abase.device)
-            d_desc = self.reader.eng.compare(d_data, abase, dd, _kind(dtype), differs)
-            self.reader.eng.copy(d_data, abase, d_desc, flags=differs)
+            differs = apply_writes(self.reader.eng, d_data, abase, items, len(writes))
             dirty = differs[:len(writes)].cpu().numpy().astype(bool)
         finally:
             for r in reads:

@@ -435,13 +435,21 @@ def _region(shape, itemsize, slices):
     return off, st, cnt
 
 
-def copy_desc(src_shape, src_slices, dst_shape, dst_slices, itemsize, src_base=0, dst_base=0):
-    """One hsds_copy_desc record: dst[dst_slices] = src[src_slices] (shapes must agree)."""
+def copy_desc(src_shape, src_slices, dst_shape, dst_slices, itemsize, src_base=0, dst_base=0,
+              src_itemsize=None, dst_itemsize=None, inner=None):
+    """One hsds_copy_desc record: dst[dst_slices] = src[src_slices] (shapes must agree).
+    `itemsize` bytes are copied per element; the element strides of the two arrays are
+    src_itemsize / dst_itemsize (default itemsize), so a record can move one field of a
+    compound element (src_base / dst_base = the field offsets).  inner = (count, stride)
+    adds a trailing dimension (the scalars of an array field)."""
     from .engine import COPY_DESC_DTYPE
-    so, sst, scnt = _region(src_shape, itemsize, src_slices)
-    do, dstr, dcnt = _region(dst_shape, itemsize, dst_slices)
+    so, sst, scnt = _region(src_shape, src_itemsize or itemsize, src_slices)
+    do, dstr, dcnt = _region(dst_shape, dst_itemsize or itemsize, dst_slices)
     if scnt != dcnt:
         raise ValueError(f"selection shapes differ: {scnt} vs {dcnt}")
+    if inner is not None:
+        scnt, dcnt = scnt + [int(inner[0])], dcnt + [int(inner[0])]
+        sst, dstr = sst + [int(inner[1])], dstr + [int(inner[1])]
     if len(scnt) > nat.MAX_RANK:
         raise NotImplementedError(f"rank > {nat.MAX_RANK}")
     rec = np.zeros(1, COPY_DESC_DTYPE)
@@ -454,6 +462,27 @@ def copy_desc(src_shape, src_slices, dst_shape, dst_slices, itemsize, src_base=0
     rec["dst_stride"][0, :rank] = dstr
     rec["count"][0, :rank] = scnt
     return rec
+
+
+def _leaves(dt, off=0):
+    """(byte offset, scalar dtype, count) of every scalar leaf of `dt`: the units numpy's
+    array_equal compares with the leaf's own semantics (float NaN / -0.0)"""
+    if dt.subdtype is not None:
+        base, shape = dt.subdtype
+        n = int(np.prod(shape))
+        if base.names:
+            return [x for i in range(n) for x in _leaves(base, off + i * base.itemsize)]
+        return [(off, base, n)]
+    if dt.names:
+        return [x for name in dt.names for x in _leaves(dt.fields[name][0], off + dt.fields[name][1])]
+    return [(off, dt, 1)]
+
+
+def _fields(dt):
+    """(name, dtype, offset) of the top-level fields; a plain dtype is one unnamed field"""
+    if not dt.names:
+        return [(None, dt, 0)]
+    return [(n, dt.fields[n][0], dt.fields[n][1]) for n in dt.names]
 
 
 def _contig_slices(shape):
@@ -479,8 +508,12 @@ def _to_dev(arr, dev):
 
 def chunkReadSelection(chunk_arr, slices=None, select_dt=None):
     """chunkUtil.chunkReadSelection (chunkUtil.py:882-929): chunk_arr[slices] as a new
-    C-contiguous array, the strided gather running on the GPU.  Field subsets of
-    compound types (select_dt) are outside the hyperslab engine."""
+    C-contiguous array, the strided gather running on the GPU.  A field subset of a
+    compound type (select_dt with fewer fields, getSubType at chunk_dn.py:488-497) is
+    gathered field by field into a zero-filled select_dt array: one copy record per field
+    (chunk field offset -> select_dt field offset), all in one launch.  A single field
+    that is an array or a compound raises as the reference's `arr[...] = out[field]`
+    does (ValueError / TypeError)."""
     import torch
     from .engine import ChunkEngine
     arr = np.asarray(chunk_arr)
@@ -490,25 +523,138 @@ def chunkReadSelection(chunk_arr, slices=None, select_dt=None):
     slices = tuple(slices)
     if len(slices) != rank:
         raise ValueError("Selection rank does not match shape rank")
-    if select_dt is not None and len(select_dt) < len(arr.dtype):
-        raise NotImplementedError("field selection is outside the hyperslab engine")
+    dt = arr.dtype
     out_shape = tuple(len(range(*s.indices(n))) for s, n in zip(slices, arr.shape))
-    itemsize = arr.dtype.itemsize
-    out = np.empty(out_shape, arr.dtype)
+    fields = None
+    if select_dt is not None and len(select_dt) < len(dt):
+        select_dt = np.dtype(select_dt)
+        fields = list(select_dt.names)
+        for f in fields:
+            if f not in (dt.names or ()):
+                raise ValueError(f"no field of name {f}")
+            if select_dt.fields[f][0] != dt.fields[f][0]:
+                raise NotImplementedError("field selection with a converted field type")
+        if len(fields) == 1:
+            fdt = dt.fields[fields[0]][0]
+            if fdt.subdtype is not None:
+                raise ValueError(f"could not broadcast the array field {fields[0]} into shape {out_shape}")
+            if fdt.names:
+                raise TypeError(f"cannot assign the compound field {fields[0]} to a one-field structure")
+    out_dt = select_dt if fields else dt
+    out = np.zeros(out_shape, out_dt)
     if out.size == 0:
         return out
     dev = torch.device("cuda", torch.cuda.current_device())
     d_src = _to_dev(arr, dev)
-    d_dst = torch.empty(out.nbytes, dtype=torch.uint8, device=dev)
-    desc = copy_desc(arr.shape, slices, out_shape, _contig_slices(out_shape), itemsize)
+    if fields:
+        d_dst = torch.zeros(out.nbytes, dtype=torch.uint8, device=dev)
+        desc = np.concatenate([copy_desc(arr.shape, slices, out_shape, _contig_slices(out_shape),
+                                         dt.fields[f][0].itemsize, src_base=dt.fields[f][1],
+                                         dst_base=out_dt.fields[f][1], src_itemsize=dt.itemsize,
+                                         dst_itemsize=out_dt.itemsize) for f in fields])
+    else:
+        d_dst = torch.empty(out.nbytes, dtype=torch.uint8, device=dev)
+        desc = copy_desc(arr.shape, slices, out_shape, _contig_slices(out_shape), dt.itemsize)
     ChunkEngine().copy(d_src, d_dst, desc)
     out.view(np.uint8).reshape(-1)[:] = d_dst.cpu().numpy()
     return out
 
 
+def write_selection_descs(chunk_shape, chunk_dt, slices, data_shape, data_dt, data_base=0, chunk_base=0):
+    """Device records for chunkWriteSelection (chunkUtil.py:932-995) of `data` (dtype
+    data_dt, C-contiguous data_shape at data_base) into chunk[slices] (chunk_base).
+
+    Units are what the reference updates as a whole: every field of data_dt when it is a
+    field subset of chunk_dt (field-wise update, one ndarray_compare per field), else the
+    whole element (one compare; numpy assigns structured elements field by field, so
+    padding bytes are left alone).  Returns a list of units, each
+    (copy records, [(kind, compare record)] over its scalar leaves): a unit differs when
+    any of its leaves differs under the leaf's own semantics (float NaN != NaN,
+    -0.0 == 0.0), and its copy records are applied only then."""
+    chunk_dt, data_dt = np.dtype(chunk_dt), np.dtype(data_dt)
+    field_update = len(data_dt) > 0 and len(data_dt) < len(chunk_dt)
+    if field_update:
+        units = [[(chunk_dt.fields[f][1], data_dt.fields[f][1], chunk_dt.fields[f][0])] for f in data_dt.names]
+    else:
+        units = [[(off, off, fdt) for _, fdt, off in _fields(chunk_dt)]]
+    full = _contig_slices(data_shape)
+    out = []
+    for parts in units:
+        copies, leaves = [], []
+        for coff, doff, fdt in parts:
+            copies.append(copy_desc(data_shape, full, chunk_shape, slices, fdt.itemsize, src_base=data_base + doff,
+                                    dst_base=chunk_base + coff, src_itemsize=data_dt.itemsize,
+                                    dst_itemsize=chunk_dt.itemsize))
+            for loff, base, n in _leaves(fdt):
+                leaves.append((_kind(base), copy_desc(data_shape, full, chunk_shape, slices, base.itemsize,
+                                                      src_base=data_base + doff + loff,
+                                                      dst_base=chunk_base + coff + loff,
+                                                      src_itemsize=data_dt.itemsize, dst_itemsize=chunk_dt.itemsize,
+                                                      inner=(n, base.itemsize) if n > 1 else None)))
+        out.append((copies, leaves))
+    return out
+
+
+def apply_writes(eng, d_data, d_chunk, items, nwrites, stream=None):
+    """Compare + conditional copy for a batch of writes: `items` = [(write index, units
+    from write_selection_descs)].  One compare launch per leaf kind (one for plain
+    dtypes) and ONE copy launch; returns the per-write changed flags (int32 device
+    tensor, no host sync)."""
+    import torch
+    from .engine import COPY_DESC_DTYPE
+    dev = d_data.device
+    by_kind, copies, copy_unit, unit_write = {}, [], [], []
+    for w, units in items:
+        for copy_recs, leaves in units:
+            u = len(unit_write)
+            unit_write.append(w)
+            copies += copy_recs
+            copy_unit += [u] * len(copy_recs)
+            for kind, rec in leaves:
+                by_kind.setdefault(kind, ([], []))
+                by_kind[kind][0].append(rec)
+                by_kind[kind][1].append(u)
+    nunits = len(unit_write)
+    flags_w = torch.zeros(max(nwrites, 1), dtype=torch.int32, device=dev)
+    if not nunits:
+        return flags_w
+    nleaf = sum(len(v[0]) for v in by_kind.values())
+    differs = torch.zeros(nleaf, dtype=torch.int32, device=dev)
+    leaf_unit, lo = [], 0
+    for kind, (recs, us) in by_kind.items():
+        eng.compare(d_data, d_chunk, np.concatenate(recs), kind, differs[lo:lo + len(recs)], stream=stream)
+        leaf_unit += us
+        lo += len(recs)
+    if nleaf == nunits and leaf_unit == list(range(nunits)) and len(copies) == nunits:
+        unit = differs                       # one leaf and one record per unit: flags as they are
+    else:
+        unit = torch.zeros(nunits, dtype=torch.int32, device=dev)
+        unit.index_add_(0, torch.tensor(leaf_unit, dtype=torch.int64, device=dev), differs)
+    cflags = unit if len(copies) == nunits and copy_unit == list(range(nunits)) else \
+        unit[torch.tensor(copy_unit, dtype=torch.int64, device=dev)]
+    eng.copy(d_data, d_chunk, np.concatenate(copies) if copies else np.zeros(0, COPY_DESC_DTYPE),
+             flags=cflags, stream=stream)
+    flags_w.index_add_(0, torch.tensor(unit_write, dtype=torch.int64, device=dev), unit)
+    return flags_w
+
+
+def _write_data(arr_dt, data):
+    """the write's data as a C-contiguous array: a field subset keeps its fields (in the
+    chunk's field types, getSubType order), anything else takes the chunk dtype"""
+    if len(data.dtype) > 0 and len(data.dtype) < len(arr_dt):
+        for f in data.dtype.names:
+            if f not in arr_dt.names:
+                raise ValueError(f"no field of name {f}")
+        sub = np.dtype([(f, arr_dt.fields[f][0]) for f in data.dtype.names])
+        return np.ascontiguousarray(data if data.dtype == sub else data.astype(sub))
+    return np.ascontiguousarray(data, dtype=arr_dt)
+
+
 def chunkWriteSelection(chunk_arr=None, slices=None, data=None):
     """chunkUtil.chunkWriteSelection (chunkUtil.py:932-995): if data differs from
-    chunk_arr[slices] (numpy array_equal semantics) write it and return True."""
+    chunk_arr[slices] (ndarray_compare = numpy array_equal semantics) write it and return
+    True.  A compound `data` with fewer fields than the chunk is a field-wise update
+    (chunkUtil.py:956-979): each field is compared and written on its own."""
     import torch
     from .engine import ChunkEngine
     arr = chunk_arr
@@ -521,23 +667,18 @@ def chunkWriteSelection(chunk_arr=None, slices=None, data=None):
         raise ValueError("Selection rank does not match dataset rank")
     if len(data.shape) != rank:
         raise ValueError("Input arr does not match dataset rank")
-    if len(data.dtype) > 0 and len(data.dtype) < len(arr.dtype):
-        raise NotImplementedError("field updates are outside the hyperslab engine")
     sel_shape = tuple(len(range(*s.indices(n))) for s, n in zip(slices, arr.shape))
     if tuple(data.shape) != sel_shape:
         raise ValueError(f"could not broadcast input array from shape {data.shape} into shape {sel_shape}")
+    data = _write_data(arr.dtype, data)
     if data.size == 0:
         return False
-    data = np.ascontiguousarray(data, dtype=arr.dtype)
     dev = torch.device("cuda", torch.cuda.current_device())
     d_chunk = _to_dev(arr, dev)
     d_data = _to_dev(data, dev)
-    desc = copy_desc(data.shape, _contig_slices(data.shape), arr.shape, tuple(slices), arr.dtype.itemsize)
-    eng = ChunkEngine()
-    differs = torch.zeros(1, dtype=torch.int32, device=dev)
-    d_desc = eng.compare(d_data, d_chunk, desc, _kind(arr.dtype), differs)
-    eng.copy(d_data, d_chunk, d_desc, flags=differs)
-    updated = bool(differs.item())
+    units = write_selection_descs(arr.shape, arr.dtype, tuple(slices), data.shape, data.dtype)
+    flags = apply_writes(ChunkEngine(), d_data, d_chunk, [(0, units)], 1)
+    updated = bool(flags[0].item())
     if updated:
         np.copyto(arr, d_chunk.cpu().numpy().view(arr.dtype).reshape(arr.shape))
     return updated
