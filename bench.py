@@ -253,13 +253,23 @@ def run_cfg3(args, dev):
         assert np.array_equal(host[p.data_slices], c[p.chunk_slices]), f"cfg3 piece {k}"
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    plan_s = 0.0
     for _ in range(args.steps):
+        # the request's plan (chunk ids, md5 owners, pieces) and its device copy records
+        # are rebuilt every step: per-request host cost inside the timed region
+        tp = time.perf_counter()
+        p_ = crawl.SelectionPlan("d-5a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", CFG3_DIMS, CFG3_LAYOUT, CFG3_SEL,
+                                 np.int16, 1)
+        plan_s += time.perf_counter() - tp
+        rd.replan(st, p_)
         rd.read(st, slab=slab, gathered=gathered, check=False)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / args.steps
     comp = sum(len(blobs[c]) for c in ids)
     out = {"value": round(plan.slab_nbytes / el / 1e9, 3), "unit": "GB/s selected",
            "decoded_GBps": round(len(ids) * csz * 2 / el / 1e9, 2), "ms_per_step": round(el * 1e3, 3),
+           "plan_ms": round(plan_s / args.steps * 1e3, 2), "plan_note": "host SelectionPlan per step; the device "
+                                                                          "record build is inside ms_per_step",
            "chunks": len(ids), "selected_bytes": plan.slab_nbytes, "compressed_bytes": comp,
            "algorithmic_GBps": round((comp + plan.slab_nbytes) / el / 1e9, 2),
            "workload": "configs[2]: int16 512x2048x2048, 16x64x128 chunks (F1 L4), "
@@ -303,11 +313,19 @@ def run_cfg1(args, dev):
         assert np.array_equal(host[p.data_slices], c[p.chunk_slices]), f"cfg1 piece {k}"
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    plan_s = 0.0
     for _ in range(args.steps):
+        tp = time.perf_counter()
+        p_ = crawl.SelectionPlan("d-0a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", CFG1_DIMS, CFG1_LAYOUT, CFG1_SEL,
+                                 np.float32, 1)
+        plan_s += time.perf_counter() - tp
+        rd.replan(st, p_)
         rd.read(st, slab=slab, gathered=gathered, check=False)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / args.steps
     out = {"value": round(plan.slab_nbytes / el / 1e9, 3), "unit": "GB/s selected", "ms_per_step": round(el * 1e3, 3),
+           "plan_ms": round(plan_s / args.steps * 1e3, 2), "plan_note": "host SelectionPlan per step; the device "
+                                                                          "record build is inside ms_per_step",
            "chunks": len(ids), "selected_bytes": plan.slab_nbytes,
            "workload": "configs[0]: f32 4096x4096, 64x64 chunks stored uncompressed, select [1000:3000,500:3500], "
                        "gather+place"}
@@ -642,7 +660,7 @@ def run_cfg4(args, dev, rank, world):
     if rank == 0:
         host = slab[:plan.slab_nbytes].view(torch.float32).reshape(plan.slab_shape)
         for r in range(world):                                      # one piece per rank vs its raw chunk
-            if not plan.by_rank[r]:
+            if not len(plan.by_rank[r]):
                 continue
             p = plan.pieces[plan.by_rank[r][0]]
             if r == 0:
@@ -652,7 +670,13 @@ def run_cfg4(args, dev, rank, world):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    plan_s = 0.0
     for _ in range(args.cfg4_steps):
+        tp = time.perf_counter()
+        p_ = crawl.SelectionPlan("d-5a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", dims, CFG4_LAYOUT, sel, np.float32,
+                                 world)
+        plan_s += time.perf_counter() - tp
+        rd.replan(st, p_)
         rd.read(st, slab=slab, gathered=gathered, check=False)
     torch.cuda.synchronize()
     if world > 1:
@@ -666,6 +690,7 @@ def run_cfg4(args, dev, rank, world):
     n_all = len(plan.pieces)
     out = {"value": round(n_all * (1 << 20) / el / 1e9, 2), "unit": "GB/s decoded (all ranks)",
            "selected_GBps": round(plan.slab_nbytes / el / 1e9, 2), "ms_per_step": round(el * 1e3, 3),
+           "plan_ms": round(plan_s / args.cfg4_steps * 1e3, 2),
            "chunks": n_all, "chunks_per_rank": [len(b) for b in plan.by_rank],
            "gathered_bytes_from_peers": int(sum(plan.rank_bytes[r] for r in range(1, world))),
            "root_piece_check": bool(ok), "steps": args.cfg4_steps,
@@ -739,8 +764,8 @@ def main():
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
     ap.add_argument("--cfg5w", type=int, default=1, help="configs[4] through the sharded write path (all N)")
     ap.add_argument("--cfg5-steps", type=int, default=3)
-    ap.add_argument("--cfg4", type=int, default=-1,
-                    help="configs[3] sharded decode+select+RCCL gather (default: on when N > 1)")
+    ap.add_argument("--cfg4", type=int, default=1,
+                    help="configs[3] sharded decode+select (+RCCL gather when N > 1)")
     ap.add_argument("--cfg4-steps", type=int, default=3)
     ap.add_argument("--cfg4-unique", type=int, default=256)
     ap.add_argument("--cfg4-scale", type=int, default=1, help="divide the cfg4 dataset extents (local checks)")
@@ -848,7 +873,7 @@ def main():
             out["cfg5_sharded_write"] = run_cfg5_sharded(args, dev, rank, world)
         except Exception as e:   # the headline stands even if this leg fails
             out["cfg5_sharded_write"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-    if (args.cfg4 == 1) or (args.cfg4 == -1 and world > 1):
+    if args.cfg4 == 1:
         try:
             out["cfg4"] = run_cfg4(args, dev, rank, world)
         except Exception as e:   # the headline stands even if this leg fails

@@ -52,6 +52,16 @@ class CopyDesc(ctypes.Structure):
                 ("count", ctypes.c_int64 * MAX_RANK), ("rank", ctypes.c_int32), ("itemsize", ctypes.c_int32)]
 
 
+PLAN_PACK, PLAN_PLACE, PLAN_GATHER, PLAN_APPLY, PLAN_APPLY_BCAST = 0, 1, 2, 3, 4
+
+
+class PlanGeom(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int32), ("itemsize", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("nk", ctypes.c_int64 * MAX_RANK),
+                ("chunk_stride", ctypes.c_int64 * MAX_RANK), ("slab_stride", ctypes.c_int64 * MAX_RANK),
+                ("step", ctypes.c_int64 * MAX_RANK), ("slab_base", ctypes.c_int64)]
+
+
 _lib = None
 
 
@@ -92,6 +102,7 @@ def lib():
         "hsds_bitshuffle_bound": (I64, [I64, I, I]),
         "hsds_bitshuffle_compress": (I64, [P, P, I64, I, I, P, I64]),
         "hsds_partition_ids": (I, [ctypes.c_char_p, I, P, I64, I, P]),
+        "hsds_plan_descs": (I, [P, P, P, P, P, P, I64, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -1694,6 +1694,90 @@ int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const h
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
 }
 
+// ---- hyperslab plan records -------------------------------------------------
+// one thread per piece: unravel the product-grid index over the per-dimension tables,
+// then the record of the requested direction (crawl.SelectionPlan._descs on the device)
+__global__ void plan_descs_kernel(hsds_plan_geom g, const int64_t* __restrict__ tabs,
+                                  const int64_t* __restrict__ piece, const int64_t* __restrict__ poff,
+                                  const int64_t* __restrict__ coff, int64_t n, hsds_copy_desc* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int R = g.rank;
+  int64_t tab0[HSDS_MAX_RANK];
+  int64_t t = 0;
+#pragma unroll
+  for (int d = 0; d < HSDS_MAX_RANK; d++) {
+    if (d < R) { tab0[d] = t; t += 3 * g.nk[d]; }
+  }
+  int64_t gi = piece[k];
+  int64_t cst[HSDS_MAX_RANK], cnt[HSDS_MAX_RANK], dst[HSDS_MAX_RANK];
+#pragma unroll
+  for (int d = HSDS_MAX_RANK - 1; d >= 0; d--) {
+    if (d < R) {
+      const int64_t nk = g.nk[d];
+      const int64_t j = gi % nk;
+      gi /= nk;
+      cst[d] = tabs[tab0[d] + j];
+      cnt[d] = tabs[tab0[d] + nk + j];
+      dst[d] = tabs[tab0[d] + 2 * nk + j];
+    } else {
+      cst[d] = 0; cnt[d] = 0; dst[d] = 0;
+    }
+  }
+  hsds_copy_desc r;
+  int64_t pst[HSDS_MAX_RANK];
+  int64_t acc = g.itemsize;
+#pragma unroll
+  for (int d = HSDS_MAX_RANK - 1; d >= 0; d--) {
+    if (d < R) { pst[d] = acc; acc *= cnt[d]; } else pst[d] = 0;
+  }
+  const bool chunk_side = g.mode == HSDS_PLAN_PACK || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST;
+  const bool to_region = g.mode == HSDS_PLAN_PLACE || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST;
+  int64_t roff = chunk_side ? coff[k] : g.slab_base;
+  int64_t rst[HSDS_MAX_RANK];
+#pragma unroll
+  for (int d = 0; d < HSDS_MAX_RANK; d++) {
+    if (d < R) {
+      roff += chunk_side ? cst[d] * g.chunk_stride[d] : dst[d] * g.slab_stride[d];
+      rst[d] = chunk_side ? g.chunk_stride[d] * g.step[d] : g.slab_stride[d];
+    } else {
+      rst[d] = 0;
+    }
+  }
+  const bool bcast = g.mode == HSDS_PLAN_APPLY_BCAST;
+  r.src_off = (uint64_t)(to_region ? poff[k] : roff);
+  r.dst_off = (uint64_t)(to_region ? roff : poff[k]);
+#pragma unroll
+  for (int d = 0; d < HSDS_MAX_RANK; d++) {
+    r.src_stride[d] = to_region ? (bcast ? 0 : pst[d]) : rst[d];
+    r.dst_stride[d] = to_region ? rst[d] : pst[d];
+    r.count[d] = cnt[d];
+  }
+  r.rank = R;
+  r.itemsize = g.itemsize;
+  out[k] = r;
+}
+
+int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d_tabs, const int64_t* d_piece,
+                    const int64_t* d_poff, const int64_t* d_coff, int64_t n, hsds_copy_desc* d_out,
+                    void* stream) {
+  if (!e || !geom || n < 0) return HSDS_ERR_ARG;
+  if (n == 0) return HSDS_OK;
+  const hsds_plan_geom g = *geom;
+  if (g.rank < 1 || g.rank > HSDS_MAX_RANK || g.itemsize < 1 || g.mode < HSDS_PLAN_PACK ||
+      g.mode > HSDS_PLAN_APPLY_BCAST || !d_tabs || !d_piece || !d_poff || !d_out)
+    return HSDS_ERR_ARG;
+  const bool chunk_side = g.mode == HSDS_PLAN_PACK || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST;
+  if (chunk_side && !d_coff) return HSDS_ERR_ARG;
+  for (int d = 0; d < g.rank; d++)
+    if (g.nk[d] < 1) return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  const int tpb = 256;
+  hipLaunchKernelGGL(plan_descs_kernel, dim3((unsigned)((n + tpb - 1) / tpb)), dim3(tpb), 0, (hipStream_t)stream, g,
+                     d_tabs, d_piece, d_poff, d_coff, n, d_out);
+  return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
 // ---- encode -----------------------------------------------------------------
 int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_desc* d_chunks, int64_t nchunks,
                             void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,

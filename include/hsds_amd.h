@@ -169,6 +169,35 @@ int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const h
 int hsds_copy_batch_if(hsds_engine* e, const void* d_src, void* d_dst, const hsds_copy_desc* d_desc,
                        int64_t n, const int32_t* d_flags, void* stream);
 
+/* Hyperslab plan geometry for hsds_plan_descs: the pieces of a selection are the
+ * Cartesian product (C order) of per-dimension tables, one entry per chunk the slice
+ * touches in that dimension (chunkUtil.getChunkIds / getChunkCoverage / getDataCoverage,
+ * chunkUtil.py:459-790): chunk-relative start, count and slab start. */
+typedef struct {
+  int32_t rank;
+  int32_t itemsize;
+  int32_t mode;                          /* HSDS_PLAN_* */
+  int32_t reserved;
+  int64_t nk[HSDS_MAX_RANK];             /* table length per dimension                 */
+  int64_t chunk_stride[HSDS_MAX_RANK];   /* C strides of a chunk (layout), bytes       */
+  int64_t slab_stride[HSDS_MAX_RANK];    /* C strides of the slab (selection shape)    */
+  int64_t step[HSDS_MAX_RANK];           /* selection step per dimension               */
+  int64_t slab_base;                     /* slab byte offset (PLACE / GATHER)          */
+} hsds_plan_geom;
+#define HSDS_PLAN_PACK 0        /* decoded chunk [chunk_sel] -> packed piece (SN read)   */
+#define HSDS_PLAN_PLACE 1       /* packed piece -> slab [data_sel]                       */
+#define HSDS_PLAN_GATHER 2      /* slab [data_sel] -> packed piece (SN write gather)     */
+#define HSDS_PLAN_APPLY 3       /* packed piece -> chunk [chunk_sel] (PUT_Chunk)         */
+#define HSDS_PLAN_APPLY_BCAST 4 /* the one element at d_poff[k] -> chunk [chunk_sel]     */
+/* One copy record per piece, built on the device (chunk_crawl.py:118-150,395-418):
+ * d_tabs holds, per dimension d in order, nk[d] chunk-relative starts, nk[d] counts and
+ * nk[d] slab starts (int64); d_piece[k] is piece k's index in the product grid,
+ * d_poff[k] its byte offset in the packed buffer and d_coff[k] (PACK / APPLY) the byte
+ * offset of its chunk array.  Records go to d_out[0..n). */
+int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d_tabs, const int64_t* d_piece,
+                    const int64_t* d_poff, const int64_t* d_coff, int64_t n, hsds_copy_desc* d_out,
+                    void* stream);
+
 /* ---- encode (write path) ---------------------------------------------------- */
 /* Batched, device-resident encode into HSDS F1 objects: chunk k (d_chunks[k].src_off /
  * src_len in d_src) becomes a Blosc1 frame with the zlib codec at level `clevel`

@@ -292,3 +292,21 @@ def test_gloo_write_scatter(world, case):
     status, rank_bytes = q.get(timeout=5)
     assert status == "ok"
     assert sum(1 for b in rank_bytes if b) >= 2
+
+
+def test_plan_grid_equals_meshgrid_product():
+    """the plan's piece arrays are the C-order product of the per-dimension tables with
+    untouched (count 0) entries dropped per dimension, as the meshgrid + mask form"""
+    from hsds_amd import crawl
+    cases = [((300, 200, 64), (64, 64, 32), (slice(3, 300, 7), slice(1, 200, 3), slice(0, 64, 5))),
+             ((1000, 4000), (10, 100), (slice(5, 1000, 37), slice(0, 4000, 250))),
+             ((50,), (7,), (slice(3, 49, 1),)),
+             ((40, 40), (8, 8), (slice(9, 10, 1), slice(0, 40, 9)))]
+    for dims, layout, sl in cases:
+        plan = crawl.SelectionPlan("d-1a2b3c4d-5e6f7a8b-9c0d-1e2f3a-4b5c6d", dims, layout, sl, np.int16, 3)
+        per = [crawl._dim_pieces(s, c) for s, c in zip(sl, layout)]
+        grids = [np.meshgrid(*[p[k] for p in per], indexing="ij") for k in range(4)]
+        cols = [np.stack([g.reshape(-1) for g in gk], axis=1) for gk in grids]
+        keep = (cols[2] > 0).all(axis=1)
+        for got, want in zip((plan.idx, plan.cstart, plan.count, plan.dstart), cols):
+            assert np.array_equal(got, want[keep])
