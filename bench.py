@@ -80,7 +80,7 @@ def make_corpus(fmt, n_unique, base_seed, threads):
 def run_format(fmt, args, dev, rank, world):
     import torch
     from hsds_amd.engine import ChunkEngine, pack_chunks
-    threads = min(16, os.cpu_count() or 1)
+    threads = box_threads()
     base_seed = 20261015 + rank * args.chunks
     raw, blobs = make_corpus(fmt, args.unique, base_seed, threads)
     order = [i % args.unique for i in range(args.chunks)]
@@ -224,7 +224,7 @@ def run_cfg3(args, dev):
     from hsds_amd import crawl
     from oracle import oracle as orc
     from concurrent.futures import ThreadPoolExecutor
-    threads = min(16, os.cpu_count() or 1)
+    threads = box_threads()
     plan = crawl.SelectionPlan("d-5a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", CFG3_DIMS, CFG3_LAYOUT, CFG3_SEL,
                                np.int16, 1)
     ids = plan.chunk_ids(0)
@@ -274,6 +274,28 @@ def run_cfg3(args, dev):
            "algorithmic_GBps": round((comp + plan.slab_nbytes) / el / 1e9, 2),
            "workload": "configs[2]: int16 512x2048x2048, 16x64x128 chunks (F1 L4), "
                        "select [0:512:2,3:2048:5,1:2048:3], decode+gather+place"}
+    if args.cpu_seconds > 0:
+        # the reference's per-chunk path on the box's cores: _uncompress (oracle c-blosc +
+        # libz, one chunk per thread) + chunkReadSelection / slab assignment (numpy)
+        ns = min(512, len(ids))
+        samp = [enc[k % nuniq] for k in range(ns)]
+        pieces = [plan.pieces[plan.by_rank[0][k]] for k in range(ns)]
+        outb = [np.empty(csz * 2, np.uint8) for _ in range(ns)]
+        cpu_slab = np.zeros(plan.slab_shape, np.int16)
+        done, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < min(args.cpu_seconds, 4.0):
+            _, stt = orc.uncompress_batch(samp, [csz * 2] * ns, "zlib", 1, 2, nthreads=threads, out=outb)
+            assert (stt == csz * 2).all()
+            for b, p in zip(outb, pieces):
+                cpu_slab[p.data_slices] = b.view(np.int16).reshape(CFG3_LAYOUT)[p.chunk_slices]
+            done += 1
+        cel = (time.perf_counter() - t1) / done
+        sel_bytes = int(sum(p.nbytes for p in pieces))
+        assert np.array_equal(cpu_slab[pieces[1].data_slices], host[pieces[1].data_slices])
+        out["cpu_baseline"] = {"value": round(sel_bytes / cel / 1e9, 4), "unit": "GB/s selected", "cores": threads,
+                               "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"{done} x {ns} of the {len(ids)} chunks: oracle decode ({threads} threads) "
+                                         "+ numpy selection into the slab"}
     del gathered, slab, st
     torch.cuda.empty_cache()
     return out
@@ -599,7 +621,7 @@ def run_cfg5(args, dev, rank=0):
                            "format": "bitshuffle+LZ4 objects (f32, 2048-element blocks, 12-byte header)"}
     if args.cpu_seconds > 0 and rank == 0:
         from concurrent.futures import ThreadPoolExecutor
-        threads = min(16, os.cpu_count() or 1)
+        threads = box_threads()
         t1 = time.perf_counter()
         done = 0
         with ThreadPoolExecutor(threads) as ex:
@@ -612,7 +634,7 @@ def run_cfg5(args, dev, rank=0):
             "value": round(done * cbytes / cel / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{done} x 1 MiB bitshuffle+LZ4 encodes (oracle transposition + greedy LZ4)"}
     if args.cpu_seconds > 0 and rank == 0:
-        threads = min(16, os.cpu_count() or 1)
+        threads = box_threads()
         t1 = time.perf_counter()
         done = 0
         while time.perf_counter() - t1 < args.cpu_seconds / 2:
@@ -711,6 +733,31 @@ def load_traffic(args, world):
     if t.get("chunks") != args.chunks or t.get("unique") != args.unique:
         return None
     return t
+
+
+def box_threads():
+    """the host CPUs this run may use: the affinity mask, capped by the CPU share the
+    box grants (OMP_NUM_THREADS is set to it on the GPU box; nproc there shows the whole
+    machine)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def calibration():
+    p = os.path.join(ROOT, "profiles", "r2_cpu_calibration.json")
+    return json.load(open(p)) if os.path.exists(p) else None
 
 
 def cpu_baseline(blobs, seconds, threads, compressor="zlib"):
@@ -827,7 +874,7 @@ def main():
                       "compressed_bytes_per_gpu": r3["comp_bytes"], "lz_kernel_ms": round(r3["kernel_ms"], 3),
                       "algorithmic_GBps": round((r3["comp_bytes"] + r3["dec_bytes"]) / (r3["kernel_ms"] / 1e3) / 1e9, 2)}
         if args.cpu_seconds > 0:
-            threads = min(16, os.cpu_count() or 1)
+            threads = box_threads()
             v, n = cpu_baseline(r3["blobs"][:256], min(args.cpu_seconds, 4.0), threads, compressor="lz4")
             out["lz4"]["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "port",
                                           "sample": f"{n} x 1 MiB Blosc-lz4 chunk decodes, oracle frame walk + LZ4, "
@@ -844,6 +891,12 @@ def main():
             out["zstd"] = {"value": round(r4["dec_bytes"] * args.steps / r4["elapsed_s"] / 1e9, 2), "unit": "GB/s",
                            "format": "Blosc-zstd frames from libblosc 1.21 (level 5, typesize 1)",
                            "compressed_bytes_per_gpu": r4["comp_bytes"], "zstd_kernel_ms": round(r4["kernel_ms"], 3)}
+            if args.cpu_seconds > 0:
+                threads = box_threads()
+                v, n = cpu_baseline(r4["blobs"][:64], min(args.cpu_seconds, 4.0), threads, compressor="zstd")
+                out["zstd"]["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+                                               "sample": f"{n} x 1 MiB Blosc-zstd chunk decodes, oracle frame walk "
+                                                         f"+ zstd restatement, {threads} threads"}
             del r4
         except Exception as e:   # corpus writer unavailable: the headline stands
             out["zstd"] = {"error": f"{type(e).__name__}: {e}"[:200]}
@@ -856,7 +909,7 @@ def main():
                         "format": "bitshuffle+LZ4 objects (shuffle=2, f32, 2048-element blocks, 12-byte header)",
                         "compressed_bytes_per_gpu": r5["comp_bytes"], "bshuf_kernel_ms": round(r5["kernel_ms"], 3)}
         if args.cpu_seconds > 0:
-            threads = min(16, os.cpu_count() or 1)
+            threads = box_threads()
             v, n = cpu_baseline_bshuf(r5["blobs"][:64], min(args.cpu_seconds, 4.0), threads)
             out["bshuf"]["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "port",
                                             "sample": f"{n} x 1 MiB bitshuffle+LZ4 chunk decodes, oracle, "
@@ -879,12 +932,25 @@ def main():
         except Exception as e:   # the headline stands even if this leg fails
             out["cfg4"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = min(16, os.cpu_count() or 1)
+        threads = box_threads()
         sample = r1["blobs"][:256]
         v, n = cpu_baseline(sample, args.cpu_seconds, threads)
+        v1, n1 = cpu_baseline(sample[:32], min(3.0, args.cpu_seconds / 4), 1)
+        cal = calibration()
         out["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+                               "cpu_model": cpu_model(), "per_core": round(v1, 4),
                                "sample": f"{n} x 1 MiB F1 chunk decodes (256 distinct) in ~{args.cpu_seconds:.0f}s, "
-                                         f"oracle c-blosc frame walk + libz inflate, {threads} threads"}
+                                         f"oracle c-blosc frame walk + libz inflate, {threads} threads (the box's "
+                                         f"CPU share); per_core: {n1} decodes on 1 thread"}
+        if cal:
+            # oracle / shimmed-reference ratio measured in the build container
+            # (tools/calibrate_cpu.py -> profiles/r2_cpu_calibration.json)
+            out["cpu_baseline"]["reference_equiv"] = round(v / cal["ratio_oracle_over_reference_8"], 3)
+            out["cpu_baseline"]["reference_equiv_per_core"] = round(v1 / cal["ratio_oracle_over_reference_1"], 4)
+            out["cpu_baseline"]["calibration"] = "profiles/r2_cpu_calibration.json"
+        if "e2e_pcie" in out:
+            # the reference's path starts and ends in host memory too: the same CPU decode
+            out["e2e_pcie"]["cpu_baseline"] = dict(out["cpu_baseline"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
