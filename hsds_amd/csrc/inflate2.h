@@ -64,6 +64,10 @@ constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 #define HZ2_RG 8
 #endif
 constexpr uint32_t RG = HZ2_RG;           // resolve (unshuffled output): bytes a lane loads before it stores
+#ifndef HZ2_RGP
+#define HZ2_RGP 12
+#endif
+constexpr uint32_t RGP = HZ2_RGP;         // resolve (plain output): bytes a lane resolves per load round trip
 #ifndef HZ2_DW
 #define HZ2_DW 2
 #endif
@@ -199,6 +203,11 @@ HZ_HD uint32_t g_take(const Src& s, GRd& r) {
   if (--r.qn == 0u) {
     r.q0 = r.f0; r.q1 = r.f1; r.q2 = r.f2; r.q3 = r.f3;
     r.qn = 4u;
+  }
+  // the refill load sits in a block of its own, after the block whose q <- f copies retire
+  // f's old values: the load can then write f's registers directly (in one block with the
+  // copies it lands in other registers, and the copy into f waits for the load)
+  if (r.qn == 4u) {
     r.qa += 4u;
     g_quad(s, r.qa, r.f0, r.f1, r.f2, r.f3);
   }
@@ -289,6 +298,8 @@ struct Job {
 struct Stats {
   uint64_t windows, blocks, stored, tokens, matches, lanes_valid, repairs, repair_lanes, cuts, batches, hops;
   uint64_t steps_a, steps_e, extra_windows;
+  uint64_t fill_max, fill_sum, span_sum;   // resolve: per-batch max lane source-map fill, total fill, spans
+  uint64_t src_in, src_far[4];             // resolve: sources inside the batch; before it within 256/1536/4096/more
 };
 
 }  // namespace hz2
@@ -806,6 +817,7 @@ HZ_UNROLL
 #else
       for (uint32_t b0 = 0; b0 < mtotal;) {
 #endif
+        HZ_T(8);
         if (stats) stats->batches++;
         const uint32_t F = LVA_AT(ro, 0, 0);
         uint32_t nb = 0, open_ = 1;
@@ -823,6 +835,17 @@ HZ_UNROLL
           for (uint32_t q = (uint32_t)lane * 2u; q < span; q += 128u) *(uint32_t*)&sh.smap[q] = 0u;
         }
         WAVE_SYNC();
+        if (stats) {
+          uint64_t mx = 0, sm = 0;
+          for (int l = 0; l < 64; l++) {
+            uint64_t f = 0;
+            for (uint32_t u = 0; u < MPL; u++)
+              if ((uint32_t)l + 64u * u < nb) f += LVA_AT(rw, u, l) >> 16;
+            mx = f > mx ? f : mx;
+            sm += f;
+          }
+          stats->fill_max += mx; stats->fill_sum += sm; stats->span_sum += span;
+        }
         LANE_LOOP {
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) {
@@ -849,7 +872,9 @@ HZ_UNROLL
             LV(nw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
           }
         }
+        HZ_T(11);
         if (PERM) {
+          HZ_T(12);
           // unshuffled output: byte-strided over the span
           LANE_LOOP {
             uint32_t a1 = LV(ra1);
@@ -906,42 +931,43 @@ HZ_UNROLL
             }
           }
           WAVE_SYNC();
+          HZ_T(12);
           LANE_LOOP {
             uint32_t a1 = LV(ra1);
             uint64_t a2 = LV(ra2);
-            for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
-              uint32_t src[RG];
+            for (uint32_t h0 = 0; h0 < span; h0 += RGP * 64u) {
+              // each match byte's source is chased through the map and its load issued at
+              // once (a literal of the batch from LDS, anything before the batch from dst);
+              // only the values and a match-byte mask stay live until the loads land
+              uint32_t bv[RGP];
+              uint32_t mb = 0;
 HZ_UNROLL
-              for (uint32_t i = 0; i < RG; i++) {
+              for (uint32_t i = 0; i < RGP; i++) {
                 const uint32_t q = h0 + (uint32_t)lane + 64u * i;
-                uint32_t y = 0xffffffffu;
+                bv[i] = 0u;
                 if (q < span) {
                   const uint32_t dq = sh.smap[q];
                   if (dq) {
-                    y = F + q - dq;
+                    uint32_t y = F + q - dq;
                     while (y >= F) {
                       const uint32_t d2 = sh.smap[y - F];
                       if (!d2) break;
                       y -= d2;
                       if (stats) stats->hops++;
                     }
+                    if (stats) {
+                      if (y >= F) stats->src_in++;
+                      else stats->src_far[F - y <= 256u ? 0 : F - y <= 1536u ? 1 : F - y <= 4096u ? 2 : 3]++;
+                    }
+                    if (y >= F) { const uint32_t by = y - xa; bv[i] = (sh.sbuf[by >> 2] >> (8u * (by & 3u))) & 0xffu; }
+                    else bv[i] = dst[y];
+                    mb |= 1u << i;
                   }
                 }
-                src[i] = y;
-              }
-              uint32_t bv[RG];
-HZ_UNROLL
-              for (uint32_t i = 0; i < RG; i++) {
-                const uint32_t y = src[i];
-                bv[i] = 0u;
-                if (y != 0xffffffffu) {
-                  if (y >= F) { const uint32_t by = y - xa; bv[i] = (sh.sbuf[by >> 2] >> (8u * (by & 3u))) & 0xffu; }
-                  else bv[i] = dst[y];
-                }
               }
 HZ_UNROLL
-              for (uint32_t i = 0; i < RG; i++) {
-                if (src[i] != 0xffffffffu) {
+              for (uint32_t i = 0; i < RGP; i++) {
+                if ((mb >> i) & 1u) {
                   const uint32_t q = h0 + (uint32_t)lane + 64u * i, x = F + q, bx = x - xa;
                   ((uint8_t*)sh.sbuf)[bx] = (uint8_t)bv[i];
                   a1 += bv[i];
@@ -955,6 +981,7 @@ HZ_UNROLL
             LV(ra2) = a2;
           }
           WAVE_SYNC();
+          HZ_T(13);
           LANE_LOOP {
             for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
               const uint32_t x0 = xa + 4u * k;

@@ -21,8 +21,8 @@ extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, 
                 : hz2::inflate_stream<hz2::Stats, false>(*sh, job, tune, ring, &st);
   if (stats_out) {
     const uint64_t v[] = {st.windows, st.blocks, st.stored, st.tokens, st.matches, st.lanes_valid, st.repairs,
-                          st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows};
-    for (int i = 0; i < 14; i++) stats_out[i] = v[i];
+                          st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows, st.fill_max, st.fill_sum, st.span_sum, st.src_in, st.src_far[0], st.src_far[1], st.src_far[2], st.src_far[3]};
+    for (int i = 0; i < 22; i++) stats_out[i] = v[i];
   }
   free(ring);
   free(sh);

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EMU = os.path.join(ROOT, "tests", "emu", "libinflate2_emu.so")
 SRC = os.path.join(ROOT, "tests", "emu", "inflate2_emu.cpp")
 STATS = ("windows blocks stored tokens matches lanes_valid repairs repair_lanes cuts batches hops "
-         "steps_a steps_e extra_windows").split()
+         "steps_a steps_e extra_windows fill_max fill_sum span_sum src_in far256 far1536 far4096 farmore").split()
 
 
 @pytest.fixture(scope="module")

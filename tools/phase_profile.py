@@ -19,8 +19,8 @@ import torch  # noqa: E402
 from bench import make_corpus, CHUNK_BYTES  # noqa: E402
 from hsds_amd.engine import ChunkEngine, pack_chunks  # noqa: E402
 
-NAMES = ["other", "blk-hdr", "tables", "A", "A'", "repair", "valid+scan", "E", "M", "trailer", "win-end",
-         "-", "-", "-", "-", "-"]
+NAMES = ["other", "blk-hdr", "tables", "A", "A'", "repair", "valid+scan", "E", "M-fill", "trailer", "win-end",
+         "M-load", "M-resolve", "M-store", "-", "-"]
 
 
 LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
