@@ -378,10 +378,22 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
             sh.prev[p - s0] = LV(hp) == LV(hh) ? (uint16_t)((p - 1u) & 0xffffu) : sh.head[LV(hh)];
         }
         WAVE_SYNC();
+        // the head of a hash is the LAST position of the step with that hash: lanes that
+        // share a hash all store, then any lane above the stored one stores again until the
+        // highest lane holds it (which lane wins one LDS store is not defined on the GPU;
+        // the CPU emulation's lane order gives the same result)
         LANE_LOOP {
           if (LV(hh) != KEY_NONE) sh.head[LV(hh)] = (uint16_t)((g + (uint32_t)lane) & 0xffffu);
         }
         WAVE_SYNC();
+        for (;;) {
+          const uint64_t redo = WAVE_BALLOT(LV(hh) != KEY_NONE && ((sh.head[LV(hh)] - g) & 0xffffu) < (uint32_t)lane);
+          if (!redo) break;
+          LANE_LOOP {
+            if ((redo >> lane) & 1ull) sh.head[LV(hh)] = (uint16_t)((g + (uint32_t)lane) & 0xffffu);
+          }
+          WAVE_SYNC();
+        }
       }
     } else if (!tune.stored) {
       // ---- exact hash chains, 64 positions per step ----

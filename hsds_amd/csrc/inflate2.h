@@ -163,14 +163,30 @@ HZ_HD Perm perm_make(uint32_t n, uint32_t N, uint32_t x0) {
 // stream base).  Bits past the stream end are whatever the clamped loads return: the decode
 // of the true path never reads them (a token reaching past the end ends the window beyond
 // limit_bits, which fails as truncated); speculative lanes may.
+//
+// Epoch refills (HZ2_EPOCH > 0).  A wave has ONE vmcnt counter for all 64 lanes, so a lane
+// that waits for its own prefetched quad waits for every load issued before it -- including
+// the quads other lanes issued one token earlier: with a per-lane refill, some lane refills
+// at almost every token and the whole wave pays a memory latency per token.  With epochs,
+// loads are issued only at wave-uniform epoch boundaries (every HZ2_EPOCH wave iterations)
+// into a third quad h; the next boundary first moves h into f (its load had a whole epoch
+// to land) and then issues the next one, so the waits inside an epoch are gone.  A lane that
+// runs dry inside an epoch takes h at once (a wait, but rare: q + f hold up to 8 words).
+#ifndef HZ2_EPOCH
+#define HZ2_EPOCH 8
+#endif
 struct GRd {
   uint64_t bb;
   uint32_t avail;
   uint32_t pos;
-  uint32_t qa;         // dword index of the quad after q (= the quad in f)
+  uint32_t qa;         // dword index of the next quad to load (epochs: into h, else into f)
   uint32_t qn;         // words left in q
   uint32_t q0, q1, q2, q3;
   uint32_t f0, f1, f2, f3;
+#if HZ2_EPOCH
+  uint32_t fh;         // bit 0: f holds a quad; bit 1: h holds an issued load
+  uint32_t h0, h1, h2, h3;
+#endif
 };
 
 struct Src {
@@ -196,6 +212,65 @@ HZ_HD void g_quad(const Src& s, uint32_t qa, uint32_t& a0, uint32_t& a1, uint32_
   memcpy(&a0, t, 4); memcpy(&a1, t + 4, 4); memcpy(&a2, t + 8, 4); memcpy(&a3, t + 12, 4);
 #endif
 }
+
+#if HZ2_EPOCH
+HZ_HD uint32_t g_take(const Src& s, GRd& r) {
+  const uint32_t w = r.q0;
+  r.q0 = r.q1; r.q1 = r.q2; r.q2 = r.q3;
+  if (--r.qn == 0u) {
+    // stream order is q, f, h, then quad qa
+    if (r.fh & 1u) {
+      r.q0 = r.f0; r.q1 = r.f1; r.q2 = r.f2; r.q3 = r.f3;
+      r.fh &= ~1u;
+    } else if (r.fh & 2u) {
+      r.q0 = r.h0; r.q1 = r.h1; r.q2 = r.h2; r.q3 = r.h3;
+      r.fh &= ~2u;
+    } else {
+      g_quad(s, r.qa, r.q0, r.q1, r.q2, r.q3);
+      r.qa += 4u;
+    }
+    r.qn = 4u;
+  }
+  return w;
+}
+
+// wave-uniform epoch boundary: h (issued an epoch ago) moves into an empty f, and an empty h
+// is issued
+HZ_HD void g_epoch(const Src& s, GRd& r) {
+  if ((r.fh & 3u) == 2u) {
+    r.f0 = r.h0; r.f1 = r.h1; r.f2 = r.h2; r.f3 = r.h3;
+    r.fh = 1u;
+  }
+  if (!(r.fh & 2u)) {
+    g_quad(s, r.qa, r.h0, r.h1, r.h2, r.h3);
+    r.qa += 4u;
+    r.fh |= 2u;
+  }
+}
+
+HZ_HD void g_init(const Src& s, GRd& r, uint32_t p) {
+  const uint32_t k = p >> 5, qa = k & ~3u, qi = k & 3u;
+  uint32_t a0, a1, a2, a3;
+  g_quad(s, qa, a0, a1, a2, a3);
+  g_quad(s, qa + 4u, r.f0, r.f1, r.f2, r.f3);
+  g_quad(s, qa + 8u, r.h0, r.h1, r.h2, r.h3);
+  r.fh = 3u;
+  r.qa = qa + 12u;
+  // shift register starts at word qi of the quad
+  r.q0 = qi == 0u ? a0 : qi == 1u ? a1 : qi == 2u ? a2 : a3;
+  r.q1 = qi == 0u ? a1 : qi == 1u ? a2 : a3;
+  r.q2 = qi == 0u ? a2 : a3;
+  r.q3 = a3;
+  r.qn = 4u - qi;
+  const uint32_t sh = p & 31u;
+  const uint32_t w0 = g_take(s, r);
+  const uint32_t w1 = g_take(s, r);
+  r.bb = (((uint64_t)w1 << 32) | w0) >> sh;
+  r.avail = 64u - sh;
+  r.pos = p;
+}
+#else
+HZ_HD void g_epoch(const Src&, GRd&) {}
 
 HZ_HD uint32_t g_take(const Src& s, GRd& r) {
   const uint32_t w = r.q0;
@@ -233,6 +308,7 @@ HZ_HD void g_init(const Src& s, GRd& r, uint32_t p) {
   r.avail = 64u - sh;
   r.pos = p;
 }
+#endif
 
 HZ_HD void g_fill(const Src& s, GRd& r) {
   if (r.avail < 32u) {
@@ -312,10 +388,18 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
 #define LV_AT(v, i) ((uint32_t)__shfl((int)(v), (int)(i), 64))
 #define LANE_ARR(T, name, n) T name[n]
 #define LVA_AT(arr, u, i) ((uint32_t)__shfl((int)hz2::sel4(arr, u), (int)(i), 64))
+// a lane counter made wave-uniform (the first active lane's), for epoch boundaries
+#define HZ2_UNI(v) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(v)))
 #else
+#define HZ2_UNI(v) (v)
 #define LV_AT(v, i) ((v)[i])
 #define LANE_ARR(T, name, n) T name[64][n]
 #define LVA_AT(arr, u, i) ((arr)[i][u])
+#endif
+#if HZ2_EPOCH
+#define HZ2_TICK(it) do { if ((HZ2_UNI(++(it)) % (uint32_t)HZ2_EPOCH) == 0u) hz2::g_epoch(S, r); } while (0)
+#else
+#define HZ2_TICK(it) do { ++(it); } while (0)
 #endif
 
 namespace hz2 {
@@ -535,17 +619,21 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         GRd r;
         g_init(S, r, p0);
         uint32_t steps = 0;
-        while (r.pos < ss) { (void)next_token(&sh, S, r); steps++; }
         uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0;
+        // one loop for the warm-up (tokens before ss are decoded and dropped: whatever they
+        // are, even invalid codes, which advance by their table length) and the segment
         while (r.pos < se) {
-          if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
+          const bool inseg = r.pos >= ss;
+          if (inseg && nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
           const uint32_t tp = r.pos;
           const uint32_t t = next_token(&sh, S, r);
-          steps++;
-          if (t == T_EOB || t == T_ERR) { e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; break; }
-          if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
-          o += tok_len(t);
-          m += (t & T_MATCH) ? 1u : 0u;
+          if (inseg) {
+            if (t == T_EOB || t == T_ERR) { e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; break; }
+            if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
+            o += tok_len(t);
+            m += (t & T_MATCH) ? 1u : 0u;
+          }
+          HZ2_TICK(steps);
         }
         sh.nrec[lane] = nr;
         sh.syncw[lane] = lane == 0 ? 0u : SYNC_NONE;
@@ -565,7 +653,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         if (e == END_NONE && (lane_) < 63) {                                                     \
           const uint32_t base = ws + (uint32_t)((lane_) + 1) * L;                                \
           const uint32_t nrn = sh.nrec[(lane_) + 1];                                             \
-          uint32_t k = 0;                                                                        \
+          uint32_t k = 0, ct = 0;                                                                \
           res = SYNC_FAIL;                                                                       \
           for (;;) {                                                                             \
             const uint32_t rel = r.pos - base;                                                   \
@@ -580,6 +668,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; res = SYNC_NONE; break; } \
             o += hz2::tok_len(t);                                                                \
             m += (t & T_MATCH) ? 1u : 0u;                                                        \
+            HZ2_TICK(ct);                                                                        \
           }                                                                                      \
         }                                                                                        \
         if ((lane_) < 63) sh.syncw[(lane_) + 1] = res;                                           \
@@ -603,7 +692,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
             GRd r;
             g_init(S, r, sh.endp[lane - 1]);
-            uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0;
+            uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0, ct = 0;
             while (r.pos < se || nr == 0) {
               if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
               const uint32_t tp = r.pos;
@@ -612,6 +701,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
               if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
               o += tok_len(t);
               m += (t & T_MATCH) ? 1u : 0u;
+              HZ2_TICK(ct);
             }
             sh.nrec[lane] = nr;
             sh.syncw[lane] = 0;                       // its path starts at record 0
@@ -734,7 +824,11 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           };
           while (r.pos < stop) {
             const uint32_t t = next_token(&sh, S, r);
+#ifndef HZ2_EPOCH_NO_E
+            HZ2_TICK(steps);
+#else
             steps++;
+#endif
             if (!(t & T_MATCH)) {
 #ifndef HZ2_EXP_NOSTORE
               if (PERM) {

@@ -223,6 +223,40 @@ def test_streams_equal_cpu_emulation(dev):
             assert out.view(np.uint8)[:r].tobytes() == fb[start + 4:start + 4 + cs].tobytes(), (seed, b)
 
 
+def test_lz4_streams_equal_cpu_emulation(dev):
+    """Blosc-lz4 objects are parsed with the approximate chains (level + 100): the hash head
+    of a step is its highest lane with that hash, on the GPU as in the emulator, so every
+    LZ4 block the GPU writes equals the emulator's block byte for byte."""
+    import ctypes
+    import os
+    from hsds_amd import codec
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu", "libdeflate_emu.so")
+    L = ctypes.CDLL(lib)
+    L.emu_lz4_block.restype = ctypes.c_int64
+    L.emu_lz4_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+    rng = np.random.default_rng(9)
+    inputs = [smooth(5, 1 << 20), rng.integers(0, 4, 400000, dtype=np.uint8).tobytes(),
+              (np.arange(300000) % 97).astype(np.uint8).tobytes()]
+    for k, data in enumerate(inputs):
+        for level in (1, 5, 9):
+            frame = codec._compress(data, compressor="lz4", level=level, shuffle=1)
+            h = header(frame)
+            if h["flags"] & 0x02:
+                continue                        # memcpyed: no LZ4 block
+            bs, nblocks = h["blocksize"], (h["nbytes"] + h["blocksize"] - 1) // h["blocksize"]
+            fb = np.frombuffer(frame, np.uint8)
+            for b in range(nblocks):
+                start = int(fb[16 + 4 * b:20 + 4 * b].view("<i4")[0])
+                cs = int(fb[start:start + 4].view("<i4")[0])
+                blk = np.frombuffer(data[b * bs:(b + 1) * bs], np.uint8)
+                if cs == len(blk):
+                    continue                    # raw split
+                out = np.zeros(len(blk) + 4096, np.uint8)
+                r = L.emu_lz4_block(blk.ctypes.data, len(blk), out.ctypes.data, out.size, 100 + level)
+                assert r == cs, (k, level, b, r, cs)
+                assert out[:r].tobytes() == fb[start + 4:start + 4 + cs].tobytes(), (k, level, b)
+
+
 # ---- the lz4 / lz4hc write path (Blosc codec 1, LZ4 blocks from the parse tokens) ----
 
 @pytest.mark.parametrize("name", sorted(INPUTS))
