@@ -274,6 +274,13 @@ def run_cfg3(args, dev):
            "algorithmic_GBps": round((comp + plan.slab_nbytes) / el / 1e9, 2),
            "workload": "configs[2]: int16 512x2048x2048, 16x64x128 chunks (F1 L4), "
                        "select [0:512:2,3:2048:5,1:2048:3], decode+gather+place"}
+    tr = load_traffic(args, 1, "_cfg3")
+    if tr is not None:
+        # HBM bytes of every kernel of one step (PMC passes) against the algorithmic bytes
+        out["traffic"] = tr["bytes_per_step"]
+        out["traffic_undoubled"] = tr["bytes_per_step_undoubled"]
+        out["traffic_ratio"] = round(tr["bytes_per_step"] / (comp + plan.slab_nbytes), 3)
+        out["traffic_source"] = tr["source"]
     if args.cpu_seconds > 0:
         # the reference's per-chunk path on the box's cores: _uncompress (oracle c-blosc +
         # libz, one chunk per thread) + chunkReadSelection / slab assignment (numpy)
@@ -723,14 +730,18 @@ def run_cfg4(args, dev, rank, world):
     return out
 
 
-def load_traffic(args, world):
-    """HBM bytes per inflate launch from the committed PMC passes (tools/pmc_traffic.sh):
-    2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
-    p = os.path.join(ROOT, "profiles", "r1_traffic.json")
+TRAFFIC_ROUND = "r2"
+
+
+def load_traffic(args, world, leg=""):
+    """HBM bytes per inflate launch (or per cfg3 step, leg="_cfg3") from the committed PMC
+    passes (tools/pmc_traffic.sh): 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md
+    HBM section) + WRITE_SIZE."""
+    p = os.path.join(ROOT, "profiles", f"{TRAFFIC_ROUND}_traffic{leg}.json")
     if not os.path.exists(p):
         return None
     t = json.load(open(p))
-    if t.get("chunks") != args.chunks or t.get("unique") != args.unique:
+    if not leg and (t.get("chunks") != args.chunks or t.get("unique") != args.unique):
         return None
     return t
 
@@ -816,6 +827,8 @@ def main():
     ap.add_argument("--cfg4-steps", type=int, default=3)
     ap.add_argument("--cfg4-unique", type=int, default=256)
     ap.add_argument("--cfg4-scale", type=int, default=1, help="divide the cfg4 dataset extents (local checks)")
+    ap.add_argument("--headline", type=int, default=1,
+                    help="0: skip the configs[1] headline and print only the selected legs (profiling passes)")
     args = ap.parse_args()
 
     import torch
@@ -827,6 +840,18 @@ def main():
         torch.distributed.init_process_group("nccl", timeout=datetime.timedelta(seconds=300))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+
+    if not args.headline:
+        legs = {}
+        if world == 1 and args.cfg3:
+            legs["cfg3"] = run_cfg3(args, dev)
+        if world == 1 and args.cfg1:
+            legs["cfg1"] = run_cfg1(args, dev)
+        if rank == 0:
+            print(json.dumps({"metric": "profiling pass (no headline)", "legs": legs}), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
 
     r1 = run_format("F1", args, dev, rank, world)
     r2 = run_format("F2", args, dev, rank, world) if args.f2 else None
@@ -862,6 +887,7 @@ def main():
     tr = load_traffic(args, world)
     if tr is not None:
         out["roofline"]["traffic"] = tr["bytes_per_launch"]
+        out["roofline"]["traffic_undoubled"] = tr.get("bytes_per_launch_undoubled")
         out["roofline"]["traffic_source"] = tr["source"]
     if r2 is not None:
         v2 = r2["dec_bytes"] * world * args.steps / r2["elapsed_s"] / 1e9

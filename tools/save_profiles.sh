@@ -12,9 +12,9 @@ if [ -f gpurun_out/traffic/traffic.json ]; then
 import json, sys
 r = sys.argv[1]
 t = json.load(open("gpurun_out/traffic/traffic.json"))
-t["source"] = f"profiles/{r}_traffic.json (tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE)"
 json.dump(t, open(f"profiles/{r}_traffic.json", "w"), indent=1)
 PY
+  [ -f gpurun_out/traffic/traffic_cfg3.json ] && cp gpurun_out/traffic/traffic_cfg3.json profiles/${R}_traffic_cfg3.json
   mkdir -p profiles/${R}_pmc_traffic
   cp gpurun_out/traffic/fetch/*counter_collection.csv gpurun_out/traffic/write/*counter_collection.csv profiles/${R}_pmc_traffic/
 fi
