@@ -72,6 +72,21 @@ constexpr uint32_t RGP = HZ2_RGP;         // resolve (plain output): bytes a lan
 #define HZ2_DW 2
 #endif
 constexpr uint32_t DW = HZ2_DW;           // resolve (plain output): dwords a lane loads before it stores
+#ifndef HZ2_OWIN
+#define HZ2_OWIN 32
+#endif
+constexpr uint32_t OWIN = HZ2_OWIN;       // phase E (plain output): literal window bytes per lane (aligned,
+                                          // written whole: partial cache lines cost an L2 fill + write-back)
+static_assert(OWIN == 32 || OWIN == 64, "OWIN: 32 or 64 bytes (the byte mask is 64 bits)");
+constexpr uint32_t OSH = OWIN == 32 ? 5u : 6u;
+// phase E: match records are staged per lane and stored as whole aligned 32-byte groups
+// (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
+// bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
+#ifndef HZ2_RGRP
+#define HZ2_RGRP 4
+#endif
+constexpr uint32_t RGRP = HZ2_RGRP;
+static_assert(RGRP == 4 || RGRP == 8, "RGRP: 4 or 8 records");
 constexpr uint32_t SYNC_NONE = 0xfeu;     // predecessor ended (EOB / ERR / CUT): lane beyond the window
 constexpr uint32_t SYNC_FAIL = 0xffu;     // predecessor never met this lane's recorded path
 constexpr uint32_t END_NONE = 0, END_EOB = 1, END_ERR = 2, END_CUT = 3;
@@ -100,7 +115,10 @@ struct alignas(16) Shared {
       uint8_t lens[320 + 32];
     };
     uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
-    alignas(16) uint8_t ostage[WAVE][32];   // phase E (plain output): each lane's current 32-byte output window
+    struct {                      // phase E
+      alignas(16) uint8_t ostage[WAVE][OWIN];   // plain output: each lane's current literal window
+      uint64_t rstage[WAVE][RGRP];              // each lane's current group of match records
+    };
     struct {                      // phase M
       uint16_t smap[SPAN];        // batch byte -> distance to its source (0: literal)
       uint32_t sbuf[SPAN / 4 + 2];   // plain output: the batch's aligned dwords, patched in LDS
@@ -797,27 +815,26 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           uint32_t o = lo_x, mi = LV(mbase);
           uint32_t a1 = 0;
           uint64_t a2 = 0;
-          uint64_t pend = 0;
-          uint32_t haspend = 0;
-          const uint32_t A = (uint32_t)((uintptr_t)job.dst & 31u);
-          uint32_t cw = 0xffffffffu, msk = 0;
+          const uint32_t m0 = mi;                          // the lane's first record
+          const uint32_t A = (uint32_t)((uintptr_t)job.dst & (OWIN - 1u));
+          uint32_t cw = 0xffffffffu;
+          uint64_t msk = 0;
           auto flush = [&]() {
             if (!msk) return;
-            const uint32_t wx = (cw << 5) - A;          // stream position of the window's byte 0
-            if ((int32_t)wx >= (int32_t)lo_x && wx + 32u <= hi_x) {
+            const uint32_t wx = (cw << OSH) - A;        // stream position of the window's byte 0
+            if ((int32_t)wx >= (int32_t)lo_x && wx + OWIN <= hi_x) {
 #if HZ_GPU
               typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
               typedef __attribute__((address_space(1))) u32x4 gu32x4;
-              const u32x4 v0 = *(const u32x4*)&sh.ostage[lane][0];
-              const u32x4 v1 = *(const u32x4*)&sh.ostage[lane][16];
-              *(gu32x4*)(dst + wx) = v0;
-              *(gu32x4*)(dst + wx + 16u) = v1;
+HZ_UNROLL
+              for (uint32_t k = 0; k < OWIN; k += 16u)
+                *(gu32x4*)(dst + wx + k) = *(const u32x4*)&sh.ostage[lane][k];
 #else
-              memcpy(dst + wx, &sh.ostage[lane][0], 32);
+              memcpy(dst + wx, &sh.ostage[lane][0], OWIN);
 #endif
             } else {
-              for (uint32_t m = msk; m; m &= m - 1u) {
-                const uint32_t b = (uint32_t)__builtin_ctz(m);
+              for (uint64_t m = msk; m; m &= m - 1u) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
                 dst[wx + b] = sh.ostage[lane][b];
               }
             }
@@ -834,10 +851,10 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
               if (PERM) {
                 dst[perm_at(P, o)] = (uint8_t)t;
               } else {
-                const uint32_t ax = A + o, w = ax >> 5;
+                const uint32_t ax = A + o, w = ax >> OSH;
                 if (w != cw) { flush(); cw = w; msk = 0; }
-                sh.ostage[lane][ax & 31u] = (uint8_t)t;
-                msk |= 1u << (ax & 31u);
+                sh.ostage[lane][ax & (OWIN - 1u)] = (uint8_t)t;
+                msk |= 1ull << (ax & (OWIN - 1u));
               }
 #endif
               a1 += t;
@@ -847,30 +864,36 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
               const uint32_t ln = (t >> 16) & 0x1ffu, d = (t & 0x7fffu) + 1u;
               if (d > o) { err = 1; break; }
               const uint64_t rv = (uint64_t)o | ((uint64_t)((ln << 16) | (d - 1u)) << 32);
-#ifndef HZ2_EXP_NOSTORE
-              if (haspend) {                           // records mi-1 (even) and mi: one 16-byte store
+#if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
+              sh.rstage[lane][mi & (RGRP - 1u)] = rv;
+              if ((mi & (RGRP - 1u)) == RGRP - 1u) {
+                const uint32_t g = mi & ~(RGRP - 1u);
+                if (g >= m0) {                         // a whole group of this lane: 32 bytes at once
 #if HZ_GPU
-                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-                typedef __attribute__((address_space(1))) u64x2 gu64x2;
-                u64x2 v;
-                v.x = pend; v.y = rv;
-                *(gu64x2*)(ring64 + mi - 1u) = v;
+                  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                  typedef __attribute__((address_space(1))) u64x2 gu64x2;
+HZ_UNROLL
+                  for (uint32_t k = 0; k < RGRP; k += 2u)
+                    *(gu64x2*)(ring64 + g + k) = *(const u64x2*)&sh.rstage[lane][k];
 #else
-                ring64[mi - 1u] = pend; ring64[mi] = rv;
+                  for (uint32_t k = 0; k < RGRP; k++) ring64[g + k] = sh.rstage[lane][k];
 #endif
-                haspend = 0;
-              } else if (!(mi & 1u)) {
-                pend = rv; haspend = 1;
-              } else {
-                ring64[mi] = rv;
+                } else {                               // the group starts in the previous lane's records
+                  for (uint32_t k = m0; k <= mi; k++) ring64[k] = sh.rstage[lane][k & (RGRP - 1u)];
+                }
               }
 #endif
               mi++;
               o += ln;
             }
           }
+#if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
+          {                                            // the lane's last, partial group
+            const uint32_t g = mi & ~(RGRP - 1u);
+            for (uint32_t k = g > m0 ? g : m0; k < mi; k++) ring64[k] = sh.rstage[lane][k & (RGRP - 1u)];
+          }
+#endif
 #ifndef HZ2_EXP_NOSTORE
-          if (haspend) ring64[mi - 1u] = pend;
           if (!PERM) flush();
 #endif
           LV(s1) = (LV(s1) + a1 % ADLER_MOD) % ADLER_MOD;

@@ -20,5 +20,6 @@ d_st = torch.zeros(n, dtype=torch.int32, device=dev)
 for _ in range(2):
     eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
 torch.cuda.synchronize()
-assert (d_st.cpu().numpy() == 0).all()
+if not os.environ.get("HZ_NOCHECK"):
+    assert (d_st.cpu().numpy() == 0).all()
 print("pmc_run done", fmt, n, eng.last_inflate_ms(), "ms")
