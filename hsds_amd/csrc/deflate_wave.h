@@ -51,6 +51,8 @@ constexpr int RING = 2 * SEG;               // LDS input ring: window + current 
 constexpr int RWORDS = RING / 4;
 constexpr int LOOK = 4;                     // bytes staged past the segment end (hashes)
 constexpr uint32_t WIN = SEG - 2 * LOOK;    // farthest match source before the segment
+constexpr uint32_t FARW = 32768;            // zlib window: with a far ring, matches reach this far
+                                            // (candidates past the LDS ring come from HBM)
 constexpr int HBITS = 11;
 constexpr int HSIZE = 1 << HBITS;
 constexpr int LANE_MAX = SEG / WAVE;        // input bytes per lane (a full segment)
@@ -69,13 +71,23 @@ struct Tune {
   uint32_t stored;   // 1: level 0, stored blocks only
   uint32_t fast_head; // 1: no exact chains (LZ4 items): prev[p] = the hash head of the
                       // previous 64-position step, head[h] = any position of this step
+  uint32_t far;       // 1: chains continue through the HBM far ring (32 KiB window; zlib
+                      // levels >= 6, where ratio outweighs the parse time it costs)
 };
+
+#if HZ_GPU
+__host__ __device__
+#endif
+inline uint32_t far_level(int level) { return level >= 6 ? 1u : 0u; }
 
 HZ_HD Tune tune_for_level(int level) {
   Tune t;
   t.too_far = 4096;
   t.stored = level <= 0 ? 1u : 0u;
   t.fast_head = 0;
+  // measured on the cfg5 slab (chain 4, L4): the far ring left the ratio unchanged (1.0018
+  // vs libz L4) and cost 45 % more parse time; deeper chains gain ratio only with it
+  t.far = far_level(level);
   switch (level) {
     case 1: t.chain = 1; t.nice = 8; break;
     case 2: t.chain = 2; t.nice = 16; break;
@@ -247,6 +259,20 @@ HZ_HD uint32_t match_len(const ParseShared& sh, uint32_t q, uint32_t p, uint32_t
 
 }  // namespace hd
 
+namespace hd {
+// far candidate q (before the LDS ring): its bytes from the stream in HBM, the current
+// position's from the ring (q + maxl <= p, so stream bytes past the end are never compared)
+HZ_HD uint32_t match_len_far(const ParseShared& sh, const EncJob& job, uint32_t q, uint32_t p, uint32_t maxl) {
+  uint32_t L = 0;
+  while (L < maxl) {
+    const uint32_t x = load_stream_word(job, q + L, job.len) ^ rd32(sh, p + L);
+    if (x) { L += (uint32_t)__builtin_ctz(x) >> 3; break; }
+    L += 4u;
+  }
+  return L < maxl ? L : maxl;
+}
+}  // namespace hd
+
 // ---- wave-collective helpers for the encoder ---------------------------------
 #if HZ_GPU
 namespace hd {
@@ -314,9 +340,15 @@ namespace hd {
 // Parse one stream into per-segment tokens and frequencies.  sp / tok: this
 // stream's first segment record / token block (SEG_TOK slots per segment).
 // Returns the adler32 of the stream input.
+//
+// far (used when tune.far): this wave's ring of FARW predecessor entries in HBM.  Every segment's chain
+// links go there after its parse, so a chain that leaves the segment goes on into earlier
+// ones and matches reach FARW (zlib's 32 KiB window) instead of the LDS ring's WIN; a far
+// candidate's bytes are read from the stream in HBM.
 HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune, SegParse* sp, uint16_t* tok,
-                            HzProf* prof = nullptr) {
+                            HzProf* prof = nullptr, uint16_t* far = nullptr) {
   (void)prof;
+  hz_gu16* const gfar = tune.far ? HZ_GLOBAL(hz_gu16*, far) : nullptr;
   const uint32_t n = job.len;
   const uint32_t nseg = nsegments(n);
   LANE_VAR(uint64_t, as1);           // adler partial sums: S1 = sum b, S2 = sum pos * b
@@ -356,7 +388,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     }
     WAVE_SYNC();
 
-    const uint32_t lo_pos = s0 > WIN ? s0 - WIN : 0u;   // farthest match source
+    const uint32_t lo_pos = s0 > WIN ? s0 - WIN : 0u;   // farthest match source in the LDS ring
     if (!tune.stored && tune.fast_head) {
       // ---- approximate chains: every candidate is still an earlier position with the
       // same hash, so any parse over them is valid; only match quality can differ ----
@@ -446,18 +478,22 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
           if (maxl >= 3u) {
             const uint32_t cur = rd32(sh, pos);
             uint32_t c16 = sh.prev[pos - s0];
+            const uint32_t maxd = gfar ? (pos < FARW ? pos : FARW) : pos - lo_pos;
             for (uint32_t depth = 0; depth < tune.chain; depth++) {
               const uint32_t d = (pos - c16) & 0xffffu;
-              if (d == 0u || d > pos - lo_pos) break;
+              if (d == 0u || d > maxd) break;
               const uint32_t q = pos - d;
+              const bool near = q >= lo_pos;
               // the next candidate's load is independent of this compare: issue it now
-              c16 = q >= s0 ? (uint32_t)sh.prev[q - s0] : pos;
-              const uint32_t x = rd32(sh, q) ^ cur;
+              c16 = q >= s0 ? (uint32_t)sh.prev[q - s0] : gfar ? (uint32_t)gfar[q & (FARW - 1u)] : pos;
+              const uint32_t x = (near ? rd32(sh, q) : load_stream_word(job, q, n)) ^ cur;
               const uint32_t L0 = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
               // only a candidate that can beat `best` is measured in full
               if (L0 >= 3u && (L0 > best || (L0 == 4u && best >= 4u))) {
                 uint32_t L = L0;
-                if (L0 == 4u && maxl > 4u) L = 4u + match_len(sh, q + 4u, pos + 4u, maxl - 4u);
+                if (L0 == 4u && maxl > 4u)
+                  L = 4u + (near ? match_len(sh, q + 4u, pos + 4u, maxl - 4u)
+                                 : match_len_far(sh, job, q + 4u, pos + 4u, maxl - 4u));
                 if (L > maxl) L = maxl;
                 if (L > best) { best = L; bd = d; if (L >= tune.nice || L == maxl) break; }
               }
@@ -502,8 +538,13 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     WAVE_SYNC();
     LANE_LOOP {
       for (int s = lane; s < NSYM; s += WAVE) out->freq[s] = sh.freq[s];
+      // the segment's chain links join the far ring once the segment is parsed (written
+      // earlier, they would overwrite links FARW back that this parse still follows)
+      if (gfar)
+        for (uint32_t i = (uint32_t)lane; i < seglen; i += WAVE) gfar[(s0 + i) & (FARW - 1u)] = sh.prev[i];
     }
-    WAVE_SYNC();
+    if (gfar) WAVE_SYNC_GLOBAL();
+    else WAVE_SYNC();
   }
   HZ_T(9);
   uint64_t S1, S2;

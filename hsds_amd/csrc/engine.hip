@@ -765,8 +765,11 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
                                                    uint32_t* __restrict__ counter, hd::SegParse* __restrict__ sp,
                                                    SegMeta* __restrict__ meta, uint16_t* __restrict__ tok,
                                                    uint32_t* __restrict__ adler, uint32_t seg_cap, int level,
-                                                   uint32_t ks, uint32_t item_cap) {
+                                                   uint32_t ks, uint32_t item_cap, uint16_t* __restrict__ far,
+                                                   uint32_t chain_ovr) {
   __shared__ hd::ParseShared sh;
+  // far: one FARW-entry chain ring per workgroup (zlib streams: 32 KiB window), or null
+  uint16_t* const my_far = far ? far + (size_t)blockIdx.x * hd::FARW : nullptr;
   const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   const int lane = threadIdx.x;
   // level > PARSE_FAST: the LZ4-only approximate-chain parse at level - PARSE_FAST
@@ -775,6 +778,7 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
     tune.fast_head = 1;
     level -= PARSE_FAST;
   }
+  if (chain_ovr) tune.chain = chain_ovr;     // development override (HSDS_DEFLATE_CHAIN)
 #ifdef HZ_PROFILE
   HzProf prof_;
   for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
@@ -797,7 +801,7 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
     const uint32_t nseg = hd::nsegments(it.len);
     if (g0 + nseg > seg_cap) continue;          // the layout phase fails the chunk
     hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
-    const uint32_t a = hd::parse_stream(sh, job, tune, sp + g0, tok + (size_t)g0 * hd::SEG_TOK, prof);
+    const uint32_t a = hd::parse_stream(sh, job, tune, sp + g0, tok + (size_t)g0 * hd::SEG_TOK, prof, my_far);
     for (uint32_t s = (uint32_t)lane; s < nseg; s += 64) {
       const uint32_t s0 = s * (uint32_t)hd::SEG;
       meta[g0 + s] = SegMeta{slot, it.len - s0 < (uint32_t)hd::SEG ? it.len - s0 : (uint32_t)hd::SEG};
@@ -1274,6 +1278,9 @@ struct hsds_engine {
   size_t ecw_bytes = 0;
   uint8_t* escr = nullptr;
   size_t escr_bytes = 0;
+  uint8_t* efar = nullptr;     // encode: zlib parse far-chain rings, one per parse workgroup
+  size_t efar_bytes = 0;
+  uint32_t enc_chain = 0;      // development override of the parse chain depth (0: the level's)
   hipEvent_t ev2, ev3;
   int ev_enc_valid = 0;
 };
@@ -1398,6 +1405,10 @@ int hsds_engine_create(int device, hsds_engine** out) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, huff_kernel, 64, 0) != hipSuccess || o2 < 1) o2 = 4;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o3, emit_kernel, 64, 0) != hipSuccess || o3 < 1) o3 = 4;
   e->parse_blocks_per_cu = o1;
+  if (const char* ev = getenv("HSDS_DEFLATE_CHAIN")) {   // development override (A/B experiments)
+    const int v = atoi(ev);
+    if (v >= 1 && v <= 4096) e->enc_chain = (uint32_t)v;
+  }
   e->huff_blocks_per_cu = o2;
   e->emit_blocks_per_cu = o3;
   // warm-up 384 bits, segments sized to 1 + 1/16 of the previous block, 4 repair rounds
@@ -1429,6 +1440,7 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (e->ews) hipFree(e->ews);
   if (e->ecw) hipFree(e->ecw);
   if (e->escr) hipFree(e->escr);
+  if (e->efar) hipFree(e->efar);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
   hipEventDestroy(e->ev2);
@@ -1853,12 +1865,20 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
     if (g > cap) g = cap;
     return (unsigned)(g < 1 ? 1 : g);
   };
+  const unsigned pgrid = grid_for(e->parse_blocks_per_cu, item_cap);
+  uint16_t* far = nullptr;
+  if (cname == HSDS_CNAME_ZLIB && hd::far_level(clevel)) {
+    // zlib levels >= 6: matches reach 32 KiB back, the chains beyond the LDS ring live in HBM
+    if (grow((void**)&e->efar, &e->efar_bytes, (size_t)pgrid * hd::FARW * 2)) return HSDS_ERR_DEVICE;
+    far = (uint16_t*)e->efar;
+  }
   hipEventRecord(e->ev2, st);
-  hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, item_cap)), dim3(64), 0, st, slots,
+  hipLaunchKernelGGL(parse_kernel, dim3(pgrid), dim3(64), 0, st, slots,
                      offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap,
                      // lz4 (the speed codec) parses with approximate chains; zlib, lz4hc and
                      // blosclz keep the exact chains
-                     cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, 0u, item_cap);
+                     cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, 0u, item_cap, far,
+                     e->enc_chain);
   if (cname == HSDS_CNAME_ZLIB) {
     hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 1, sp, meta, sc, seg_cap, clevel);
@@ -2004,7 +2024,7 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
   };
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, slot_cap)), dim3(64), 0, st, slots, offs,
                      segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, PARSE_FAST + BSHUF_PARSE_LEVEL, 0u,
-                     slot_cap);
+                     slot_cap, (uint16_t*)nullptr, 0u);
   const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, slot_cap);
   hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,
                      seg_cap, BSHUF_PARSE_LEVEL, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, 0, 0, 0u, slot_cap);

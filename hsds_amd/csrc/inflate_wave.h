@@ -37,6 +37,7 @@ typedef __attribute__((address_space(1))) uint8_t hz_gu8;
 typedef __attribute__((address_space(1))) const uint8_t hz_gcu8;
 typedef __attribute__((address_space(1))) uint32_t hz_gu32;
 typedef __attribute__((address_space(1))) const uint32_t hz_gcu32;
+typedef __attribute__((address_space(1))) uint16_t hz_gu16;
 #define HZ_GLOBAL(T, p) ((T)(uintptr_t)(p))
 #define HZ_UNROLL _Pragma("unroll")
 #define LANE_VAR(T, name) T name
@@ -68,6 +69,7 @@ typedef uint8_t hz_gu8;
 typedef const uint8_t hz_gcu8;
 typedef uint32_t hz_gu32;
 typedef const uint32_t hz_gcu32;
+typedef uint16_t hz_gu16;
 #define HZ_GLOBAL(T, p) ((T)(p))
 #define HZ_UNROLL
 #define LANE_VAR(T, name) T name[64]

@@ -9,7 +9,8 @@
 #include "../../hsds_amd/csrc/deflate_wave.h"
 #include "../../hsds_amd/csrc/lz4_enc.h"
 
-static int64_t run(const hd::EncJob& job, const hd::Tune& tune, uint8_t* dst, uint32_t cap) {
+// far: the HBM far-chain ring is handed over (the parse uses it when tune.far, as the engine)
+static int64_t run(const hd::EncJob& job, const hd::Tune& tune, uint8_t* dst, uint32_t cap, int far = 1) {
   const uint32_t nseg = hd::nsegments(job.len);
   std::vector<hd::SegParse> sp(nseg);
   std::vector<hd::SegCode> sc(nseg);
@@ -17,7 +18,8 @@ static int64_t run(const hd::EncJob& job, const hd::Tune& tune, uint8_t* dst, ui
   hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
   hd::HuffShared* hs = (hd::HuffShared*)calloc(1, sizeof(hd::HuffShared));
   hd::EmitShared* es = (hd::EmitShared*)calloc(1, sizeof(hd::EmitShared));
-  const uint32_t adler = hd::parse_stream(*ps, job, tune, sp.data(), tok.data());
+  std::vector<uint16_t> fr(hd::FARW, 0);
+  const uint32_t adler = hd::parse_stream(*ps, job, tune, sp.data(), tok.data(), nullptr, far ? fr.data() : nullptr);
   for (uint32_t s = 0; s < nseg; s++) {
     const uint32_t s0 = s * (uint32_t)hd::SEG;
     const uint32_t seglen = job.len - s0 < (uint32_t)hd::SEG ? job.len - s0 : (uint32_t)hd::SEG;
@@ -59,6 +61,16 @@ extern "C" int64_t emu_deflate(const uint8_t* src, uint32_t n, uint8_t* dst, uin
                                int chain_override) {
   hd::Tune tune = hd::tune_for_level(level);
   if (chain_override > 0) tune.chain = (uint32_t)chain_override;
+  hd::EncJob job = {src, n, level, 1u, 0u, 0u};
+  return run(job, tune, dst, cap);
+}
+
+// far = 0 / 1: the parse without / with the far ring at any level (size comparison in the tests)
+extern "C" int64_t emu_deflate_far(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level,
+                                   int chain_override, int far) {
+  hd::Tune tune = hd::tune_for_level(level);
+  if (chain_override > 0) tune.chain = (uint32_t)chain_override;
+  tune.far = far ? 1u : 0u;
   hd::EncJob job = {src, n, level, 1u, 0u, 0u};
   return run(job, tune, dst, cap);
 }

@@ -110,3 +110,39 @@ def test_shuffled_block_gather(emu, ts):
         r = emu.emu_deflate_shuffled(block.ctypes.data, n, out.ctypes.data, n + 1024, 4, ts, neb, off)
         assert r > 0
         assert zlib.decompress(out.view(np.uint8)[:r].tobytes()) == shuffled[off:off + n]
+
+
+def enc_far(emu, b, level, far, chain=0):
+    emu.emu_deflate_far.restype = ctypes.c_int64
+    emu.emu_deflate_far.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int]
+    a = np.frombuffer(b, np.uint8)
+    out = np.zeros(len(b) // 4 + 300, np.uint32)
+    r = emu.emu_deflate_far(a.ctypes.data, len(b), out.ctypes.data, len(b) + 1024, level, chain, far)
+    assert r > 0
+    return out.view(np.uint8)[:r].tobytes()
+
+
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_far_ring_reaches_the_32k_window(emu, level):
+    # a 20 000-byte random block repeated: its copy lies beyond the LDS ring (8 KiB) but
+    # inside zlib's 32 KiB window, so only the far chains find it
+    rng = np.random.default_rng(11)
+    blk = rng.integers(0, 256, 20000, dtype=np.uint8).tobytes()
+    b = blk + blk + blk[:5000]
+    near, far = enc_far(emu, b, level, 0), enc_far(emu, b, level, 1)
+    assert zlib.decompress(near) == b and zlib.decompress(far) == b
+    assert len(far) < 0.8 * len(near), (len(far), len(near))
+    if level >= 6:    # the levels that use the far ring: chains deep enough past the 11-bit
+        #              hash collisions of 20 000 random positions
+        assert len(far) < 1.07 * len(zlib.compress(b, level)), (len(far), len(zlib.compress(b, level)))
+        assert enc(emu, b, level) == far
+
+
+def test_far_ring_with_deep_chains_on_row_walks(emu):
+    # cfg5's worst chunks (row random walks from 0): deep chains gain only with the far ring
+    rng = np.random.default_rng(5)
+    a = np.round(np.cumsum(rng.normal(size=(128, 512)), axis=1), 2).astype(np.float32).tobytes()
+    near, far = enc_far(emu, a, 4, 0, 32), enc_far(emu, a, 4, 1, 32)
+    assert zlib.decompress(far) == a
+    assert len(far) < 0.97 * len(near), (len(far), len(near))

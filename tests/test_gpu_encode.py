@@ -206,8 +206,11 @@ def test_streams_equal_cpu_emulation(dev):
     L.emu_deflate.restype = ctypes.c_int64
     L.emu_deflate.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
                               ctypes.c_int]
-    for seed, level, n in ((1, 4, 1 << 20), (2, 1, 1 << 19), (3, 9, 300000), (4, 5, 70001)):
+    for seed, level, n in ((1, 4, 1 << 20), (2, 1, 1 << 19), (3, 9, 300000), (4, 5, 70001), (5, 6, 262144)):
         data = smooth(seed, n - n % 4) + bytes(n % 4)
+        if seed == 5:   # repeats 20 000 bytes back: the far chain ring in HBM (levels >= 6)
+            blk = np.random.default_rng(seed).integers(0, 256, 20000, dtype=np.uint8).tobytes()
+            data = (blk * 14)[:n]
         frame = codec._compress(data, compressor="zlib", level=level, shuffle=1)
         h = header(frame)
         assert not (h["flags"] & 0x02)
