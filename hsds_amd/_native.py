@@ -103,6 +103,8 @@ def lib():
         "hsds_bitshuffle_compress": (I64, [P, P, I64, I, I, P, I64]),
         "hsds_partition_ids": (I, [ctypes.c_char_p, I, P, I64, I, P]),
         "hsds_plan_descs": (I, [P, P, P, P, P, P, I64, P, P]),
+        "hsds_host_map": (I, [P, P, U64, ctypes.POINTER(ctypes.c_void_p)]),
+        "hsds_host_unmap": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

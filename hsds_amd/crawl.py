@@ -274,6 +274,19 @@ class SelectionPlan:
             raise ValueError("one decoded chunk offset per owned piece expected")
         return _recs(self._descs(ii, True, chunk_offsets, packed_base, False))
 
+    def direct_descs(self, rank, chunk_offsets, slab_base=0):
+        """Read without a gather: decoded chunk k (at chunk_offsets[k]) [chunk_sel] ->
+        slab[data_sel] at slab_base, for this rank's pieces (pack and place fused: each GPU
+        writes its pieces straight into the response buffer)."""
+        ii = self.by_rank[rank]
+        if len(chunk_offsets) != len(ii):
+            raise ValueError("one decoded chunk offset per owned piece expected")
+        m = self._descs(ii, True, chunk_offsets, 0, False)          # chunk side -> (packed)
+        p = self._descs(ii, False, slab_base, 0, True)              # (packed) -> slab side
+        m[:, 1] = p[:, 1]
+        m[:, 10:18] = p[:, 10:18]
+        return _recs(m)
+
     def place_descs(self, ranks=None):
         """Read: gathered buffer (rank r's packed bytes at rank_base[r]) -> slab[data_slices]."""
         rs = range(self.world) if ranks is None else ranks
@@ -638,3 +651,161 @@ def scatter_exchange(scattered, plan, rank, root=0, group=None, device=None):
         else:
             dist.recv(out[:nb], root, group=group)
     return out
+
+
+class PagedReader:
+    """GET_Value with stream pagination (chunk_sn.py:1085-1135) on the sharded GPU path.
+
+    getSelectionPagination (dsetUtil.py:689-800) cuts the selection along its first
+    dimension of extent > 1 into pages of at most max_request_size bytes; pages are read
+    in order and each page's bytes are handed to `sink(page_no, page_selection, host_u8)`
+    -- the reference's resp.write(arrayToBytes(arr)) -- so the response is the pages
+    concatenated.  Per page every rank decodes only the chunks it does not already hold:
+    its decoded chunks live in a slot pool and a chunk shared by consecutive pages (pages
+    cut through chunk rows) is decoded once, as the DN's chunk cache would serve it.
+
+    mode "gather": pack -> RCCL gather to the root -> place into a device page slab ->
+    one D2H into the host page buffer.  mode "direct" (no gather): every rank places its
+    pieces straight into the host page buffer (hsds_host_map'ed; with world > 1 a
+    /dev/shm file every rank of the node maps, `shm_path`), then a barrier.
+
+    get_blobs(chunk_ids) -> {chunk_id: stored object bytes / uint8 array}; an id
+    without an object reads as the fill value."""
+
+    def __init__(self, dset_id, dims, layout, selection, dtype, world, rank, device, max_request_size=100 << 20,
+                 compressor="zlib", shuffle=1, mode="gather", root=0, group=None, shm_path=None):
+        import torch
+        from .engine import ChunkEngine, HostBuffer
+        if mode not in ("gather", "direct"):
+            raise ValueError("mode: gather or direct")
+        self.dset_id, self.dims, self.layout = dset_id, tuple(dims), tuple(layout)
+        self.dtype = np.dtype(dtype)
+        self.world, self.rank, self.root, self.group = int(world), int(rank), root, group
+        self.device = torch.device(device)
+        self.compressor, self.shuffle, self.mode = compressor, shuffle, mode
+        self.pages = sel.getSelectionPagination(tuple(selection), self.dims, self.dtype.itemsize, max_request_size)
+        self.page_bytes = [int(np.prod(sel.getSelectionShape(p), dtype=np.int64)) * self.dtype.itemsize
+                           for p in self.pages]
+        self.eng = ChunkEngine(self.device.index)
+        self.torch = torch
+        cap = max(self.page_bytes) if self.page_bytes else 1
+        if mode == "direct":
+            shared = self.world > 1
+            if shared and shm_path is None:
+                raise ValueError("direct mode with world > 1 needs a shm_path every rank maps")
+            if shared and self.rank != self.root:
+                import torch.distributed as dist
+                dist.barrier(group=group)                       # the root has created the file
+                self.host = HostBuffer(cap, self.device, path=shm_path, create=False)
+            else:
+                self.host = HostBuffer(cap, self.device, path=shm_path if shared else None)
+                if shared:
+                    import torch.distributed as dist
+                    dist.barrier(group=group)
+        else:
+            self.host = torch.empty(cap, dtype=torch.uint8).pin_memory() if self.rank == root else None
+        self.csize = int(np.prod(self.layout, dtype=np.int64)) * self.dtype.itemsize
+        self.cstride = _align(self.csize, 256)
+        self.pool = None
+        self.slot_of = {}                      # chunk id -> pool slot
+        self.stats = {"pages": 0, "decoded": 0, "reused": 0}
+
+    def _slots(self, ids):
+        """Pool slots for this page's chunk ids: keep the ones already decoded, free the
+        rest, hand free slots to new ids.  Returns (offsets, new ids, their slots)."""
+        torch = self.torch
+        keep = {c: self.slot_of[c] for c in ids if c in self.slot_of}
+        need = len(ids)
+        if self.pool is None or self.pool.numel() < need * self.cstride:
+            # a bigger pool: the decoded chunks keep their slot offsets
+            big = torch.empty(max(2 * need, 1) * self.cstride, dtype=torch.uint8, device=self.device)
+            if self.pool is not None:
+                big[:self.pool.numel()].copy_(self.pool)
+            self.pool = big
+        nslots = self.pool.numel() // self.cstride
+        used = set(keep.values())
+        free = (k for k in range(nslots) if k not in used)
+        new, new_slots = [], []
+        for c in ids:
+            if c not in keep:
+                k = next(free)
+                keep[c] = k
+                new.append(c)
+                new_slots.append(k)
+        self.slot_of = keep
+        offs = np.array([keep[c] * self.cstride for c in ids], np.int64)
+        return offs, new, new_slots
+
+    def _decode(self, new, new_slots, get_blobs, fill_value):
+        from .engine import CHUNK_DESC_DTYPE, pack_chunks, to_device_bytes
+        torch = self.torch
+        blobs = get_blobs(new) if new else {}
+        present = [(c, k) for c, k in zip(new, new_slots) if c in blobs]
+        missing = [k for c, k in zip(new, new_slots) if c not in blobs]
+        if present:
+            src, descs, _ = pack_chunks([blobs[c] for c, _ in present], [self.csize] * len(present))
+            descs["dst_off"] = np.array([k * self.cstride for _, k in present], np.uint64)
+            d_src = torch.from_numpy(src).to(self.device)
+            st = torch.full((len(present),), 99, dtype=torch.int32, device=self.device)
+            self.eng.decode(d_src, descs, self.pool, st, compressor=self.compressor, shuffle=self.shuffle,
+                            itemsize=self.dtype.itemsize)
+            bad = st.ne(0)
+            if bool(bad.any()):
+                raise RuntimeError("chunk decode failed: " + str(torch.unique(st).tolist()))
+        if missing:
+            fill = np.zeros(self.layout, self.dtype)
+            if fill_value is not None:
+                fill[...] = fill_value
+            d_fill = torch.from_numpy(fill.view(np.uint8).reshape(-1).copy()).to(self.device)
+            for k in missing:
+                self.pool[k * self.cstride:k * self.cstride + self.csize].copy_(d_fill)
+        self.stats["decoded"] += len(new)
+
+    def read(self, get_blobs, sink, fill_value=None):
+        """Read every page in order; returns the total bytes handed to `sink` (root)."""
+        torch = self.torch
+        total = 0
+        for pno, page in enumerate(self.pages):
+            plan = SelectionPlan(self.dset_id, self.dims, self.layout, page, self.dtype, self.world)
+            ids = plan.chunk_ids(self.rank)
+            offs, new, new_slots = self._slots(ids)
+            self.stats["reused"] += len(ids) - len(new)
+            self._decode(new, new_slots, get_blobs, fill_value)
+            nb = self.page_bytes[pno]
+            if self.mode == "direct":
+                if len(ids):
+                    self.eng.copy(self.pool, self.host, plan.direct_descs(self.rank, offs))
+                torch.cuda.synchronize(self.device)
+                if self.world > 1:
+                    import torch.distributed as dist
+                    dist.barrier(group=self.group)
+                if self.rank == self.root:
+                    sink(pno, page, self.host.array[:nb])
+                if self.world > 1:
+                    dist.barrier(group=self.group)           # the page buffer is free again
+            else:
+                if self.rank == self.root:
+                    gathered = torch.empty(max(plan.gathered_nbytes, 1), dtype=torch.uint8, device=self.device)
+                    b = int(plan.rank_base[self.root])
+                    packed = gathered[b:b + max(plan.rank_bytes[self.root], 1)]
+                else:
+                    gathered = None
+                    packed = torch.empty(max(plan.rank_bytes[self.rank], 1), dtype=torch.uint8, device=self.device)
+                if len(ids):
+                    self.eng.copy(self.pool, packed, plan.device_descs(nat.PLAN_PACK, self.device, ranks=[self.rank],
+                                                                       chunk_offsets=offs))
+                got = exchange(packed, plan, self.rank, self.root, self.group, gathered) if self.world > 1 \
+                    else gathered
+                if self.rank == self.root:
+                    slab = torch.empty(max(nb, 1), dtype=torch.uint8, device=self.device)
+                    if len(plan.idx):
+                        self.eng.copy(got, slab, plan.device_descs(nat.PLAN_PLACE, self.device))
+                    self.host[:nb].copy_(slab[:nb])
+                    sink(pno, page, self.host[:nb].numpy())
+            total += nb
+            self.stats["pages"] += 1
+        return total
+
+    def close(self):
+        if self.mode == "direct":
+            self.host.close()

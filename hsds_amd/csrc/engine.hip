@@ -1770,6 +1770,25 @@ __global__ void plan_descs_kernel(hsds_plan_geom g, const int64_t* __restrict__ 
   out[k] = r;
 }
 
+int hsds_host_map(hsds_engine* e, void* p, uint64_t n, void** d_ptr) {
+  if (!e || !p || !n || !d_ptr) return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (hipHostRegister(p, (size_t)n, hipHostRegisterMapped) != hipSuccess) return HSDS_ERR_DEVICE;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    hipHostUnregister(p);
+    return HSDS_ERR_DEVICE;
+  }
+  *d_ptr = d;
+  return HSDS_OK;
+}
+
+int hsds_host_unmap(hsds_engine* e, void* p) {
+  if (!e || !p) return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  return hipHostUnregister(p) == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
 int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d_tabs, const int64_t* d_piece,
                     const int64_t* d_poff, const int64_t* d_coff, int64_t n, hsds_copy_desc* d_out,
                     void* stream) {

@@ -7,6 +7,8 @@ hsds/datanode_lib.py:796-945, 948-1142) and copies one selection per chunk
 request's chunks go to the GPU in one call.  torch is used only for device memory
 and streams; all byte work happens in the C-ABI kernels.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -28,9 +30,61 @@ def _stream_handle(stream):
 def _ptr(t):
     if t is None:
         return None
+    if isinstance(t, HostBuffer):
+        return t.d_ptr
     if not t.is_cuda:
         raise ValueError("device tensor expected")
     return t.data_ptr()
+
+
+class HostBuffer:
+    """Page-locked host memory that kernels of `device` write directly (hsds_host_map):
+    the response buffer of the "no gather" sharded read.  `path`: a shared-memory file
+    (/dev/shm) that every rank of the node maps, so all GPUs place their pieces into the
+    same buffer; otherwise private memory.  `.array` is the host uint8 view."""
+
+    def __init__(self, nbytes, device, path=None, create=True):
+        import mmap
+        import os as _os
+        self.nbytes = int(nbytes)
+        self.device = torch.device(device)
+        self.path = path
+        if path is None:
+            self._mm = mmap.mmap(-1, self.nbytes)
+        else:
+            if create:
+                fd = _os.open(path, _os.O_RDWR | _os.O_CREAT, 0o600)
+                _os.ftruncate(fd, self.nbytes)
+            else:
+                fd = _os.open(path, _os.O_RDWR)
+            try:
+                self._mm = mmap.mmap(fd, self.nbytes)
+            finally:
+                _os.close(fd)
+        self.array = np.frombuffer(self._mm, np.uint8, self.nbytes)
+        self.array[::4096] = self.array[::4096]          # fault the pages in before locking them
+        self._eng = nat.engine(self.device.index)
+        self._hptr = self.array.ctypes.data
+        d = ctypes.c_void_p()
+        rc = nat.lib().hsds_host_map(self._eng.h, self._hptr, self.nbytes, ctypes.byref(d))
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_host_map")
+        self.d_ptr = int(d.value)
+
+    def close(self):
+        if self._hptr:
+            nat.lib().hsds_host_unmap(self._eng.h, self._hptr)
+            self._hptr = 0
+            # the mapping closes with its last numpy view (pages handed to a sink may
+            # still be referenced)
+            self.array = None
+            self._mm = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def to_device_bytes(arr, device):

@@ -198,6 +198,15 @@ int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d
                     const int64_t* d_poff, const int64_t* d_coff, int64_t n, hsds_copy_desc* d_out,
                     void* stream);
 
+/* ---- host response buffers (the "no gather" sharded read) ---------
+ * The SN streams each page of a GET_Value to the client (chunk_sn.py:1085-1135): the
+ * bytes end in host memory.  hsds_host_map page-locks n bytes of host memory at p
+ * (private, or a shared-memory mapping every rank of the node maps) and returns the
+ * address kernels on the engine's device write through (zero-copy over PCIe), so each GPU
+ * places its own pieces straight into the response: no gather over xGMI. */
+int hsds_host_map(hsds_engine* e, void* p, uint64_t n, void** d_ptr);
+int hsds_host_unmap(hsds_engine* e, void* p);
+
 /* ---- encode (write path) ---------------------------------------------------- */
 /* Batched, device-resident encode into HSDS F1 objects: chunk k (d_chunks[k].src_off /
  * src_len in d_src) becomes a Blosc1 frame with the zlib codec at level `clevel`

@@ -310,3 +310,51 @@ def test_plan_grid_equals_meshgrid_product():
         keep = (cols[2] > 0).all(axis=1)
         for got, want in zip((plan.idx, plan.cstart, plan.count, plan.dstart), cols):
             assert np.array_equal(got, want[keep])
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("world", [1, 3])
+def test_direct_descs_place_every_rank_into_one_slab(case, world):
+    """No-gather read: each rank writes its own pieces chunk -> slab (pack and place
+    fused); all ranks together fill the whole selection."""
+    dims, layout, dt, selection = CASES[case]
+    full = _full(dims, dt)
+    plan = crawl.SelectionPlan(DSET, dims, layout, selection, dt, world)
+    slab = np.zeros(plan.slab_nbytes + 64, np.uint8)
+    cbytes = plan.chunk_nbytes
+    for r in range(world):
+        ids = plan.chunk_ids(r)
+        if not ids:
+            continue
+        dec = np.concatenate([chunk_array(full, plan.layout, c).view(np.uint8).reshape(-1) for c in ids])
+        apply_descs(dec, slab, plan.direct_descs(r, [k * cbytes for k in range(len(ids))], slab_base=32))
+    assert np.array_equal(slab[32:32 + plan.slab_nbytes].view(dt).reshape(plan.slab_shape), full[selection])
+
+
+@pytest.mark.parametrize("case", [0, 1, 2, 5])
+def test_pages_concatenate_to_the_selection(case):
+    """GET_Value streams getSelectionPagination's pages in order (chunk_sn.py:1085-1135):
+    the pages' slabs concatenated are the whole selection's bytes."""
+    dims, layout, dt, selection = CASES[case]
+    full = _full(dims, dt)
+    isz = np.dtype(dt).itemsize
+    size = int(np.prod(sel.getSelectionShape(selection))) * isz
+    pages = sel.getSelectionPagination(selection, dims, isz, max(size // 5, 1))
+    assert len(pages) > 1
+    out = []
+    for page in pages:
+        plan = crawl.SelectionPlan(DSET, dims, layout, page, dt, 2)
+        slab = np.zeros(plan.slab_nbytes, np.uint8)
+        for r in range(2):
+            ids = plan.chunk_ids(r)
+            if ids:
+                dec = np.concatenate([chunk_array(full, layout, c).view(np.uint8).reshape(-1) for c in ids])
+                apply_descs(dec, slab, plan.direct_descs(r, [k * plan.chunk_nbytes for k in range(len(ids))]))
+        out.append(slab)
+    # the reference streams full[page] for each page; those are the selection's rows in
+    # order except where a stepped first slice starts off its step lattice (case 5: the
+    # reference rounds page ends to multiples of the step, dsetUtil.py:759-770)
+    want = np.concatenate([full[p].reshape(-1) for p in pages])
+    assert np.array_equal(np.concatenate(out).view(dt), want)
+    if case != 5:
+        assert np.array_equal(want, full[selection].reshape(-1))
