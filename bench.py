@@ -740,6 +740,77 @@ def run_cfg4(args, dev, rank, world):
 TRAFFIC_ROUND = "r2"
 
 
+def run_cfg4_full(args, dev, rank, world):
+    """configs[3], full-extent variant: f32 131072 x 131072 in 512x512 chunks, selection
+    [:, :] (64 GiB), read as GET_Value streams it -- getSelectionPagination pages of at
+    most max_request_size (100 MiB: 659 pages of 199 rows) -- by crawl.PagedReader over the
+    md5-sharded chunks, in both modes: "gather" (pack, RCCL gather to rank 0, place, D2H
+    of each page) and "direct" (no gather: every GPU writes its pieces of the page straight
+    into the pinned host page buffer, shared by the node's ranks through /dev/shm).  The
+    stored objects are staged in HBM first (each chunk id its own copy); each page's
+    bytes go to a sink that stands in for resp.write."""
+    import torch
+    import torch.distributed as dist
+    from hsds_amd import crawl
+    threads = max(1, min(16, (os.cpu_count() or 1) // max(1, world)))
+    sc = max(1, args.cfg4_scale)
+    dims = tuple(d // sc for d in CFG4_DIMS)
+    full_sel = tuple(slice(0, d, 1) for d in dims)
+    dset = "d-5a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d"
+    plan = crawl.SelectionPlan(dset, dims, CFG4_LAYOUT, full_sel, np.float32, world)
+    ids = plan.chunk_ids(rank)
+    nuniq = min(args.cfg4_unique, len(ids))
+    raw, enc = make_corpus("F1", nuniq, 20261015 + 7919 * rank, threads)
+    blobs = {cid: enc[k % nuniq] for k, cid in enumerate(ids)}
+    first = {cid: k % nuniq for k, cid in enumerate(ids)}
+    eng_src = crawl.stage_objects(blobs, ids, dev)
+    del blobs
+    out = {}
+    port = os.environ.get("MASTER_PORT", "0")
+    for mode in ("direct", "gather"):
+        shm = f"/dev/shm/hsds_amd_bench_{port}_{os.getuid()}" if (mode == "direct" and world > 1) else None
+        rd = crawl.PagedReader(dset, dims, CFG4_LAYOUT, full_sel, np.float32, world, rank, dev,
+                               max_request_size=args.max_request_size, mode=mode, shm_path=shm)
+        checked = {"ok": 1, "bytes": 0}
+        c00 = plan.prefix + "0_0"
+
+        def sink(pno, page, b):
+            checked["bytes"] += len(b)
+            if pno == 0 and c00 in first:
+                # row 0, columns 0..511 of the page = row 0 of chunk (0, 0)
+                want = raw[first[c00]].view(np.float32)[:CFG4_LAYOUT[1]]
+                checked["ok"] &= int(np.array_equal(np.asarray(b[:CFG4_LAYOUT[1] * 4]).view(np.float32), want))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        total = rd.read(eng_src, sink)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        rd.close()
+        if shm and rank == 0 and os.path.exists(shm):
+            os.unlink(shm)
+        out[mode] = {"value": round(total / el / 1e9, 2), "unit": "GB/s selected (response bytes, all ranks)",
+                     "seconds": round(el, 3), "pages": len(rd.pages), "response_bytes": total,
+                     "chunk_decodes_rank0": rd.stats["decoded"], "chunk_reuses_rank0": rd.stats["reused"],
+                     "decoded_GBps": round(len(plan.idx) * plan.chunk_nbytes / el / 1e9, 2),
+                     "page0_check": bool(checked["ok"]) if rank == 0 else None}
+        del rd
+        torch.cuda.empty_cache()
+    out["workload"] = (f"configs[3] full extent: f32 {dims[0]}x{dims[1]}, 512x512 chunks (F1 L4), [:, :], "
+                       f"GET_Value pagination at max_request_size {args.max_request_size} B, "
+                       f"md5-sharded over {world} rank(s)")
+    del eng_src
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(args, world, leg=""):
     """HBM bytes per inflate launch (or per cfg3 step, leg="_cfg3") from the committed PMC
     passes (tools/pmc_traffic.sh): 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md
@@ -834,6 +905,9 @@ def main():
     ap.add_argument("--cfg4-steps", type=int, default=3)
     ap.add_argument("--cfg4-unique", type=int, default=256)
     ap.add_argument("--cfg4-scale", type=int, default=1, help="divide the cfg4 dataset extents (local checks)")
+    ap.add_argument("--cfg4-full", type=int, default=1,
+                    help="configs[3] full-extent read through GET_Value pagination (gather and no-gather modes)")
+    ap.add_argument("--max-request-size", type=int, default=100 << 20, help="SN max_request_size (config.yml: 100m)")
     ap.add_argument("--headline", type=int, default=1,
                     help="0: skip the configs[1] headline and print only the selected legs (profiling passes)")
     args = ap.parse_args()
@@ -856,6 +930,8 @@ def main():
             legs["cfg1"] = run_cfg1(args, dev)
         if world == 1 and args.cfg5:
             legs["cfg5"] = run_cfg5(args, dev, rank)
+        if args.cfg4_full:
+            legs["cfg4_full"] = run_cfg4_full(args, dev, rank, world)
         if rank == 0:
             print(json.dumps({"metric": "profiling pass (no headline)", "legs": legs}), flush=True)
         if world > 1:
@@ -966,6 +1042,11 @@ def main():
             out["cfg4"] = run_cfg4(args, dev, rank, world)
         except Exception as e:   # the headline stands even if this leg fails
             out["cfg4"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if args.cfg4_full == 1:
+        try:
+            out["cfg4_full"] = run_cfg4_full(args, dev, rank, world)
+        except Exception as e:   # the headline stands even if this leg fails
+            out["cfg4_full"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = box_threads()
         sample = r1["blobs"][:256]

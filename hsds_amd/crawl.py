@@ -380,6 +380,44 @@ def exchange(packed, plan, rank, root=0, group=None, gathered=None):
     return gathered
 
 
+def stage_objects(blobs, ids, device, eng=None, replicate=True):
+    """Stored objects of chunk ids `ids` (dict chunk_id -> bytes / uint8 array; absent ids
+    are missing chunks) staged in HBM.  An object shared by several ids (bench corpora)
+    crosses PCIe once; with `replicate` every id still gets its own copy at a distinct HBM
+    address (one copy launch), so no decode reads another chunk's bytes from cache.
+    Returns (d_src, {chunk_id: (src_off, src_len)})."""
+    import torch
+    from .engine import COPY_DESC_DTYPE, ChunkEngine, pack_chunks
+    present = [c for c in ids if c in blobs]
+    uniq, objs, which = {}, [], []
+    for c in present:
+        b = blobs[c]
+        k = uniq.setdefault(id(b), len(objs))
+        if k == len(objs):
+            objs.append(b)
+        which.append(k)
+    if not present:
+        return torch.empty(1, dtype=torch.uint8, device=device), {}
+    usrc, udescs, _ = pack_chunks(objs, [0] * len(objs))
+    d_usrc = torch.from_numpy(np.concatenate([usrc, np.zeros(16, np.uint8)])).to(device)
+    lens = np.array([len(objs[k]) for k in which], np.int64)
+    if not replicate:
+        offs = udescs["src_off"][which].astype(np.int64)
+        return d_usrc, {c: (int(o), int(n)) for c, o, n in zip(present, offs, lens)}
+    alen = (lens + 255) // 256 * 256
+    soff = np.concatenate([[0], np.cumsum(alen)[:-1]]).astype(np.int64)
+    d_src = torch.empty(max(int(alen.sum()), 1), dtype=torch.uint8, device=device)
+    rec = np.zeros(len(present), COPY_DESC_DTYPE)
+    rec["src_off"] = udescs["src_off"][which]
+    rec["dst_off"] = soff
+    rec["rank"], rec["itemsize"] = 2, 16
+    rec["count"][:, 0] = (lens + 15) // 16
+    rec["count"][:, 1] = 1
+    rec["src_stride"][:, 0] = rec["dst_stride"][:, 0] = 16
+    (eng or ChunkEngine(device.index)).copy(d_usrc, d_src, rec)
+    return d_src, {c: (int(o), int(n)) for c, o, n in zip(present, soff, lens)}
+
+
 class ShardedReader:
     """GPU read of a hyperslab: decode owned chunks -> pack -> exchange -> place."""
 
@@ -395,43 +433,19 @@ class ShardedReader:
     def upload(self, blobs, fill_value=None):
         """Stage the stored objects of this rank's chunks (dict chunk_id -> bytes,
         absent ids are missing chunks) in HBM.  Returns the staged batch."""
-        from .engine import pack_chunks, to_device_bytes
+        from .engine import CHUNK_DESC_DTYPE, to_device_bytes
         torch = self.torch
         ids = self.plan.chunk_ids(self.rank)
         present = [cid for cid in ids if cid in blobs]
         # an object shared by many chunk ids (bench corpora) crosses PCIe once and is
-        # replicated into the batch layout on the device (one copy launch)
-        uniq, objs, which = {}, [], []
-        for c in present:
-            b = blobs[c]
-            k = uniq.setdefault(id(b), len(objs))
-            if k == len(objs):
-                objs.append(b)
-            which.append(k)
-        if len(objs) * 2 <= len(present):
-            usrc, udescs, _ = pack_chunks(objs, [0] * len(objs))
-            lens = np.array([len(objs[k]) for k in which], np.int64)
-            alen = (lens + 255) // 256 * 256
-            soff = np.concatenate([[0], np.cumsum(alen)[:-1]]).astype(np.int64)
-            descs = np.zeros(len(present), udescs.dtype)
-            descs["src_off"], descs["src_len"] = soff, lens
-            descs["dst_len"] = self.plan.chunk_nbytes
-            descs["dst_off"] = np.arange(len(present), dtype=np.int64) * _align(self.plan.chunk_nbytes, 256)
-            ext = len(present) * _align(self.plan.chunk_nbytes, 256)
-            d_src = torch.empty(max(int(alen.sum()), 1), dtype=torch.uint8, device=self.device)
-            from .engine import COPY_DESC_DTYPE
-            rec = np.zeros(len(present), COPY_DESC_DTYPE)
-            rec["src_off"] = udescs["src_off"][which]
-            rec["dst_off"] = soff
-            rec["rank"], rec["itemsize"] = 2, 16
-            rec["count"][:, 0] = (lens + 15) // 16
-            rec["count"][:, 1] = 1
-            rec["src_stride"][:, 0] = rec["dst_stride"][:, 0] = 16
-            d_usrc = torch.from_numpy(np.concatenate([usrc, np.zeros(16, np.uint8)])).to(self.device)
-            self.eng.copy(d_usrc, d_src, rec)
-        else:
-            src, descs, ext = pack_chunks([blobs[c] for c in present], [self.plan.chunk_nbytes] * len(present))
-            d_src = torch.from_numpy(src).to(self.device)
+        # replicated into the batch layout on the device (stage_objects)
+        d_src, table = stage_objects(blobs, ids, self.device, self.eng)
+        descs = np.zeros(len(present), CHUNK_DESC_DTYPE)
+        descs["src_off"] = [table[c][0] for c in present]
+        descs["src_len"] = [table[c][1] for c in present]
+        descs["dst_len"] = self.plan.chunk_nbytes
+        descs["dst_off"] = np.arange(len(present), dtype=np.int64) * _align(self.plan.chunk_nbytes, 256)
+        ext = len(present) * _align(self.plan.chunk_nbytes, 256)
         # missing chunks get their own fill-value slot after the decoded ones
         slot = {c: int(descs[k]["dst_off"]) for k, c in enumerate(present)}
         for c in ids:
@@ -669,8 +683,10 @@ class PagedReader:
     pieces straight into the host page buffer (hsds_host_map'ed; with world > 1 a
     /dev/shm file every rank of the node maps, `shm_path`), then a barrier.
 
-    get_blobs(chunk_ids) -> {chunk_id: stored object bytes / uint8 array}; an id
-    without an object reads as the fill value."""
+    `source` is get_blobs(chunk_ids) -> {chunk_id: stored object bytes / uint8 array}
+    (host objects, staged per decode batch), or a (d_src, {chunk_id: (src_off, src_len)})
+    pair of objects already in HBM (stage_objects); an id without an object reads as the
+    fill value."""
 
     def __init__(self, dset_id, dims, layout, selection, dtype, world, rank, device, max_request_size=100 << 20,
                  compressor="zlib", shuffle=1, mode="gather", root=0, group=None, shm_path=None):
@@ -736,16 +752,24 @@ class PagedReader:
         offs = np.array([keep[c] * self.cstride for c in ids], np.int64)
         return offs, new, new_slots
 
-    def _decode(self, new, new_slots, get_blobs, fill_value):
-        from .engine import CHUNK_DESC_DTYPE, pack_chunks, to_device_bytes
+    def _decode(self, new, new_slots, source, fill_value):
+        from .engine import CHUNK_DESC_DTYPE, pack_chunks
         torch = self.torch
-        blobs = get_blobs(new) if new else {}
-        present = [(c, k) for c, k in zip(new, new_slots) if c in blobs]
-        missing = [k for c, k in zip(new, new_slots) if c not in blobs]
+        staged = isinstance(source, tuple)
+        table = source[1] if staged else (source(new) if new else {})
+        present = [(c, k) for c, k in zip(new, new_slots) if c in table]
+        missing = [k for c, k in zip(new, new_slots) if c not in table]
         if present:
-            src, descs, _ = pack_chunks([blobs[c] for c, _ in present], [self.csize] * len(present))
+            if staged:
+                d_src = source[0]
+                descs = np.zeros(len(present), CHUNK_DESC_DTYPE)
+                descs["src_off"] = [table[c][0] for c, _ in present]
+                descs["src_len"] = [table[c][1] for c, _ in present]
+                descs["dst_len"] = self.csize
+            else:
+                src, descs, _ = pack_chunks([table[c] for c, _ in present], [self.csize] * len(present))
+                d_src = torch.from_numpy(src).to(self.device)
             descs["dst_off"] = np.array([k * self.cstride for _, k in present], np.uint64)
-            d_src = torch.from_numpy(src).to(self.device)
             st = torch.full((len(present),), 99, dtype=torch.int32, device=self.device)
             self.eng.decode(d_src, descs, self.pool, st, compressor=self.compressor, shuffle=self.shuffle,
                             itemsize=self.dtype.itemsize)
@@ -761,7 +785,7 @@ class PagedReader:
                 self.pool[k * self.cstride:k * self.cstride + self.csize].copy_(d_fill)
         self.stats["decoded"] += len(new)
 
-    def read(self, get_blobs, sink, fill_value=None):
+    def read(self, source, sink, fill_value=None):
         """Read every page in order; returns the total bytes handed to `sink` (root)."""
         torch = self.torch
         total = 0
@@ -770,7 +794,7 @@ class PagedReader:
             ids = plan.chunk_ids(self.rank)
             offs, new, new_slots = self._slots(ids)
             self.stats["reused"] += len(ids) - len(new)
-            self._decode(new, new_slots, get_blobs, fill_value)
+            self._decode(new, new_slots, source, fill_value)
             nb = self.page_bytes[pno]
             if self.mode == "direct":
                 if len(ids):

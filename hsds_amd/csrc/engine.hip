@@ -1,25 +1,27 @@
 // engine.hip -- MI355X (gfx950) chunk codec + hyperslab engine behind include/hsds_amd.h.
 //
 // Kernels (all batched over many chunks, one launch per stage):
-//   frame_walk_kernel   one thread per chunk: Blosc1 / zlib / raw detection
-//                       (storUtil._uncompress, storUtil.py:182-235) and emission of
-//                       one work item per deflate stream / raw split
-//   scan_kernel         exclusive scan of items per chunk (single workgroup)
-//   inflate_kernel      persistent waves pull stream items from a device counter;
-//                       one wavefront decodes one zlib stream (inflate_wave.h)
-//   lz_kernel           the same for LZ4 / BloscLZ Blosc splits (lz_wave.h)
+//  decode (storUtil._uncompress, storUtil.py:182-235)
+//   frame_walk_kernel   one thread per chunk: Blosc1 / zlib / raw detection and emission
+//                       of one work item per deflate stream / LZ / zstd / raw split into
+//                       a compact item pool (no per-chunk split cap)
+//   inflate2_kernel     persistent waves pull zlib / raw items from a device counter; one
+//                       wavefront decodes one zlib stream (inflate2.h), writing through
+//                       the byte-unshuffle output map (F2, Blosc typesize > 1)
+//   lz_kernel           LZ4 / BloscLZ Blosc splits, 8 per wavefront (lz_wave.h)
 //   zstd_kernel         zstd Blosc splits, one wavefront per split (zstd_wave.h)
-//   bshuf_kernel        bitshuffle+LZ4 chunks (shuffle = 2), one wavefront per chunk
-//                       (bshuf.h)
-//   unshuffle_kernel    byte unshuffle of staged chunks / Blosc blocks
-//   copy_kernel / compare_kernel   strided N-d region copies (hyperslab gather /
-//                       scatter, chunkUtil.py:882-995, chunk_crawl.py:418)
-//   enc_plan_kernel     one thread per chunk: c-blosc 1.21 frame geometry of
-//                       storUtil._compress (storUtil.py:238-281), one item per split
-//   deflate_kernel      persistent waves; one wavefront encodes one zlib stream
-//                       (deflate_wave.h)
-//   frame_kernel        one workgroup per chunk: Blosc1 header, bstarts, raw-split and
-//                       memcpyed fallbacks, payload copies into the final frame
+//   bshuf_kernel        bitshuffle+LZ4 chunks (shuffle = 2), one wavefront per chunk (bshuf.h)
+//   unshuffle_kernel    byte unshuffle of staged LZ / zstd Blosc blocks with typesize > 1
+//  hyperslab copies (chunkUtil.py:882-995, chunk_crawl.py:118-150,395-418)
+//   copy_kernel / compare_kernel   strided N-d region copies / numpy-equal compares
+//   plan_descs_kernel   one thread per piece: copy records of a hyperslab plan
+//  encode (storUtil._compress, storUtil.py:238-281)
+//   enc_plan_kernel     one thread per chunk: c-blosc 1.21 frame geometry, one item per split
+//   parse_kernel        persistent waves, one zlib / LZ stream each: hash chains + parse
+//   huff_kernel, emit_kernel     one wave per 8 KiB segment: Huffman code, bit emission
+//   lz4_block_kernel    LZ4 / BloscLZ blocks from the parse tokens (lz4_enc.h)
+//   layout_kernel, raw_copy_kernel   frame layout, raw splits and memcpyed payloads
+//   bs_*_kernel         bitshuffle+LZ4 writer (plan, fill, transposition, layout)
 // Every launch is asynchronous on the caller's stream; no host synchronisation
 // inside the batched entry points.
 #include <hip/hip_runtime.h>

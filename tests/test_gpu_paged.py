@@ -39,17 +39,21 @@ def _blobs(full, missing=()):
 
 
 @pytest.mark.parametrize("mode", ["gather", "direct"])
-def test_paged_read_matches_numpy(mode):
+@pytest.mark.parametrize("staged", [False, True])
+def test_paged_read_matches_numpy(mode, staged):
     import torch
     full = _data()
     blobs = _blobs(full, missing={(3, 1)})
     size = int(np.prod(sel.getSelectionShape(SELECT))) * 4
-    rd = crawl.PagedReader(DSET, DIMS, LAYOUT, SELECT, np.float32, 1, 0, torch.device("cuda", 0),
-                           max_request_size=size // 6, mode=mode)
+    dev = torch.device("cuda", 0)
+    rd = crawl.PagedReader(DSET, DIMS, LAYOUT, SELECT, np.float32, 1, 0, dev, max_request_size=size // 6, mode=mode)
     assert len(rd.pages) >= 6
     got = []
-    n = rd.read(lambda ids: {c: blobs[c] for c in ids if c in blobs},
-                lambda pno, page, b: got.append(np.array(b, copy=True)), fill_value=-1.5)
+    if staged:     # objects already in HBM (one copy per chunk id)
+        source = crawl.stage_objects(blobs, sorted(blobs), dev)
+    else:          # host objects fetched per decode batch
+        source = lambda ids: {c: blobs[c] for c in ids if c in blobs}   # noqa: E731
+    n = rd.read(source, lambda pno, page, b: got.append(np.array(b, copy=True)), fill_value=-1.5)
     rd.close()
     assert n == size
     want = full.copy()

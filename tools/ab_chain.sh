@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 for c in "$@"; do
   HSDS_DEFLATE_CHAIN=$c timeout -k 10 300 python bench.py --headline 0 --steps 3 --warmup 1 --cpu-seconds 0 \
-    --cfg3 0 --cfg1 0 --cfg5 1 > gpurun_out/abc_$c.log 2>&1
+    --cfg3 0 --cfg1 0 --cfg5 1 --cfg4-full 0 > gpurun_out/abc_$c.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "chain $c rc=$rc"; tail -5 gpurun_out/abc_$c.log; exit $rc; }
   python - $c gpurun_out/abc_$c.log <<'PY'
 import json, sys

@@ -9,7 +9,7 @@ RND=${RND:-r2}
 OUT=$R/gpurun_out/traffic
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-OFF="--cpu-seconds 0 --f2 0 --e2e 0 --cfg5 0 --cfg5w 0 --cfg4 0 --lz4 0 --zstd 0 --bshuf 0 --cfg1 0"
+OFF="--cpu-seconds 0 --f2 0 --e2e 0 --cfg5 0 --cfg5w 0 --cfg4 0 --cfg4-full 0 --lz4 0 --zstd 0 --bshuf 0 --cfg1 0"
 ARGS="--steps 1 --warmup 1 --cfg3 0 $OFF"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- \
   python3 $R/bench.py $ARGS > $OUT/fetch.log 2>&1
