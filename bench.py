@@ -599,6 +599,44 @@ def run_cfg5(args, dev, rank=0):
                          "ms_per_step": round(el4 * 1e3, 3), "compressed_bytes": comp4,
                          "encode_ms": round(eng.last_deflate_ms(), 3),
                          "format": "Blosc-lz4 frames (typesize 1, c-blosc lz4 blocksize), parse tokens -> LZ4 blocks"}
+    # the same scatter + encode for a zstd dataset (Blosc-zstd frames, level 5)
+    def step_zstd():
+        eng.copy(slab_u8, chunks, d_cd, stream=stream)
+        eng.encode(chunks, d_desc, frames, sizes, st, clevel=5, shuffle=1, typesize=1, stream=stream,
+                   compressor="zstd")
+
+    step_zstd()
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0, "zstd encode status errors"
+    o = int(descs[n // 5]["dst_off"])
+    fr = frames[o:o + int(sizes[n // 5])].cpu().numpy().tobytes()
+    assert orc.uncompress(fr, "zstd", 1, 1, cbytes) == chunks[(n // 5) * cbytes:(n // 5 + 1) * cbytes].cpu().numpy().tobytes()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_zstd()
+    torch.cuda.synchronize()
+    elz = (time.perf_counter() - t0) / args.steps
+    compz = int(sizes.sum())
+    zr = None
+    try:   # libblosc's own zstd objects for the same sampled chunks (the reference's c-blosc)
+        import ctypes
+        lb = ctypes.CDLL("/opt/conda/lib/libblosc.so.1")
+        lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
+                                          ctypes.c_size_t, ctypes.c_int]
+        refz = 0
+        for x in samp:
+            ob = np.empty(x.size + 64, np.uint8)
+            refz += lb.blosc_compress_ctx(5, 1, 1, x.size, x.ctypes.data, ob.ctypes.data, ob.size, b"zstd", 0, 1)
+        zr = round(sum(int(sizes[k]) for k in ks) / refz, 4)
+    except OSError:
+        pass
+    out["zstd_encode"] = {"value": round(slab_bytes / elz / 1e9, 2), "unit": "GB/s slab (scatter + encode)",
+                          "ms_per_step": round(elz * 1e3, 3), "compressed_bytes": compz,
+                          "encode_ms": round(eng.last_deflate_ms(), 3), "size_vs_libblosc_zstd": zr,
+                          "format": "Blosc-zstd frames (HCR blocksize, never split): raw literals + predefined "
+                                    "sequence tables, one zstd block per 8 KiB"}
     # the same scatter + encode for a bitshuffle dataset (storUtil._shuffle codec 2:
     # bitshuffle+LZ4 objects, f32, 2048-element blocks, no outer compressor)
     from hsds_amd import _native as nat

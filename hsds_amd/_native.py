@@ -22,14 +22,14 @@ ERR_ARG = -6
 ERR_DEVICE = -7
 
 COMP_NONE, COMP_ZLIB, COMP_OTHER = 0, 1, 2
-CNAME_ZLIB, CNAME_LZ4, CNAME_LZ4HC, CNAME_BLOSCLZ = 0, 1, 2, 3
+CNAME_ZLIB, CNAME_LZ4, CNAME_LZ4HC, CNAME_BLOSCLZ, CNAME_ZSTD = 0, 1, 2, 3, 4
 
 
 def cname_code(compressor):
     """storUtil._compress compressor -> HSDS_CNAME_* (None when the engine has no encoder for it)"""
     if compressor in ("gzip", "deflate", "zlib"):
         return CNAME_ZLIB
-    return {"lz4": CNAME_LZ4, "lz4hc": CNAME_LZ4HC, "blosclz": CNAME_BLOSCLZ}.get(compressor)
+    return {"lz4": CNAME_LZ4, "lz4hc": CNAME_LZ4HC, "blosclz": CNAME_BLOSCLZ, "zstd": CNAME_ZSTD}.get(compressor)
 SHUFFLE_NONE, SHUFFLE_BYTE, SHUFFLE_BIT = 0, 1, 2
 MAX_RANK = 8
 KIND_BYTES, KIND_F16, KIND_F32, KIND_F64, KIND_C64, KIND_C128 = 0, 1, 2, 3, 4, 5

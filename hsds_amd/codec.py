@@ -13,7 +13,7 @@ Same names, argument meaning and error behaviour as the reference:
     (storUtil.py:103-131) through the bitshuffle encode kernels.
 
 All byte work runs on the MI355X through the C ABI (include/hsds_amd.h); there is
-no CPU fallback.  The zstd writer and the snappy codec raise NotImplementedError.
+no CPU fallback.  The snappy codec raises NotImplementedError.
 """
 import numpy as np
 
@@ -189,8 +189,9 @@ def _compress(data, compressor=None, level=5, shuffle=0, dtype=None, chunk_shape
     storUtil.py:255-257; lz4 and lz4hc carry LZ4 blocks, blosclz BloscLZ), typesize 1 because the
     reference always hands Blosc a bytes object, and the byte-shuffle flag from
     `shuffle`.  Differences from the reference, by design:
-      * the zstd encoder is outside this engine and raises NotImplementedError
-        (the reference would encode it with c-blosc);
+      * zstd splits are the GPU writer's frames (raw literals, predefined sequence
+        tables, one block per 8 KiB; zstd_enc.h), not libzstd's bytes: any valid frame
+        decodes identically through c-blosc;
       * bitshuffle (shuffle=2) objects carry the GPU LZ4 writer's blocks, not liblz4's
         (any valid block: bitshuffle.decompress_lz4 reads both);
       * an encoder failure raises instead of silently storing the raw bytes

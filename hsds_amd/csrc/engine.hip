@@ -41,6 +41,7 @@
 #include "lz4_enc.h"
 #include "zstd_wave.h"
 #include "bshuf.h"
+#include "zstd_enc.h"
 
 #ifndef HZ_ZSTD_WPE
 #define HZ_ZSTD_WPE 3      // zstd_kernel waves per SIMD the compiler must allow (VGPR budget)
@@ -661,7 +662,9 @@ struct SegMeta {       // parse -> huffman
 
 // c-blosc 1.21 compute_blocksize (oracle.c orc_blosc_blocksize_codec): the HCR codecs
 // (zlib, lz4hc) start from 2 x L1 and double again at level 9, lz4 from L1
-__device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint64_t nbytes, int hcr) {
+// (zstd: HCR sizes, but c-blosc never splits zstd blocks, so no split enlargement;
+// pinned against libblosc 1.21 zstd headers, tests/test_oracle_golden.py)
+__device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint64_t nbytes, int hcr, int splittable = 1) {
   if (nbytes < ts) return 1;
   uint64_t bs = nbytes;
   if (nbytes >= 32 * 1024) {
@@ -676,7 +679,7 @@ __device__ __forceinline__ uint64_t enc_blocksize(int clevel, uint32_t ts, uint6
       default: bs *= hcr ? 16 : 8; break;
     }
   }
-  if (clevel > 0 && ts <= 16 && bs / ts >= 128) {
+  if (splittable && clevel > 0 && ts <= 16 && bs / ts >= 128) {
     if (bs > (1u << 18)) bs = 1u << 18;
     bs *= ts;
     if (bs < (1u << 16)) bs = 1u << 16;
@@ -704,15 +707,17 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
   const uint64_t nbytes = c.src_len;
   int st = HSDS_OK;
   uint32_t cnt = 0, nseg = 0;
-  // Blosc1 codec: zlib 3, lz4 / lz4hc 1, blosclz 0
-  const uint32_t fmt = cname == HSDS_CNAME_ZLIB ? 3u : cname == HSDS_CNAME_BLOSCLZ ? 0u : 1u;
+  // Blosc1 codec: zlib 3, zstd 4, lz4 / lz4hc 1, blosclz 0
+  const uint32_t fmt = cname == HSDS_CNAME_ZLIB ? 3u : cname == HSDS_CNAME_ZSTD ? 4u : cname == HSDS_CNAME_BLOSCLZ ? 0u : 1u;
+  const int zstd = cname == HSDS_CNAME_ZSTD;
   EncGeom g = {nbytes, 0, 0, (fmt << 5) | (shuffle ? 1u : 0u), ts, 0};
   if (c.dst_len < nbytes + 16 || nbytes >= (1ull << 31) - 16 || (c.dst_off & 3)) {
     st = HSDS_ERR_ARG;
   } else {
-    const uint64_t bs = enc_blocksize(clevel, ts, nbytes, cname == HSDS_CNAME_ZLIB || cname == HSDS_CNAME_LZ4HC);
+    const uint64_t bs = enc_blocksize(clevel, ts, nbytes, cname == HSDS_CNAME_ZLIB || cname == HSDS_CNAME_LZ4HC || zstd,
+                                      !zstd);
     g.bs = bs;
-    if (!(ts <= 16 && bs / ts >= 128)) g.flags |= 0x10;
+    if (zstd || !(ts <= 16 && bs / ts >= 128)) g.flags |= 0x10;
     g.memcpyed = (nbytes < 128 || clevel <= 0) ? 1u : 0u;
     const uint64_t nblocks = bs ? (nbytes + bs - 1) / bs : 0;
     const uint64_t leftover = bs ? nbytes % bs : 0;
@@ -1027,6 +1032,77 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
   }
 }
 
+// zstd write path (zstd_enc.h): one lane per 8 KiB segment writes that segment as one zstd
+// block into its scratch slot; zstd_size_kernel sums a stream's blocks for the layout;
+// zstd_write_kernel (one wave per stream) writes the frame header and moves the blocks
+__global__ void __launch_bounds__(64) zstd_seg_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                      const SegMeta* __restrict__ meta,
+                                                      const EncItem* __restrict__ slots,
+                                                      const hd::SegParse* __restrict__ sp,
+                                                      const uint16_t* __restrict__ tok, uint8_t* __restrict__ zscr,
+                                                      uint32_t* __restrict__ zsz, uint32_t seg_cap, int level) {
+  __shared__ hze::Tabs T;
+  if (threadIdx.x == 0) hze::build_all(T);
+  __syncthreads();
+  uint32_t total = segoffs[nchunks];
+  if (total > seg_cap) total = seg_cap;
+  const uint32_t s = blockIdx.x * 64u + threadIdx.x;
+  if (s >= total) return;
+  const SegMeta m = meta[s];
+  const EncItem it = slots[m.item];
+  const uint32_t g0 = segoffs[it.chunk] + it.seg0;
+  const uint32_t seg = s - g0;
+  hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
+  const uint32_t last = seg + 1 == hd::nsegments(it.len) ? 1u : 0u;
+  zsz[s] = hze::encode_segment(T, tok + (size_t)s * hd::SEG_TOK, sp + s, job, seg * (uint32_t)hd::SEG, m.seglen, last,
+                               zscr + (size_t)s * hze::ZCAP, hze::ZCAP);
+}
+
+__global__ void zstd_size_kernel(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ segoffs,
+                                 int64_t nchunks, const EncItem* __restrict__ slots, const uint32_t* __restrict__ zsz,
+                                 uint32_t* __restrict__ lzsize, uint32_t seg_cap, uint32_t item_cap) {
+  const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
+  const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= total) return;
+  const EncItem it = slots[item];
+  const uint32_t g0 = segoffs[it.chunk] + it.seg0, ns = hd::nsegments(it.len);
+  if (g0 + ns > seg_cap) { lzsize[item] = 0xffffffffu; return; }
+  uint64_t sz = hze::frame_header_size(it.len);
+  for (uint32_t k = 0; k < ns; k++) sz += zsz[g0 + k];
+  lzsize[item] = sz < 0xffffffffull ? (uint32_t)sz : 0xffffffffu;
+}
+
+__global__ void __launch_bounds__(64) zstd_write_kernel(const uint32_t* __restrict__ offs,
+                                                        const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                        const EncItem* __restrict__ slots,
+                                                        const uint8_t* __restrict__ zscr,
+                                                        const uint32_t* __restrict__ zsz,
+                                                        const hsds_chunk_desc* __restrict__ chunks, uint8_t* dst_base,
+                                                        const EncGeom* __restrict__ geom,
+                                                        const ItemOut* __restrict__ iout,
+                                                        const int32_t* __restrict__ status, uint32_t seg_cap,
+                                                        uint32_t item_cap) {
+  const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
+  for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
+    const EncItem it = slots[item];
+    const int64_t ci = it.chunk;
+    if (status[ci] != HSDS_OK || geom[ci].memcpyed || iout[item].raw) continue;
+    const uint32_t g0 = segoffs[ci] + it.seg0, ns = hd::nsegments(it.len);
+    if (g0 + ns > seg_cap) continue;
+    uint8_t* o = dst_base + chunks[ci].dst_off + iout[item].pos;
+    uint8_t hdr[16];
+    const uint32_t h = hze::frame_header(hdr, it.len);
+    if (threadIdx.x < h) o[threadIdx.x] = hdr[threadIdx.x];
+    uint64_t p = h;
+    for (uint32_t k = 0; k < ns; k++) {
+      const uint32_t n = zsz[g0 + k];
+      const uint8_t* src = zscr + (size_t)(g0 + k) * hze::ZCAP;
+      for (uint32_t i = threadIdx.x; i < n; i += 64u) o[p + i] = src[i];
+      p += n;
+    }
+  }
+}
+
 // bounded unaligned 32-bit load: bytes [p, p+4) of a buffer whose valid bytes are [b, e)
 __device__ __forceinline__ uint32_t ld32u(const uint8_t* p, const uint8_t* b, const uint8_t* e) {
   const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
@@ -1282,6 +1358,8 @@ struct hsds_engine {
   size_t escr_bytes = 0;
   uint8_t* efar = nullptr;     // encode: zlib parse far-chain rings, one per parse workgroup
   size_t efar_bytes = 0;
+  uint8_t* ezs = nullptr;      // encode: zstd block scratch (one ZCAP slot + size per segment)
+  size_t ezs_bytes = 0;
   uint32_t enc_chain = 0;      // development override of the parse chain depth (0: the level's)
   hipEvent_t ev2, ev3;
   int ev_enc_valid = 0;
@@ -1443,6 +1521,7 @@ void hsds_engine_destroy(hsds_engine* e) {
   if (e->ecw) hipFree(e->ecw);
   if (e->escr) hipFree(e->escr);
   if (e->efar) hipFree(e->efar);
+  if (e->ezs) hipFree(e->ezs);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
   hipEventDestroy(e->ev2);
@@ -1816,7 +1895,8 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
                             void* d_dst, uint64_t dst_extent, int64_t* d_sizes, int32_t* d_status, int clevel,
                             int shuffle, int typesize, int cname, void* stream) {
   if (!e || nchunks < 0 || (nchunks && (!d_src || !d_chunks || !d_dst || !d_sizes || !d_status))) return HSDS_ERR_ARG;
-  if (cname != HSDS_CNAME_ZLIB && cname != HSDS_CNAME_LZ4 && cname != HSDS_CNAME_LZ4HC && cname != HSDS_CNAME_BLOSCLZ)
+  if (cname != HSDS_CNAME_ZLIB && cname != HSDS_CNAME_LZ4 && cname != HSDS_CNAME_LZ4HC && cname != HSDS_CNAME_BLOSCLZ &&
+      cname != HSDS_CNAME_ZSTD)
     return HSDS_ERR_ARG;
   if (clevel < 0 || clevel > 9 || (shuffle != HSDS_SHUFFLE_NONE && shuffle != HSDS_SHUFFLE_BYTE)) return HSDS_ERR_ARG;
   if (((uintptr_t)d_dst & 3u) != 0) return HSDS_ERR_ARG;
@@ -1888,8 +1968,8 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   };
   const unsigned pgrid = grid_for(e->parse_blocks_per_cu, item_cap);
   uint16_t* far = nullptr;
-  if (cname == HSDS_CNAME_ZLIB && hd::far_level(clevel)) {
-    // zlib levels >= 6: matches reach 32 KiB back, the chains beyond the LDS ring live in HBM
+  if ((cname == HSDS_CNAME_ZLIB || cname == HSDS_CNAME_ZSTD) && hd::far_level(clevel)) {
+    // levels >= 6: matches reach 32 KiB back, the chains beyond the LDS ring live in HBM
     if (grow((void**)&e->efar, &e->efar_bytes, (size_t)pgrid * hd::FARW * 2)) return HSDS_ERR_DEVICE;
     far = (uint16_t*)e->efar;
   }
@@ -1900,7 +1980,19 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
                      // blosclz keep the exact chains
                      cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, 0u, item_cap, far,
                      e->enc_chain);
-  if (cname == HSDS_CNAME_ZLIB) {
+  if (cname == HSDS_CNAME_ZSTD) {
+    if (grow((void**)&e->ezs, &e->ezs_bytes, (size_t)seg_cap * (hze::ZCAP + 4) + 256)) return HSDS_ERR_DEVICE;
+    uint8_t* zscr = e->ezs;
+    uint32_t* zsz = (uint32_t*)(e->ezs + (size_t)seg_cap * hze::ZCAP);
+    hipLaunchKernelGGL(zstd_seg_kernel, dim3((seg_cap + 63) / 64), dim3(64), 0, st, segoffs, nchunks, meta, slots, sp,
+                       tok, zscr, zsz, seg_cap, clevel);
+    hipLaunchKernelGGL(zstd_size_kernel, dim3((item_cap + 255) / 256), dim3(256), 0, st, offs, segoffs, nchunks, slots,
+                       zsz, lzsize, seg_cap, item_cap);
+    hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,
+                       offs, segoffs, geom, sc, adler, iout, so, d_sizes, d_status, seg_cap, clevel, (const uint32_t*)lzsize);
+    hipLaunchKernelGGL(zstd_write_kernel, dim3(grid_for(16, item_cap)), dim3(64), 0, st, offs, segoffs, nchunks, slots,
+                       zscr, zsz, d_chunks, (uint8_t*)d_dst, geom, iout, d_status, seg_cap, item_cap);
+  } else if (cname == HSDS_CNAME_ZLIB) {
     hipLaunchKernelGGL(huff_kernel, dim3(grid_for(e->huff_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                        nchunks, ctr + 1, sp, meta, sc, seg_cap, clevel);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,

@@ -58,6 +58,7 @@ extern "C" {
 #define HSDS_CNAME_LZ4 1        /* "lz4": Blosc codec 1, c-blosc's lz4 blocksize   */
 #define HSDS_CNAME_LZ4HC 2      /* "lz4hc": Blosc codec 1, HCR blocksize           */
 #define HSDS_CNAME_BLOSCLZ 3    /* "blosclz": Blosc codec 0, c-blosc's L1 blocksize */
+#define HSDS_CNAME_ZSTD 4       /* "zstd": Blosc codec 4, HCR blocksize, never split */
 
 /* shuffle codes (storUtil.BYTE_SHUFFLE / BIT_SHUFFLE) */
 #define HSDS_SHUFFLE_NONE 0

@@ -8,6 +8,7 @@
 #include <vector>
 #include "../../hsds_amd/csrc/deflate_wave.h"
 #include "../../hsds_amd/csrc/lz4_enc.h"
+#include "../../hsds_amd/csrc/zstd_enc.h"
 
 // far: the HBM far-chain ring is handed over (the parse uses it when tune.far, as the engine)
 static int64_t run(const hd::EncJob& job, const hd::Tune& tune, uint8_t* dst, uint32_t cap, int far = 1) {
@@ -116,6 +117,37 @@ extern "C" int64_t emu_blosclz_block(const uint8_t* src, uint32_t n, uint8_t* ds
   if (sz > cap) return -1;
   const uint32_t sz2 = lze::blosclz_block_wave(sp.data(), tok.data(), job, dst, 1);
   return sz2 == sz ? (int64_t)sz : -2;
+}
+
+// zstd frame of one Blosc block (the zstd writer): parse, then one zstd block per 8 KiB
+// segment (zstd_enc.h), behind the frame header.  Returns the frame size or -1 past cap.
+extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level) {
+  const uint32_t nseg = hd::nsegments(n);
+  std::vector<hd::SegParse> sp(nseg);
+  std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
+  hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
+  std::vector<uint16_t> fr(hd::FARW, 0);
+  hd::EncJob job = {src, n, level, 1u, 0u, 0u};
+  hd::parse_stream(*ps, job, hd::tune_for_level(level), sp.data(), tok.data(), nullptr, fr.data());
+  free(ps);
+  hze::Tabs T;
+  hze::build_all(T);
+  std::vector<uint8_t> blk(hze::ZCAP);
+  uint8_t hdr[16];
+  const uint32_t h = hze::frame_header(hdr, n);
+  uint64_t pos = 0;
+  auto put = [&](const uint8_t* p, uint32_t k) {
+    for (uint32_t i = 0; i < k; i++, pos++) if (pos < cap) dst[pos] = p[i];
+  };
+  put(hdr, h);
+  for (uint32_t s = 0; s < nseg; s++) {
+    const uint32_t s0 = s * (uint32_t)hd::SEG;
+    const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
+    const uint32_t k = hze::encode_segment(T, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], job, s0, seglen,
+                                           s + 1 == nseg ? 1u : 0u, blk.data(), hze::ZCAP);
+    put(blk.data(), k);
+  }
+  return pos <= cap ? (int64_t)pos : -1;
 }
 
 extern "C" int emu_parse_shared_bytes() { return (int)sizeof(hd::ParseShared); }

@@ -366,3 +366,57 @@ def test_bitshuffle_deflate_batch_fails_per_chunk(dev, oracle_lib):
             assert isinstance(r, codec.HTTPInternalServerError), (i, r)
         else:
             assert r.cpu().numpy().tobytes() == truth[f"k{i}"], i
+
+
+def test_put_and_flush_zstd_dataset(dev, oracle_lib):
+    """A zstd-filtered dataset (H5Z_FILTER_ZSTD 32015): PUT_Chunk on stored Blosc-zstd
+    objects (written by libblosc, as the reference would), flush through the GPU zstd
+    writer; the objects decode through the oracle and read back through the GPU."""
+    import ctypes
+    import os
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    from hsds_amd.filters import getFilterOps
+    p = "/opt/conda/lib/libblosc.so.1"
+    if not os.path.exists(p):
+        pytest.skip("libblosc absent")
+    lb = ctypes.CDLL(p)
+    lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    orc = oracle_lib
+    dims = (128, 256)
+    dt = np.dtype("<f4")
+    rng = np.random.default_rng(13)
+    ops = getFilterOps({"filter_map": {}}, "d-z", [{"class": "H5Z_FILTER_SHUFFLE", "id": 2, "name": "shuffle"},
+                                                   {"class": "H5Z_FILTER_ZSTD", "id": 32015, "name": "zstd"}],
+                       dtype=dt, chunk_shape=dims)
+    assert ops["compressor"] == "zstd"
+    truth, store = {}, {}
+    for i in range(4):
+        a = np.round(np.cumsum(rng.normal(size=dims[0] * dims[1])), 2).astype(dt).reshape(dims)
+        truth[f"c-z_{i}_0"] = a
+        out = np.empty(a.nbytes + 64, np.uint8)
+        k = lb.blosc_compress_ctx(ops["level"], 1, 1, a.nbytes, a.ctypes.data, out.ctypes.data, out.size, b"zstd", 0, 1)
+        store[f"k{i}"] = out[:k].tobytes()
+    keys = {f"c-z_{i}_0": f"k{i}" for i in range(4)}
+    cs = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    sel = (slice(3, 128, 2), slice(10, 250, 7))
+    d = np.round(rng.normal(size=(len(range(3, 128, 2)), len(range(10, 250, 7)))), 3).astype(dt)
+    writes = [(ChunkRead(f"c-z_{i}_0", f"k{i}"), sel, d) for i in (1, 3)]
+    assert cs.put_selections(writes, dt, dims, filter_ops=ops) == [True, True]
+    flushed = {}
+    ids = cs.flush(lambda k, b: flushed.__setitem__(k, b), filter_ops=ops, keys=keys)
+    assert sorted(ids) == ["c-z_1_0", "c-z_3_0"]
+    for cid in ids:
+        f = flushed[keys[cid]]
+        assert f[2] >> 5 == 4                      # Blosc codec 4: zstd
+        want = truth[cid].copy()
+        want[sel] = d
+        assert orc.uncompress(f, "zstd", 1, 4, want.nbytes) == want.tobytes(), cid
+    store.update(flushed)
+    cs2 = ChunkStore(lambda k, o, n: store.get(k), mem_target=1 << 24, device=dev)
+    res = cs2.get_chunks([ChunkRead(c, keys[c]) for c in sorted(keys)], dt, dims, filter_ops=ops)
+    for cid, r in zip(sorted(keys), res):
+        want = truth[cid].copy()
+        if cid in ids:
+            want[sel] = d
+        assert r.cpu().numpy().tobytes() == want.tobytes(), cid

@@ -348,3 +348,115 @@ def test_lz4_batch_mixed_gpu_roundtrip(dev, oracle_lib):
     dec = g_dst.cpu().numpy()
     for d, r in zip(data, pdescs):
         assert dec[int(r["dst_off"]):int(r["dst_off"]) + len(d)].tobytes() == d
+
+
+# ---- the zstd write path (Blosc codec 4, zstd_enc.h blocks from the parse tokens) ----
+
+def _libblosc():
+    import ctypes
+    import os
+    p = "/opt/conda/lib/libblosc.so.1"
+    if not os.path.exists(p):
+        pytest.skip("libblosc absent")
+    lb = ctypes.CDLL(p)
+    lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    lb.blosc_decompress_ctx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return lb
+
+
+@pytest.mark.parametrize("name", sorted(INPUTS))
+@pytest.mark.parametrize("level", [1, 5, 9])
+def test_zstd_compress_matches_libblosc_geometry_and_decodes(dev, oracle_lib, name, level):
+    """storUtil._compress(compressor="zstd"): the Blosc header (flags, typesize, nbytes,
+    blocksize) equals libblosc 1.21's for the same input and level, and the object decodes
+    to the input through libblosc's own blosc_decompress (the reference's c-blosc), the
+    oracle and the GPU decoder."""
+    from hsds_amd import codec
+    lb = _libblosc()
+    data = INPUTS[name]()
+    n = len(data)
+    frame = codec._compress(data, compressor="zstd", level=level, shuffle=1)
+    h = header(frame)
+    a = np.frombuffer(data, np.uint8) if n else np.zeros(1, np.uint8)
+    ref = np.empty(n + 64, np.uint8)
+    k = lb.blosc_compress_ctx(level, 1, 1, n, a.ctypes.data, ref.ctypes.data, ref.size, b"zstd", 0, 1)
+    assert k > 0
+    r = header(ref[:k].tobytes())
+    assert (h["version"], h["typesize"], h["nbytes"], h["blocksize"]) == (r["version"], r["typesize"], r["nbytes"],
+                                                                          r["blocksize"])
+    if not (h["flags"] & 0x02) and not (r["flags"] & 0x02):
+        assert h["flags"] == r["flags"]
+    assert h["cbytes"] == len(frame) <= n + 16
+    if n:
+        back = np.zeros(n, np.uint8)
+        f = np.frombuffer(frame, np.uint8)
+        assert lb.blosc_decompress_ctx(f.ctypes.data, back.ctypes.data, n, 1) == n
+        assert back.tobytes() == data
+        assert oracle_lib.uncompress(frame, "zstd", 1, 1, n) == data
+        assert codec._uncompress(frame, compressor="zstd", shuffle=1, dtype=np.dtype("u1"), chunk_shape=(n,)) == data
+
+
+@pytest.mark.parametrize("ts", [2, 4, 8, 32])
+def test_zstd_batch_typesize_shuffle(dev, oracle_lib, ts):
+    import torch
+    from hsds_amd.engine import ChunkEngine, encode_descs, pack_chunks
+    data = [smooth(800 + ts, 1 << 18), smooth(900 + ts, 65536 * 3 + 4 * ts), bytes(70000 // ts * ts),
+            smooth(950 + ts, 1 << 20)]
+    descs, sext, dext = encode_descs([len(d) for d in data])
+    src = np.zeros(max(sext, 1), np.uint8)
+    for d, r in zip(data, descs):
+        src[int(r["src_off"]):int(r["src_off"]) + len(d)] = np.frombuffer(d, np.uint8)
+    d_src = torch.from_numpy(src).to(dev)
+    d_dst = torch.zeros(dext, dtype=torch.uint8, device=dev)
+    sizes = torch.zeros(len(data), dtype=torch.int64, device=dev)
+    st = torch.full((len(data),), 99, dtype=torch.int32, device=dev)
+    eng = ChunkEngine(0)
+    eng.encode(d_src, descs, d_dst, sizes, st, clevel=5, shuffle=1, typesize=ts, compressor="zstd")
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    out = d_dst.cpu().numpy()
+    frames = [out[int(r["dst_off"]):int(r["dst_off"]) + int(n)].tobytes() for r, n in zip(descs, sizes.cpu().numpy())]
+    for d, f in zip(data, frames):
+        h = header(f)
+        assert h["typesize"] == ts and h["flags"] & 0x10 and h["flags"] >> 5 == 4
+        assert oracle_lib.uncompress(f, "zstd", 1, ts, len(d)) == d
+    # and back through the GPU decoder (zstd_kernel + unshuffle)
+    psrc, pdescs, ext = pack_chunks(frames, [len(d) for d in data])
+    g_dst = torch.zeros(ext, dtype=torch.uint8, device=dev)
+    g_st = torch.full((len(data),), 99, dtype=torch.int32, device=dev)
+    eng.decode(torch.from_numpy(psrc).to(dev), pdescs, g_dst, g_st, compressor="zstd", shuffle=1, itemsize=ts)
+    torch.cuda.synchronize()
+    assert (g_st.cpu().numpy() == 0).all()
+    got = g_dst.cpu().numpy()
+    for d, r in zip(data, pdescs):
+        assert got[int(r["dst_off"]):int(r["dst_off"]) + len(d)].tobytes() == d
+
+
+def test_zstd_streams_equal_cpu_emulation(dev):
+    """The GPU zstd writer and the CPU emulation run the same source (zstd_enc.h over the
+    deflate parse): every split's zstd frame equals the emulator's bytes."""
+    import ctypes
+    import os
+    from hsds_amd import codec
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu", "libdeflate_emu.so")
+    L = ctypes.CDLL(lib)
+    L.emu_zstd_frame.restype = ctypes.c_int64
+    L.emu_zstd_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+    for seed, level, n in ((1, 5, 1 << 20), (2, 1, 1 << 19), (3, 9, 300000), (4, 6, 70001)):
+        data = smooth(seed, n - n % 4) + bytes(n % 4)
+        frame = codec._compress(data, compressor="zstd", level=level, shuffle=1)
+        h = header(frame)
+        assert not (h["flags"] & 0x02)
+        bs, nblocks = h["blocksize"], (h["nbytes"] + h["blocksize"] - 1) // h["blocksize"]
+        fb = np.frombuffer(frame, np.uint8)
+        for b in range(nblocks):
+            start = int(fb[16 + 4 * b:20 + 4 * b].view("<i4")[0])
+            cs = int(fb[start:start + 4].view("<i4")[0])
+            blk = np.frombuffer(data[b * bs:(b + 1) * bs], np.uint8)
+            if cs == len(blk):
+                continue                    # raw split
+            out = np.zeros(len(blk) + 4096, np.uint8)
+            r = L.emu_zstd_frame(blk.ctypes.data, len(blk), out.ctypes.data, out.size, level)
+            assert r == cs, (seed, b, r, cs)
+            assert out[:r].tobytes() == fb[start + 4:start + 4 + cs].tobytes(), (seed, b)

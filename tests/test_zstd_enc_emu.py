@@ -1,0 +1,138 @@
+"""CPU emulation of the zstd block writer (hsds_amd/csrc/zstd_enc.h, the GPU source
+compiled for the host): frames of the emulated parse + per-segment zstd blocks must decode
+to the input through libzstd 1.4.9 (the image's /opt/conda library; numcodecs' c-blosc
+vendors a zstd of the same format) and through the oracle's RFC 8878 restatement
+(orc_zstd_decode, pinned by the reference's zstd objects).  The Blosc-zstd frame geometry
+(HCR block size, never split) is pinned against libblosc 1.21 headers.  Test
+infrastructure only."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tests", "emu", "libdeflate_emu.so")
+LIBZSTD = "/opt/conda/lib/libzstd.so.1"
+LIBBLOSC = "/opt/conda/lib/libblosc.so.1"
+
+
+@pytest.fixture(scope="module")
+def emu():
+    if not os.path.exists(LIB):
+        pytest.skip("emulator not built")
+    L = ctypes.CDLL(LIB)
+    L.emu_zstd_frame.restype = ctypes.c_int64
+    L.emu_zstd_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+    return L
+
+
+@pytest.fixture(scope="module")
+def zstd():
+    if not os.path.exists(LIBZSTD):
+        pytest.skip("libzstd absent")
+    Z = ctypes.CDLL(LIBZSTD)
+    Z.ZSTD_decompress.restype = ctypes.c_size_t
+    Z.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    Z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    Z.ZSTD_compress.restype = ctypes.c_size_t
+    Z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return Z
+
+
+def frame(emu, a, level):
+    a = np.ascontiguousarray(a, np.uint8)
+    out = np.zeros(a.size + a.size // 64 + 1024, np.uint8)
+    k = emu.emu_zstd_frame(a.ctypes.data if a.size else 0, a.size, out.ctypes.data, out.size, level)
+    assert k > 0
+    return out[:k].tobytes()
+
+
+def unzstd(Z, f, n):
+    s = np.frombuffer(f, np.uint8)
+    out = np.zeros(n + 16, np.uint8)
+    r = Z.ZSTD_decompress(out.ctypes.data, out.size, s.ctypes.data, len(f))
+    assert not Z.ZSTD_isError(r), r
+    return out[:r].tobytes()
+
+
+def _smooth(rng, n):
+    return np.round(np.cumsum(rng.normal(size=n // 4)), 2).astype(np.float32).view(np.uint8)
+
+
+CASES = {
+    "smooth_256k": lambda r: _smooth(r, 1 << 18),
+    "smooth_odd": lambda r: np.concatenate([_smooth(r, 70000), np.arange(3, dtype=np.uint8)]),
+    "zeros_100k": lambda r: np.zeros(100000, np.uint8),
+    "random_30k": lambda r: r.integers(0, 256, 30000, dtype=np.uint8),
+    "runs": lambda r: np.repeat(r.integers(0, 4, 3000, dtype=np.uint8), r.integers(1, 40, 3000)),
+    "int16": lambda r: (np.cumsum(r.normal(size=40000)) * 100).astype("<i2").view(np.uint8),
+    "text": lambda r: np.frombuffer((b"the quick brown fox jumps over the lazy dog. " * 3000)[:70001], np.uint8),
+    "tiny": lambda r: np.frombuffer(b"abcabcabcabcabcXYZ" * 3, np.uint8),
+    "one_seg_edge": lambda r: np.concatenate([_smooth(r, 8192), np.zeros(1, np.uint8)]),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("level", [1, 5, 9])
+def test_frames_decode_through_libzstd_and_oracle(emu, zstd, name, level):
+    from oracle import oracle as orc
+    rng = np.random.default_rng(sum(map(ord, name)))
+    a = np.ascontiguousarray(CASES[name](rng), np.uint8)
+    f = frame(emu, a, level)
+    assert f[:4] == b"\x28\xb5\x2f\xfd"
+    assert unzstd(zstd, f, a.size) == a.tobytes()
+    assert orc.zstd_decode(f, a.size) == a.tobytes()
+
+
+def test_ratio_on_smooth_f32(emu, zstd):
+    # raw literals + predefined sequence tables: larger than libzstd's Huffman-coded
+    # literals; the bound documents the gap (zstd writer)
+    rng = np.random.default_rng(20261015)
+    ours = ref = 0
+    for _ in range(2):
+        a = _smooth(rng, 1 << 18)
+        ours += len(frame(emu, a, 5))
+        out = np.zeros(a.size + 1024, np.uint8)
+        ref += zstd.ZSTD_compress(out.ctypes.data, out.size, a.ctypes.data, a.size, 5)
+    assert ours / ref < 1.35, ours / ref
+
+
+def _blosc_zstd_header(lb, a, level, ts):
+    out = np.empty(a.size + 64, np.uint8)
+    k = lb.blosc_compress_ctx(level, 1, ts, a.size, a.ctypes.data, out.ctypes.data, out.size, b"zstd", 0, 1)
+    assert k > 0
+    return int(out[2]), int(out[8:12].view("<u4")[0])
+
+
+def hcr_blocksize_nosplit(level, ts, nbytes):
+    """c-blosc 1.21 compute_blocksize for zstd as hsds_amd restates it (engine.hip
+    enc_blocksize, splittable = 0): HCR base, no split enlargement."""
+    if nbytes < ts:
+        return 1
+    bs = nbytes
+    if nbytes >= 32 * 1024:
+        bs = 64 * 1024
+        bs = {0: bs // 4, 1: bs // 2, 2: bs, 3: bs * 2, 4: bs * 4, 5: bs * 4}.get(level, bs * (8 if level < 9 else 16))
+    bs = min(bs, nbytes)
+    return bs // ts * ts if bs > ts else bs
+
+
+def test_blosc_zstd_geometry_against_libblosc():
+    if not os.path.exists(LIBBLOSC):
+        pytest.skip("libblosc absent")
+    lb = ctypes.CDLL(LIBBLOSC)
+    lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    rng = np.random.default_rng(0)
+    n = 0
+    for nbytes in (200, 5000, 40000, 70000, 200000, 1 << 20, 3 << 20):
+        a = np.zeros(nbytes, np.uint8)          # the geometry does not depend on the bytes
+        a[::7] = rng.integers(0, 4, a[::7].size, dtype=np.uint8)
+        for level in range(10):
+            for ts in ((1, 2, 4, 8, 16, 17, 32) if nbytes < (1 << 20) else (1, 17)):
+                flags, bs = _blosc_zstd_header(lb, a, level, ts)
+                assert bs == hcr_blocksize_nosplit(level, ts, nbytes), (nbytes, level, ts, bs)
+                assert flags & 0x10 and flags >> 5 == 4, (nbytes, level, ts, flags)
+                n += 1
+    assert n == 5 * 70 + 2 * 20
