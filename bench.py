@@ -837,6 +837,7 @@ def run_cfg4_full(args, dev, rank, world):
         out[mode] = {"value": round(total / el / 1e9, 2), "unit": "GB/s selected (response bytes, all ranks)",
                      "seconds": round(el, 3), "pages": len(rd.pages), "response_bytes": total,
                      "chunk_decodes_rank0": rd.stats["decoded"], "chunk_reuses_rank0": rd.stats["reused"],
+                     "decode_batches_rank0": rd.stats["decode_batches"],
                      "decoded_GBps": round(len(plan.idx) * plan.chunk_nbytes / el / 1e9, 2),
                      "page0_check": bool(checked["ok"]) if rank == 0 else None}
         del rd

@@ -689,7 +689,7 @@ class PagedReader:
     fill value."""
 
     def __init__(self, dset_id, dims, layout, selection, dtype, world, rank, device, max_request_size=100 << 20,
-                 compressor="zlib", shuffle=1, mode="gather", root=0, group=None, shm_path=None):
+                 compressor="zlib", shuffle=1, mode="gather", root=0, group=None, shm_path=None, batch_chunks=2048):
         import torch
         from .engine import ChunkEngine, HostBuffer
         if mode not in ("gather", "direct"):
@@ -720,15 +720,20 @@ class PagedReader:
                     dist.barrier(group=group)
         else:
             self.host = torch.empty(cap, dtype=torch.uint8).pin_memory() if self.rank == root else None
+        # decode look-ahead: a page whose chunks are not all resident decodes them together
+        # with the next pages' missing chunks, up to batch_chunks per rank (one page's chunk
+        # row alone is a quarter of a decode round)
+        self.batch_chunks = max(1, int(batch_chunks))
         self.csize = int(np.prod(self.layout, dtype=np.int64)) * self.dtype.itemsize
         self.cstride = _align(self.csize, 256)
         self.pool = None
         self.slot_of = {}                      # chunk id -> pool slot
-        self.stats = {"pages": 0, "decoded": 0, "reused": 0}
+        self.stats = {"pages": 0, "decoded": 0, "reused": 0, "decode_batches": 0}
 
     def _slots(self, ids):
-        """Pool slots for this page's chunk ids: keep the ones already decoded, free the
-        rest, hand free slots to new ids.  Returns (offsets, new ids, their slots)."""
+        """Pool slots for the chunk ids `ids` (a page and its look-ahead): keep the ones
+        already decoded, free the rest, hand free slots to new ids.  Returns (offsets,
+        new ids, their slots)."""
         torch = self.torch
         keep = {c: self.slot_of[c] for c in ids if c in self.slot_of}
         need = len(ids)
@@ -789,12 +794,35 @@ class PagedReader:
         """Read every page in order; returns the total bytes handed to `sink` (root)."""
         torch = self.torch
         total = 0
+        plans = {}
+
+        def plan_of(q):
+            if q not in plans:
+                plans[q] = SelectionPlan(self.dset_id, self.dims, self.layout, self.pages[q], self.dtype, self.world)
+            return plans[q]
         for pno, page in enumerate(self.pages):
-            plan = SelectionPlan(self.dset_id, self.dims, self.layout, page, self.dtype, self.world)
+            plan = plan_of(pno)
+            plans.pop(pno - 1, None)
             ids = plan.chunk_ids(self.rank)
-            offs, new, new_slots = self._slots(ids)
-            self.stats["reused"] += len(ids) - len(new)
-            self._decode(new, new_slots, source, fill_value)
+            if any(c not in self.slot_of for c in ids):
+                want, seen = list(ids), set(ids)
+                nnew = sum(1 for c in ids if c not in self.slot_of)
+                q = pno + 1
+                while q < len(self.pages) and nnew < self.batch_chunks:
+                    for c in plan_of(q).chunk_ids(self.rank):
+                        if c not in seen:
+                            seen.add(c)
+                            want.append(c)
+                            nnew += c not in self.slot_of
+                    q += 1
+                _, new, new_slots = self._slots(want)
+                self._decode(new, new_slots, source, fill_value)
+                self.stats["decode_batches"] += 1
+            else:
+                new = []
+            offs = np.array([self.slot_of[c] * self.cstride for c in ids], np.int64)
+            fresh = set(new)
+            self.stats["reused"] += sum(1 for c in ids if c not in fresh)
             nb = self.page_bytes[pno]
             if self.mode == "direct":
                 if len(ids):

@@ -79,6 +79,11 @@ constexpr uint32_t OWIN = HZ2_OWIN;       // phase E (plain output): literal win
                                           // written whole: partial cache lines cost an L2 fill + write-back)
 static_assert(OWIN == 32 || OWIN == 64, "OWIN: 32 or 64 bytes (the byte mask is 64 bits)");
 constexpr uint32_t OSH = OWIN == 32 ? 5u : 6u;
+#if HZ2_OWIN == 64
+typedef uint64_t OMask;
+#else
+typedef uint32_t OMask;
+#endif
 // phase E: match records are staged per lane and stored as whole aligned 32-byte groups
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
 // bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
@@ -818,7 +823,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           const uint32_t m0 = mi;                          // the lane's first record
           const uint32_t A = (uint32_t)((uintptr_t)job.dst & (OWIN - 1u));
           uint32_t cw = 0xffffffffu;
-          uint64_t msk = 0;
+          OMask msk = 0;                                   // bytes of the window written
           auto flush = [&]() {
             if (!msk) return;
             const uint32_t wx = (cw << OSH) - A;        // stream position of the window's byte 0
@@ -854,7 +859,7 @@ HZ_UNROLL
                 const uint32_t ax = A + o, w = ax >> OSH;
                 if (w != cw) { flush(); cw = w; msk = 0; }
                 sh.ostage[lane][ax & (OWIN - 1u)] = (uint8_t)t;
-                msk |= 1ull << (ax & (OWIN - 1u));
+                msk |= (OMask)1 << (ax & (OWIN - 1u));
               }
 #endif
               a1 += t;

@@ -46,7 +46,8 @@ def test_paged_read_matches_numpy(mode, staged):
     blobs = _blobs(full, missing={(3, 1)})
     size = int(np.prod(sel.getSelectionShape(SELECT))) * 4
     dev = torch.device("cuda", 0)
-    rd = crawl.PagedReader(DSET, DIMS, LAYOUT, SELECT, np.float32, 1, 0, dev, max_request_size=size // 6, mode=mode)
+    rd = crawl.PagedReader(DSET, DIMS, LAYOUT, SELECT, np.float32, 1, 0, dev, max_request_size=size // 6, mode=mode,
+                           batch_chunks=6)
     assert len(rd.pages) >= 6
     got = []
     if staged:     # objects already in HBM (one copy per chunk id)
@@ -62,6 +63,7 @@ def test_paged_read_matches_numpy(mode, staged):
     # chunk rows shared by consecutive pages were decoded once
     assert rd.stats["reused"] > 0
     assert rd.stats["decoded"] == len(blobs) + 1          # every chunk once (+ the fill-value one)
+    assert 1 < rd.stats["decode_batches"] < len(rd.pages)  # look-ahead: several pages per decode batch
 
 
 def test_direct_placement_from_two_ranks_into_one_shared_buffer(tmp_path):
