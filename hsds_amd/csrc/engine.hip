@@ -1035,12 +1035,27 @@ __global__ void __launch_bounds__(64) lz4_block_kernel(const EncItem* __restrict
 // zstd write path (zstd_enc.h): one lane per 8 KiB segment writes that segment as one zstd
 // block into its scratch slot; zstd_size_kernel sums a stream's blocks for the layout;
 // zstd_write_kernel (one wave per stream) writes the frame header and moves the blocks
+__global__ void __launch_bounds__(64) zstd_lit_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                      const hd::SegParse* __restrict__ sp,
+                                                      const uint16_t* __restrict__ tok, uint8_t* __restrict__ lsec,
+                                                      uint32_t* __restrict__ lsz, uint32_t seg_cap) {
+  __shared__ hze::LitShared sh;
+  uint32_t total = segoffs[nchunks];
+  if (total > seg_cap) total = seg_cap;
+  for (uint32_t s = blockIdx.x; s < total; s += gridDim.x) {
+    const uint32_t n = hze::lit_section(sh, tok + (size_t)s * hd::SEG_TOK, sp + s, lsec + (size_t)s * hze::LCAP);
+    if (threadIdx.x == 0) lsz[s] = n;
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(64) zstd_seg_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
                                                       const SegMeta* __restrict__ meta,
                                                       const EncItem* __restrict__ slots,
                                                       const hd::SegParse* __restrict__ sp,
                                                       const uint16_t* __restrict__ tok, uint8_t* __restrict__ zscr,
-                                                      uint32_t* __restrict__ zsz, uint32_t seg_cap, int level) {
+                                                      uint32_t* __restrict__ zsz, const uint8_t* __restrict__ lsec,
+                                                      const uint32_t* __restrict__ lsz, uint32_t seg_cap, int level) {
   __shared__ hze::Tabs T;
   if (threadIdx.x == 0) hze::build_all(T);
   __syncthreads();
@@ -1055,7 +1070,7 @@ __global__ void __launch_bounds__(64) zstd_seg_kernel(const uint32_t* __restrict
   hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
   const uint32_t last = seg + 1 == hd::nsegments(it.len) ? 1u : 0u;
   zsz[s] = hze::encode_segment(T, tok + (size_t)s * hd::SEG_TOK, sp + s, job, seg * (uint32_t)hd::SEG, m.seglen, last,
-                               zscr + (size_t)s * hze::ZCAP, hze::ZCAP);
+                               zscr + (size_t)s * hze::ZCAP, hze::ZCAP, lsec + (size_t)s * hze::LCAP, lsz[s]);
 }
 
 __global__ void zstd_size_kernel(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ segoffs,
@@ -1348,6 +1363,7 @@ struct hsds_engine {
   int ev_valid = 0;
   // encode workspace (items, sizes, geometry) and per-split output scratch
   int parse_blocks_per_cu = 1;
+  int zlit_blocks_per_cu = 1;
   int huff_blocks_per_cu = 1;
   int emit_blocks_per_cu = 1;
   uint8_t* ews = nullptr;
@@ -1485,6 +1501,11 @@ int hsds_engine_create(int device, hsds_engine** out) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, huff_kernel, 64, 0) != hipSuccess || o2 < 1) o2 = 4;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o3, emit_kernel, 64, 0) != hipSuccess || o3 < 1) o3 = 4;
   e->parse_blocks_per_cu = o1;
+  {
+    int oz = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&oz, zstd_lit_kernel, 64, 0) != hipSuccess || oz < 1) oz = 4;
+    e->zlit_blocks_per_cu = oz;
+  }
   if (const char* ev = getenv("HSDS_DEFLATE_CHAIN")) {   // development override (A/B experiments)
     const int v = atoi(ev);
     if (v >= 1 && v <= 4096) e->enc_chain = (uint32_t)v;
@@ -1981,11 +2002,18 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
                      cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, 0u, item_cap, far,
                      e->enc_chain);
   if (cname == HSDS_CNAME_ZSTD) {
-    if (grow((void**)&e->ezs, &e->ezs_bytes, (size_t)seg_cap * (hze::ZCAP + 4) + 256)) return HSDS_ERR_DEVICE;
+    if (grow((void**)&e->ezs, &e->ezs_bytes, (size_t)seg_cap * (hze::ZCAP + hze::LCAP + 8) + 256)) return HSDS_ERR_DEVICE;
     uint8_t* zscr = e->ezs;
-    uint32_t* zsz = (uint32_t*)(e->ezs + (size_t)seg_cap * hze::ZCAP);
+    uint8_t* lsec = zscr + (size_t)seg_cap * hze::ZCAP;
+    uint32_t* zsz = (uint32_t*)(lsec + (size_t)seg_cap * hze::LCAP);
+    uint32_t* lsz = zsz + seg_cap;
+    if (hze::huff_lit_level(clevel))
+      hipLaunchKernelGGL(zstd_lit_kernel, dim3(grid_for(e->zlit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
+                         nchunks, sp, tok, lsec, lsz, seg_cap);
+    else if (hipMemsetAsync(lsz, 0, (size_t)seg_cap * 4, st) != hipSuccess)
+      return HSDS_ERR_DEVICE;
     hipLaunchKernelGGL(zstd_seg_kernel, dim3((seg_cap + 63) / 64), dim3(64), 0, st, segoffs, nchunks, meta, slots, sp,
-                       tok, zscr, zsz, seg_cap, clevel);
+                       tok, zscr, zsz, lsec, lsz, seg_cap, clevel);
     hipLaunchKernelGGL(zstd_size_kernel, dim3((item_cap + 255) / 256), dim3(256), 0, st, offs, segoffs, nchunks, slots,
                        zsz, lzsize, seg_cap, item_cap);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,

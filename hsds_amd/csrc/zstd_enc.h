@@ -9,13 +9,17 @@
 // Format written (every choice is a legal RFC 8878 encoding):
 //   frame    magic, Single_Segment header with the content size, no checksum, one block
 //            per 8 KiB parse segment (the deflate encoder's P phase gives the matches);
-//   block    Compressed_Block: Raw_Literals_Block (the literal bytes in order) + a
-//            sequences section in Predefined_Mode for literal lengths, offsets and match
-//            lengths (offsets as Offset_Value = offset + 3: no repeat codes); a block whose
-//            content would not be smaller than the segment is a Raw_Block.
-// A lane walks its segment's tokens forward (literal bytes) and backward (sequences are
-// FSE-encoded from the last to the first, as ZSTD_encodeSequences does), so no sequence
-// store is needed.
+//   block    Compressed_Block: a Compressed_Literals_Block (the segment's own Huffman code,
+//            limited to 11 bits, its weights FSE-compressed; 4 streams) -- or the literal
+//            bytes raw when that is not smaller -- and a sequences section in
+//            Predefined_Mode for literal lengths, offsets and match lengths (offsets as
+//            Offset_Value = offset + 3: no repeat codes); a block whose content would not be
+//            smaller than the segment is a Raw_Block.
+// lit_section: one wavefront per segment builds the literals section (token walk per parse
+// lane, the deflate encoder's cooperative Huffman build, weights + 4 streams).
+// encode_segment: one lane per segment walks the tokens forward (raw literals when there
+// is no literals section) and backward (sequences are FSE-encoded from the last to the
+// first, as ZSTD_encodeSequences does), so no sequence store is needed.
 //
 // SINGLE SOURCE for the HIP kernels (engine.hip) and the CPU emulation (tests/emu/deflate_emu.cpp).
 #pragma once
@@ -25,6 +29,9 @@
 namespace hze {
 
 constexpr uint32_t ZCAP = (uint32_t)hd::SEG + 64u;   // scratch bytes per segment block
+constexpr uint32_t LCAP = (uint32_t)hd::SEG + 512u;  // scratch bytes per segment literals section
+constexpr uint32_t HUF_MAXBITS = 11;
+constexpr uint32_t STRM = ((uint32_t)hd::SEG / 4u * HUF_MAXBITS + 7u) / 8u + 16u;   // one Huffman stream, max
 constexpr uint32_t MAXSYM = 53;
 
 // FSE compression table of one predefined distribution (FSE_buildCTable)
@@ -40,23 +47,21 @@ struct Tabs {
 
 HZ_HD uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
-// which: 0 LL (36 codes, log 6), 1 OF (29, log 5), 2 ML (53, log 6)
-HZ_HD void build(CTab& t, uint32_t which) {
-  const uint32_t n = which == 0 ? 36u : which == 1 ? 29u : 53u;
-  const uint32_t log = which == 1 ? 5u : 6u;
+// FSE_buildCTable for normalized counts norm[0..n) (-1: a low-probability symbol) at `log`
+HZ_HD void build_norm(CTab& t, const int16_t* norm, uint32_t n, uint32_t log) {
   const uint32_t size = 1u << log, mask = size - 1u, step = (size >> 1) + (size >> 3) + 3u;
   uint8_t sym[64];
   uint32_t cumul[MAXSYM + 1];
   uint32_t high = size - 1u;
   cumul[0] = 0;
   for (uint32_t s = 0; s < n; s++) {
-    const int32_t c = zs::def_norm(which, s);
+    const int32_t c = norm[s];
     if (c == -1) { cumul[s + 1] = cumul[s] + 1u; sym[high--] = (uint8_t)s; }
     else cumul[s + 1] = cumul[s] + (uint32_t)c;
   }
   uint32_t pos = 0;
   for (uint32_t s = 0; s < n; s++) {
-    const int32_t c = zs::def_norm(which, s);
+    const int32_t c = norm[s];
     for (int32_t k = 0; k < c; k++) {
       sym[pos] = (uint8_t)s;
       pos = (pos + step) & mask;
@@ -66,7 +71,7 @@ HZ_HD void build(CTab& t, uint32_t which) {
   for (uint32_t u = 0; u < size; u++) t.state[cumul[sym[u]]++] = (uint16_t)(size + u);
   uint32_t total = 0;
   for (uint32_t s = 0; s < n; s++) {
-    const int32_t c = zs::def_norm(which, s);
+    const int32_t c = norm[s];
     if (c == 0) {
       t.dnb[s] = (int32_t)(((log + 1u) << 16) - size);
       t.dfs[s] = 0;
@@ -83,6 +88,14 @@ HZ_HD void build(CTab& t, uint32_t which) {
     }
   }
   t.log = log;
+}
+
+// which: 0 LL (36 codes, log 6), 1 OF (29, log 5), 2 ML (53, log 6): the predefined tables
+HZ_HD void build(CTab& t, uint32_t which) {
+  const uint32_t n = which == 0 ? 36u : which == 1 ? 29u : 53u;
+  int16_t norm[MAXSYM];
+  for (uint32_t s = 0; s < n; s++) norm[s] = zs::def_norm(which, s);
+  build_norm(t, norm, n, which == 1 ? 5u : 6u);
 }
 
 HZ_HD void build_all(Tabs& T) {
@@ -167,11 +180,244 @@ HZ_HD void block_header(uint8_t* out, uint32_t last, uint32_t type, uint32_t siz
   out[2] = (uint8_t)(h >> 16);
 }
 
+// Huffman-coded literals from this level on: on the cfg5 slab they cut the objects by 2 %
+// (1.236 -> 1.211 of libblosc-zstd's size) for 2.5x the encode time (290 -> 724 ms), so
+// the speed levels keep raw literals (the literal bytes of float data are near 8 bits of
+// entropy; the sequences section is where libzstd gains)
+#if HZ_GPU
+__host__ __device__
+#endif
+inline uint32_t huff_lit_level(int level) { return level >= 6 ? 1u : 0u; }
+
+// ---- literals section (Compressed_Literals_Block, 4 streams) ----------------------------
+struct LitShared {
+  hd::HuffShared hs;
+  uint8_t lit[hd::SEG];
+  uint8_t strm[4][STRM];
+  uint8_t tree[132];                // Huffman_Tree_Description (header byte + FSE weights)
+  uint8_t w[256];                   // Huffman weights (lane 0's serial build)
+  CTab wt;                          // their FSE table
+  uint16_t val[256];
+  uint32_t cnt[hd::WAVE], base[hd::WAVE];
+  uint32_t ssize[4];
+  uint32_t nlit, tsize, ok, size;
+};
+
+// FSE_writeNCount (zstd fse_compress.c) of norm[0..n) at `log` into out; returns bytes
+HZ_HD uint32_t write_ncount(uint8_t* out, const int16_t* norm, uint32_t n, uint32_t log) {
+  uint32_t o = 0;
+  const int32_t size = 1 << log;
+  int32_t remaining = size + 1, threshold = size, nbits = (int32_t)log + 1;
+  uint32_t bs = log - 5u;            // table log - FSE_MIN_TABLELOG, 4 bits
+  int32_t bc = 4;
+  uint32_t sym = 0;
+  int prev0 = 0;
+  while (sym < n && remaining > 1) {
+    if (prev0) {
+      uint32_t start = sym;
+      while (sym < n && !norm[sym]) sym++;
+      if (sym >= n) break;
+      while (sym >= start + 24u) {
+        start += 24u;
+        bs += 0xffffu << bc;
+        out[o++] = (uint8_t)bs; out[o++] = (uint8_t)(bs >> 8);
+        bs >>= 16;
+      }
+      while (sym >= start + 3u) { start += 3u; bs += 3u << bc; bc += 2; }
+      bs += (sym - start) << bc;
+      bc += 2;
+      if (bc > 16) { out[o++] = (uint8_t)bs; out[o++] = (uint8_t)(bs >> 8); bs >>= 16; bc -= 16; }
+    }
+    int32_t count = norm[sym++];
+    const int32_t mx = (2 * threshold - 1) - remaining;
+    remaining -= count < 0 ? -count : count;
+    count++;
+    if (count >= threshold) count += mx;
+    bs += (uint32_t)count << bc;
+    bc += nbits;
+    bc -= count < mx ? 1 : 0;
+    prev0 = count == 1;
+    while (remaining < threshold) { nbits--; threshold >>= 1; }
+    if (bc > 16) { out[o++] = (uint8_t)bs; out[o++] = (uint8_t)(bs >> 8); bs >>= 16; bc -= 16; }
+  }
+  out[o++] = (uint8_t)bs;
+  out[o++] = (uint8_t)(bs >> 8);
+  o -= 2u - (uint32_t)((bc + 7) / 8);
+  return o;
+}
+
+// Huffman_Tree_Description of the code lengths len[0..256) into sh.tree (header byte
+// = size of the FSE-compressed weights); values in sh.val.  Returns 0 when the weights
+// cannot be FSE-described (a single weight value, or >= 128 bytes).
+HZ_HD uint32_t huff_tree(LitShared& sh, const uint8_t* len) {
+  uint32_t maxb = 0, last = 0;
+  for (uint32_t s = 0; s < 256u; s++) if (len[s]) { maxb = len[s] > maxb ? len[s] : maxb; last = s; }
+  // values (HUF_buildCTable): longest codes get the smallest values, symbol order within a length
+  uint32_t nper[HUF_MAXBITS + 2] = {0}, vper[HUF_MAXBITS + 2] = {0};
+  for (uint32_t s = 0; s < 256u; s++) if (len[s]) nper[len[s]]++;
+  {
+    uint32_t mn = 0;
+    for (uint32_t b = maxb; b > 0; b--) { vper[b] = mn; mn += nper[b]; mn >>= 1; }
+  }
+  for (uint32_t s = 0; s < 256u; s++) sh.val[s] = len[s] ? (uint16_t)vper[len[s]]++ : (uint16_t)0;
+  // weights of symbols 0 .. last-1 (the last symbol's weight is implied)
+  uint8_t* const w = sh.w;
+  uint32_t wc[HUF_MAXBITS + 2] = {0};
+  for (uint32_t s = 0; s < last; s++) { w[s] = len[s] ? (uint8_t)(maxb + 1u - len[s]) : 0u; wc[w[s]]++; }
+  uint32_t nw = last, distinct = 0, maxw = 0;
+  for (uint32_t v = 0; v <= maxb; v++) if (wc[v]) { distinct++; maxw = v; }
+  if (nw < 2u || distinct < 2u) return 0;
+  // normalized weight counts at log 6 (any distribution summing to 64 with every used
+  // value >= 1 is a valid description)
+  const uint32_t LOG = 6;
+  int16_t norm[HUF_MAXBITS + 2];
+  int32_t sum = 0, big = 0;
+  for (uint32_t v = 0; v <= maxw; v++) {
+    int32_t c = wc[v] ? (int32_t)((wc[v] << LOG) / nw) : 0;
+    if (wc[v] && c < 1) c = 1;
+    norm[v] = (int16_t)c;
+    sum += c;
+    if (c > norm[big]) big = (int32_t)v;
+  }
+  while (sum > (1 << LOG)) {
+    int32_t m = 0;
+    for (uint32_t v = 0; v <= maxw; v++) if (norm[v] > norm[m]) m = (int32_t)v;
+    norm[m]--;
+    sum--;
+  }
+  norm[big] = (int16_t)(norm[big] + ((1 << LOG) - sum));
+  CTab& t = sh.wt;
+  build_norm(t, norm, maxw + 1u, LOG);
+  uint32_t o = 1u + write_ncount(sh.tree + 1, norm, maxw + 1u, LOG);
+  // two interleaved states, from the last weight back (FSE_compress_usingCTable)
+  BitW bw = {0, 0, o, 131u, sh.tree, 0};
+  uint32_t s1 = 0, s2 = 0;
+  int32_t i = (int32_t)nw - 1;
+  if (nw & 1u) {
+    s1 = fse_init(t, w[i--]);
+    s2 = fse_init(t, w[i--]);
+    fse_enc(bw, t, s1, w[i--]);
+  } else {
+    s2 = fse_init(t, w[i--]);
+    s1 = fse_init(t, w[i--]);
+  }
+  while (i >= 0) {
+    fse_enc(bw, t, s2, w[i--]);
+    fse_enc(bw, t, s1, w[i--]);
+  }
+  bw_add(bw, s2, LOG);
+  bw_add(bw, s1, LOG);
+  bw_add(bw, 1u, 1u);
+  if (bw.n) bw_add(bw, 0u, 8u - bw.n);
+  if (bw.over || bw.pos - 1u >= 128u) return 0;
+  sh.tree[0] = (uint8_t)(bw.pos - 1u);
+  return bw.pos;
+}
+
+// One wavefront: the segment's literals section into out (LCAP bytes); returns its size,
+// or 0 when raw literals are not larger (encode_segment then writes them raw).
+HZ_HD uint32_t lit_section(LitShared& sh, const uint16_t* tok, const hd::SegParse* sp, uint8_t* out) {
+  hz_gcu8* const gt = HZ_GLOBAL(hz_gcu8*, tok);
+  auto slot = [&](uint32_t k, uint32_t l) -> uint32_t {
+    const uint32_t i = hd::tslot(k, (int)l);
+    return (uint32_t)gt[2u * i] | ((uint32_t)gt[2u * i + 1u] << 8);
+  };
+  // literal bytes in stream order: parse lane l's literals after those of lanes < l
+  LANE_LOOP {
+    uint32_t c = 0;
+    const uint32_t ns = sp->nslot[lane];
+    for (uint32_t k = 0; k < ns;) {
+      if (slot(k, (uint32_t)lane) & 0x8000u) { k += 2; continue; }
+      c++;
+      k++;
+    }
+    sh.cnt[lane] = c;
+  }
+  WAVE_SYNC();
+  LANE_LOOP {
+    if (lane == 0) {
+      uint32_t b = 0;
+      for (int l = 0; l < hd::WAVE; l++) { sh.base[l] = b; b += sh.cnt[l]; }
+      sh.nlit = b;
+    }
+  }
+  WAVE_SYNC();
+  const uint32_t nlit = sh.nlit;
+  if (nlit < 64u) return 0;
+  LANE_LOOP {
+    uint32_t b = sh.base[lane];
+    const uint32_t ns = sp->nslot[lane];
+    for (uint32_t k = 0; k < ns;) {
+      const uint32_t v = slot(k, (uint32_t)lane);
+      if (v & 0x8000u) { k += 2; continue; }
+      sh.lit[b++] = (uint8_t)v;
+      k++;
+    }
+    for (int q = lane; q < 256; q += hd::WAVE) sh.hs.freq[q] = sp->freq[q];
+  }
+  WAVE_SYNC();
+  HD_BUILD_HUFF(sh.hs, sh.hs.freq, 256, 256, (int)HUF_MAXBITS, sh.hs.len_ll, sh.hs.code_ll);
+  LANE_LOOP {
+    if (lane == 0) sh.tsize = huff_tree(sh, sh.hs.len_ll);
+  }
+  WAVE_SYNC();
+  if (!sh.tsize) return 0;
+  // four streams, each encoded from its last literal back (HUF_compress1X), lanes 0-3
+  const uint32_t segsz = (nlit + 3u) / 4u;
+  LANE_LOOP {
+    if (lane < 4) {
+      const uint32_t a = (uint32_t)lane * segsz, b = lane == 3 ? nlit : a + segsz;
+      BitW bw = {0, 0, 0, STRM, sh.strm[lane], 0};
+      for (uint32_t i = b; i > a; i--) {
+        const uint32_t c = sh.lit[i - 1u];
+        bw_add(bw, sh.val[c], sh.hs.len_ll[c]);
+      }
+      bw_add(bw, 1u, 1u);
+      if (bw.n) bw_add(bw, 0u, 8u - bw.n);
+      sh.ssize[lane] = bw.over ? 0xffffu + 1u : bw.pos;
+    }
+  }
+  WAVE_SYNC();
+  LANE_LOOP {
+    if (lane == 0) {
+      uint32_t ok = 1, csize = sh.tsize + 6u;
+      for (int k = 0; k < 4; k++) { csize += sh.ssize[k]; ok &= sh.ssize[k] <= 0xffffu && (k == 3 || sh.ssize[k]); }
+      const uint32_t hsz = (nlit < 1024u && csize < 1024u) ? 3u : 4u;
+      const uint32_t rawsz = nlit + (nlit < 32u ? 1u : nlit < 4096u ? 2u : 3u);
+      if (!ok || hsz + csize >= rawsz || csize >= (1u << 14)) {
+        sh.size = 0;
+      } else {
+        // Literals_Section_Header: type 2, size format 1 (3 bytes, 10-bit sizes) or 2 (4 bytes)
+        const uint32_t h = 2u | ((hsz == 3u ? 1u : 2u) << 2) | (nlit << 4) | (csize << (hsz == 3u ? 14u : 18u));
+        for (uint32_t i = 0; i < hsz; i++) out[i] = (uint8_t)(h >> (8u * i));
+        uint32_t o = hsz;
+        for (uint32_t i = 0; i < sh.tsize; i++) out[o++] = sh.tree[i];
+        for (int k = 0; k < 3; k++) { out[o++] = (uint8_t)sh.ssize[k]; out[o++] = (uint8_t)(sh.ssize[k] >> 8); }
+        sh.base[0] = o;                                // where stream 0 starts
+        sh.size = hsz + csize;
+      }
+    }
+  }
+  WAVE_SYNC();
+  const uint32_t size = sh.size;
+  if (!size) return 0;
+  LANE_LOOP {
+    uint32_t o = sh.base[0];
+    for (int k = 0; k < 4; k++) {
+      for (uint32_t i = (uint32_t)lane; i < sh.ssize[k]; i += hd::WAVE) out[o + i] = sh.strm[k][i];
+      o += sh.ssize[k];
+    }
+  }
+  WAVE_SYNC();
+  return size;
+}
+
 // Writes segment `seg` of a stream as one zstd block (header included) at out (cap bytes
 // of scratch, >= ZCAP).  tok / sp: the segment's parse tokens and counts; job / s0: the
 // stream input (a raw block copies the segment from it).  Returns the block size.
 HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegParse* sp, const hd::EncJob& job,
-                              uint32_t s0, uint32_t seglen, uint32_t last, uint8_t* out, uint32_t cap) {
+                              uint32_t s0, uint32_t seglen, uint32_t last, uint8_t* out, uint32_t cap,
+                              const uint8_t* lsec = nullptr, uint32_t lsize = 0) {
   hz_gcu8* const gt = HZ_GLOBAL(hz_gcu8*, tok);
   auto slot = [&](uint32_t k, uint32_t l) -> uint32_t {
     const uint32_t i = hd::tslot(k, (int)l);
@@ -182,8 +428,10 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
   for (uint32_t s = 257; s < 286u; s++) nseq += sp->freq[s];
   int over = 0;
   uint32_t p = 3;
-  // literals section header (Raw_Literals_Block)
-  if (nlit < 32u) {
+  if (lsize) {
+    // the Huffman-coded literals section (lit_section)
+    for (uint32_t i = 0; i < lsize; i++) put8(out, p, cap, lsec[i], over);
+  } else if (nlit < 32u) {
     put8(out, p, cap, nlit << 3, over);
   } else if (nlit < 4096u) {
     put8(out, p, cap, (1u << 2) | ((nlit & 15u) << 4), over);
@@ -194,7 +442,7 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
     put8(out, p, cap, nlit >> 12, over);
   }
   // literal bytes, forward over the lanes' token ranges
-  for (uint32_t l = 0; l < (uint32_t)hd::WAVE && !over; l++) {
+  for (uint32_t l = 0; l < (uint32_t)hd::WAVE && !over && !lsize; l++) {
     const uint32_t ns = sp->nslot[l];
     for (uint32_t k = 0; k < ns;) {
       const uint32_t v = slot(k, l);

@@ -132,7 +132,8 @@ extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, 
   free(ps);
   hze::Tabs T;
   hze::build_all(T);
-  std::vector<uint8_t> blk(hze::ZCAP);
+  std::vector<uint8_t> blk(hze::ZCAP), lsec(hze::LCAP);
+  hze::LitShared* ls = (hze::LitShared*)calloc(1, sizeof(hze::LitShared));
   uint8_t hdr[16];
   const uint32_t h = hze::frame_header(hdr, n);
   uint64_t pos = 0;
@@ -143,10 +144,13 @@ extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, 
   for (uint32_t s = 0; s < nseg; s++) {
     const uint32_t s0 = s * (uint32_t)hd::SEG;
     const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
+    const uint32_t lsz = !hze::huff_lit_level(level) ? 0u
+                         : hze::lit_section(*ls, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], lsec.data());
     const uint32_t k = hze::encode_segment(T, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], job, s0, seglen,
-                                           s + 1 == nseg ? 1u : 0u, blk.data(), hze::ZCAP);
+                                           s + 1 == nseg ? 1u : 0u, blk.data(), hze::ZCAP, lsec.data(), lsz);
     put(blk.data(), k);
   }
+  free(ls);
   return pos <= cap ? (int64_t)pos : -1;
 }
 
