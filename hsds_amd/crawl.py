@@ -689,8 +689,7 @@ class PagedReader:
     fill value."""
 
     def __init__(self, dset_id, dims, layout, selection, dtype, world, rank, device, max_request_size=100 << 20,
-                 compressor="zlib", shuffle=1, mode="gather", root=0, group=None, shm_path=None, batch_chunks=2048,
-                 overlap=True):
+                 compressor="zlib", shuffle=1, mode="gather", root=0, group=None, shm_path=None, batch_chunks=2048):
         import torch
         from .engine import ChunkEngine, HostBuffer
         if mode not in ("gather", "direct"):
@@ -725,9 +724,6 @@ class PagedReader:
         # with the next pages' missing chunks, up to batch_chunks per rank (one page's chunk
         # row alone is a quarter of a decode round)
         self.batch_chunks = max(1, int(batch_chunks))
-        # overlap: the next look-ahead batch decodes on a second stream while this one's
-        # pages are placed (the pool holds both)
-        self.overlap = bool(overlap)
         self.csize = int(np.prod(self.layout, dtype=np.int64)) * self.dtype.itemsize
         self.cstride = _align(self.csize, 256)
         self.pool = None
@@ -742,9 +738,7 @@ class PagedReader:
         keep = {c: self.slot_of[c] for c in ids if c in self.slot_of}
         need = len(ids)
         if self.pool is None or self.pool.numel() < need * self.cstride:
-            # a bigger pool: the decoded chunks keep their slot offsets (nothing may be in
-            # flight on either stream while they move)
-            torch.cuda.synchronize(self.device)
+            # a bigger pool: the decoded chunks keep their slot offsets
             big = torch.empty(max(2 * need, 1) * self.cstride, dtype=torch.uint8, device=self.device)
             if self.pool is not None:
                 big[:self.pool.numel()].copy_(self.pool)
@@ -763,9 +757,7 @@ class PagedReader:
         offs = np.array([keep[c] * self.cstride for c in ids], np.int64)
         return offs, new, new_slots
 
-    def _decode(self, new, new_slots, source, fill_value, stream=None):
-        """Decode the new chunks into their slots on `stream`; returns the status tensor
-        (checked when a page first needs the batch) or None."""
+    def _decode(self, new, new_slots, source, fill_value):
         from .engine import CHUNK_DESC_DTYPE, pack_chunks
         torch = self.torch
         staged = isinstance(source, tuple)
@@ -785,9 +777,10 @@ class PagedReader:
             descs["dst_off"] = np.array([k * self.cstride for _, k in present], np.uint64)
             st = torch.full((len(present),), 99, dtype=torch.int32, device=self.device)
             self.eng.decode(d_src, descs, self.pool, st, compressor=self.compressor, shuffle=self.shuffle,
-                            itemsize=self.dtype.itemsize, stream=stream)
-        else:
-            st = None
+                            itemsize=self.dtype.itemsize)
+            bad = st.ne(0)
+            if bool(bad.any()):
+                raise RuntimeError("chunk decode failed: " + str(torch.unique(st).tolist()))
         if missing:
             fill = np.zeros(self.layout, self.dtype)
             if fill_value is not None:
@@ -796,84 +789,45 @@ class PagedReader:
             for k in missing:
                 self.pool[k * self.cstride:k * self.cstride + self.csize].copy_(d_fill)
         self.stats["decoded"] += len(new)
-        return st
 
     def read(self, source, sink, fill_value=None):
         """Read every page in order; returns the total bytes handed to `sink` (root)."""
         torch = self.torch
         total = 0
         plans = {}
-        npg = len(self.pages)
-        main = torch.cuda.current_stream(self.device)
-        dec = torch.cuda.Stream(self.device) if self.overlap else main
 
         def plan_of(q):
             if q not in plans:
                 plans[q] = SelectionPlan(self.dset_id, self.dims, self.layout, self.pages[q], self.dtype, self.world)
             return plans[q]
-
-        windows = []             # scheduled decode batches: [first page, end page, event, status, checked]
-        state = {"end": 0}       # pages [0, end) are covered by scheduled batches
-
-        def schedule(cur):
-            # chunks still needed by pages [cur, end) plus a new batch of pages from `end`
-            want, seen = [], set()
-            for q in range(cur, state["end"]):
-                for c in plan_of(q).chunk_ids(self.rank):
-                    if c not in seen:
-                        seen.add(c)
-                        want.append(c)
-            nnew, q = 0, state["end"]
-            while q < npg and (nnew < self.batch_chunks or q == state["end"]):
-                for c in plan_of(q).chunk_ids(self.rank):
-                    if c not in seen:
-                        seen.add(c)
-                        want.append(c)
-                        nnew += c not in self.slot_of
-                q += 1
-            if self.pool is None:
-                # room for a batch in flight next to the one being placed
-                self.pool = torch.empty(max(3 * len(want), 1) * self.cstride, dtype=torch.uint8, device=self.device)
-            # slots freed here were last read by page placements on the main stream
-            ev_main = torch.cuda.Event()
-            ev_main.record(main)
-            dec.wait_event(ev_main)
-            _, new, new_slots = self._slots(want)
-            with torch.cuda.stream(dec):
-                st = self._decode(new, new_slots, source, fill_value, stream=dec)
-            ev = torch.cuda.Event()
-            ev.record(dec)
-            windows.append([state["end"], q, ev, st, False, set(new)])
-            state["end"] = q
-            self.stats["decode_batches"] += 1
-
         for pno, page in enumerate(self.pages):
             plan = plan_of(pno)
             plans.pop(pno - 1, None)
             ids = plan.chunk_ids(self.rank)
-            if pno >= state["end"]:
-                schedule(pno)
-            while windows and windows[0][1] <= pno:
-                windows.pop(0)
-            if self.overlap and state["end"] < npg and len(windows) < 2:
-                schedule(pno)                      # the next batch decodes behind this one's pages
-            w = windows[0]
-            main.wait_event(w[2])
-            if not w[4]:
-                w[4] = True
-                if w[3] is not None:
-                    w[2].synchronize()
-                    if bool(w[3].ne(0).any()):
-                        raise RuntimeError("chunk decode failed: " + str(torch.unique(w[3]).tolist()))
-            new = [c for c in ids if c in w[5]] if pno == w[0] else []
+            if any(c not in self.slot_of for c in ids):
+                want, seen = list(ids), set(ids)
+                nnew = sum(1 for c in ids if c not in self.slot_of)
+                q = pno + 1
+                while q < len(self.pages) and nnew < self.batch_chunks:
+                    for c in plan_of(q).chunk_ids(self.rank):
+                        if c not in seen:
+                            seen.add(c)
+                            want.append(c)
+                            nnew += c not in self.slot_of
+                    q += 1
+                _, new, new_slots = self._slots(want)
+                self._decode(new, new_slots, source, fill_value)
+                self.stats["decode_batches"] += 1
+            else:
+                new = []
             offs = np.array([self.slot_of[c] * self.cstride for c in ids], np.int64)
             fresh = set(new)
             self.stats["reused"] += sum(1 for c in ids if c not in fresh)
             nb = self.page_bytes[pno]
             if self.mode == "direct":
                 if len(ids):
-                    self.eng.copy(self.pool, self.host, plan.direct_descs(self.rank, offs), stream=main)
-                main.synchronize()                   # (not the device: the next batch may be decoding)
+                    self.eng.copy(self.pool, self.host, plan.direct_descs(self.rank, offs))
+                torch.cuda.synchronize(self.device)
                 if self.world > 1:
                     import torch.distributed as dist
                     dist.barrier(group=self.group)
