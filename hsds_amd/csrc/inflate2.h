@@ -999,8 +999,9 @@ HZ_UNROLL
           HZ_T(12);
           // unshuffled output: byte-strided over the span
           LANE_LOOP {
-            uint32_t a1 = LV(ra1);
-            uint64_t a2 = LV(ra2);
+            // adler: sum b and the batch-relative sum (x - F) b in 32 bits (a lane's <= SPAN/64
+            // bytes of the batch keep it below 2^32), folded into the 64-bit sum once per batch
+            uint32_t a1 = 0, b2 = 0;
             for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
               uint32_t src[RG];
 HZ_UNROLL
@@ -1030,12 +1031,12 @@ HZ_UNROLL
                   const uint32_t x = F + h0 + (uint32_t)lane + 64u * i;
                   dst[perm_at(P, x)] = (uint8_t)bv[i];
                   a1 += bv[i];
-                  a2 += (uint64_t)x * bv[i];
+                  b2 += (x - F) * bv[i];
                 }
               }
             }
-            LV(ra1) = a1;
-            LV(ra2) = a2;
+            LV(ra1) += a1;
+            LV(ra2) += (uint64_t)F * a1 + b2;
           }
         } else {
           // plain output: the aligned dwords covering the span are loaded (coalesced) into
@@ -1055,8 +1056,7 @@ HZ_UNROLL
           WAVE_SYNC();
           HZ_T(12);
           LANE_LOOP {
-            uint32_t a1 = LV(ra1);
-            uint64_t a2 = LV(ra2);
+            uint32_t a1 = 0, b2 = 0;                          // as above
             for (uint32_t h0 = 0; h0 < span; h0 += RGP * 64u) {
               // each match byte's source is chased through the map and its load issued at
               // once (a literal of the batch from LDS, anything before the batch from dst);
@@ -1093,14 +1093,14 @@ HZ_UNROLL
                   const uint32_t q = h0 + (uint32_t)lane + 64u * i, x = F + q, bx = x - xa;
                   ((uint8_t*)sh.sbuf)[bx] = (uint8_t)bv[i];
                   a1 += bv[i];
-                  a2 += (uint64_t)x * bv[i];
+                  b2 += (x - F) * bv[i];
                   const uint32_t x0 = xa + (bx & ~3u);               // its dword, as in the stores below
                   if (!(x0 + 4u <= dst_len && (int32_t)x0 >= 0)) dst[x] = (uint8_t)bv[i];
                 }
               }
             }
-            LV(ra1) = a1;
-            LV(ra2) = a2;
+            LV(ra1) += a1;
+            LV(ra2) += (uint64_t)F * a1 + b2;
           }
           WAVE_SYNC();
           HZ_T(13);
