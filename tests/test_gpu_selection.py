@@ -78,6 +78,12 @@ CASES = [
     ((96, 80, 70), (16, 32, 32), np.int16, (slice(0, 96, 2), slice(3, 80, 5), slice(1, 70, 3)), 4),
     ((300, 260), (128, 128), np.float32, (slice(0, 300, 1), slice(0, 260, 1)), 2),
     ((300, 260), (128, 128), np.float32, (slice(0, 300, 4), slice(0, 260, 4)), 8),
+    # the configs' own chunk layouts: cfg3 (16x64x128 int16, its strided selection), cfg4
+    # (512x512 f32, [::4, ::4] and a full extent) over 8 ranks, and cfg1's uncompressed 64x64
+    ((48, 192, 256), (16, 64, 128), np.int16, (slice(0, 48, 2), slice(3, 192, 5), slice(1, 256, 3)), 8),
+    ((1536, 1280), (512, 512), np.float32, (slice(0, 1536, 4), slice(0, 1280, 4)), 8),
+    ((1100, 700), (512, 512), np.float32, (slice(0, 1100, 1), slice(0, 700, 1)), 8),
+    ((300, 260), (64, 64), np.float32, (slice(10, 290, 1), slice(5, 250, 1)), 3, None),
 ]
 
 
@@ -88,7 +94,8 @@ def test_sharded_read_matches_numpy(case, dev, oracle_lib):
     kernels and descriptors the multi-GPU run uses around the RCCL exchange."""
     import torch
     from hsds_amd import crawl, selection as sel
-    dims, layout, dt, selection, world = CASES[case]
+    dims, layout, dt, selection, world = CASES[case][:5]
+    comp = CASES[case][5] if len(CASES[case]) > 5 else "zlib"
     rng = np.random.default_rng(case)
     full = (np.cumsum(rng.normal(size=dims), axis=-1) * 100).astype(dt)
     plan = crawl.SelectionPlan("d-0a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", dims, layout, selection, dt, world)
@@ -105,8 +112,8 @@ def test_sharded_read_matches_numpy(case, dev, oracle_lib):
             c = np.zeros(layout, dt)
             reg = tuple(slice(i * L, min((i + 1) * L, n)) for i, L, n in zip(idx, layout, dims))
             c[tuple(slice(0, s.stop - s.start) for s in reg)] = full[reg]
-            blobs[cid] = oracle_lib.blosc_encode(c.tobytes(), typesize=1, clevel=4, shuffle=1)
-        rd = crawl.ShardedReader(plan, r, dev, root=0)
+            blobs[cid] = oracle_lib.blosc_encode(c.tobytes(), typesize=1, clevel=4, shuffle=1) if comp else c.tobytes()
+        rd = crawl.ShardedReader(plan, r, dev, root=0, compressor=comp, shuffle=1 if comp else 0)
         st = rd.upload(blobs, fill_value=fill)
         b = int(plan.rank_base[r])
         rd.decode_and_pack(st, gathered[b:b + max(plan.rank_bytes[r], 1)])
