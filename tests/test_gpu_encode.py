@@ -461,3 +461,46 @@ def test_zstd_streams_equal_cpu_emulation(dev):
             r = L.emu_zstd_frame(blk.ctypes.data, len(blk), out.ctypes.data, out.size, level)
             assert r == cs, (seed, b, r, cs)
             assert out[:r].tobytes() == fb[start + 4:start + 4 + cs].tobytes(), (seed, b)
+
+
+@pytest.mark.parametrize("cname", ["zlib", "lz4", "zstd"])
+def test_full_size_roundtrip_configs1(dev, oracle_lib, cname):
+    """BASELINE.json configs[1] at full size (4096 x 1 MiB f32 chunks, 4 GiB): GPU encode ->
+    GPU decode is the identity on every byte (compared on the device), and sampled frames
+    decode through the oracle to the same chunks (size-independent round-trip property)."""
+    import torch
+    from hsds_amd.engine import ChunkEngine, encode_descs, to_device_bytes
+    n, cb = 4096, 1 << 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    chunks = torch.empty(n * cb, dtype=torch.uint8, device=dev)
+    view = chunks.view(torch.float32).view(n, cb // 4)
+    for k in range(0, n, 512):
+        z = torch.randn((512, cb // 4), generator=g, device=dev, dtype=torch.float32)
+        view[k:k + 512] = torch.round(torch.cumsum(z, dim=1) * 100) / 100
+        del z
+    descs, _, dext = encode_descs([cb] * n)
+    frames = torch.empty(dext, dtype=torch.uint8, device=dev)
+    sizes = torch.zeros(n, dtype=torch.int64, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    eng = ChunkEngine(0)
+    eng.encode(chunks, to_device_bytes(descs, dev), frames, sizes, st, clevel=4, shuffle=1, typesize=1,
+               compressor=cname)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    # decode straight from the frame slots (dst_off of the encode descriptors)
+    ddescs = descs.copy()
+    ddescs["src_off"], ddescs["src_len"] = descs["dst_off"], sizes.cpu().numpy()
+    ddescs["dst_off"], ddescs["dst_len"] = descs["src_off"], cb
+    back = torch.empty_like(chunks)
+    dst = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    eng.decode(frames, to_device_bytes(ddescs, dev), back, dst, compressor="zlib" if cname == "zlib" else cname,
+               shuffle=1, itemsize=1)
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0
+    assert torch.equal(back, chunks)
+    hs = sizes.cpu().numpy()
+    for k in (0, 1234, n - 1):
+        o = int(descs[k]["dst_off"])
+        fr = frames[o:o + int(hs[k])].cpu().numpy().tobytes()
+        assert oracle_lib.uncompress(fr, cname, 1, 1, cb) == chunks[k * cb:(k + 1) * cb].cpu().numpy().tobytes()
