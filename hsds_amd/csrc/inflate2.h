@@ -198,9 +198,20 @@ HZ_HD Perm perm_make(uint32_t n, uint32_t N, uint32_t x0) {
 #ifndef HZ2_EPOCH
 #define HZ2_EPOCH 8
 #endif
+// HZ2_ALIGNBIT: the current two stream words (lo, hi) and a bit offset sh < 32 in lo, so at
+// least 33 bits are always there: a peek is one funnel shift (v_alignbit_b32) and a drop adds
+// to sh, taking the next word when it crosses 32 -- instead of a 64-bit bit buffer shifted
+// on every drop and refilled before every symbol
+#ifndef HZ2_ALIGNBIT
+#define HZ2_ALIGNBIT 1
+#endif
 struct GRd {
+#if HZ2_ALIGNBIT
+  uint32_t lo, hi, sh;
+#else
   uint64_t bb;
   uint32_t avail;
+#endif
   uint32_t pos;
   uint32_t qa;         // dword index of the next quad to load (epochs: into h, else into f)
   uint32_t qn;         // words left in q
@@ -288,8 +299,12 @@ HZ_HD void g_init(const Src& s, GRd& r, uint32_t p) {
   const uint32_t sh = p & 31u;
   const uint32_t w0 = g_take(s, r);
   const uint32_t w1 = g_take(s, r);
+#if HZ2_ALIGNBIT
+  r.lo = w0; r.hi = w1; r.sh = sh;
+#else
   r.bb = (((uint64_t)w1 << 32) | w0) >> sh;
   r.avail = 64u - sh;
+#endif
   r.pos = p;
 }
 #else
@@ -327,12 +342,39 @@ HZ_HD void g_init(const Src& s, GRd& r, uint32_t p) {
   const uint32_t sh = p & 31u;
   const uint32_t w0 = g_take(s, r);
   const uint32_t w1 = g_take(s, r);
+#if HZ2_ALIGNBIT
+  r.lo = w0; r.hi = w1; r.sh = sh;
+#else
   r.bb = (((uint64_t)w1 << 32) | w0) >> sh;
   r.avail = 64u - sh;
+#endif
   r.pos = p;
 }
 #endif
 
+#if HZ2_ALIGNBIT
+HZ_HD void g_fill(const Src&, GRd&) {}      // >= 33 bits are always there
+
+// the 32 stream bits from r.pos
+HZ_HD uint32_t g_peek(const GRd& r) {
+#if HZ_GPU
+  return __builtin_amdgcn_alignbit(r.hi, r.lo, r.sh);
+#else
+  return (uint32_t)((((uint64_t)r.hi << 32) | r.lo) >> r.sh);
+#endif
+}
+
+// n <= 32
+HZ_HD void g_drop(const Src& s, GRd& r, uint32_t n) {
+  r.pos += n;
+  r.sh += n;
+  if (r.sh >= 32u) {
+    r.sh -= 32u;
+    r.lo = r.hi;
+    r.hi = g_take(s, r);
+  }
+}
+#else
 HZ_HD void g_fill(const Src& s, GRd& r) {
   if (r.avail < 32u) {
     r.bb |= (uint64_t)g_take(s, r) << r.avail;
@@ -340,7 +382,10 @@ HZ_HD void g_fill(const Src& s, GRd& r) {
   }
 }
 
-HZ_HD void g_drop(GRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n; }
+HZ_HD uint32_t g_peek(const GRd& r) { return (uint32_t)r.bb; }
+
+HZ_HD void g_drop(const Src&, GRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n; }
+#endif
 
 HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
   uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
@@ -357,23 +402,25 @@ HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
 // T_MATCH | len << 16 | (dist - 1).  Invalid codes advance by their table length.
 HZ_HD uint32_t next_token(const Shared* sh, const Src& s, GRd& r) {
   g_fill(s, r);
-  const uint32_t e = lookup_ll(sh, r.bb);
+  const uint32_t bits = g_peek(r);
+  const uint32_t e = lookup_ll(sh, bits);
   const uint32_t nb = e & 15u, p = e >> 4;
   const uint32_t q = p - 257u;
   const int islen = q < 29u;
   const uint32_t xb = (islen && q >= 8u && q < 28u) ? (q - 4u) >> 2 : 0u;
   const uint32_t base = q < 8u ? q + 3u : q == 28u ? 258u : ((4u | (q & 3u)) << xb) + 3u;
-  const uint32_t len = base + ((uint32_t)(r.bb >> nb) & hz::bmask(xb));
-  g_drop(r, nb + xb);
+  const uint32_t len = base + ((bits >> nb) & hz::bmask(xb));
+  g_drop(s, r, nb + xb);
   uint32_t tok = p <= 256u ? p : T_ERR;
   if (islen) {
     g_fill(s, r);
-    const uint32_t ed = lookup_d(sh, r.bb);
+    const uint32_t dbits = g_peek(r);
+    const uint32_t ed = lookup_d(sh, dbits);
     const uint32_t nd = ed & 15u, d = ed >> 4;
     const int ok = d < 30u;
     const uint32_t xd = (ok && d >= 2u) ? (d - 2u) >> 1 : 0u;
-    const uint32_t dist = (d < 4u ? d + 1u : ((2u | (d & 1u)) << xd) + 1u) + ((uint32_t)(r.bb >> nd) & hz::bmask(xd));
-    g_drop(r, ok ? nd + xd : nd);
+    const uint32_t dist = (d < 4u ? d + 1u : ((2u | (d & 1u)) << xd) + 1u) + ((dbits >> nd) & hz::bmask(xd));
+    g_drop(s, r, ok ? nd + xd : nd);
     tok = ok ? (T_MATCH | (len << 16) | (dist - 1u)) : T_ERR;
   }
   return tok;
@@ -460,7 +507,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
   {
     GRd r;
     g_init(S, r, S.lo * 8u);
-    const uint64_t two = r.bb;
+    const uint64_t two = g_peek(r);
     const uint32_t cmf = (uint32_t)(two & 0xffu), flg = (uint32_t)((two >> 8) & 0xffu);
     if ((cmf & 0x0f) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0) return ST_DATA;
     if (flg & 0x20) return ST_DATA;   // preset dictionary: Z_NEED_DICT
@@ -476,7 +523,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
     {
       GRd r;
       g_init(S, r, pos);
-      h3 = (uint32_t)(r.bb & 7u);
+      h3 = (uint32_t)(g_peek(r) & 7u);
     }
     const uint32_t block_start = pos;
     pos += 3;
@@ -489,7 +536,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       if (pos + 32u > limit_bits) return ST_TRUNC;
       GRd r;
       g_init(S, r, pos);
-      const uint32_t ln = (uint32_t)(r.bb & 0xffffffffu);
+      const uint32_t ln = (uint32_t)(g_peek(r) & 0xffffffffu);
       const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
       if ((len ^ 0xffffu) != nlen) return ST_DATA;
       pos += 32u;
@@ -528,16 +575,16 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           GRd r;
           g_init(S, r, pos);
           g_fill(S, r);
-          const uint32_t hlit = (uint32_t)(r.bb & 31u) + 257u, hdist = (uint32_t)((r.bb >> 5) & 31u) + 1u;
-          const uint32_t hclen = (uint32_t)((r.bb >> 10) & 15u) + 4u;
-          g_drop(r, 14);
+          const uint32_t hlit = (uint32_t)(g_peek(r) & 31u) + 257u, hdist = (uint32_t)((g_peek(r) >> 5) & 31u) + 1u;
+          const uint32_t hclen = (uint32_t)((g_peek(r) >> 10) & 15u) + 4u;
+          g_drop(S, r, 14);
           if (hlit > 286 || hdist > 30) st = ST_DATA;
           uint16_t* cl = sh.sorted_cl;
           for (int i = 0; i < 19; i++) cl[i] = 0;
           for (uint32_t i = 0; i < hclen; i++) {
             g_fill(S, r);
-            cl[hz::cl_order(i)] = (uint16_t)(r.bb & 7u);
-            g_drop(r, 3);
+            cl[hz::cl_order(i)] = (uint16_t)(g_peek(r) & 7u);
+            g_drop(S, r, 3);
           }
           uint16_t* cnt = sh.cnt_cl;
           for (int l = 0; l < 16; l++) cnt[l] = 0;
@@ -567,16 +614,16 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           while (st == ST_OK && n < total) {
             if (r.pos > limit_bits + 64u) { st = ST_TRUNC; break; }
             g_fill(S, r);
-            const uint32_t e = clut[r.bb & 127u];
+            const uint32_t e = clut[g_peek(r) & 127u];
             const uint32_t sym = e & 0xffu, l = e >> 8;
-            g_drop(r, l);
+            g_drop(S, r, l);
             if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
             uint32_t rep, val = 0;
             if (sym == 16) {
               if (n == 0) { st = ST_DATA; break; }
-              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(r.bb & 3u); g_drop(r, 2);
-            } else if (sym == 17) { rep = 3 + (uint32_t)(r.bb & 7u); g_drop(r, 3); }
-            else { rep = 11 + (uint32_t)(r.bb & 127u); g_drop(r, 7); }
+              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(g_peek(r) & 3u); g_drop(S, r, 2);
+            } else if (sym == 17) { rep = 3 + (uint32_t)(g_peek(r) & 7u); g_drop(S, r, 3); }
+            else { rep = 11 + (uint32_t)(g_peek(r) & 127u); g_drop(S, r, 7); }
             if (n + rep > total) { st = ST_DATA; break; }
             for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
           }
@@ -1149,7 +1196,7 @@ HZ_UNROLL
   {
     GRd r;
     g_init(S, r, pos);
-    t32 = (uint32_t)(r.bb & 0xffffffffu);
+    t32 = (uint32_t)(g_peek(r) & 0xffffffffu);
   }
   const uint32_t want = (t32 >> 24) | ((t32 >> 8) & 0xff00u) | ((t32 << 8) & 0xff0000u) | (t32 << 24);
   uint64_t S1 = 0, S2 = 0;
