@@ -317,11 +317,8 @@ HZ_HD uint32_t huff_tree(LitShared& sh, const uint8_t* len) {
 // One wavefront: the segment's literals section into out (LCAP bytes); returns its size,
 // or 0 when raw literals are not larger (encode_segment then writes them raw).
 HZ_HD uint32_t lit_section(LitShared& sh, const uint16_t* tok, const hd::SegParse* sp, uint8_t* out) {
-  hz_gcu8* const gt = HZ_GLOBAL(hz_gcu8*, tok);
-  auto slot = [&](uint32_t k, uint32_t l) -> uint32_t {
-    const uint32_t i = hd::tslot(k, (int)l);
-    return (uint32_t)gt[2u * i] | ((uint32_t)gt[2u * i + 1u] << 8);
-  };
+  const hz_gu16* const gt = HZ_GLOBAL(const hz_gu16*, tok);
+  auto slot = [&](uint32_t k, uint32_t l) -> uint32_t { return gt[hd::tslot(k, (int)l)]; };
   // literal bytes in stream order: parse lane l's literals after those of lanes < l
   LANE_LOOP {
     uint32_t c = 0;
@@ -418,11 +415,8 @@ HZ_HD uint32_t lit_section(LitShared& sh, const uint16_t* tok, const hd::SegPars
 HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegParse* sp, const hd::EncJob& job,
                               uint32_t s0, uint32_t seglen, uint32_t last, uint8_t* out, uint32_t cap,
                               const uint8_t* lsec = nullptr, uint32_t lsize = 0) {
-  hz_gcu8* const gt = HZ_GLOBAL(hz_gcu8*, tok);
-  auto slot = [&](uint32_t k, uint32_t l) -> uint32_t {
-    const uint32_t i = hd::tslot(k, (int)l);
-    return (uint32_t)gt[2u * i] | ((uint32_t)gt[2u * i + 1u] << 8);
-  };
+  const hz_gu16* const gt = HZ_GLOBAL(const hz_gu16*, tok);
+  auto slot = [&](uint32_t k, uint32_t l) -> uint32_t { return gt[hd::tslot(k, (int)l)]; };
   uint32_t nlit = 0, nseq = 0;
   for (uint32_t s = 0; s < 256u; s++) nlit += sp->freq[s];
   for (uint32_t s = 257; s < 286u; s++) nseq += sp->freq[s];
