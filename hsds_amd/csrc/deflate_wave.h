@@ -133,9 +133,13 @@ HZ_HD uint32_t dist_extra_bits(uint32_t s) { return s < 4u ? 0u : (s - 2u) / 2u;
 HZ_HD uint32_t fixed_ll_len(uint32_t s) { return s < 144u ? 8u : s < 256u ? 9u : s < 280u ? 7u : 8u; }
 HZ_HD uint32_t cl_extra_bits(uint32_t sym) { return sym == 16u ? 2u : sym == 17u ? 3u : sym == 18u ? 7u : 0u; }
 HZ_HD uint32_t rev16(uint32_t code, uint32_t len) {
+#if HZ_GPU
+  return len ? __builtin_bitreverse32(code) >> (32u - len) : 0u;     // one v_bfrev_b32
+#else
   uint32_t r = 0;
   for (uint32_t i = 0; i < len; i++) { r = (r << 1) | (code & 1u); code >>= 1; }
   return r;
+#endif
 }
 
 HZ_HD void lds_add(uint32_t* p, uint32_t v) {

@@ -1,0 +1,15 @@
+#!/bin/bash
+# cfg5 encode legs (zlib / lz4 / zstd / bitshuffle) for several builds: tools/ab_encode_libs.sh a.so b.so ...
+set -o pipefail
+mkdir -p gpurun_out
+for lib in "$@"; do
+  HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --headline 0 --steps 3 --warmup 1 --cpu-seconds 0 \
+    --cfg3 0 --cfg1 0 --cfg5 1 --cfg4-full 0 > gpurun_out/abe_$(basename $lib).log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -5 gpurun_out/abe_$(basename $lib).log; exit $rc; }
+  python - $lib gpurun_out/abe_$(basename $lib).log <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])["legs"]["cfg5"]
+print(f"{sys.argv[1]:20s} zlib {d['value']:6.2f} GB/s ({d['deflate_kernel_ms']:7.2f} ms)  lz4 {d['lz4_encode']['value']:6.2f}  "
+      f"zstd {d['zstd_encode']['value']:6.2f}  bshuf {d['bshuf_encode']['value']:6.2f}  size {d['size_vs_libz']}")
+PY
+done
