@@ -588,8 +588,9 @@ struct HuffShared {
 
 // Serial part of the Huffman build (lane 0): keys[0..n) are sorted ascending by
 // (frequency, symbol).  Minimum-redundancy lengths in place (Moffat & Katajainen
-// 1995), Kraft-exact limiting to maxbits, lengths assigned longest-first to the
-// least frequent symbols, then canonical codes (RFC 1951 3.2.2), bit-reversed.
+// 1995) and Kraft-exact limiting to maxbits give the code count per length
+// (bl_count) and the first canonical code per length (next_code, RFC 1951 3.2.2);
+// the lanes then assign lengths and codes (HD_BUILD_HUFF).
 HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens, uint16_t* codes, int nsym) {
   uint32_t* A = sh.work;
   for (int i = 0; i < n; i++) A[i] = sh.keys[i] >> 9;
@@ -632,24 +633,14 @@ HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens
       total--;
     }
   }
-  // lengths: the most frequent symbols (end of keys) get the shortest codes
-  {
-    int j = n;
-    for (int l = 1; l <= maxbits; l++) {
-      for (uint32_t c = sh.bl_count[l]; c > 0; c--) lens[sh.keys[--j] & 511u] = (uint8_t)l;
-    }
-  }
-  // canonical codes
+  // lengths and canonical codes: by all lanes (huff_assign), from bl_count
+  (void)lens; (void)codes; (void)nsym;
   {
     uint32_t code = 0;
     sh.bl_count[0] = 0;
     for (int l = 1; l <= 15; l++) {
       code = (code + sh.bl_count[l - 1]) << 1;
       sh.next_code[l] = code;
-    }
-    for (int s = 0; s < nsym; s++) {
-      const uint32_t l = lens[s];
-      codes[s] = l ? (uint16_t)rev16(sh.next_code[l]++, l) : (uint16_t)0;
     }
   }
 }
@@ -695,6 +686,38 @@ HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens
       if (lane == 0) hd::huff_lengths_serial(sh, (int)(sh).cnt, (MAXBITS), (LENS), (CODES), (N)); \
     }                                                                                           \
     WAVE_SYNC();                                                                                \
+    /* lengths: the most frequent symbols (end of keys) get the shortest codes */              \
+    LANE_LOOP {                                                                                 \
+      const int _n = (int)(sh).cnt;                                                             \
+      for (int _i = lane; _i < _n; _i += 64) {                                                  \
+        const uint32_t _r = (uint32_t)(_n - 1 - _i);                                            \
+        uint32_t _l = 1, _acc = (sh).bl_count[1];                                               \
+        while (_acc <= _r && _l < 15u) { _l++; _acc += (sh).bl_count[_l]; }                     \
+        (LENS)[(sh).keys[_i] & 511u] = (uint8_t)_l;                                             \
+      }                                                                                         \
+    }                                                                                           \
+    WAVE_SYNC();                                                                                \
+    /* canonical codes: rank within a length by ballots, 64 symbols at a time */               \
+    for (int _c = 0; _c < (N); _c += 64) {                                                      \
+      LANE_VAR(uint32_t, _ln);                                                                  \
+      LANE_LOOP {                                                                               \
+        LV(_ln) = _c + lane < (N) ? (uint32_t)(LENS)[_c + lane] : 0u;                           \
+        if (_c + lane < (N)) (CODES)[_c + lane] = 0;                                            \
+      }                                                                                         \
+      for (uint32_t _L = 1; _L <= (uint32_t)(MAXBITS); _L++) {                                  \
+        const uint64_t _m = WAVE_BALLOT(LV(_ln) == _L);                                         \
+        if (!_m) continue;                                                                      \
+        LANE_LOOP {                                                                             \
+          if (LV(_ln) == _L) {                                                                  \
+            const uint64_t _below = lane ? (_m & ((~0ull) >> (64 - lane))) : 0ull;              \
+            (CODES)[_c + lane] = (uint16_t)hd::rev16((sh).next_code[_L] + hz::popc64(_below), _L); \
+          }                                                                                     \
+        }                                                                                       \
+        WAVE_SYNC();                                                                            \
+        LANE_LOOP { if (lane == 0) (sh).next_code[_L] += hz::popc64(_m); }                      \
+        WAVE_SYNC();                                                                            \
+      }                                                                                         \
+    }                                                                                           \
   } while (0)
 
 // code-length sequence (RFC 1951 3.2.7) of len_ll[0..hlit) ++ len_d[0..hdist),
