@@ -966,8 +966,11 @@ HZ_HD void emit_segment(EmitShared& sh, const SegOut& so, const SegCode* sc, con
   } else {
     LANE_VAR(uint32_t, nb);
     LANE_VAR(uint32_t, hb);
+    // block header: 3 bits, and for a dynamic block HLIT / HDIST / HCLEN, the code-length
+    // code lengths (3 bits each) and the run-length coded code lengths -- written by all
+    // lanes at their bit offsets (a serial lane-0 writer spent ~300 LDS atomics per block)
+    uint32_t hbits_all = 3;
     LANE_LOOP {
-      uint32_t hbits = 3;
       if (lane == 0) {
         BitW w;
         bw_init(w, off0);
@@ -976,21 +979,59 @@ HZ_HD void emit_segment(EmitShared& sh, const SegOut& so, const SegCode* sc, con
           bw_put(sh.stage, w, sc->hlit - 257u, 5);
           bw_put(sh.stage, w, sc->hdist - 1u, 5);
           bw_put(sh.stage, w, sc->hclen - 4u, 4);
-          hbits += 14u + 3u * sc->hclen;
-          for (uint32_t i = 0; i < sc->hclen; i++) bw_put(sh.stage, w, sh.cl[hz::cl_order(i)] & 15u, 3);
-          for (uint32_t i = 0; i < sc->nrle; i++) {
-            const uint32_t e = sh.rle[i];
-            const uint32_t sym = e & 0xffu;
-            const uint32_t c = sh.cl[sym];
-            bw_put(sh.stage, w, c >> 4, c & 15u);
-            const uint32_t xb = cl_extra_bits(sym);
-            if (xb) bw_put(sh.stage, w, e >> 8, xb);
-            hbits += (c & 15u) + xb;
-          }
         }
         bw_flush(sh.stage, w);
       }
-      LV(hb) = lane == 0 ? hbits : 0u;
+      if (btype == 2 && (uint32_t)lane < sc->hclen) {
+        BitW w;
+        bw_init(w, off0 + 17u + 3u * (uint32_t)lane);
+        bw_put(sh.stage, w, sh.cl[hz::cl_order((uint32_t)lane)] & 15u, 3);
+        bw_flush(sh.stage, w);
+      }
+    }
+    if (btype == 2) {
+      uint32_t base = off0 + 17u + 3u * sc->hclen;
+      const uint32_t nrle = sc->nrle;
+      for (uint32_t c0 = 0; c0 < nrle; c0 += WAVE) {
+        LANE_VAR(uint32_t, rb);
+        LANE_LOOP {
+          const uint32_t i = c0 + (uint32_t)lane;
+          uint32_t b = 0;
+          if (i < nrle) {
+            const uint32_t e = sh.rle[i];
+            b = (sh.cl[e & 0xffu] & 15u) + cl_extra_bits(e & 0xffu);
+          }
+          LV(rb) = b;
+        }
+        LANE_VAR(uint32_t, ro);
+        uint32_t chunk_bits;
+#if HZ_GPU
+        ro = hz::wave_excl_scan(rb, (int)threadIdx.x);
+        chunk_bits = hz::wave_sum(rb);
+#else
+        chunk_bits = 0;
+        for (int l = 0; l < 64; l++) { ro[l] = chunk_bits; chunk_bits += rb[l]; }
+#endif
+        LANE_LOOP {
+          const uint32_t i = c0 + (uint32_t)lane;
+          if (i < nrle) {
+            const uint32_t e = sh.rle[i];
+            const uint32_t sym = e & 0xffu;
+            const uint32_t c = sh.cl[sym];
+            BitW w;
+            bw_init(w, base + LV(ro));
+            bw_put(sh.stage, w, c >> 4, c & 15u);
+            const uint32_t xb = cl_extra_bits(sym);
+            if (xb) bw_put(sh.stage, w, e >> 8, xb);
+            bw_flush(sh.stage, w);
+          }
+        }
+        base += chunk_bits;
+      }
+      hbits_all = base - off0;
+    }
+    LANE_LOOP {
+      LV(hb) = lane == 0 ? hbits_all : 0u;
       // pass 1: bits of this lane's tokens
       uint32_t bits = 0;
       const uint32_t ns = sp->nslot[lane];
