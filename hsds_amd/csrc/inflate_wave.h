@@ -459,6 +459,23 @@ struct TableArgs {
 
 }  // namespace hz
 
+#if HZ_GPU
+#define HZ_UNIFORM(x) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(x)))
+// exclusive scan of the low 24 bits of lane variable v into o, total into t
+#define HZ_SCAN_LOW24(v, o, t)                                \
+  do {                                                        \
+    o = hz::wave_excl_scan((v) & 0xffffffu, (int)threadIdx.x); \
+    t = hz::wave_sum((v) & 0xffffffu);                        \
+  } while (0)
+#else
+#define HZ_UNIFORM(x) ((uint32_t)(x))
+#define HZ_SCAN_LOW24(v, o, t)                                                              \
+  do {                                                                                      \
+    t = 0;                                                                                  \
+    for (int _ln = 0; _ln < 64; _ln++) { o[_ln] = t; t += v[_ln] & 0xffffffu; }             \
+  } while (0)
+#endif
+
 // Table build as a macro-free function per driver is awkward because it needs
 // ballots; it is written once in the SIMT style below.
 #define HZ_BUILD_TABLE(sh, A, status_out)                                               \
@@ -497,72 +514,90 @@ struct TableArgs {
       }                                                                                 \
     }                                                                                   \
     WAVE_SYNC();                                                                        \
-    /* canonical order: ranks within a length via ballots, 64 symbols at a time */     \
-    for (int _c = 0; _c < (A).n; _c += 64) {                                            \
-      LANE_VAR(int, _l);                                                                \
-      LANE_LOOP { LV(_l) = _c + lane < (A).n ? (A).lens[_c + lane] : 0; }               \
-      for (int L = 1; L <= 15; L++) {                                                   \
-        if (!(A).cnt[L]) continue;                                                      \
-        const uint64_t m = WAVE_BALLOT(LV(_l) == L);                                    \
-        if (!m) continue;                                                               \
-        LANE_LOOP {                                                                     \
-          if (LV(_l) == L) {                                                            \
-            const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;        \
-            (A).sorted[(sh).tb_next[L] + hz::popc64(below)] = (uint16_t)(_c + lane);    \
+    /* per-length counts, first codes and offsets, read once into wave-uniform registers */ \
+    uint32_t _cn[16], _fc[16], _of[16];                                                 \
+    _Pragma("unroll") for (int _q = 0; _q < 16; _q++) {                                 \
+      _cn[_q] = HZ_UNIFORM(_q ? (A).cnt[_q] : 0);                                       \
+      _fc[_q] = HZ_UNIFORM(_q ? (sh).tb_first[_q] : 0);                                 \
+      _of[_q] = HZ_UNIFORM(_q ? (sh).tb_offs[_q] : 0);                                  \
+    }                                                                                   \
+    /* canonical order: ranks within a length via ballots, 64 symbols at a time; the  \
+       running offset per length stays in registers (no LDS round trip per length) */  \
+    {                                                                                   \
+      uint32_t _nx[16];                                                                 \
+      _Pragma("unroll") for (int _q = 0; _q < 16; _q++) _nx[_q] = _of[_q];              \
+      for (int _c = 0; _c < (A).n; _c += 64) {                                          \
+        LANE_VAR(int, _l);                                                              \
+        LANE_LOOP { LV(_l) = _c + lane < (A).n ? (A).lens[_c + lane] : 0; }             \
+        _Pragma("unroll") for (int L = 1; L <= 15; L++) {                               \
+          if (!_cn[L]) continue;                                                        \
+          const uint64_t m = WAVE_BALLOT(LV(_l) == L);                                  \
+          if (!m) continue;                                                             \
+          LANE_LOOP {                                                                   \
+            if (LV(_l) == L) {                                                          \
+              const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;      \
+              (A).sorted[_nx[L] + hz::popc64(below)] = (uint16_t)(_c + lane);           \
+            }                                                                           \
           }                                                                             \
+          _nx[L] += (uint32_t)hz::popc64(m);                                            \
         }                                                                               \
-        WAVE_SYNC();                                                                    \
-        LANE_LOOP { if (lane == 0) (sh).tb_next[L] = (uint16_t)((sh).tb_next[L] + hz::popc64(m)); } \
-        WAVE_SYNC();                                                                    \
       }                                                                                 \
     }                                                                                   \
-    /* LUT fill: every root index decoded canonically (balanced across lanes) */       \
+    WAVE_SYNC();                                                                        \
+    /* LUT fill: every root index tested against each length's canonical range (no   \
+       loop-carried chain: a prefix-free code matches at most one length) */           \
     LANE_LOOP {                                                                         \
       for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
-        int code = 0, first = 0, index = 0; uint32_t bits = (uint32_t)idx;              \
+        const uint32_t rc = hz::rev_bits((uint32_t)idx, (A).root);                      \
         uint32_t e = hz::ent_sym(1, hz::SYM_BAD);                                       \
-        for (int len = 1; len <= (A).root; len++) {                                     \
-          code |= (int)(bits & 1u); bits >>= 1;                                         \
-          int count = (A).cnt[len];                                                     \
-          if (code - count < first) {                                                   \
-            uint32_t sym = (A).sorted[index + (code - first)];                          \
-            e = hz::ent_sym((uint32_t)len, sym);                                        \
-            break;                                                                      \
-          }                                                                             \
-          index += count; first += count; first <<= 1; code <<= 1;                     \
+        _Pragma("unroll") for (int len = 1; len <= 15; len++) {                         \
+          if (len > (A).root) break;                                                    \
+          const uint32_t d = (rc >> ((A).root - len)) - _fc[len];                       \
+          if (d < _cn[len]) e = hz::ent_sym((uint32_t)len, (A).sorted[_of[len] + d]);   \
         }                                                                               \
         (A).lut[idx] = (uint16_t)e;                                                     \
       }                                                                                 \
     }                                                                                   \
     WAVE_SYNC();                                                                        \
-    /* second level: lane 0 allocates one subtable per root prefix of longer codes */  \
+    /* second level: one subtable per root prefix of longer codes.  Codes with the     \
+       same prefix are contiguous in canonical order; the last of a run (the longest)  \
+       sizes its subtable, and a scan over the runs places them */                      \
     const int _R = (A).root;                                                            \
     const int _k0 = (sh).tb_offs[_R + 1], _k1 = (sh).tb_offs[16];                       \
     if (_k1 > _k0) {                                                                    \
-      LANE_LOOP {                                                                       \
-        if (lane == 0) {                                                                \
-          int used = 0, k = _k0;                                                        \
-          while (k < _k1) {                                                             \
-            /* codes with the same root prefix are contiguous in canonical order */     \
+      uint32_t _used = 0;                                                               \
+      for (int _b = _k0; _b < _k1; _b += 64) {                                          \
+        LANE_VAR(uint32_t, _sz);                                                        \
+        LANE_VAR(uint32_t, _pp);                                                        \
+        LANE_VAR(uint32_t, _ox);                                                        \
+        LANE_LOOP {                                                                     \
+          const int k = _b + lane;                                                      \
+          uint32_t sz = 0, p = 0;                                                       \
+          if (k < _k1) {                                                                \
             const int l0 = (A).lens[(A).sorted[k]];                                     \
-            const int p = ((int)(sh).tb_first[l0] + (k - (int)(sh).tb_offs[l0])) >> (l0 - _R); \
-            int k2 = k, lmax = l0;                                                      \
-            while (k2 < _k1) {                                                          \
-              const int l2 = (A).lens[(A).sorted[k2]];                                  \
-              const int p2 = ((int)(sh).tb_first[l2] + (k2 - (int)(sh).tb_offs[l2])) >> (l2 - _R); \
-              if (p2 != p) break;                                                       \
-              lmax = l2; k2++;                                                          \
+            p = (uint32_t)(((int)(sh).tb_first[l0] + (k - (int)(sh).tb_offs[l0])) >> (l0 - _R)); \
+            int last = k + 1 == _k1;                                                    \
+            if (!last) {                                                                \
+              const int l1 = (A).lens[(A).sorted[k + 1]];                               \
+              last = (uint32_t)(((int)(sh).tb_first[l1] + (k + 1 - (int)(sh).tb_offs[l1])) >> (l1 - _R)) != p; \
             }                                                                           \
-            const int sb = lmax - _R;                                                   \
-            /* <= nsub for every complete code (see LL_SUB/D_SUB); a table that would  \
-               not fit is rejected instead of written past its end */                   \
-            if (used + (1 << sb) > (A).nsub) { (sh).u_status = hz::ST_DATA; break; }    \
-            (A).lut[hz::rev_bits((uint32_t)p, _R)] = hz::ent_sub((uint32_t)used, (uint32_t)sb); \
-            used += 1 << sb;                                                            \
-            k = k2;                                                                     \
+            if (last) sz = (uint32_t)(l0 - _R);                                         \
+            sz = last ? (1u << sz) | (sz << 24) : 0u;                                   \
           }                                                                             \
+          LV(_sz) = sz; LV(_pp) = p;                                                    \
         }                                                                               \
+        uint32_t _tot;                                                                  \
+        HZ_SCAN_LOW24(_sz, _ox, _tot);                                                  \
+        LANE_LOOP {                                                                     \
+          if (LV(_sz))                                                                  \
+            (A).lut[hz::rev_bits(LV(_pp), _R)] =                                        \
+                hz::ent_sub(_used + LV(_ox), LV(_sz) >> 24);                             \
+        }                                                                               \
+        _used += _tot;                                                                  \
       }                                                                                 \
+      /* <= nsub for every complete code (see LL_SUB/D_SUB); a table that would not    \
+         fit is rejected before any subtable entry is written */                        \
+      LANE_LOOP { if (lane == 0 && _used > (uint32_t)(A).nsub) (sh).u_status = hz::ST_DATA; } \
       WAVE_SYNC();                                                                      \
       /* fill subtables by symbol (zlib-style replication) */                           \
       LANE_LOOP {                                                                       \
