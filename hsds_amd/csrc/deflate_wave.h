@@ -591,10 +591,9 @@ struct HuffShared {
 // 1995) and Kraft-exact limiting to maxbits give the code count per length
 // (bl_count) and the first canonical code per length (next_code, RFC 1951 3.2.2);
 // the lanes then assign lengths and codes (HD_BUILD_HUFF).
-HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens, uint16_t* codes, int nsym) {
+HZ_HD void huff_parents_serial(HuffShared& sh, int n) {
   uint32_t* A = sh.work;
   for (int i = 0; i < n; i++) A[i] = sh.keys[i] >> 9;
-  for (int l = 0; l <= 16; l++) sh.bl_count[l] = 0;
   // phase 1: parents, left to right
   A[0] += A[1];
   int root = 0, leaf = 2;
@@ -604,13 +603,61 @@ HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens
     if (leaf >= n || (root < next && A[root] < A[leaf])) { A[next] += A[root]; A[root++] = (uint32_t)next; }
     else A[next] += A[leaf++];
   }
-  // phase 2: internal node depths, right to left
-  A[n - 2] = 0;
-  for (int next = n - 3; next >= 0; next--) A[next] = A[A[next]] + 1u;
+}
+
+// Phase 2 (all lanes): the depth of every internal node by pointer jumping.  After
+// phase 1 A[i] (i < n - 2) is the parent of internal node i (parents lie to the right)
+// and n - 2 is the root.  Each word packs pointer | depth-so-far << 16; ceil(log2 n)
+// rounds of (d += d[p], p = p[p]) leave every node pointing at the root with its depth,
+// the value the serial right-to-left pass A[i] = A[A[i]] + 1 computes.
+#define HD_HUFF_DEPTHS(sh, NN)                                                           \
+  do {                                                                                    \
+    const int _n = (NN);                                                                  \
+    uint32_t* const _A = (sh).work;                                                       \
+    LANE_LOOP {                                                                           \
+      for (int _i = lane; _i < _n - 1; _i += 64)                                          \
+        _A[_i] = _i == _n - 2 ? (uint32_t)_i : (_A[_i] | (1u << 16));                     \
+    }                                                                                     \
+    WAVE_SYNC();                                                                          \
+    for (int _s = 1; _s < _n; _s <<= 1) {                                                 \
+      LANE_VAR(uint32_t, _v0); LANE_VAR(uint32_t, _v1); LANE_VAR(uint32_t, _v2);          \
+      LANE_VAR(uint32_t, _v3); LANE_VAR(uint32_t, _v4);                                   \
+      LANE_LOOP {                                                                         \
+        uint32_t _t[5];                                                                   \
+        HZ_UNROLL for (int _k = 0; _k < 5; _k++) {                                        \
+          const int _i = lane + 64 * _k;                                                  \
+          uint32_t _x = 0;                                                                \
+          if (_i < _n - 1) {                                                              \
+            const uint32_t _a = _A[_i], _b = _A[_a & 0xffffu];                            \
+            _x = (_b & 0xffffu) | (((_a >> 16) + (_b >> 16)) << 16);                      \
+          }                                                                               \
+          _t[_k] = _x;                                                                    \
+        }                                                                                 \
+        LV(_v0) = _t[0]; LV(_v1) = _t[1]; LV(_v2) = _t[2]; LV(_v3) = _t[3]; LV(_v4) = _t[4]; \
+      }                                                                                   \
+      WAVE_SYNC();                                                                        \
+      LANE_LOOP {                                                                         \
+        const uint32_t _t[5] = {LV(_v0), LV(_v1), LV(_v2), LV(_v3), LV(_v4)};             \
+        HZ_UNROLL for (int _k = 0; _k < 5; _k++) {                                        \
+          const int _i = lane + 64 * _k;                                                  \
+          if (_i < _n - 1) _A[_i] = _t[_k];                                               \
+        }                                                                                 \
+      }                                                                                   \
+      WAVE_SYNC();                                                                        \
+    }                                                                                     \
+    LANE_LOOP { for (int _i = lane; _i < _n - 1; _i += 64) _A[_i] >>= 16; }               \
+    WAVE_SYNC();                                                                          \
+  } while (0)
+
+// Serial phase 3 (lane 0): leaf depths -> counts per length, the length limit and the
+// first canonical code per length.
+HZ_HD void huff_counts_serial(HuffShared& sh, int n, int maxbits) {
+  uint32_t* A = sh.work;
+  for (int l = 0; l <= 16; l++) sh.bl_count[l] = 0;
   // phase 3: leaf depths -> counts per length
   {
     int avbl = 1, used = 0, dpth = 0;
-    root = n - 2;
+    int root = n - 2;
     while (avbl > 0) {
       while (root >= 0 && (int)A[root] == dpth) { used++; root--; }
       while (avbl > used) { sh.bl_count[dpth > 16 ? 16 : dpth]++; avbl--; }
@@ -633,8 +680,7 @@ HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens
       total--;
     }
   }
-  // lengths and canonical codes: by all lanes (huff_assign), from bl_count
-  (void)lens; (void)codes; (void)nsym;
+  // lengths and canonical codes: by all lanes (HD_BUILD_HUFF), from bl_count
   {
     uint32_t code = 0;
     sh.bl_count[0] = 0;
@@ -682,9 +728,10 @@ HZ_HD void huff_lengths_serial(HuffShared& sh, int n, int maxbits, uint8_t* lens
         WAVE_SYNC();                                                                            \
       }                                                                                         \
     }                                                                                           \
-    LANE_LOOP {                                                                                 \
-      if (lane == 0) hd::huff_lengths_serial(sh, (int)(sh).cnt, (MAXBITS), (LENS), (CODES), (N)); \
-    }                                                                                           \
+    LANE_LOOP { if (lane == 0) hd::huff_parents_serial(sh, (int)(sh).cnt); }                  \
+    WAVE_SYNC();                                                                                \
+    HD_HUFF_DEPTHS(sh, (int)(sh).cnt);                                                          \
+    LANE_LOOP { if (lane == 0) hd::huff_counts_serial(sh, (int)(sh).cnt, (MAXBITS)); }         \
     WAVE_SYNC();                                                                                \
     /* lengths: the most frequent symbols (end of keys) get the shortest codes */              \
     LANE_LOOP {                                                                                 \
