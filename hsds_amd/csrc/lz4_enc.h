@@ -59,8 +59,10 @@ HZ_HD uint32_t in_byte(InRd& in, uint32_t pos) {
 // Literal runs of RUN_MIN bytes or more are not copied by the lane that owns their
 // sequence (a run can span many lanes' token ranges, up to a whole incompressible
 // block): the lane reserves the bytes and lists the run; the whole wave then copies
-// the listed runs (flush_runs), 64 bytes per instruction.
+// the listed runs (flush_runs), 64 bytes per instruction, CP_UNR independent loads in
+// flight per lane before their stores (one memory latency per 64 * CP_UNR bytes).
 constexpr uint32_t RUN_MIN = 64;
+constexpr uint32_t CP_UNR = 8;
 constexpr uint32_t RUN_CAP = 136;        // > SEG / RUN_MIN + carried run + final run
 struct CopyRun {
   hz_gu8* dst;
@@ -90,19 +92,55 @@ static
 #endif
 inline void flush_runs(CopyList* cl, const hd::EncJob& job) {
   WAVE_SYNC();
+#ifdef HZ_EXP_NOFLUSH
+  const uint32_t nr = 0;
+#else
   const uint32_t nr = cl->n < RUN_CAP ? cl->n : RUN_CAP;
+#endif
   hz_gcu8* s = HZ_GLOBAL(hz_gcu8*, job.src);
   for (uint32_t k = 0; k < nr; k++) {
     hz_gu8* const d = cl->r[k].dst;
     const uint32_t src = cl->r[k].src, len = cl->r[k].len;
     LANE_LOOP {
-      for (uint32_t i = (uint32_t)lane; i < len; i += 64u)
-        d[i] = job.ts > 1u ? s[hd::shuffled_src_index(job.off + src + i, job.ts, job.neb)] : s[src + i];
+      for (uint32_t i0 = 0; i0 < len; i0 += 64u * CP_UNR) {
+        uint8_t v[CP_UNR];
+HZ_UNROLL
+        for (uint32_t j = 0; j < CP_UNR; j++) {
+          const uint32_t i = i0 + 64u * j + (uint32_t)lane;
+          v[j] = i < len ? (job.ts > 1u ? s[hd::shuffled_src_index(job.off + src + i, job.ts, job.neb)] : s[src + i]) : 0;
+        }
+HZ_UNROLL
+        for (uint32_t j = 0; j < CP_UNR; j++) {
+          const uint32_t i = i0 + 64u * j + (uint32_t)lane;
+          if (i < len) d[i] = v[j];
+        }
+      }
     }
   }
   WAVE_SYNC();
   LANE_LOOP { if (lane == 0) cl->n = 0; }
   WAVE_SYNC();
+}
+
+// literal bytes [l0, l1) of a direct (ts == 1) split to o, 32 bytes per round: the 9
+// dwords covering a round are loaded together, so a round costs one memory latency
+// (the byte reader's refills cost one per 4 - 8 bytes)
+HZ_HD void copy_lits(Out& o, const InRd& in, uint32_t l0, uint32_t l1) {
+  for (uint32_t p = l0; p < l1; p += 32u) {
+    const uint32_t ap = p + in.r.lo, w0 = ap >> 2, sh = (ap & 3u) * 8u;
+    uint32_t dw[9];
+HZ_UNROLL
+    for (uint32_t k = 0; k < 9u; k++) dw[k] = hz::load_word(in.r.base, w0 + k, in.r.lo, in.r.hi);
+    const uint32_t cnt = l1 - p < 32u ? l1 - p : 32u;
+HZ_UNROLL
+    for (uint32_t k = 0; k < 8u; k++) {
+      const uint32_t v = sh ? (dw[k] >> sh) | (dw[k + 1] << (32u - sh)) : dw[k];
+HZ_UNROLL
+      for (uint32_t b = 0; b < 4u; b++)
+        if (4u * k + b < cnt) o.p[o.n + 4u * k + b] = (uint8_t)(v >> (8u * b));
+    }
+    o.n += cnt;
+  }
 }
 
 // one sequence: literals [l0, l1), then a match (ml >= 4) of distance dist; ml == 0:
@@ -115,7 +153,12 @@ HZ_HD void sequence(Out& o, InRd& in, uint32_t l0, uint32_t l1, uint32_t dist, u
   if (ll >= 15u) put_len(o, ll - 15u);
   if (o.write) {
     if (ll >= RUN_MIN && defer_run(cl, o.p + o.n, l0, ll)) o.n += ll;
+#ifdef HZ_EXP_NOLIT
+    else o.n += ll;
+#else
+    else if (in.ts == 1u) copy_lits(o, in, l0, l1);
     else for (uint32_t p = l0; p < l1; p++) put(o, in_byte(in, p));
+#endif
   } else {
     o.n += ll;
   }
