@@ -61,9 +61,12 @@ HZ_HD uint32_t in_byte(InRd& in, uint32_t pos) {
 // block): the lane reserves the bytes and lists the run; the whole wave then copies
 // the listed runs (flush_runs), 64 bytes per instruction, CP_UNR independent loads in
 // flight per lane before their stores (one memory latency per 64 * CP_UNR bytes).
-constexpr uint32_t RUN_MIN = 64;
+#ifndef HZ_RUN_MIN
+#define HZ_RUN_MIN 32
+#endif
+constexpr uint32_t RUN_MIN = HZ_RUN_MIN;
 constexpr uint32_t CP_UNR = 8;
-constexpr uint32_t RUN_CAP = 136;        // > SEG / RUN_MIN + carried run + final run
+constexpr uint32_t RUN_CAP = 8192u / RUN_MIN + 8u;   // > SEG / RUN_MIN + carried run + final run
 struct CopyRun {
   hz_gu8* dst;
   uint32_t src, len;
@@ -125,15 +128,19 @@ HZ_UNROLL
 // literal bytes [l0, l1) of a direct (ts == 1) split to o, 32 bytes per round: the 9
 // dwords covering a round are loaded together, so a round costs one memory latency
 // (the byte reader's refills cost one per 4 - 8 bytes)
+#ifndef HZ_LIT_ROUND
+#define HZ_LIT_ROUND 32
+#endif
 HZ_HD void copy_lits(Out& o, const InRd& in, uint32_t l0, uint32_t l1) {
-  for (uint32_t p = l0; p < l1; p += 32u) {
+  constexpr uint32_t RB = HZ_LIT_ROUND, RW = RB / 4u;
+  for (uint32_t p = l0; p < l1; p += RB) {
     const uint32_t ap = p + in.r.lo, w0 = ap >> 2, sh = (ap & 3u) * 8u;
-    uint32_t dw[9];
+    uint32_t dw[RW + 1];
 HZ_UNROLL
-    for (uint32_t k = 0; k < 9u; k++) dw[k] = hz::load_word(in.r.base, w0 + k, in.r.lo, in.r.hi);
-    const uint32_t cnt = l1 - p < 32u ? l1 - p : 32u;
+    for (uint32_t k = 0; k <= RW; k++) dw[k] = hz::load_word(in.r.base, w0 + k, in.r.lo, in.r.hi);
+    const uint32_t cnt = l1 - p < RB ? l1 - p : RB;
 HZ_UNROLL
-    for (uint32_t k = 0; k < 8u; k++) {
+    for (uint32_t k = 0; k < RW; k++) {
       const uint32_t v = sh ? (dw[k] >> sh) | (dw[k + 1] << (32u - sh)) : dw[k];
 HZ_UNROLL
       for (uint32_t b = 0; b < 4u; b++)
