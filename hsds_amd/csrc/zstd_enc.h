@@ -409,14 +409,53 @@ HZ_HD uint32_t lit_section(LitShared& sh, const uint16_t* tok, const hd::SegPars
   return size;
 }
 
+// The 16-bit token slots of parse lane l (ns of them; slots 2w, 2w + 1 share the dword
+// w * WAVE + l), forward or backward, loaded 8 dwords at a time: a batch costs one memory
+// latency instead of one per slot (the block writes in between would otherwise keep the
+// compiler from hoisting the loads).
+template <class F>
+HZ_HD void slots_fwd(hz_gcu32* gw, uint32_t ns, uint32_t l, F&& f) {
+  const uint32_t nw = (ns + 1u) >> 1;
+  for (uint32_t w0 = 0; w0 < nw; w0 += 8u) {
+    uint32_t wv[8];
+HZ_UNROLL
+    for (uint32_t i = 0; i < 8u; i++) wv[i] = w0 + i < nw ? gw[(size_t)(w0 + i) * (uint32_t)hd::WAVE + l] : 0u;
+    const uint32_t cnt = nw - w0 < 8u ? nw - w0 : 8u;
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t word = wv[0];
+HZ_UNROLL
+      for (uint32_t i = 0; i + 1 < 8u; i++) wv[i] = wv[i + 1];
+      f(word & 0xffffu);
+      if (2u * (w0 + k) + 1u < ns) f(word >> 16);
+    }
+  }
+}
+template <class F>
+HZ_HD void slots_bwd(hz_gcu32* gw, uint32_t ns, uint32_t l, F&& f) {
+  uint32_t w1 = (ns + 1u) >> 1;
+  while (w1 > 0) {
+    const uint32_t cnt = w1 < 8u ? w1 : 8u;
+    uint32_t wv[8];
+HZ_UNROLL
+    for (uint32_t i = 0; i < 8u; i++) wv[i] = i < cnt ? gw[(size_t)(w1 - 1u - i) * (uint32_t)hd::WAVE + l] : 0u;
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t word = wv[0];
+HZ_UNROLL
+      for (uint32_t i = 0; i + 1 < 8u; i++) wv[i] = wv[i + 1];
+      if (2u * (w1 - 1u - k) + 1u < ns) f(word >> 16);
+      f(word & 0xffffu);
+    }
+    w1 -= cnt;
+  }
+}
+
 // Writes segment `seg` of a stream as one zstd block (header included) at out (cap bytes
 // of scratch, >= ZCAP).  tok / sp: the segment's parse tokens and counts; job / s0: the
 // stream input (a raw block copies the segment from it).  Returns the block size.
 HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegParse* sp, const hd::EncJob& job,
                               uint32_t s0, uint32_t seglen, uint32_t last, uint8_t* out, uint32_t cap,
                               const uint8_t* lsec = nullptr, uint32_t lsize = 0) {
-  const hz_gu16* const gt = HZ_GLOBAL(const hz_gu16*, tok);
-  auto slot = [&](uint32_t k, uint32_t l) -> uint32_t { return gt[hd::tslot(k, (int)l)]; };
+  hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
   uint32_t nlit = 0, nseq = 0;
   for (uint32_t s = 0; s < 256u; s++) nlit += sp->freq[s];
   for (uint32_t s = 257; s < 286u; s++) nseq += sp->freq[s];
@@ -437,13 +476,12 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
   }
   // literal bytes, forward over the lanes' token ranges
   for (uint32_t l = 0; l < (uint32_t)hd::WAVE && !over && !lsize; l++) {
-    const uint32_t ns = sp->nslot[l];
-    for (uint32_t k = 0; k < ns;) {
-      const uint32_t v = slot(k, l);
-      if (v & 0x8000u) { k += 2; continue; }
-      put8(out, p, cap, v, over);
-      k++;
-    }
+    uint32_t skip = 0;                               // the distance slot after a match length
+    slots_fwd(gw, sp->nslot[l], l, [&](uint32_t v) {
+      if (skip) skip = 0;
+      else if (v & 0x8000u) skip = 1;
+      else put8(out, p, cap, v, over);
+    });
   }
   // sequences section header
   if (nseq < 128u) {
@@ -480,24 +518,23 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
       bw_add(w, q.ofv, q.ofc);
     };
     for (int32_t l = hd::WAVE - 1; l >= 0 && !w.over; l--) {
-      int32_t k = (int32_t)sp->nslot[l] - 1;
-      while (k >= 0) {
-        const uint32_t v = slot((uint32_t)k, (uint32_t)l);
-        if (k >= 1) {
-          const uint32_t u = slot((uint32_t)k - 1u, (uint32_t)l);
-          if (u & 0x8000u) {                         // (k-1, k): a match
-            if (have) emit(run, pml, poff);
-            have = 1;
-            pml = (u & 0x7fffu) + 3u;
-            poff = v + 1u;
-            run = 0;
-            k -= 2;
-            continue;
-          }
+      // backward: slot k is held until slot k - 1 shows whether (k - 1, k) is a match
+      uint32_t pend = 0, hold = 0;
+      slots_bwd(gw, sp->nslot[l], (uint32_t)l, [&](uint32_t u) {
+        if (!hold) { pend = u; hold = 1; return; }
+        if (u & 0x8000u) {                           // (u, pend): a match
+          if (have) emit(run, pml, poff);
+          have = 1;
+          pml = (u & 0x7fffu) + 3u;
+          poff = pend + 1u;
+          run = 0;
+          hold = 0;
+        } else {
+          run++;                                     // pend: a literal (trailing ones belong to no sequence)
+          pend = u;
         }
-        run++;                                       // a literal (trailing ones belong to no sequence)
-        k--;
-      }
+      });
+      if (hold) run++;
     }
     if (have) emit(run, pml, poff);
     bw_add(w, sml, T.ml.log);
@@ -512,9 +549,14 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
   if (over || csize >= seglen) {
     // Raw_Block: the segment's bytes
     block_header(out, last, 0u, seglen);
-    for (uint32_t i = 0; i < seglen; i++) {
-      const uint32_t q = s0 + i;
-      out[3u + i] = (uint8_t)(hd::load_stream_word(job, q & ~3u, job.len) >> (8u * (q & 3u)));
+    // s0 is a multiple of the segment size: 8 aligned stream words per round, loaded together
+    for (uint32_t i0 = 0; i0 < seglen; i0 += 32u) {
+      uint32_t wv[8];
+HZ_UNROLL
+      for (uint32_t k = 0; k < 8u; k++) wv[k] = i0 + 4u * k < seglen ? hd::load_stream_word(job, s0 + i0 + 4u * k, job.len) : 0u;
+HZ_UNROLL
+      for (uint32_t k = 0; k < 32u; k++)
+        if (i0 + k < seglen) out[3u + i0 + k] = (uint8_t)(wv[k >> 2] >> (8u * (k & 3u)));
     }
     return 3u + seglen;
   }
