@@ -475,13 +475,26 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
     put8(out, p, cap, nlit >> 12, over);
   }
   // literal bytes, forward over the lanes' token ranges
-  for (uint32_t l = 0; l < (uint32_t)hd::WAVE && !over && !lsize; l++) {
-    uint32_t skip = 0;                               // the distance slot after a match length
-    slots_fwd(gw, sp->nslot[l], l, [&](uint32_t v) {
-      if (skip) skip = 0;
-      else if (v & 0x8000u) skip = 1;
-      else put8(out, p, cap, v, over);
-    });
+  // (gathered in a register and stored a dword at a time: the lane's scratch block is
+  // 4-byte aligned; bytes already written below p in the first word are kept)
+  if (!lsize && !over) {
+    if (p + nlit > cap) {
+      over = 1;
+    } else {
+      uint32_t acc = 0;
+      for (uint32_t b = 0; b < (p & 3u); b++) acc |= (uint32_t)out[(p & ~3u) + b] << (8u * b);
+      for (uint32_t l = 0; l < (uint32_t)hd::WAVE; l++) {
+        uint32_t skip = 0;                             // the distance slot after a match length
+        slots_fwd(gw, sp->nslot[l], l, [&](uint32_t v) {
+          if (skip) { skip = 0; return; }
+          if (v & 0x8000u) { skip = 1; return; }
+          acc |= v << (8u * (p & 3u));
+          p++;
+          if (!(p & 3u)) { *(uint32_t*)(out + p - 4u) = acc; acc = 0; }
+        });
+      }
+      for (uint32_t b = 0; b < (p & 3u); b++) out[(p & ~3u) + b] = (uint8_t)(acc >> (8u * b));
+    }
   }
   // sequences section header
   if (nseq < 128u) {
