@@ -138,6 +138,42 @@ HZ_HD void bw_add(BitW& w, uint32_t v, uint32_t nb) {
     w.n -= 8u;
   }
 }
+// the sequences' bit writer: bits gather in a 64-bit register and leave as aligned
+// dwords (the lane's scratch block is 4-byte aligned); pos is the byte position of acc's
+// bit 0 (aligned)
+struct BitD {
+  uint64_t acc;
+  uint32_t n;
+  uint32_t pos, cap;
+  uint8_t* out;
+  int over;
+};
+// starts at byte p, keeping the bytes already written below p in its dword
+HZ_HD void bd_init(BitD& w, uint8_t* out, uint32_t p, uint32_t cap, int over) {
+  w.out = out; w.cap = cap; w.over = over;
+  w.pos = p & ~3u; w.n = 8u * (p & 3u); w.acc = 0;
+  for (uint32_t b = 0; b < (p & 3u); b++) w.acc |= (uint64_t)out[w.pos + b] << (8u * b);
+}
+HZ_HD void bw_add(BitD& w, uint32_t v, uint32_t nb) {
+  w.acc |= (uint64_t)(v & (nb >= 32u ? 0xffffffffu : ((1u << nb) - 1u))) << w.n;
+  w.n += nb;
+  if (w.n >= 32u) {
+    if (w.pos + 4u <= w.cap) *(uint32_t*)(w.out + w.pos) = (uint32_t)w.acc;
+    else w.over = 1;
+    w.pos += 4u;
+    w.acc >>= 32;
+    w.n -= 32u;
+  }
+}
+// pads to a byte, writes the last bytes; returns the end position
+HZ_HD uint32_t bd_finish(BitD& w) {
+  if (w.n & 7u) bw_add(w, 0u, 8u - (w.n & 7u));
+  for (uint32_t b = 0; b < w.n / 8u; b++) {
+    if (w.pos + b < w.cap) w.out[w.pos + b] = (uint8_t)(w.acc >> (8u * b));
+    else w.over = 1;
+  }
+  return w.pos + w.n / 8u;
+}
 HZ_HD void put8(uint8_t* out, uint32_t& p, uint32_t cap, uint32_t v, int& over) {
   if (p < cap) out[p] = (uint8_t)v;
   else over = 1;
@@ -150,7 +186,8 @@ HZ_HD uint32_t fse_init(const CTab& t, uint32_t s) {
   const uint32_t value = (nbo << 16) - (uint32_t)t.dnb[s];
   return t.state[(value >> nbo) + t.dfs[s]];
 }
-HZ_HD void fse_enc(BitW& w, const CTab& t, uint32_t& st, uint32_t s) {
+template <class W>
+HZ_HD void fse_enc(W& w, const CTab& t, uint32_t& st, uint32_t s) {
   const uint32_t nbo = (uint32_t)((st + (uint32_t)t.dnb[s]) >> 16);
   bw_add(w, st, nbo);
   st = t.state[(st >> nbo) + t.dfs[s]];
@@ -509,7 +546,8 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
   }
   if (nseq) {
     put8(out, p, cap, 0u, over);                     // Predefined_Mode x 3
-    BitW w = {0, 0, p, cap, out, over};
+    BitD w;
+    bd_init(w, out, p, cap, over);
     uint32_t sll = 0, sof = 0, sml = 0;
     // backward walk: a match's literal run is known once the walk reaches the match
     // before it (or the segment start), so each sequence is encoded one match late
@@ -554,8 +592,7 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
     bw_add(w, sof, T.of.log);
     bw_add(w, sll, T.ll.log);
     bw_add(w, 1u, 1u);                               // end mark
-    if (w.n) bw_add(w, 0u, 8u - w.n);
-    p = w.pos;
+    p = bd_finish(w);
     over = w.over;
   }
   const uint32_t csize = p - 3u;
