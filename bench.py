@@ -4,6 +4,11 @@ float32 chunks) -- BASELINE.json `metric`, configs[1] (4096-chunk batch per GPU)
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
 
+`--gpus N` with no WORLD_SIZE in the environment starts the N rank processes itself
+(before anything touches the GPU: children, not exec) on 127.0.0.1 and exits with the
+worst rank's status; N larger than the visible devices is an error, never a silent
+one-GPU run.  Under an outside launcher (torchrun) WORLD_SIZE must equal N.
+
 A step = one hsds_decode_batch over the rank's 4096 stored chunks (inputs already in
 HBM).  Chunks are HSDS-native F1 objects (Blosc1 frame, zlib inner codec, typesize 1,
 4 x 256 KiB zlib streams per chunk) produced by the oracle's c-blosc 1.21
@@ -920,9 +925,60 @@ def cpu_baseline_bshuf(blobs, seconds, threads):
     return done * CHUNK_BYTES / el / 1e9, done
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, dry_run=False):
+    """Start one bench.py rank per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in each
+    child's environment), forward their output, return the worst exit status.  The parent
+    never initialises the GPU (device_count() does not, on this image)."""
+    import subprocess
+    if not dry_run:
+        import torch
+        have = torch.cuda.device_count()
+        if n > have:
+            print(f"bench.py: --gpus {n} but {have} visible GPU(s)", file=sys.stderr, flush=True)
+            return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def dry_run_rank(args):
+    """--dry-run: the rank layout alone over gloo (CPU tests): one JSON line from rank 0
+    with the world the collective backend sees."""
+    import datetime
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
+        t = __import__("torch").tensor([rank])
+        dist.all_reduce(t)
+        seen = dist.get_world_size()
+        assert int(t) == world * (world - 1) // 2
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "rccl_world": seen, "gpus_arg": args.gpus}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", type=int, default=0, help="1: rank layout only, gloo, no GPU (CPU tests)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chunks", type=int, default=4096)
@@ -950,6 +1006,15 @@ def main():
     ap.add_argument("--headline", type=int, default=1,
                     help="0: skip the configs[1] headline and print only the selected legs (profiling passes)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], dry_run=bool(args.dry_run)))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry_run:
+        dry_run_rank(args)
+        return
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -990,6 +1055,7 @@ def main():
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
+        "rccl_world": torch.distributed.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),

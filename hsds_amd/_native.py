@@ -154,8 +154,13 @@ class Engine:
         except Exception:
             pass
 
-    def set_tuning(self, seg_over16=1, warmup_bits=384, rounds=4):
-        rc = lib().hsds_set_tuning(self.h, seg_over16, warmup_bits, 0, rounds)
+    def set_tuning(self, seg_over16=None, warmup_bits=None, rounds=None):
+        """Inflate tuning; a setting left at None keeps the engine's current value
+        (hsds_engine_create's defaults: the GPU-swept ones)."""
+        keep = 0xFFFFFFFF
+        rc = lib().hsds_set_tuning(self.h, keep if seg_over16 is None else seg_over16,
+                                   keep if warmup_bits is None else warmup_bits, 0,
+                                   -1 if rounds is None else rounds)
         if rc != OK:
             raise NativeError(rc, "hsds_set_tuning")
 

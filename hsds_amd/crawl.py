@@ -557,6 +557,10 @@ class ShardedWriter:
     def __init__(self, plan, rank, store, root=0, group=None):
         import torch
         from .engine import ChunkEngine
+        dt = np.dtype(plan.dtype)
+        if dt.names or dt.subdtype is not None:
+            raise NotImplementedError("ShardedWriter takes scalar dtypes (ChunkStore.put_pieces); "
+                                      "write compound datasets with ChunkStore.put_selections")
         self.plan, self.rank, self.store, self.root, self.group = plan, rank, store, root, group
         self.device = store.cache.arena.buf.device
         self.eng = ChunkEngine(self.device.index)

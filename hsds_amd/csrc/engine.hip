@@ -95,9 +95,21 @@ __device__ __forceinline__ hz2::Perm item_perm(const Item& it) {
 // (storUtil.py:182-235).  The walk runs twice: once to count the chunk's items, then -- after
 // one atomic allocation from the batch's item pool -- to write them, so a chunk may have any
 // number of Blosc splits (pool capacity: 8 per chunk + 1 per 2 KiB of destination).
+// A batch whose items exceed the pool fails only the chunks that do not fit (pool_reserve).
 // zlib streams and raw spans carry their unshuffle map (item_perm); LZ / zstd splits of a
 // shuffled frame are staged in tmp and unshuffled by unshuffle_kernel.
 // -------------------------------------------------------------------------
+// reserve n consecutive pool slots without ever moving the fill count past cap
+__device__ __forceinline__ int pool_reserve(uint32_t* ctr, uint32_t n, uint32_t cap, uint32_t* base) {
+  uint32_t cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (n > cap || cur > cap - n) return 0;
+    const uint32_t prev = atomicCAS(ctr, cur, cur + n);
+    if (prev == cur) { *base = cur; return 1; }
+    cur = prev;
+  }
+}
+
 __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hsds_chunk_desc* __restrict__ chunks,
                                   int64_t nchunks, uint8_t* dst_base, uint8_t* tmp_base, Item* __restrict__ pool,
                                   uint32_t pool_cap, uint32_t* __restrict__ pool_ctr, ChunkMeta* __restrict__ meta,
@@ -105,8 +117,8 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
                                   uint32_t* __restrict__ kind_counts, int32_t* __restrict__ status,
                                   int compressor, int shuffle, int itemsize, int inexact) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ci >= nchunks) return;
-  const hsds_chunk_desc c = chunks[ci];
+  const bool valid = ci < nchunks;      // every lane stays for the wave-wide pool reservation
+  const hsds_chunk_desc c = chunks[valid ? ci : 0];
   const uint8_t* s = src_base + c.src_off;
   const uint64_t L = c.src_len, n = c.dst_len;
   uint8_t* out = dst_base + c.dst_off;
@@ -115,7 +127,7 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
   uint32_t cnt = 0, base = 0, nlz = 0, nzs = 0;
   Item* slot = nullptr;
   ChunkMeta m = {0, (uint64_t)out, 0, 0, 0, (uint32_t)n};
-  for (int pass = 0; pass < 2; pass++) {
+  auto walk = [&](int pass) {
     cnt = 0; nlz = 0; nzs = 0;
     m.mode = 0;
     auto emit = [&](uint32_t kind, const uint8_t* sp, uint64_t sl, uint8_t* dp, uint64_t dl) {
@@ -201,13 +213,39 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
     } else {
       st = HSDS_ERR_UNSUPPORTED;
     }
-    if (st != HSDS_OK) { cnt = 0; m.mode = 0; break; }
-    if (pass == 0) {
-      if (cnt == 0) break;
-      base = atomicAdd(pool_ctr, cnt);
-      if (base + cnt > pool_cap || base + cnt < base) { st = HSDS_ERR_UNSUPPORTED; cnt = 0; m.mode = 0; break; }
-      slot = pool + base;
+    if (st != HSDS_OK) { cnt = 0; m.mode = 0; }
+  };
+  if (valid) walk(0);
+  // pool reservation, wave-wide: one compare-and-swap for the wave's items, so the fill
+  // count never passes pool_cap.  If they do not fit, the wave's chunks reserve one at a
+  // time: an oversized chunk fails alone (HSDS_ERR_UNSUPPORTED) and its neighbours keep
+  // their slots; no consumer ever sees a slot that was not written.
+  {
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t want = (valid && st == HSDS_OK) ? cnt : 0u;
+    const uint32_t off = hz::wave_excl_scan(want, lane);
+    const uint32_t tot = hz::wave_sum(want);
+    if (tot) {
+      uint32_t wb = 0;
+      int ok = 0;
+      if (lane == 0) ok = pool_reserve(pool_ctr, tot, pool_cap, &wb);
+      ok = __shfl(ok, 0, 64);
+      wb = (uint32_t)__shfl((int)wb, 0, 64);
+      if (ok) {
+        base = wb + off;
+      } else {
+        for (int l = 0; l < 64; l++) {
+          if (lane == l && want) {
+            if (!pool_reserve(pool_ctr, want, pool_cap, &base)) { st = HSDS_ERR_UNSUPPORTED; cnt = 0; m.mode = 0; }
+          }
+        }
+      }
     }
+  }
+  if (!valid) return;
+  if (st == HSDS_OK && cnt) {
+    slot = pool + base;
+    walk(1);
   }
   // items per decoder (kind_counts[0]: LZ splits for lz_kernel, [1]: zlib + raw for
   // inflate2_kernel, [2]: zstd), so that a kernel with nothing to do exits at once
@@ -1229,8 +1267,8 @@ __global__ void bs_plan_kernel(const hsds_chunk_desc* __restrict__ chunks, int64
                                EncGeom* __restrict__ geom, int32_t* __restrict__ status, uint32_t es,
                                uint32_t block, uint64_t src_extent) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ci >= nchunks) return;
-  const hsds_chunk_desc c = chunks[ci];
+  const bool valid = ci < nchunks;      // every lane stays for the wave-wide pool reservation
+  const hsds_chunk_desc c = chunks[valid ? ci : 0];
   const uint64_t n = c.src_len;
   const uint32_t bsz = block ? block : bs::default_block(es);
   EncGeom g = {n, bsz, 0, 0, es, 0};
@@ -1560,10 +1598,13 @@ void hsds_engine_destroy(hsds_engine* e) {
 int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t unused, int32_t rounds) {
   (void)unused;
   if (!e) return HSDS_ERR_ARG;
-  if (seg_over16 > 16u || warmup_bits > 4096u || rounds < 0 || rounds > 64) return HSDS_ERR_ARG;
-  e->tune.over16 = seg_over16;
-  e->tune.W = warmup_bits;
-  e->tune.max_rounds = rounds;
+  // HSDS_TUNE_KEEP (0xffffffff; -1 for rounds) leaves a setting as it is
+  if ((seg_over16 > 16u && seg_over16 != HSDS_TUNE_KEEP) || (warmup_bits > 4096u && warmup_bits != HSDS_TUNE_KEEP) ||
+      rounds < -1 || rounds > 64)
+    return HSDS_ERR_ARG;
+  if (seg_over16 != HSDS_TUNE_KEEP) e->tune.over16 = seg_over16;
+  if (warmup_bits != HSDS_TUNE_KEEP) e->tune.W = warmup_bits;
+  if (rounds >= 0) e->tune.max_rounds = rounds;
   return HSDS_OK;
 }
 
@@ -1592,8 +1633,9 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
     e->ev_valid = 1;
     return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
   }
-  // workspace: the item pool (8 per chunk + 1 per 2 KiB of destination: any c-blosc frame
-  // fits, whatever its number of splits), chunk meta and the unshuffle list
+  // workspace: the item pool (8 per chunk + 1 per 2 KiB of destination: HSDS's frames fit
+  // many times over; a frame with more splits -- tiny blocks of a wide type -- fails alone,
+  // frame_walk_kernel's pool_reserve), chunk meta and the unshuffle list
   const uint64_t cap64 = (uint64_t)nchunks * 8u + dst_extent / 2048u + 64u;
   const uint32_t pool_cap = cap64 > 0xffffffffull ? 0xffffffffu : (uint32_t)cap64;
   const size_t sz_pool = ((size_t)pool_cap * sizeof(Item) + 255) & ~(size_t)255;

@@ -733,6 +733,8 @@ class ChunkStore:
                 elif isinstance(v, HTTPNotFound):
                     v = None                               # 404: no chunk
                 out[r.chunk_id] = v
+            for key in init:
+                self.cache.unpin(key)
         return [out[r.chunk_id] for r in reads]
 
     def _fill_new(self, keys, dtype, chunk_dims, fill_value):
@@ -754,8 +756,12 @@ class ChunkStore:
         d_pat = torch.from_numpy(np.ascontiguousarray(pat).copy()).to(abase.device)
         recs = np.zeros(len(keys), COPY_DESC_DTYPE)
         for k, key in enumerate(keys):
-            slot = self.cache.reserve(key, chunk_dims, dtype)
+            # pinned: a later reserve of this batch must not evict an earlier fill slot
+            # (get_chunks unpins them once it has read them back)
+            slot = self.cache.reserve(key, chunk_dims, dtype, pin=True)
             if slot is None:
+                for kk in keys[:k]:
+                    self.cache.unpin(kk)
                 raise MemoryError("chunk cache full of dirty chunks")
             recs[k]["dst_off"] = slot.data_ptr() - abase.data_ptr()
         recs["src_off"] = 0
@@ -846,6 +852,12 @@ class ChunkStore:
         import torch
         from .selection import _kind
         dtype = np.dtype(dtype)
+        if dtype.names or dtype.subdtype is not None:
+            # the whole-element compare below has one kind per dtype; compound / subarray
+            # elements compare leaf by leaf (NaN fields, -0.0) in put_selections
+            # (write_selection_descs), which the sharded path does not build
+            raise NotImplementedError("put_pieces (the sharded write path) takes scalar dtypes; "
+                                      "compound datasets go through put_selections")
         chunk_dims = tuple(int(c) for c in chunk_dims)
         if len({r.chunk_id for r in reads}) != len(reads):
             raise ValueError("put_pieces takes each chunk once")

@@ -99,3 +99,28 @@ def test_encode_many_split_chunks(dev, oracle_lib, cname):
     st2, outs = _gpu_decode(dev, frames, [len(d) for d in data], cname, 4)
     assert (st2 == 0).all(), st2
     assert all(o == d for o, d in zip(outs, data))
+
+
+def test_pool_overflow_fails_only_that_chunk(dev, oracle_lib):
+    """a legal frame with more splits than the batch's item pool holds (typesize 16, 2 KiB
+    blocks: 16 splits per block, 8192 items for 1 MiB) fails alone with HSDS_ERR_UNSUPPORTED;
+    the chunks before and after it in the same batch decode byte-exact (the pool
+    fill count never passes its capacity, no consumer reads an unwritten slot)"""
+    orc = oracle_lib
+    good = [smooth(20 + i, 1 << 20) for i in range(5)]
+    bad = smooth(30, 1 << 20)
+    bad_frame = orc.blosc_encode_lz4(bad, typesize=16, blocksize=2048, shuffle=1)
+    assert nsplits(bad_frame) == 8192
+    assert orc.blosc_decode(bad_frame, len(bad)) == bad          # a valid c-blosc frame
+    frames = [orc.blosc_encode_lz4(d, typesize=4, blocksize=65536, shuffle=1) for d in good]
+    order = [frames[0], frames[1], bad_frame, frames[2], frames[3], frames[4]]
+    data = [good[0], good[1], bad, good[2], good[3], good[4]]
+    st, outs = _gpu_decode(dev, order, [len(d) for d in data], "lz4", 4)
+    assert st[2] == -5, st          # HSDS_ERR_UNSUPPORTED
+    for i in (0, 1, 3, 4, 5):
+        assert st[i] == 0, st
+        assert outs[i] == data[i]
+    # the same engine decodes a normal batch afterwards (no stale items left behind)
+    st, outs = _gpu_decode(dev, frames, [len(d) for d in good], "lz4", 4)
+    assert (st == 0).all(), st
+    assert outs == good
