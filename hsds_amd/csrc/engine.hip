@@ -42,6 +42,7 @@
 #include "zstd_wave.h"
 #include "bshuf.h"
 #include "zstd_enc.h"
+#include "region.h"
 
 #ifndef HZ_ZSTD_WPE
 #define HZ_ZSTD_WPE 3      // zstd_kernel waves per SIMD the compiler must allow (VGPR budget)
@@ -584,79 +585,73 @@ __global__ void shuffle_kernel(const uint8_t* __restrict__ in, uint8_t* __restri
 }
 
 // -------------------------------------------------------------------------
-// strided region copy / compare (numpy basic slicing)
+// strided region copy / compare (numpy basic slicing: chunkUtil.py:882-995,
+// chunk_crawl.py:118-150,395-418), as streaming kernels
+//
+// A record is first normalised (nreg_make): dims of count 1 dropped, an innermost dim
+// that is contiguous on both sides folded into bytes, and outer dims that continue their
+// inner neighbour on both sides merged into it -- a 512 x 2048-byte chunk piece of a slab
+// row becomes 512 rows of one 2048-byte run, a whole contiguous chunk one run.  The work
+// unit is a ROW (all dims but the innermost); a wave takes a group of rows, its lanes split
+// evenly between them (lanes per row = the power of two covering the row's units), and a
+// row's offsets come from one 32-bit mixed-radix unravel per row, not per element.
+//  - contiguous runs: 16-byte slots of the DESTINATION, every full slot one 16-byte store;
+//    its source by one 16-byte load (same alignment), four dword loads (alignment equal
+//    mod 4) or five dword loads and byte funnel shifts; only a run's first and last slot
+//    move bytes singly.  Four slots per lane are in flight before the first store.
+//  - strided elements with a contiguous destination (the chunk -> packed piece gathers of
+//    a stepped selection): a lane gathers the 16 / itemsize elements of one destination
+//    slot and stores them as one 16-byte store.
+//  - anything else: one element per lane, typed loads / stores when aligned.
 // -------------------------------------------------------------------------
-struct RegionIter {
-  int rank;
-  int64_t count[HSDS_MAX_RANK];
-};
-
-__device__ __forceinline__ void region_offsets(const hsds_copy_desc& d, int64_t e, int64_t& so, int64_t& doff) {
-  so = (int64_t)d.src_off;
-  doff = (int64_t)d.dst_off;
-  for (int k = d.rank - 1; k >= 0; k--) {
-    const int64_t c = d.count[k];
-    const int64_t i = e % c;
-    e /= c;
-    so += i * d.src_stride[k];
-    doff += i * d.dst_stride[k];
-  }
-}
-
-__device__ __forceinline__ void copy_elem(const uint8_t* s, uint8_t* d, int itemsize) {
-  if (itemsize == 16 && !(((uintptr_t)s | (uintptr_t)d) & 15)) { *(uint4*)d = *(const uint4*)s; return; }
-  if (itemsize == 4 && !(((uintptr_t)s | (uintptr_t)d) & 3)) { *(uint32_t*)d = *(const uint32_t*)s; return; }
-  if (itemsize == 8 && !(((uintptr_t)s | (uintptr_t)d) & 7)) { *(uint64_t*)d = *(const uint64_t*)s; return; }
-  if (itemsize == 2 && !(((uintptr_t)s | (uintptr_t)d) & 1)) { *(uint16_t*)d = *(const uint16_t*)s; return; }
-  for (int b = 0; b < itemsize; b++) d[b] = s[b];
-}
-
-__global__ void copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                            const hsds_copy_desc* __restrict__ descs, int64_t n,
-                            const int32_t* __restrict__ flags) {
+// grid: x splits a record's row groups, y walks the records; 4 waves per block.  The
+// normalised record lives in LDS (its dims are indexed at run time).
+__global__ void __launch_bounds__(256) copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   const hsds_copy_desc* __restrict__ descs, int64_t n,
+                                                   const int32_t* __restrict__ flags) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * 4u;
+  __shared__ rg::NReg sr;
+  __shared__ int sok;
   for (int64_t di = blockIdx.y; di < n; di += gridDim.y) {
     if (flags && !flags[di]) continue;
-    const hsds_copy_desc d = descs[di];
-    int64_t total = 1;
-    for (int k = 0; k < d.rank; k++) total *= d.count[k];
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-      int64_t so, doff;
-      region_offsets(d, e, so, doff);
-      copy_elem(src + so, dst + doff, d.itemsize);
+    if (threadIdx.x == 0) sok = rg::nreg_make(descs[di], 1, sr);
+    __syncthreads();
+    if (sok) {
+      const rg::Plan p = rg::plan_copy(sr);
+      for (uint64_t g = wave; g < p.ngroups; g += nwaves) rg::copy_group(src, dst, sr, p, g, lane);
     }
+    __syncthreads();
   }
 }
 
-__device__ __forceinline__ int elem_differs(const uint8_t* a, const uint8_t* b, int itemsize, int kind) {
-  switch (kind) {
-    case HSDS_KIND_F32: { float x, y; memcpy(&x, a, 4); memcpy(&y, b, 4); return !(x == y); }
-    case HSDS_KIND_F64: { double x, y; memcpy(&x, a, 8); memcpy(&y, b, 8); return !(x == y); }
-    case HSDS_KIND_F16: { _Float16 x, y; memcpy(&x, a, 2); memcpy(&y, b, 2); return !(x == y); }
-    case HSDS_KIND_C64: { float x[2], y[2]; memcpy(x, a, 8); memcpy(y, b, 8); return !(x[0] == y[0] && x[1] == y[1]); }
-    case HSDS_KIND_C128: { double x[2], y[2]; memcpy(x, a, 16); memcpy(y, b, 16); return !(x[0] == y[0] && x[1] == y[1]); }
-    default: {
-      for (int k = 0; k < itemsize; k++) if (a[k] != b[k]) return 1;
-      return 0;
-    }
-  }
-}
-
-// d_b: new data (desc.src_*), d_a: chunk (desc.dst_*)
-__global__ void compare_kernel(const uint8_t* __restrict__ b, const uint8_t* __restrict__ a,
-                               const hsds_copy_desc* __restrict__ descs, int64_t n, int kind,
-                               int32_t* __restrict__ differs) {
+// d_b: new data (desc.src_*), d_a: chunk (desc.dst_*).  Bytewise kinds compare 16-byte
+// pieces of contiguous runs, float kinds element by element; a wave stops at the first
+// difference it sees, every wave once its record is marked.
+__global__ void __launch_bounds__(256) compare_kernel(const uint8_t* __restrict__ b, const uint8_t* __restrict__ a,
+                                                      const hsds_copy_desc* __restrict__ descs, int64_t n, int kind,
+                                                      int32_t* __restrict__ differs) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * 4u;
+  __shared__ rg::NReg sr;
+  __shared__ int sok;
   for (int64_t di = blockIdx.y; di < n; di += gridDim.y) {
-    const hsds_copy_desc d = descs[di];
-    int64_t total = 1;
-    for (int k = 0; k < d.rank; k++) total *= d.count[k];
-    int found = 0;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total && !found;
-         e += (int64_t)gridDim.x * blockDim.x) {
-      int64_t so, doff;
-      region_offsets(d, e, so, doff);
-      found = elem_differs(a + doff, b + so, d.itemsize, kind);
+    if (threadIdx.x == 0) sok = rg::nreg_make(descs[di], kind == HSDS_KIND_BYTES, sr);
+    __syncthreads();
+    if (sok) {
+      const rg::Plan p = rg::plan_compare(sr);
+      for (uint64_t g = wave; g < p.ngroups; g += nwaves) {
+        if (__hip_atomic_load(&differs[di], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        const int found = rg::compare_group(b, a, sr, p, g, lane, kind);
+        if (__any(found)) {
+          if (lane == 0) atomicOr(&differs[di], 1);
+          break;
+        }
+      }
     }
-    if (__any(found) && (threadIdx.x & 63) == 0) atomicOr(&differs[di], 1);
+    __syncthreads();
   }
 }
 
@@ -1267,8 +1262,8 @@ __global__ void bs_plan_kernel(const hsds_chunk_desc* __restrict__ chunks, int64
                                EncGeom* __restrict__ geom, int32_t* __restrict__ status, uint32_t es,
                                uint32_t block, uint64_t src_extent) {
   const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = ci < nchunks;      // every lane stays for the wave-wide pool reservation
-  const hsds_chunk_desc c = chunks[valid ? ci : 0];
+  if (ci >= nchunks) return;
+  const hsds_chunk_desc c = chunks[ci];
   const uint64_t n = c.src_len;
   const uint32_t bsz = block ? block : bs::default_block(es);
   EncGeom g = {n, bsz, 0, 0, es, 0};
@@ -1823,12 +1818,19 @@ int hsds_unshuffle(hsds_engine* e, const void* src, int64_t n, int itemsize, voi
   return host_shuffle(e, src, n, itemsize, dst, 1);
 }
 
+// blocks per record: enough blocks in all (~4096: 16 per CU) whatever the record count
+static unsigned copy_gx(int64_t n) {
+  const int64_t y = n < 65535 ? n : 65535;
+  int64_t x = 4096 / (y > 0 ? y : 1);
+  return (unsigned)(x < 1 ? 1 : x > 2048 ? 2048 : x);
+}
+
 static int launch_copy(const void* d_src, void* d_dst, const hsds_copy_desc* d_desc, int64_t n, const int32_t* flags,
                        void* stream) {
   if (n < 0 || (n && (!d_src || !d_dst || !d_desc))) return HSDS_ERR_ARG;
   if (n == 0) return HSDS_OK;
   const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
-  hipLaunchKernelGGL(copy_kernel, dim3(8, gy), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d_src,
+  hipLaunchKernelGGL(copy_kernel, dim3(copy_gx(n), gy), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d_src,
                      (uint8_t*)d_dst, d_desc, n, flags);
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
 }
@@ -1852,7 +1854,7 @@ int hsds_compare_batch(hsds_engine* e, const void* d_b, const void* d_a, const h
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(zero_i32_kernel, dim3(64), dim3(256), 0, st, d_differs, n);
   const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
-  hipLaunchKernelGGL(compare_kernel, dim3(8, gy), dim3(256), 0, st, (const uint8_t*)d_b, (const uint8_t*)d_a,
+  hipLaunchKernelGGL(compare_kernel, dim3(copy_gx(n), gy), dim3(256), 0, st, (const uint8_t*)d_b, (const uint8_t*)d_a,
                      d_desc, n, kind, d_differs);
   return hipGetLastError() == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
 }

@@ -247,6 +247,17 @@ HZ_HD void g_quad(const Src& s, uint32_t qa, uint32_t& a0, uint32_t& a1, uint32_
 #endif
 }
 
+// vmcnt(0) as an instruction the compiler's wait pass sees: the rare refill paths below
+// drain their load INSIDE their branch, so no register of the common path is left
+// "possibly pending" at the merge (a pending register there makes the compiler put an
+// s_waitcnt vmcnt(0) on the common path -- one full memory latency per token for the wave,
+// waiting on the epoch prefetch as well)
+#if HZ_GPU && !defined(HZ2_NOVMWAIT)
+#define HZ2_VMWAIT() __builtin_amdgcn_s_waitcnt(0x0F70)
+#else
+#define HZ2_VMWAIT() do { } while (0)
+#endif
+
 #if HZ2_EPOCH
 HZ_HD uint32_t g_take(const Src& s, GRd& r) {
   const uint32_t w = r.q0;
@@ -257,10 +268,12 @@ HZ_HD uint32_t g_take(const Src& s, GRd& r) {
       r.q0 = r.f0; r.q1 = r.f1; r.q2 = r.f2; r.q3 = r.f3;
       r.fh &= ~1u;
     } else if (r.fh & 2u) {
+      HZ2_VMWAIT();
       r.q0 = r.h0; r.q1 = r.h1; r.q2 = r.h2; r.q3 = r.h3;
       r.fh &= ~2u;
     } else {
       g_quad(s, r.qa, r.q0, r.q1, r.q2, r.q3);
+      HZ2_VMWAIT();
       r.qa += 4u;
     }
     r.qn = 4u;
