@@ -574,7 +574,16 @@ def run_cfg5(args, dev, rank=0):
     ref0 = sum(len(orc.blosc_encode(chunks[k * cbytes:(k + 1) * cbytes].cpu().numpy(), typesize=1, clevel=4,
                                     shuffle=1)) for k in k0)
     ours0 = sum(int(hs[k]) for k in k0)
+    # the slab -> chunk scatter alone (copy_kernel), HIP events on the launch stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(5):
+        eng.copy(slab_u8, chunks, d_cd, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    scat_ms = e0.elapsed_time(e1) / 5
     out = {"value": round(slab_bytes / el / 1e9, 2), "unit": "GB/s slab (scatter + encode)",
+           "scatter_ms": round(scat_ms, 3), "scatter_GBps": round(2 * slab_bytes / (scat_ms / 1e3) / 1e9, 1),
            "ms_per_step": round(el * 1e3, 3), "chunks": n, "slab_bytes": slab_bytes, "compressed_bytes": comp,
            "algorithmic_GBps": round((slab_bytes + comp) / el / 1e9, 2),
            "deflate_kernel_ms": round(kern[-1], 3),
@@ -888,6 +897,41 @@ def cpu_model():
     return "unknown"
 
 
+def copy_ceiling(dev, nbytes=2 << 30, reps=5):
+    """Measured HIP streaming-copy ceilings (BASELINE 4): a device-to-device
+    hipMemcpyAsync (torch copy_) and the engine's copy_kernel on one contiguous record of
+    the same bytes; GB/s of read + write bytes, HIP events on the launch stream."""
+    import torch
+    from hsds_amd.engine import ChunkEngine, COPY_DESC_DTYPE, to_device_bytes
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(7)
+    rec = np.zeros(1, COPY_DESC_DTYPE)
+    rec["rank"], rec["itemsize"] = 1, 16
+    rec["count"][0, 0] = nbytes // 16
+    rec["src_stride"][0, 0] = rec["dst_stride"][0, 0] = 16
+    d_rec = to_device_bytes(rec, dev)
+    eng = ChunkEngine(dev.index)
+    stream = torch.cuda.current_stream()
+    out = {}
+    for name, fn in (("hipMemcpy_d2d", lambda: b.copy_(a)),
+                     ("copy_kernel", lambda: eng.copy(a, b, d_rec, stream=stream))):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[name] = round(2 * nbytes / (ms / 1e3) / 1e9, 1)
+    assert bool((b[:4096] == 7).all())
+    del a, b
+    torch.cuda.empty_cache()
+    return out
+
+
 def calibration():
     p = os.path.join(ROOT, "profiles", "r2_cpu_calibration.json")
     return json.load(open(p)) if os.path.exists(p) else None
@@ -986,6 +1030,7 @@ def main():
     ap.add_argument("--f2", type=int, default=1, help="also measure F2 (HDF5 zlib+shuffle) chunks")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-timing", type=int, default=0)
+    ap.add_argument("--copy-ceiling", type=int, default=1, help="measure the HIP streaming-copy ceiling (2 GiB)")
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     ap.add_argument("--lz4", type=int, default=1, help="also measure Blosc-lz4 1 MiB chunks (N=1)")
@@ -1074,6 +1119,10 @@ def main():
                      "kernel": "inflate2_kernel", "kernel_ms": round(r1["kernel_ms"], 3),
                      "bytes_per_launch": launch_bytes},
     }
+    if args.copy_ceiling:
+        cc = copy_ceiling(dev)
+        out["roofline"]["copy_ceiling_GBps"] = max(cc.values())
+        out["roofline"]["copy_ceiling"] = cc
     tr = load_traffic(args, world)
     if tr is not None:
         out["roofline"]["traffic"] = tr["bytes_per_launch"]

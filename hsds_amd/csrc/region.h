@@ -120,13 +120,39 @@ RG_HD uint32_t pow2_at_least(uint32_t v) { return v <= 1u ? 1u : 1u << (32 - __b
 
 // how a region's rows are cut: units per row (destination slots or elements), lanes per
 // row (a power of two), rows per wave group
+// (a row longer than UPIECE units is cut into pieces, one wave group each, so one long
+// contiguous run still spreads over the whole grid)
+constexpr uint32_t UPIECE = 4096;
 struct Plan {
   uint32_t C, lpr, rpw;
   int64_t iss, ids;
   int isz;
   int run, gather;
+  uint32_t pieces;     // wave groups per row (1 unless the row is longer than UPIECE units)
   uint64_t ngroups;
 };
+
+RG_HD void plan_groups(const NReg& n, uint32_t units, Plan& p) {
+  p.lpr = units >= 64u ? 64u : pow2_at_least(units);
+  p.rpw = 64u / p.lpr;
+  p.pieces = units > UPIECE ? (units + UPIECE - 1u) / UPIECE : 1u;
+  p.ngroups = p.pieces > 1u ? n.nrows * p.pieces : (n.nrows + p.rpw - 1u) / p.rpw;
+}
+
+// row q and the unit range [u0, u1) of group g for this lane's row slot
+RG_HD bool group_row(const NReg& n, const Plan& p, uint64_t g, uint32_t rsub, uint64_t& q, uint32_t& u0, uint32_t& u1) {
+  if (p.pieces > 1u) {
+    q = g / p.pieces;
+    const uint32_t k = (uint32_t)(g - q * p.pieces);
+    u0 = k * UPIECE;
+    u1 = u0 + UPIECE;
+  } else {
+    q = g * p.rpw + rsub;
+    u0 = 0u;
+    u1 = 0xffffffffu;
+  }
+  return q < n.nrows;
+}
 
 RG_HD Plan plan_copy(const NReg& n) {
   Plan p;
@@ -137,9 +163,7 @@ RG_HD Plan plan_copy(const NReg& n) {
   p.run = p.isz == 1 && p.iss == 1 && p.ids == 1;
   p.gather = !p.run && p.ids == p.isz && (p.isz == 1 || p.isz == 2 || p.isz == 4 || p.isz == 8);
   const uint32_t units = p.run ? (p.C + 30u) / 16u : p.gather ? (p.C * (uint32_t)p.isz + 30u) / 16u : p.C;
-  p.lpr = units >= 64u ? 64u : pow2_at_least(units);
-  p.rpw = 64u / p.lpr;
-  p.ngroups = (n.nrows + p.rpw - 1u) / p.rpw;
+  plan_groups(n, units, p);
   return p;
 }
 
@@ -178,8 +202,9 @@ RG_HD uint64_t load_elem(const uint8_t* p, int isz) {
 // lane `lane` of the wave that copies row group g of region n
 RG_HD void copy_group(const uint8_t* src, uint8_t* dst, const NReg& n, const Plan& p, uint64_t g, uint32_t lane) {
   const uint32_t sub = lane & (p.lpr - 1u), rsub = lane / p.lpr;
-  const uint64_t q = g * p.rpw + rsub;
-  if (q >= n.nrows) return;
+  uint64_t q;
+  uint32_t u0, u1;
+  if (!group_row(n, p, g, rsub, q, u0, u1)) return;
   int64_t so, doff;
   nreg_row(n, q, so, doff);
   const uint8_t* s = src + so;
@@ -189,9 +214,10 @@ RG_HD void copy_group(const uint8_t* src, uint8_t* dst, const NReg& n, const Pla
     const uint32_t bytes = p.run ? p.C : p.C * (uint32_t)isz;
     const uintptr_t d0 = (uintptr_t)d, dend = d0 + bytes;
     const uintptr_t x00 = d0 & ~(uintptr_t)15;
-    const uint32_t nslots = (uint32_t)((dend - x00 + 15u) >> 4);
+    const uint32_t nall = (uint32_t)((dend - x00 + 15u) >> 4);
+    const uint32_t nslots = nall < u1 ? nall : u1;
     const bool ealign = p.run || !(d0 & (uintptr_t)(isz - 1));
-    for (uint32_t j0 = sub; j0 < nslots; j0 += 4u * p.lpr) {
+    for (uint32_t j0 = u0 + sub; j0 < nslots; j0 += 4u * p.lpr) {
       rg_v4 v[4];
       uint32_t full = 0;
       for (uint32_t u = 0; u < 4u; u++) {
@@ -236,7 +262,8 @@ RG_HD void copy_group(const uint8_t* src, uint8_t* dst, const NReg& n, const Pla
       }
     }
   } else {
-    for (uint32_t e = sub; e < p.C; e += p.lpr) copy_elem(s + (int64_t)e * p.iss, d + (int64_t)e * p.ids, isz);
+    const uint32_t e1 = p.C < u1 ? p.C : u1;
+    for (uint32_t e = u0 + sub; e < e1; e += p.lpr) copy_elem(s + (int64_t)e * p.iss, d + (int64_t)e * p.ids, isz);
   }
 }
 
@@ -278,9 +305,7 @@ RG_HD Plan plan_compare(const NReg& n) {
   p.run = p.isz == 1 && p.iss == 1 && p.ids == 1;
   p.gather = 0;
   const uint32_t units = p.run ? (p.C + 15u) / 16u : p.C;
-  p.lpr = units >= 64u ? 64u : pow2_at_least(units);
-  p.rpw = 64u / p.lpr;
-  p.ngroups = (n.nrows + p.rpw - 1u) / p.rpw;
+  plan_groups(n, units, p);
   return p;
 }
 
@@ -289,16 +314,17 @@ RG_HD Plan plan_compare(const NReg& n) {
 RG_HD int compare_group(const uint8_t* b, const uint8_t* a, const NReg& n, const Plan& p, uint64_t g, uint32_t lane,
                         int kind) {
   const uint32_t sub = lane & (p.lpr - 1u), rsub = lane / p.lpr;
-  const uint64_t q = g * p.rpw + rsub;
-  if (q >= n.nrows) return 0;
+  uint64_t q;
+  uint32_t u0, u1;
+  if (!group_row(n, p, g, rsub, q, u0, u1)) return 0;
   int64_t so, doff;
   nreg_row(n, q, so, doff);
   const uint8_t* pb = b + so;
   const uint8_t* pa = a + doff;
   int found = 0;
   if (p.run) {
-    const uint32_t units = (p.C + 15u) / 16u;
-    for (uint32_t j = sub; j < units && !found; j += p.lpr) {
+    const uint32_t nall = (p.C + 15u) / 16u, units = nall < u1 ? nall : u1;
+    for (uint32_t j = u0 + sub; j < units && !found; j += p.lpr) {
       const uint32_t o = 16u * j, m = p.C - o < 16u ? p.C - o : 16u;
       if (m == 16u && !((((uintptr_t)(pa + o)) | (uintptr_t)(pb + o)) & 15u)) {
         const rg_v4 x = *(const rg_v4*)(pa + o), y = *(const rg_v4*)(pb + o);
@@ -308,7 +334,8 @@ RG_HD int compare_group(const uint8_t* b, const uint8_t* a, const NReg& n, const
       }
     }
   } else {
-    for (uint32_t e = sub; e < p.C && !found; e += p.lpr)
+    const uint32_t e1 = p.C < u1 ? p.C : u1;
+    for (uint32_t e = u0 + sub; e < e1 && !found; e += p.lpr)
       found = elem_differs(pa + (int64_t)e * p.ids, pb + (int64_t)e * p.iss, p.isz, kind);
   }
   return found;

@@ -104,3 +104,33 @@ def test_compare_single_difference(emu, isz, kind):
         an[pos:pos + 4] = np.array([-0.0], np.float32).view(np.uint8)
         b[pos:pos + 4] = np.array([0.0], np.float32).view(np.uint8)
         assert run(b, an)[0] == 0                    # -0.0 == 0.0
+
+
+@pytest.mark.parametrize("n,so,do,isz", [(3 << 20, 0, 0, 1), ((3 << 20) + 5, 3, 17, 1), (1 << 20, 8, 4, 4),
+                                          (200000, 2, 6, 2)])
+def test_long_rows_are_split(emu, n, so, do, isz):
+    """one long row (a whole contiguous chunk, a 3 MiB run) is cut into pieces; strided
+    long rows too"""
+    from hsds_amd.engine import COPY_DESC_DTYPE
+    rng = np.random.default_rng(n)
+    step = 1 if isz == 1 else 3
+    src = rng.integers(0, 256, so + n * isz * step + 64, dtype=np.uint8)
+    rec = np.zeros(1, COPY_DESC_DTYPE)
+    rec["src_off"], rec["dst_off"], rec["rank"], rec["itemsize"] = so, do, 1, isz
+    rec["count"][0, 0] = n
+    rec["src_stride"][0, 0] = isz * step
+    rec["dst_stride"][0, 0] = isz
+    dst0 = rng.integers(0, 256, do + n * isz + 64, dtype=np.uint8)
+    assert (_copy(emu, src, dst0, rec, nwaves=7) == _model(src, dst0, rec)).all()
+    # compare over the same long row: equal, then one byte changed near the end
+    rec2 = rec.copy()
+    rec2["src_stride"][0, 0] = isz
+    rec2["src_off"] = do
+    a = dst0.copy()
+    differs = np.zeros(1, np.int32)
+    emu.emu_compare(a.ctypes.data, a.ctypes.data, rec2.ctypes.data, 1, 0, differs.ctypes.data)
+    assert differs[0] == 0
+    b = a.copy()
+    b[do + n * isz - 2] ^= 1
+    emu.emu_compare(b.ctypes.data, a.ctypes.data, rec2.ctypes.data, 1, 0, differs.ctypes.data)
+    assert differs[0] == 1
