@@ -48,7 +48,7 @@ using hz::T_MATCH;
 using hz::ADLER_MOD;
 
 #ifndef HZ2_K
-#define HZ2_K 16
+#define HZ2_K 8
 #endif
 constexpr int K = HZ2_K;                  // recorded token starts per lane
 constexpr uint32_t LMIN = 64;
@@ -73,12 +73,12 @@ constexpr uint32_t RGP = HZ2_RGP;         // resolve (plain output): bytes a lan
 #endif
 constexpr uint32_t DW = HZ2_DW;           // resolve (plain output): dwords a lane loads before it stores
 #ifndef HZ2_OWIN
-#define HZ2_OWIN 32
+#define HZ2_OWIN 16
 #endif
 constexpr uint32_t OWIN = HZ2_OWIN;       // phase E (plain output): literal window bytes per lane (aligned,
                                           // written whole: partial cache lines cost an L2 fill + write-back)
-static_assert(OWIN == 32 || OWIN == 64, "OWIN: 32 or 64 bytes (the byte mask is 64 bits)");
-constexpr uint32_t OSH = OWIN == 32 ? 5u : 6u;
+static_assert(OWIN == 16 || OWIN == 32 || OWIN == 64, "OWIN: 16, 32 or 64 bytes (the byte mask is 64 bits)");
+constexpr uint32_t OSH = OWIN == 16 ? 4u : OWIN == 32 ? 5u : 6u;
 #if HZ2_OWIN == 64
 typedef uint64_t OMask;
 #else
@@ -88,10 +88,26 @@ typedef uint32_t OMask;
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
 // bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
 #ifndef HZ2_RGRP
-#define HZ2_RGRP 4
+#define HZ2_RGRP 2
 #endif
 constexpr uint32_t RGRP = HZ2_RGRP;
-static_assert(RGRP == 4 || RGRP == 8, "RGRP: 4 or 8 records");
+static_assert(RGRP == 2 || RGRP == 4 || RGRP == 8, "RGRP: 2, 4 or 8 records");
+// bit ring (phases A .. E): RS stream words per lane in LDS, refilled a quad at a time at
+// wave-uniform ticks; a token reads at most 48 bits, so a window advances at most 1.5
+// words per token
+#ifndef HZ2_RS
+#define HZ2_RS 12
+#endif
+constexpr uint32_t RS = HZ2_RS;           // ring words per lane (a multiple of 4)
+#ifndef HZ2_TICKN
+#define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 4)
+#endif
+constexpr uint32_t TICKN = HZ2_TICKN;     // tokens between ring refills
+static_assert(RS % 4 == 0 && RS >= 8, "RS: whole quads");
+// ring words a lane needs at a tick: TICKN tokens move the window at most
+// (31 + 48 (TICKN - 1)) / 32 words before the last one, which reads words c+3 and c+4
+constexpr uint32_t NEED = (31u + 48u * (TICKN - 1u)) / 32u + 5u;
+static_assert(NEED <= RS, "ring too small for TICKN");
 constexpr uint32_t SYNC_NONE = 0xfeu;     // predecessor ended (EOB / ERR / CUT): lane beyond the window
 constexpr uint32_t SYNC_FAIL = 0xffu;     // predecessor never met this lane's recorded path
 constexpr uint32_t END_NONE = 0, END_EOB = 1, END_ERR = 2, END_CUT = 3;
@@ -119,10 +135,16 @@ struct alignas(16) Shared {
       uint16_t sorted_cl[20];
       uint8_t lens[320 + 32];
     };
-    uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
-    struct {                      // phase E
-      alignas(16) uint8_t ostage[WAVE][OWIN];   // plain output: each lane's current literal window
-      uint64_t rstage[WAVE][RGRP];              // each lane's current group of match records
+    struct {                      // phases A .. E
+      uint32_t bring[RS + 1][WAVE];   // each lane's bit ring: stream word j in slot j % RS (word-major:
+                                      // lanes hit distinct banks); slot RS mirrors slot 0
+      union {
+        uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
+        struct {                      // phase E
+          alignas(16) uint8_t ostage[WAVE][OWIN];   // plain output: each lane's current literal window
+          uint64_t rstage[WAVE][RGRP];              // each lane's current group of match records
+        };
+      };
     };
     struct {                      // phase M
       uint16_t smap[SPAN];        // batch byte -> distance to its source (0: literal)
@@ -439,6 +461,148 @@ HZ_HD uint32_t next_token(const Shared* sh, const Src& s, GRd& r) {
   return tok;
 }
 
+// ---- the bit ring reader (phases A, A', R, E) --------------------------------------------
+// A lane's stream position is word c (of the 16-byte aligned base) plus sh bits.  The window
+// w0..w2 holds words c..c+2 (>= 64 bits past the position whatever sh is, so a whole token
+// -- at most 48 bits -- decodes from one window); n0 n1 are ring words c+3 c+4, read at the
+// start of every token so the advance (by 0, 1 or 2 words) is a few masked merges, no branch.
+// The ring holds words [wr - RS, wr).  It is refilled at wave-uniform ticks, every TICKN
+// tokens: the quads that fit are loaded and written at once, so no load is ever in flight
+// across a token (a load kept in flight in loop-carried registers makes the compiler copy
+// them, and wait for the load, on every token).
+struct BR {
+  uint32_t w0, w1, w2, sh, c;
+  uint32_t n0, n1;
+  uint32_t wr;
+};
+
+HZ_HD uint32_t br_pos(const BR& r) { return r.c * 32u + r.sh; }
+
+HZ_HD void br_put(Shared& sh, int lane, uint32_t j, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+  const uint32_t k = j % RS;                  // j % 4 == 0 and RS % 4 == 0: the quad never wraps
+  sh.bring[k][lane] = a0;
+  sh.bring[k + 1u][lane] = a1;
+  sh.bring[k + 2u][lane] = a2;
+  sh.bring[k + 3u][lane] = a3;
+  if (k == 0u) sh.bring[RS][lane] = a0;
+}
+
+// ring words c+3 and c+4 (slot (c+3) % RS and the next; the mirror covers the wrap)
+HZ_HD void br_next(const Shared& sh, int lane, BR& r) {
+  const uint32_t k = (r.c + 3u) % RS;
+  r.n0 = sh.bring[k][lane];
+  r.n1 = sh.bring[k + 1u][lane];
+}
+
+// refill: the quads that fit (their slots hold only words below c+3, i.e. wr <= c + RS - 1),
+// all loads issued before the first write.  Leaves wr in [c + RS, c + RS + 3]: every word a
+// token reads within the next TICKN tokens is in the ring (NEED <= RS).
+HZ_HD void br_fill(Shared& sh, int lane, const Src& S, BR& r) {
+  if (r.wr + 1u > r.c + RS) return;
+  const uint32_t nq = (r.c + RS + 3u - r.wr) >> 2;     // 1 .. 4
+  uint32_t a[16];
+  g_quad(S, r.wr, a[0], a[1], a[2], a[3]);
+  if (nq > 1u) g_quad(S, r.wr + 4u, a[4], a[5], a[6], a[7]);
+  if (nq > 2u) g_quad(S, r.wr + 8u, a[8], a[9], a[10], a[11]);
+  if (nq > 3u) g_quad(S, r.wr + 12u, a[12], a[13], a[14], a[15]);
+  br_put(sh, lane, r.wr, a[0], a[1], a[2], a[3]);
+  if (nq > 1u) br_put(sh, lane, r.wr + 4u, a[4], a[5], a[6], a[7]);
+  if (nq > 2u) br_put(sh, lane, r.wr + 8u, a[8], a[9], a[10], a[11]);
+  if (nq > 3u) br_put(sh, lane, r.wr + 12u, a[12], a[13], a[14], a[15]);
+  r.wr += 4u * nq;
+}
+
+// position p: the window (words c .. c+2) from two quad loads and a full ring (from quad q)
+HZ_HD void br_init(Shared& sh, int lane, const Src& S, BR& r, uint32_t p) {
+  const uint32_t c = p >> 5, q = c & ~3u, i = c - q;
+  uint32_t a[8];
+  g_quad(S, q, a[0], a[1], a[2], a[3]);
+  g_quad(S, q + 4u, a[4], a[5], a[6], a[7]);
+  // words c, c+1, c+2 = a[i], a[i+1], a[i+2] (selects: no dynamically indexed array)
+  r.w0 = i == 0u ? a[0] : i == 1u ? a[1] : i == 2u ? a[2] : a[3];
+  r.w1 = i == 0u ? a[1] : i == 1u ? a[2] : i == 2u ? a[3] : a[4];
+  r.w2 = i == 0u ? a[2] : i == 1u ? a[3] : i == 2u ? a[4] : a[5];
+  r.sh = p & 31u;
+  r.c = c;
+  br_put(sh, lane, q, a[0], a[1], a[2], a[3]);
+  br_put(sh, lane, q + 4u, a[4], a[5], a[6], a[7]);
+  r.wr = q + 8u;
+  br_fill(sh, lane, S, r);
+}
+
+HZ_HD void br_tick(Shared& sh, int lane, const Src& S, BR& r) { br_fill(sh, lane, S, r); }
+
+// advance by n <= 48 bits (n0 n1 must hold ring words c+3, c+4).  The window moves by
+// k = 0, 1 or 2 words as masked merges of SSA values: written as selects between fields of
+// the reader, the compiler turns them into an indexed load of the struct (a scratch copy)
+HZ_HD void br_adv(BR& r, uint32_t n) {
+  const uint32_t a0 = r.w0, a1 = r.w1, a2 = r.w2, a3 = r.n0, a4 = r.n1;
+  const uint32_t t = r.sh + n;
+  const uint32_t k = t >> 5;
+#if HZ_GPU
+  const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)(k + 1u), 1, 1);   // k >= 1: all ones
+  const uint32_t m2 = (uint32_t)__builtin_amdgcn_sbfe((int)k, 1, 1);          // k >= 2: all ones
+#else
+  const uint32_t m1 = k >= 1u ? ~0u : 0u, m2 = k >= 2u ? ~0u : 0u;
+#endif
+  r.w0 = a0 ^ ((a0 ^ a1) & m1) ^ ((a1 ^ a2) & m2);
+  r.w1 = a1 ^ ((a1 ^ a2) & m1) ^ ((a2 ^ a3) & m2);
+  r.w2 = a2 ^ ((a2 ^ a3) & m1) ^ ((a3 ^ a4) & m2);
+  r.sh = t & 31u;
+  r.c += k;
+}
+
+HZ_HD uint32_t bfe32(uint32_t v, uint32_t off, uint32_t w) {
+#if HZ_GPU
+  return __builtin_amdgcn_ubfe(v, off, w);
+#else
+  return w ? (uint32_t)((v >> off) & ((1ull << w) - 1u)) : 0u;
+#endif
+}
+
+HZ_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if HZ_GPU
+  return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (sh & 31u));
+#endif
+}
+
+enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_ERR = 3 };
+struct Tok {
+  uint32_t n;      // bits
+  uint32_t kind;   // TK_*
+  uint32_t len;    // output bytes (1 for a literal)
+  uint32_t v;      // literal byte, or the match distance
+};
+
+// one token at the reader's position, from the rich tables (hz::ent_rich): literal/length
+// symbol, its extra bits, the distance symbol and its extra bits all from the 64-bit window
+HZ_HD Tok rtok(const Shared* sh, const BR& r) {
+  const uint32_t lo = funnel(r.w1, r.w0, r.sh), hi = funnel(r.w2, r.w1, r.sh);
+  uint32_t e = sh->lut_ll[lo & ((1u << LL_ROOT) - 1u)];
+  if (!(e & 15u)) e = sh->lut_ll[(1u << LL_ROOT) + ((e >> 4) & 511u) + bfe32(lo, LL_ROOT, e >> 13)];
+  const uint32_t nb = e & 15u, x = (e >> 4) & 7u, v = e >> 7;
+  Tok t;
+  if (x == 7u) {                                // literal, EOB or an invalid code
+    t.n = nb;
+    t.kind = v < 256u ? TK_LIT : v == 256u ? TK_EOB : TK_ERR;
+    t.len = 1u;
+    t.v = v;
+    return t;
+  }
+  const uint32_t s1 = nb + x;
+  t.len = v + bfe32(lo, nb, x);
+  const uint32_t dl = funnel(hi, lo, s1);
+  uint32_t ed = sh->lut_d[dl & ((1u << D_ROOT) - 1u)];
+  if (!(ed & 15u)) ed = sh->lut_d[(1u << D_ROOT) + ((ed >> 4) & 511u) + bfe32(dl, D_ROOT, ed >> 13)];
+  const uint32_t nd = ed & 15u, xd = (ed >> 4) & 15u;
+  t.v = (((ed >> 8) & 7u) << xd) + ((ed >> 11) & 1u) + bfe32(dl, nd, xd);
+  t.kind = (ed >> 12) & 1u ? TK_ERR : TK_MATCH;
+  t.n = s1 + ((ed >> 12) & 1u ? nd : nd + xd);
+  return t;
+}
+
 // a[u] for a register array and a runtime u < MPL (no dynamic register indexing)
 HZ_HD uint32_t sel4(const uint32_t* a, uint32_t u) { return u == 0u ? a[0] : u == 1u ? a[1] : u == 2u ? a[2] : a[3]; }
 
@@ -484,6 +648,8 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
 #else
 #define HZ2_TICK(it) do { ++(it); } while (0)
 #endif
+// ring reader tick (r: the lane's hz2::BR)
+#define HZ2_RTICK(it) do { if ((HZ2_UNI(++(it)) % hz2::TICKN) == 0u) hz2::br_tick(sh, lane, S, r); } while (0)
 
 namespace hz2 {
 
@@ -663,10 +829,10 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
     HZ_T(2);
     {
       int bst = ST_OK;
-      hz::TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB};
+      hz::TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB, 1};
       HZ_BUILD_TABLE(sh, tll, bst);
       if (bst != ST_OK) return bst;
-      hz::TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB};
+      hz::TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB, 1};
       HZ_BUILD_TABLE(sh, td, bst);
       if (bst != ST_OK) return bst;
     }
@@ -691,7 +857,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
 
       HZ_T(3);
       // -------- phase A: warm-up + own segment, first K token starts recorded --------
-      LANE_VAR(GRd, rd);
+      LANE_VAR(BR, rd);
       LANE_VAR(uint32_t, co);      // output bytes since the first record
       LANE_VAR(uint32_t, cm);      // matches since the first record
       LANE_VAR(uint32_t, ek);      // END_*
@@ -699,24 +865,27 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       LANE_LOOP {
         const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
         const uint32_t p0 = (lane > 0 && ss - ws > W) ? ss - W : ws;
-        GRd r;
-        g_init(S, r, p0);
+        BR r;
+        br_init(sh, lane, S, r, p0);
         uint32_t steps = 0;
         uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0;
         // one loop for the warm-up (tokens before ss are decoded and dropped: whatever they
         // are, even invalid codes, which advance by their table length) and the segment
-        while (r.pos < se) {
-          const bool inseg = r.pos >= ss;
-          if (inseg && nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
-          const uint32_t tp = r.pos;
-          const uint32_t t = next_token(&sh, S, r);
+        for (;;) {
+          const uint32_t tp = br_pos(r);
+          if (tp >= se) break;
+          br_next(sh, lane, r);
+          const bool inseg = tp >= ss;
+          if (inseg && nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m); nr++; }
+          const Tok t = rtok(&sh, r);
           if (inseg) {
-            if (t == T_EOB || t == T_ERR) { e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; break; }
-            if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
-            o += tok_len(t);
-            m += (t & T_MATCH) ? 1u : 0u;
+            if (t.kind >= TK_EOB) { e = t.kind == TK_EOB ? END_EOB : END_ERR; after = tp + t.n; break; }
+            if (m >= MCAP_LANE && t.kind == TK_MATCH) { e = END_CUT; break; }
+            o += t.len;
+            m += t.kind;
           }
-          HZ2_TICK(steps);
+          br_adv(r, t.n);
+          HZ2_RTICK(steps);
         }
         sh.nrec[lane] = nr;
         sh.syncw[lane] = lane == 0 ? 0u : SYNC_NONE;
@@ -730,7 +899,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       // (a lane that ended leaves its successor at SYNC_NONE)
 #define HZ2_CONTINUE(lane_)                                                                      \
       do {                                                                                       \
-        GRd r = LV(rd);                                                                          \
+        BR r = LV(rd);                                                                           \
         uint32_t o = LV(co), m = LV(cm), e = LV(ek), after = LV(ea);                             \
         uint32_t res = SYNC_NONE;                                                                \
         if (e == END_NONE && (lane_) < 63) {                                                     \
@@ -739,23 +908,25 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           uint32_t k = 0, ct = 0;                                                                \
           res = SYNC_FAIL;                                                                       \
           for (;;) {                                                                             \
-            const uint32_t rel = r.pos - base;                                                   \
+            const uint32_t tp = hz2::br_pos(r);                                                  \
+            const uint32_t rel = tp - base;                                                      \
             while (k < nrn && hz2::rec_rel(sh.rec[k][(lane_) + 1]) < rel) k++;                   \
             if (k >= nrn) break;                                                                 \
             if (hz2::rec_rel(sh.rec[k][(lane_) + 1]) == rel) { res = k; break; }                 \
-            const uint32_t tp = r.pos;                                                           \
-            const uint32_t t = hz2::next_token(&sh, S, r);                                       \
-            if (t == T_EOB || t == T_ERR) {                                                      \
-              e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; res = SYNC_NONE; break; \
+            hz2::br_next(sh, lane, r);                                                           \
+            const hz2::Tok t = hz2::rtok(&sh, r);                                                \
+            if (t.kind >= hz2::TK_EOB) {                                                         \
+              e = t.kind == hz2::TK_EOB ? END_EOB : END_ERR; after = tp + t.n; res = SYNC_NONE; break; \
             }                                                                                    \
-            if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; res = SYNC_NONE; break; } \
-            o += hz2::tok_len(t);                                                                \
-            m += (t & T_MATCH) ? 1u : 0u;                                                        \
-            HZ2_TICK(ct);                                                                        \
+            if (m >= MCAP_LANE && t.kind == hz2::TK_MATCH) { e = END_CUT; res = SYNC_NONE; break; } \
+            o += t.len;                                                                          \
+            m += t.kind;                                                                         \
+            hz2::br_adv(r, t.n);                                                                 \
+            HZ2_RTICK(ct);                                                                       \
           }                                                                                      \
         }                                                                                        \
         if ((lane_) < 63) sh.syncw[(lane_) + 1] = res;                                           \
-        sh.endp[lane_] = r.pos;                                                                  \
+        sh.endp[lane_] = hz2::br_pos(r);                                                         \
         LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;                          \
       } while (0)
       LANE_LOOP { HZ2_CONTINUE(lane); }
@@ -773,18 +944,21 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         LANE_LOOP {
           if ((redo_m >> lane) & 1ull) {
             const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
-            GRd r;
-            g_init(S, r, sh.endp[lane - 1]);
+            BR r;
+            br_init(sh, lane, S, r, sh.endp[lane - 1]);
             uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0, ct = 0;
-            while (r.pos < se || nr == 0) {
-              if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(r.pos - ss, o, m); nr++; }
-              const uint32_t tp = r.pos;
-              const uint32_t t = next_token(&sh, S, r);
-              if (t == T_EOB || t == T_ERR) { e = t == T_EOB ? END_EOB : END_ERR; after = r.pos; r.pos = tp; break; }
-              if (m >= MCAP_LANE && (t & T_MATCH)) { e = END_CUT; r.pos = tp; break; }
-              o += tok_len(t);
-              m += (t & T_MATCH) ? 1u : 0u;
-              HZ2_TICK(ct);
+            for (;;) {
+              const uint32_t tp = br_pos(r);
+              if (!(tp < se || nr == 0)) break;
+              br_next(sh, lane, r);
+              if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m); nr++; }
+              const Tok t = rtok(&sh, r);
+              if (t.kind >= TK_EOB) { e = t.kind == TK_EOB ? END_EOB : END_ERR; after = tp + t.n; break; }
+              if (m >= MCAP_LANE && t.kind == TK_MATCH) { e = END_CUT; break; }
+              o += t.len;
+              m += t.kind;
+              br_adv(r, t.n);
+              HZ2_RTICK(ct);
             }
             sh.nrec[lane] = nr;
             sh.syncw[lane] = 0;                       // its path starts at record 0
@@ -873,8 +1047,8 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         int err = 0;
         uint32_t steps = 0;
         if ((uint32_t)lane < V) {
-          GRd r;
-          g_init(S, r, LV(sbit));
+          BR r;
+          br_init(sh, lane, S, r, LV(sbit));
           const uint32_t stop = sh.endp[lane];
           const uint32_t lo_x = out + LV(obase), hi_x = lo_x + LV(wout);
           uint32_t o = lo_x, mi = LV(mbase);
@@ -904,14 +1078,13 @@ HZ_UNROLL
               }
             }
           };
-          while (r.pos < stop) {
-            const uint32_t t = next_token(&sh, S, r);
-#ifndef HZ2_EPOCH_NO_E
-            HZ2_TICK(steps);
-#else
-            steps++;
-#endif
-            if (!(t & T_MATCH)) {
+          while (br_pos(r) < stop) {
+            br_next(sh, lane, r);
+            const Tok tk = rtok(&sh, r);
+            br_adv(r, tk.n);
+            HZ2_RTICK(steps);
+            if (tk.kind == TK_LIT) {
+              const uint32_t t = tk.v;
 #ifndef HZ2_EXP_NOSTORE
               if (PERM) {
                 dst[perm_at(P, o)] = (uint8_t)t;
@@ -926,8 +1099,9 @@ HZ_UNROLL
               a2 += (uint64_t)o * t;
               o++;
             } else {
-              const uint32_t ln = (t >> 16) & 0x1ffu, d = (t & 0x7fffu) + 1u;
-              if (d > o) { err = 1; break; }
+              // a match (E decodes ranges A verified: an EOB / invalid code here is a bug)
+              const uint32_t ln = tk.len, d = tk.v;
+              if (d > o || tk.kind != TK_MATCH) { err = 1; break; }
               const uint64_t rv = (uint64_t)o | ((uint64_t)((ln << 16) | (d - 1u)) << 32);
 #if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
               sh.rstage[lane][mi & (RGRP - 1u)] = rv;

@@ -150,6 +150,28 @@ constexpr int ST_UNSUP = -5;
 constexpr uint32_t SYM_BAD = 0xfffu;
 HZ_HD uint16_t ent_sym(uint32_t len, uint32_t sym) { return (uint16_t)(len | (sym << 4)); }
 HZ_HD uint16_t ent_sub(uint32_t off, uint32_t sb) { return (uint16_t)((off << 4) | (sb << 13)); }
+// "rich" symbol entries (inflate2.h): the length / distance base and extra bits come from
+// the table instead of per-token arithmetic.
+//  literal/length (kind 1): bits 0-3 code length, 4-6 extra bits x (7: literal / EOB /
+//    invalid), 7-15 value v (literal byte, 256 = EOB, 257 = invalid, or the length base)
+//  distance (kind 2): bits 0-3 code length, 4-7 extra bits, 8-10 b, 11 one, 12 invalid:
+//    distance = (b << extra) + one + extra value
+// Subtable links keep ent_sub's layout (code length field 0).
+HZ_HD uint16_t ent_rich(int kind, uint32_t len, uint32_t sym) {
+  if (kind == 1) {
+    if (sym <= 256u) return (uint16_t)(len | (7u << 4) | (sym << 7));
+    if (sym > 285u) return (uint16_t)(len | (7u << 4) | (257u << 7));
+    const uint32_t q = sym - 257u;
+    const uint32_t x = (q < 8u || q == 28u) ? 0u : (q - 4u) >> 2;
+    const uint32_t base = q < 8u ? q + 3u : q == 28u ? 258u : ((4u | (q & 3u)) << x) + 3u;
+    return (uint16_t)(len | (x << 4) | (base << 7));
+  }
+  if (sym >= 30u) return (uint16_t)(len | (1u << 12));
+  const uint32_t x = sym < 4u ? 0u : (sym - 2u) >> 1;
+  const uint32_t b = sym < 4u ? sym + 1u : 2u | (sym & 1u);
+  const uint32_t one = sym < 4u ? 0u : 1u;
+  return (uint16_t)(len | (x << 4) | (b << 8) | (one << 11));
+}
 
 // tokens (decoder result): literal = byte; match = 0x80000000 | len<<16 | (dist-1); EOB / ERR
 constexpr uint32_t T_MATCH = 0x80000000u;
@@ -455,6 +477,7 @@ struct TableArgs {
   int root;
   int kind;
   int nsub;     // second-level capacity after the 2^root root entries
+  int rich;     // 1: ent_rich symbol entries (inflate2.h), 0: ent_sym
 };
 
 }  // namespace hz
@@ -549,11 +572,12 @@ struct TableArgs {
     LANE_LOOP {                                                                         \
       for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
         const uint32_t rc = hz::rev_bits((uint32_t)idx, (A).root);                      \
-        uint32_t e = hz::ent_sym(1, hz::SYM_BAD);                                       \
+        uint32_t e = (A).rich ? hz::ent_rich((A).kind, 1, hz::SYM_BAD) : hz::ent_sym(1, hz::SYM_BAD); \
         _Pragma("unroll") for (int len = 1; len <= 15; len++) {                         \
           if (len > (A).root) break;                                                    \
           const uint32_t d = (rc >> ((A).root - len)) - _fc[len];                       \
-          if (d < _cn[len]) e = hz::ent_sym((uint32_t)len, (A).sorted[_of[len] + d]);   \
+          if (d < _cn[len]) e = (A).rich ? hz::ent_rich((A).kind, (uint32_t)len, (A).sorted[_of[len] + d]) \
+                                         : hz::ent_sym((uint32_t)len, (A).sorted[_of[len] + d]); \
         }                                                                               \
         (A).lut[idx] = (uint16_t)e;                                                     \
       }                                                                                 \
@@ -611,7 +635,7 @@ struct TableArgs {
           const int sb = (int)(re >> 13), off = (1 << _R) + (int)((re >> 4) & 511u);    \
           const int tl = len - _R;                                                      \
           const uint32_t j0 = hz::rev_bits((uint32_t)(c & ((1 << tl) - 1)), tl);        \
-          const uint16_t e = hz::ent_sym((uint32_t)len, sym);                           \
+          const uint16_t e = (A).rich ? hz::ent_rich((A).kind, (uint32_t)len, sym) : hz::ent_sym((uint32_t)len, sym); \
           for (int m = 0; m < (1 << (sb - tl)); m++) (A).lut[off + (j0 | (m << tl))] = e; \
         }                                                                               \
       }                                                                                 \
