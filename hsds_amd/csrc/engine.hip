@@ -1552,8 +1552,9 @@ int hsds_engine_create(int device, hsds_engine** out) {
   e->huff_blocks_per_cu = o2;
   e->emit_blocks_per_cu = o3;
   // warm-up 512 bits, segments sized to 1 + 1/16 of the previous block, 4 repair rounds
-  e->tune.W = 512;          // GPU sweep (tools/ab_tune.sh): 256 / 320 / 384 / 448 / 512 / 576 bits ->
-                            // F1 103.5 / 104.8 / 107.4 / 107.6 / 108.7 / 108.9 GB/s
+  e->tune.W = 768;          // GPU sweep (tools/ab_tune.sh), bit-ring decoder with K = 8 recorded starts:
+                            // 384 / 512 / 640 / 768 bits -> F1 116.2 / 119.5 / 120.9 / 121.6 GB/s
+                            // (round 2, register reader, K = 16: 512 best at 108.7)
   e->tune.max_rounds = 4;
   e->tune.over16 = 1;
   // development override (A/B experiments): "W,rounds,over16"

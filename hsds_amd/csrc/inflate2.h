@@ -139,6 +139,7 @@ struct alignas(16) Shared {
       uint32_t bring[RS + 1][WAVE];   // each lane's bit ring: stream word j in slot j % RS (word-major:
                                       // lanes hit distinct banks); slot RS mirrors slot 0
       union {
+        uint32_t hbits[256];          // dynamic block header: 8192 stream bits from the header's quad
         uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
         struct {                      // phase E
           alignas(16) uint8_t ostage[WAVE][OWIN];   // plain output: each lane's current literal window
@@ -568,6 +569,20 @@ HZ_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
+#if HZ_GPU
+#define HZ2_HM __device__ __forceinline__
+#else
+#define HZ2_HM inline
+#endif
+// lane 0's reader over the dynamic header's bits in LDS (sh.hbits)
+struct HR {
+  const uint32_t* b;
+  uint32_t p, base;
+  HZ2_HM uint32_t peek() const { return funnel(b[(p >> 5) + 1u], b[p >> 5], p & 31u); }
+  HZ2_HM void drop(uint32_t n) { p += n; }
+  HZ2_HM uint32_t pos() const { return base + p; }
+};
+
 enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_ERR = 3 };
 struct Tok {
   uint32_t n;      // bits
@@ -747,23 +762,29 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       }
       WAVE_SYNC();
     } else {
-      // dynamic header (RFC 1951 3.2.7), decoded serially by lane 0
+      // dynamic header (RFC 1951 3.2.7): the wave loads the 8192 stream bits from the header's
+      // quad into LDS at once (a header is at most 14 + 19 x 3 + 320 x 14 bits), then lane 0
+      // decodes it serially from LDS -- no global load latency per refill
+      const uint32_t hq = (pos >> 5) & ~3u;
+      LANE_LOOP {
+        uint32_t a0, a1, a2, a3;
+        g_quad(S, hq + 4u * (uint32_t)lane, a0, a1, a2, a3);
+        sh.hbits[4 * lane] = a0; sh.hbits[4 * lane + 1] = a1; sh.hbits[4 * lane + 2] = a2; sh.hbits[4 * lane + 3] = a3;
+      }
+      WAVE_SYNC();
       LANE_LOOP {
         if (lane == 0) {
           int st = ST_OK;
-          GRd r;
-          g_init(S, r, pos);
-          g_fill(S, r);
-          const uint32_t hlit = (uint32_t)(g_peek(r) & 31u) + 257u, hdist = (uint32_t)((g_peek(r) >> 5) & 31u) + 1u;
-          const uint32_t hclen = (uint32_t)((g_peek(r) >> 10) & 15u) + 4u;
-          g_drop(S, r, 14);
+          HR r = {sh.hbits, pos - hq * 32u, hq * 32u};
+          const uint32_t hlit = (r.peek() & 31u) + 257u, hdist = ((r.peek() >> 5) & 31u) + 1u;
+          const uint32_t hclen = ((r.peek() >> 10) & 15u) + 4u;
+          r.drop(14);
           if (hlit > 286 || hdist > 30) st = ST_DATA;
           uint16_t* cl = sh.sorted_cl;
           for (int i = 0; i < 19; i++) cl[i] = 0;
           for (uint32_t i = 0; i < hclen; i++) {
-            g_fill(S, r);
-            cl[hz::cl_order(i)] = (uint16_t)(g_peek(r) & 7u);
-            g_drop(S, r, 3);
+            cl[hz::cl_order(i)] = (uint16_t)(r.peek() & 7u);
+            r.drop(3);
           }
           uint16_t* cnt = sh.cnt_cl;
           for (int l = 0; l < 16; l++) cnt[l] = 0;
@@ -791,22 +812,21 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           const uint32_t total = hlit + hdist;
           uint32_t n = 0;
           while (st == ST_OK && n < total) {
-            if (r.pos > limit_bits + 64u) { st = ST_TRUNC; break; }
-            g_fill(S, r);
-            const uint32_t e = clut[g_peek(r) & 127u];
+            if (r.pos() > limit_bits + 64u) { st = ST_TRUNC; break; }
+            const uint32_t e = clut[r.peek() & 127u];
             const uint32_t sym = e & 0xffu, l = e >> 8;
-            g_drop(S, r, l);
+            r.drop(l);
             if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
             uint32_t rep, val = 0;
             if (sym == 16) {
               if (n == 0) { st = ST_DATA; break; }
-              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(g_peek(r) & 3u); g_drop(S, r, 2);
-            } else if (sym == 17) { rep = 3 + (uint32_t)(g_peek(r) & 7u); g_drop(S, r, 3); }
-            else { rep = 11 + (uint32_t)(g_peek(r) & 127u); g_drop(S, r, 7); }
+              val = sh.lens[n - 1]; rep = 3 + (r.peek() & 3u); r.drop(2);
+            } else if (sym == 17) { rep = 3 + (r.peek() & 7u); r.drop(3); }
+            else { rep = 11 + (r.peek() & 127u); r.drop(7); }
             if (n + rep > total) { st = ST_DATA; break; }
             for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
           }
-          if (st == ST_OK && r.pos > limit_bits) st = ST_TRUNC;
+          if (st == ST_OK && r.pos() > limit_bits) st = ST_TRUNC;
           if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;   // missing end-of-block code
           if (st == ST_OK) {
             for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
@@ -814,7 +834,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
           }
           sh.u_status = st;
-          sh.u_pos = r.pos;
+          sh.u_pos = r.pos();
           sh.u_nlen = hlit;
           sh.u_ndist = hdist;
         }

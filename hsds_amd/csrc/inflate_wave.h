@@ -572,13 +572,13 @@ struct TableArgs {
     LANE_LOOP {                                                                         \
       for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
         const uint32_t rc = hz::rev_bits((uint32_t)idx, (A).root);                      \
-        uint32_t e = (A).rich ? hz::ent_rich((A).kind, 1, hz::SYM_BAD) : hz::ent_sym(1, hz::SYM_BAD); \
+        uint32_t el = 1, es = hz::SYM_BAD;                                            \
         _Pragma("unroll") for (int len = 1; len <= 15; len++) {                         \
           if (len > (A).root) break;                                                    \
           const uint32_t d = (rc >> ((A).root - len)) - _fc[len];                       \
-          if (d < _cn[len]) e = (A).rich ? hz::ent_rich((A).kind, (uint32_t)len, (A).sorted[_of[len] + d]) \
-                                         : hz::ent_sym((uint32_t)len, (A).sorted[_of[len] + d]); \
+          if (d < _cn[len]) { el = (uint32_t)len; es = (A).sorted[_of[len] + d]; }      \
         }                                                                               \
+        const uint32_t e = (A).rich ? hz::ent_rich((A).kind, el, es) : hz::ent_sym(el, es); \
         (A).lut[idx] = (uint16_t)e;                                                     \
       }                                                                                 \
     }                                                                                   \
