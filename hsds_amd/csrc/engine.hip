@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -1418,6 +1419,31 @@ struct hsds_engine {
   uint32_t enc_chain = 0;      // development override of the parse chain depth (0: the level's)
   hipEvent_t ev2, ev3;
   int ev_enc_valid = 0;
+  // re-entrancy (SURVEY 8b "Threading"): every entry point that uses the workspace holds mu
+  // while it enqueues, and a call on another stream first waits for the workspace's last
+  // use (ws_ev) -- so a DN running calls from a thread pool, on any streams, never races
+  std::recursive_mutex mu;
+  hipEvent_t ws_ev;
+  hipStream_t ws_st = nullptr;
+  int ws_ev_valid = 0;
+};
+
+// holds the engine for one workspace use on `stream` (see hsds_engine::mu)
+struct WsGuard {
+  hsds_engine* e;
+  hipStream_t st;
+  WsGuard(hsds_engine* e_, void* stream) : e(e_), st((hipStream_t)stream) {
+    e->mu.lock();
+    if (e->ws_ev_valid && e->ws_st != st) hipStreamWaitEvent(st, e->ws_ev, 0);
+  }
+  ~WsGuard() {
+    hipEventRecord(e->ws_ev, st);
+    e->ws_st = st;
+    e->ws_ev_valid = 1;
+    e->mu.unlock();
+  }
+  WsGuard(const WsGuard&) = delete;
+  WsGuard& operator=(const WsGuard&) = delete;
 };
 
 static int grow(void** p, size_t* have, size_t need) {
@@ -1566,7 +1592,8 @@ int hsds_engine_create(int device, hsds_engine** out) {
     }
   }
   if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
-      hipEventCreate(&e->ev2) != hipSuccess || hipEventCreate(&e->ev3) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
+      hipEventCreate(&e->ev2) != hipSuccess || hipEventCreate(&e->ev3) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ws_ev, hipEventDisableTiming) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
   *out = e;
   return HSDS_OK;
 }
@@ -1588,6 +1615,7 @@ void hsds_engine_destroy(hsds_engine* e) {
   hipEventDestroy(e->ev1);
   hipEventDestroy(e->ev2);
   hipEventDestroy(e->ev3);
+  hipEventDestroy(e->ws_ev);
   delete e;
 }
 
@@ -1612,6 +1640,7 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   if (nchunks == 0) return HSDS_OK;
   if (nchunks > (int64_t)(1u << 24)) return HSDS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
+  WsGuard guard(e, stream);
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
   if (shuffle == HSDS_SHUFFLE_BIT && compressor == HSDS_COMP_NONE) {
     // bitshuffle+LZ4 objects as stored (no outer compressor): bshuf_kernel alone
@@ -1746,6 +1775,7 @@ int64_t hsds_uncompress(hsds_engine* e, const void* src, int64_t srclen, int com
                         void* dst, int64_t expected) {
   if (!e || srclen < 0 || (srclen && !src) || (expected && !dst)) return HSDS_ERR_ARG;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  WsGuard guard(e, nullptr);
   const int inexact = expected < 0;
   if (inexact) expected = -expected;
   // device staging: [src bytes | chunk descriptor] and [dst bytes | status]
@@ -1803,6 +1833,7 @@ static int host_shuffle(hsds_engine* e, const void* src, int64_t n, int itemsize
   if (!e || n < 0 || itemsize < 1 || (n && (!src || !dst))) return HSDS_ERR_ARG;
   if (n == 0) return HSDS_OK;
   hipSetDevice(e->device);
+  WsGuard guard(e, nullptr);
   if (grow((void**)&e->h_dev_src, &e->h_dev_src_bytes, (size_t)n)) return HSDS_ERR_DEVICE;
   if (grow((void**)&e->h_dev_dst, &e->h_dev_dst_bytes, (size_t)n)) return HSDS_ERR_DEVICE;
   if (hipMemcpy(e->h_dev_src, src, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) return HSDS_ERR_DEVICE;
@@ -1977,6 +2008,7 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   if (nchunks > (int64_t)(1u << 22)) return HSDS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  WsGuard guard(e, stream);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   // per-chunk plan arrays (own buffer: they survive the resize of the split / segment area)
   const size_t sz_counts = al((size_t)nchunks * 4);
@@ -2114,6 +2146,7 @@ int64_t hsds_compress_codec(hsds_engine* e, const void* src, int64_t n, int clev
                             int cname, void* dst, int64_t cap) {
   if (!e || n < 0 || (n && !src) || !dst || cap < n + 16) return HSDS_ERR_ARG;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  WsGuard guard(e, nullptr);
   const size_t desc_off = ((size_t)n + 255) & ~(size_t)255;
   const size_t frame_cap = (size_t)n + 16;
   const size_t stat_off = (frame_cap + 255) & ~(size_t)255;
@@ -2153,6 +2186,7 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
   if (nchunks > (int64_t)(1u << 22)) return HSDS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  WsGuard guard(e, stream);
   const uint32_t es = (uint32_t)itemsize;
   const uint64_t bsz = block ? (uint64_t)block : host_bshuf_default_block(es);
   // work areas and the transposition staging are sized by the batch's own bytes (sum of
@@ -2245,6 +2279,7 @@ int64_t hsds_bitshuffle_compress(hsds_engine* e, const void* src, int64_t n, int
   if (!e || bound < 0 || (n && !src) || !dst || cap < 12) return HSDS_ERR_ARG;
   if (n % itemsize) return HSDS_ERR_ARG;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  WsGuard guard(e, nullptr);
   const size_t desc_off = ((size_t)n + 255) & ~(size_t)255;
   const size_t stat_off = ((size_t)bound + 255) & ~(size_t)255;
   if (grow((void**)&e->h_dev_src, &e->h_dev_src_bytes, desc_off + sizeof(hsds_chunk_desc))) return HSDS_ERR_DEVICE;

@@ -60,6 +60,7 @@ constexpr uint32_t SPAN = 1536;           // resolve batch: output bytes covered
 constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
 static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
+constexpr uint32_t SVN = (SPAN / 4u + 2u + WAVE - 1u) / WAVE;   // span dwords per lane (plain output)
 #ifndef HZ2_RG
 #define HZ2_RG 8
 #endif
@@ -1207,6 +1208,22 @@ HZ_UNROLL
         const uint32_t last_o = LVA_AT(ro, (nb - 1u) >> 6, (nb - 1u) & 63u);
         const uint32_t last_w = LVA_AT(rw, (nb - 1u) >> 6, (nb - 1u) & 63u);
         const uint32_t span = last_o + (last_w >> 16) - F;
+        // plain output: the span's aligned dwords are loaded first, into registers, so their
+        // round trip overlaps the source-map fill and the record prefetch (issued after them,
+        // so waiting for these does not wait for the prefetch)
+        const uint32_t mis = PERM ? 0u : (uint32_t)((uintptr_t)(job.dst + F) & 3u);
+        const uint32_t xa = F - mis;                           // stream position of dword 0
+        const uint32_t ndw = (span + mis + 3u) >> 2;
+        LANE_ARR(uint32_t, sv, SVN);
+        if (!PERM) {
+          LANE_LOOP {
+HZ_UNROLL
+            for (uint32_t k = 0; k < SVN; k++) {
+              const uint32_t kk = (uint32_t)lane + 64u * k, x0 = xa + 4u * kk;
+              LV(sv)[k] = (kk < ndw && x0 + 4u <= dst_len && (int32_t)x0 >= 0) ? *(hz_gu32*)(dst + x0) : 0u;
+            }
+          }
+        }
         LANE_LOOP {
           for (uint32_t q = (uint32_t)lane * 2u; q < span; q += 128u) *(uint32_t*)&sh.smap[q] = 0u;
         }
@@ -1298,13 +1315,11 @@ HZ_UNROLL
           // from dst, a literal of the batch from LDS), and the dwords are stored back
           // (coalesced) -- one load round trip and one store drain per batch.  Dwords
           // reaching outside the stream's output store their match bytes one by one.
-          const uint32_t mis = (uint32_t)((uintptr_t)(job.dst + F) & 3u);
-          const uint32_t xa = F - mis;                           // stream position of dword 0
-          const uint32_t ndw = (span + mis + 3u) >> 2;
           LANE_LOOP {
-            for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
-              const uint32_t x0 = xa + 4u * k;
-              sh.sbuf[k] = (x0 + 4u <= dst_len && (int32_t)x0 >= 0) ? *(hz_gu32*)(dst + x0) : 0u;
+HZ_UNROLL
+            for (uint32_t k = 0; k < SVN; k++) {
+              const uint32_t kk = (uint32_t)lane + 64u * k;
+              if (kk < ndw) sh.sbuf[kk] = LV(sv)[k];
             }
           }
           WAVE_SYNC();

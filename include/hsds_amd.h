@@ -24,10 +24,13 @@
  *                        <- storUtil.py:94-131 _shuffle(codec=2, ...) (bitshuffle.compress_lz4 behind
  *                           the 12-byte header), reached from _compress(shuffle=2) (storUtil.py:243-251)
  *
- * Threading: an engine is bound to one device and may be used from one host thread
- * at a time (HSDS data nodes are single-threaded asyncio processes).  All *_batch
- * calls are asynchronous on the given hipStream_t (pass NULL for the default
- * stream); host-buffer calls are synchronous.
+ * Threading: an engine is bound to one device and is re-entrant: its calls may come from
+ * any host threads (a DN running them off the event loop in a thread pool).  Calls that
+ * use the engine's workspace (decode, encode, the host-buffer codec calls) hold an
+ * engine mutex while they enqueue, and a call on a different stream than the previous
+ * workspace user first waits (hipStreamWaitEvent) for that use to finish on the device.
+ * All *_batch calls are asynchronous on the given hipStream_t (pass NULL for the
+ * default stream); host-buffer calls are synchronous.
  */
 #ifndef HSDS_AMD_H
 #define HSDS_AMD_H
