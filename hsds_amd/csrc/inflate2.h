@@ -66,7 +66,7 @@ constexpr uint32_t SVN = (SPAN / 4u + 2u + WAVE - 1u) / WAVE;   // span dwords p
 #endif
 constexpr uint32_t RG = HZ2_RG;           // resolve (unshuffled output): bytes a lane loads before it stores
 #ifndef HZ2_RGP
-#define HZ2_RGP 12
+#define HZ2_RGP 24
 #endif
 constexpr uint32_t RGP = HZ2_RGP;         // resolve (plain output): bytes a lane resolves per load round trip
 #ifndef HZ2_DW
