@@ -211,6 +211,13 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
       if (shuffle == HSDS_SHUFFLE_BIT) st = HSDS_ERR_UNSUPPORTED;
       else if (shuf_n && (n % (uint64_t)itemsize)) st = HSDS_ERR_ARG;
       else if (shuf_n && itemsize > 255) st = HSDS_ERR_UNSUPPORTED;
+      else if (shuf_n && tmp) {
+        // F2 chunk: inflated in stream order into tmp (the plain output path: literal windows
+        // and whole-dword match resolve), then unshuffled by unshuffle_kernel -- cheaper than
+        // byte stores through the output map (measured: DESIGN.md section 5)
+        emit(ITEM_ZLIB, s, L, tmp, n);
+        m.mode = 1; m.tmp = (uint64_t)tmp; m.ts = (uint32_t)itemsize; m.bs = (uint32_t)n;
+      }
       else emit((inexact && !shuf_n ? (ITEM_ZLIB | ITEM_INEXACT) : ITEM_ZLIB) | shuf_n, s, L, out, n);
     } else {
       st = HSDS_ERR_UNSUPPORTED;
@@ -1675,10 +1682,13 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   // [0] inflate item counter, [1] meta list count, [2] inexact size, [3] LZ item counter,
   // [4] LZ items, [5] zlib + raw items, [6] zstd items, [7] zstd item counter, [8] pool fill
   uint32_t* ctr = (uint32_t*)w;
-  // staging for LZ / zstd Blosc frames with typesize > 1 (zlib and raw items land unshuffled
-  // through their output map): only batches of a non-zlib codec can have them
+  // staging for LZ / zstd Blosc frames with typesize > 1 and for shuffled F2 chunks (both
+  // unshuffled by unshuffle_kernel afterwards; zlib Blosc splits and raw items land
+  // unshuffled through their output map)
   uint8_t* tmp = nullptr;
-  if (compressor == HSDS_COMP_OTHER) {
+  static const int f2_stage = getenv("HSDS_F2_FUSED") ? 0 : 1;   // A/B: 0 = unshuffle fused into inflate
+  if (compressor == HSDS_COMP_OTHER ||
+      (f2_stage && compressor == HSDS_COMP_ZLIB && shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1)) {
     if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
     tmp = e->tmp;
   }
