@@ -38,6 +38,39 @@ HZ_HD uint64_t t8x8(uint64_t x) {
   return x;
 }
 
+// inverse bit transposition of row byte q of a block of cnt elements (cnt % 8 == 0, row =
+// cnt / 8) of es bytes: elements 8 q .. 8 q + 7, all es bytes, from in (transposed) to out
+HZ_HD void untrans_row(hz_gcu8* in, hz_gu8* out, uint32_t q, uint32_t row, uint32_t es) {
+  hz_gu8* o = out + (uint64_t)q * 8u * es;
+  if (es <= 8u) {
+    uint64_t el[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // element 8q + m, bytes packed little-endian
+    for (uint32_t j = 0; j < es; j++) {
+      uint64_t x = 0;
+      for (uint32_t k = 0; k < 8u; k++) x |= (uint64_t)in[(uint64_t)(j * 8u + k) * row + q] << (8u * k);
+      const uint64_t y = t8x8(x);                  // byte m: byte j of element 8q + m
+      for (uint32_t m = 0; m < 8u; m++) el[m] |= ((y >> (8u * m)) & 0xffull) << (8u * j);
+    }
+    if (es == 4u && !(((uintptr_t)o) & 3u)) {
+      for (uint32_t m = 0; m < 8u; m++) *(hz_gu32*)(o + 4u * m) = (uint32_t)el[m];
+    } else if (es == 8u && !(((uintptr_t)o) & 3u)) {
+      for (uint32_t m = 0; m < 8u; m++) {
+        *(hz_gu32*)(o + 8u * m) = (uint32_t)el[m];
+        *(hz_gu32*)(o + 8u * m + 4u) = (uint32_t)(el[m] >> 32);
+      }
+    } else {
+      for (uint32_t m = 0; m < 8u; m++)
+        for (uint32_t j = 0; j < es; j++) o[m * es + j] = (uint8_t)(el[m] >> (8u * j));
+    }
+  } else {
+    for (uint32_t j = 0; j < es; j++) {
+      uint64_t x = 0;
+      for (uint32_t k = 0; k < 8u; k++) x |= (uint64_t)in[(uint64_t)(j * 8u + k) * row + q] << (8u * k);
+      const uint64_t y = t8x8(x);
+      for (uint32_t m = 0; m < 8u; m++) o[m * es + j] = (uint8_t)(y >> (8u * m));
+    }
+  }
+}
+
 // inverse bit transposition of one block: cnt elements (cnt % 8 == 0) of es bytes from
 // in (transposed) to out.  Work item = 8 elements (one row byte q) x all es bytes.
 #if HZ_GPU
@@ -48,36 +81,7 @@ static
 inline void untrans_block(hz_gcu8* in, hz_gu8* out, uint32_t cnt, uint32_t es) {
   const uint32_t row = cnt / 8u;
   LANE_LOOP {
-    for (uint32_t q = (uint32_t)lane; q < row; q += 64u) {
-      hz_gu8* o = out + (uint64_t)q * 8u * es;
-      if (es <= 8u) {
-        uint64_t el[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // element 8q + m, bytes packed little-endian
-        for (uint32_t j = 0; j < es; j++) {
-          uint64_t x = 0;
-          for (uint32_t k = 0; k < 8u; k++) x |= (uint64_t)in[(uint64_t)(j * 8u + k) * row + q] << (8u * k);
-          const uint64_t y = t8x8(x);                  // byte m: byte j of element 8q + m
-          for (uint32_t m = 0; m < 8u; m++) el[m] |= ((y >> (8u * m)) & 0xffull) << (8u * j);
-        }
-        if (es == 4u && !(((uintptr_t)o) & 3u)) {
-          for (uint32_t m = 0; m < 8u; m++) *(hz_gu32*)(o + 4u * m) = (uint32_t)el[m];
-        } else if (es == 8u && !(((uintptr_t)o) & 3u)) {
-          for (uint32_t m = 0; m < 8u; m++) {
-            *(hz_gu32*)(o + 8u * m) = (uint32_t)el[m];
-            *(hz_gu32*)(o + 8u * m + 4u) = (uint32_t)(el[m] >> 32);
-          }
-        } else {
-          for (uint32_t m = 0; m < 8u; m++)
-            for (uint32_t j = 0; j < es; j++) o[m * es + j] = (uint8_t)(el[m] >> (8u * j));
-        }
-      } else {
-        for (uint32_t j = 0; j < es; j++) {
-          uint64_t x = 0;
-          for (uint32_t k = 0; k < 8u; k++) x |= (uint64_t)in[(uint64_t)(j * 8u + k) * row + q] << (8u * k);
-          const uint64_t y = t8x8(x);
-          for (uint32_t m = 0; m < 8u; m++) o[m * es + j] = (uint8_t)(y >> (8u * m));
-        }
-      }
-    }
+    for (uint32_t q = (uint32_t)lane; q < row; q += 64u) untrans_row(in, out, q, row, es);
   }
 }
 

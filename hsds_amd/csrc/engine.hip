@@ -6,12 +6,12 @@
 //                       of one work item per deflate stream / LZ / zstd / raw split into
 //                       a compact item pool (no per-chunk split cap)
 //   inflate2_kernel     persistent waves pull zlib / raw items from a device counter; one
-//                       wavefront decodes one zlib stream (inflate2.h), writing through
-//                       the byte-unshuffle output map (F2, Blosc typesize > 1)
+//                       wavefront decodes one zlib stream (inflate2.h) in stream order
 //   lz_kernel           LZ4 / BloscLZ Blosc splits, 8 per wavefront (lz_wave.h)
 //   zstd_kernel         zstd Blosc splits, one wavefront per split (zstd_wave.h)
 //   bshuf_kernel        bitshuffle+LZ4 chunks (shuffle = 2), one wavefront per chunk (bshuf.h)
-//   unshuffle_kernel    byte unshuffle of staged LZ / zstd Blosc blocks with typesize > 1
+//   unshuffle_kernel    byte / bit unshuffle of staged chunks: shuffled Blosc blocks (any
+//                       codec), HDF5-shuffled F2 streams
 //  hyperslab copies (chunkUtil.py:882-995, chunk_crawl.py:118-150,395-418)
 //   copy_kernel / compare_kernel   strided N-d region copies / numpy-equal compares
 //   plan_descs_kernel   one thread per piece: copy records of a hyperslab plan
@@ -54,12 +54,11 @@ namespace {
 
 
 // ITEM_LZ4 / ITEM_BLOSCLZ: Blosc splits of the byte-LZ77 codecs (lz_wave.h)
-enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_ZSTD = 4, ITEM_INEXACT = 0x100,
-                  ITEM_PLANE = 1u << 24 };
+enum : uint32_t { ITEM_ZLIB = 0, ITEM_RAW = 1, ITEM_LZ4 = 2, ITEM_BLOSCLZ = 3, ITEM_ZSTD = 4, ITEM_INEXACT = 0x100 };
 
 // decode work item (32 bytes): one zlib stream / raw span / LZ split.  kind word: bits 0-7
-// decoder, bit 8 inexact size, bits 16-23 byte-unshuffle element size n (<= 1: none), bit 24
-// plane split (the item is plane j, bits 25-29, of a Blosc block whose base is `dst`)
+// decoder, bit 8 inexact size, bits 16-23 byte-unshuffle element size n of a raw span (<= 1:
+// none; compressed items always write plain bytes)
 struct Item {
   uint64_t src;
   uint64_t dst;
@@ -72,7 +71,7 @@ struct Item {
 struct ChunkMeta {     // post-decode unshuffle of LZ / zstd Blosc blocks staged in tmp
   uint64_t tmp;        // staged (shuffled) bytes
   uint64_t dst;
-  uint32_t mode;       // 0 none, 1 Blosc blocks (ts, bs)
+  uint32_t mode;       // 0 none, 1 byte unshuffle of Blosc blocks (ts, bs), 2 bit unshuffle of Blosc blocks
   uint32_t ts;
   uint32_t bs;
   uint32_t nbytes;
@@ -83,11 +82,10 @@ __device__ __forceinline__ uint32_t rd32le(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// output map of an item (hz2::Perm): F2 chunks and Blosc shuffled blocks land unshuffled
+// output map of an item (hz2::Perm): a shuffled raw span (shuffle-only objects) lands unshuffled
 __device__ __forceinline__ hz2::Perm item_perm(const Item& it) {
   const uint32_t n = (it.kind >> 16) & 0xffu;
   if (n <= 1u) return hz2::perm_make(1u, 1u, 0u);
-  if (it.kind & ITEM_PLANE) return hz2::perm_make(n, it.dst_len, ((it.kind >> 25) & 31u) * it.dst_len);
   return hz2::perm_make(n, it.dst_len / n, 0u);
 }
 
@@ -98,8 +96,9 @@ __device__ __forceinline__ hz2::Perm item_perm(const Item& it) {
 // one atomic allocation from the batch's item pool -- to write them, so a chunk may have any
 // number of Blosc splits (pool capacity: 8 per chunk + 1 per 2 KiB of destination).
 // A batch whose items exceed the pool fails only the chunks that do not fit (pool_reserve).
-// zlib streams and raw spans carry their unshuffle map (item_perm); LZ / zstd splits of a
-// shuffled frame are staged in tmp and unshuffled by unshuffle_kernel.
+// Every decoder writes plain bytes: the splits of a shuffled (byte or bit) Blosc frame and a
+// shuffled F2 stream are staged in tmp and unshuffled by unshuffle_kernel; only a shuffled
+// raw object carries an unshuffle map (item_perm).
 // -------------------------------------------------------------------------
 // reserve n consecutive pool slots without ever moving the fill count past cap
 __device__ __forceinline__ int pool_reserve(uint32_t* ctr, uint32_t n, uint32_t cap, uint32_t* base) {
@@ -167,16 +166,18 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
           else emit(ITEM_RAW, s + 16, nbytes, out, nbytes);
         } else if (codec != 3 && codec != 1 && codec != 0 && codec != 4) st = HSDS_ERR_UNSUPPORTED;   // snappy
         else if (verlz != 1) st = HSDS_ERR_FRAME;
-        else if (flags & 0x04) st = HSDS_ERR_UNSUPPORTED;
         else if (nbytes > 0) {
           if (bs == 0 || bs > nbytes) st = HSDS_ERR_FRAME;
           else {
             const uint64_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
             const uint64_t hdr = 16 + 4 * nblocks;
+            // c-blosc 1.21 blosc_d: byte unshuffle when 0x01 and typesize > 1, else bit
+            // unshuffle when 0x04 (any typesize; oracle orc_blosc_decode)
             const int doshuffle = (flags & 0x01) && ts > 1;
-            // zlib streams / raw splits land unshuffled through their output map; the LZ
-            // decoders write plain bytes, so their shuffled frames go through tmp
-            const int staged = doshuffle && kind != ITEM_ZLIB;
+            const int dobit = !doshuffle && (flags & 0x04);
+            // every decoder writes plain bytes: shuffled frames go through tmp and are
+            // unshuffled (byte or bit) by unshuffle_kernel
+            const int staged = doshuffle || dobit;
             if (staged && !tmp) st = HSDS_ERR_UNSUPPORTED;
             uint8_t* target = staged ? tmp : out;
             if (hdr > cbytes) st = HSDS_ERR_FRAME;
@@ -193,17 +194,11 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
                 p += 4;
                 if (cs < 0 || p + cs > (int64_t)cbytes) { st = HSDS_ERR_FRAME; break; }
                 const uint32_t k = (uint64_t)cs == neblock ? ITEM_RAW : kind;
-                if (doshuffle && !staged) {
-                  // plane split j of the block (nspl == ts), or the whole shuffled block
-                  const uint32_t pm = (ts << 16) | (nspl > 1 ? ITEM_PLANE | (j << 25) : 0u);
-                  emit(k | pm, s + p, (uint64_t)cs, out + b * bs, neblock);
-                } else {
-                  emit(k, s + p, (uint64_t)cs, target + b * bs + j * neblock, neblock);
-                }
+                emit(k, s + p, (uint64_t)cs, target + b * bs + j * neblock, neblock);
                 p += cs;
               }
             }
-            if (staged) { m.mode = 1; m.tmp = (uint64_t)tmp; m.ts = ts; m.bs = (uint32_t)bs; }
+            if (staged) { m.mode = dobit ? 2u : 1u; m.tmp = (uint64_t)tmp; m.ts = ts; m.bs = (uint32_t)bs; }
           }
         }
       }
@@ -218,7 +213,8 @@ __global__ void frame_walk_kernel(const uint8_t* __restrict__ src_base, const hs
         emit(ITEM_ZLIB, s, L, tmp, n);
         m.mode = 1; m.tmp = (uint64_t)tmp; m.ts = (uint32_t)itemsize; m.bs = (uint32_t)n;
       }
-      else emit((inexact && !shuf_n ? (ITEM_ZLIB | ITEM_INEXACT) : ITEM_ZLIB) | shuf_n, s, L, out, n);
+      else if (shuf_n) st = HSDS_ERR_UNSUPPORTED;       // (compressed batches always have tmp)
+      else emit(inexact ? (ITEM_ZLIB | ITEM_INEXACT) : ITEM_ZLIB, s, L, out, n);
     } else {
       st = HSDS_ERR_UNSUPPORTED;
     }
@@ -307,7 +303,8 @@ __global__ void scan_kernel(const uint32_t* __restrict__ counts, uint32_t* __res
 // -------------------------------------------------------------------------
 // inflate: persistent 64-thread workgroups; each pulls items from the pool until the
 // pool's fill count is reached.  zlib streams go to hz2::inflate_stream (inflate2.h) with
-// the wave's own match ring (rings + blockIdx.x * RING_BYTES); raw spans are copied.
+// the wave's own scratch (rings + blockIdx.x * SCRATCH_BYTES: match ring + literal stream);
+// raw spans are copied.
 // -------------------------------------------------------------------------
 __device__ __forceinline__ void raw_copy(const Item& it, int lane) {
   const uint8_t* sp = (const uint8_t*)it.src;
@@ -332,7 +329,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) in
   if (kind_counts[1] == 0) return;   // only LZ / zstd splits in this batch
   const uint32_t total = *pool_ctr;
   const int lane = threadIdx.x;
-  uint8_t* ring = rings + (size_t)blockIdx.x * hz2::RING_BYTES;
+  uint8_t* ring = rings + (size_t)blockIdx.x * hz2::SCRATCH_BYTES;
 #ifdef HZ_PROFILE
   HzProf prof_;
   for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
@@ -357,8 +354,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) in
       hz2::Job job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
                       (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr,
                       item_perm(it)};
-      if (job.perm.n > 1u) st = hz2::inflate_stream<hz2::Stats, true>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
-      else st = hz2::inflate_stream<hz2::Stats, false>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
+      st = hz2::inflate_stream<hz2::Stats>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
     } else {
       continue;                        // lz_kernel's / zstd_kernel's item
     }
@@ -579,7 +575,18 @@ __global__ void __launch_bounds__(256) unshuffle_kernel(const ChunkMeta* __restr
     uint8_t* out = (uint8_t*)m.dst;
     for (uint64_t b0 = 0; b0 < m.nbytes; b0 += m.bs) {
       const uint64_t bsz = m.nbytes - b0 < m.bs ? m.nbytes - b0 : m.bs;
-      shuffle_span<true>(in + b0, out + b0, bsz, m.ts, threadIdx.x, blockDim.x);
+      if (m.mode == 1u) {
+        shuffle_span<true>(in + b0, out + b0, bsz, m.ts, threadIdx.x, blockDim.x);
+        continue;
+      }
+      // bitunshuffle (c-blosc 1.21, format version 2): the block's bsz / ts elements are
+      // untransposed when their count is a multiple of 8, else the block stays as decoded;
+      // bytes past the last whole element stay as decoded
+      const uint32_t ne = (uint32_t)(bsz / m.ts);
+      const uint32_t body = (ne & 7u) ? 0u : ne * m.ts;
+      for (uint32_t q = threadIdx.x; q < ne / 8u && body; q += blockDim.x)
+        bs::untrans_row(HZ_GLOBAL(hz_gcu8*, in + b0), HZ_GLOBAL(hz_gu8*, out + b0), q, ne / 8u, m.ts);
+      for (uint64_t i = body + threadIdx.x; i < bsz; i += blockDim.x) out[b0 + i] = in[b0 + i];
     }
   }
 }
@@ -1682,13 +1689,13 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   // [0] inflate item counter, [1] meta list count, [2] inexact size, [3] LZ item counter,
   // [4] LZ items, [5] zlib + raw items, [6] zstd items, [7] zstd item counter, [8] pool fill
   uint32_t* ctr = (uint32_t*)w;
-  // staging for LZ / zstd Blosc frames with typesize > 1 and for shuffled F2 chunks (both
-  // unshuffled by unshuffle_kernel afterwards; zlib Blosc splits and raw items land
-  // unshuffled through their output map)
+  // staging for LZ / zstd Blosc frames with typesize > 1, bitshuffled Blosc frames and
+  // shuffled F2 chunks (unshuffled by unshuffle_kernel afterwards; zlib Blosc splits and
+  // raw items land unshuffled through their output map)
   uint8_t* tmp = nullptr;
-  static const int f2_stage = getenv("HSDS_F2_FUSED") ? 0 : 1;   // A/B: 0 = unshuffle fused into inflate
-  if (compressor == HSDS_COMP_OTHER ||
-      (f2_stage && compressor == HSDS_COMP_ZLIB && shuffle == HSDS_SHUFFLE_BYTE && itemsize > 1)) {
+  // (Blosc frames with the bitshuffle flag can come with any codec: every compressed batch
+  // has the staging; it is grown once and only touched by frames that need it)
+  if (compressor != HSDS_COMP_NONE) {
     if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
     tmp = e->tmp;
   }
@@ -1696,7 +1703,7 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   int64_t grid = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
   if (grid > nchunks * 64) grid = nchunks * 64;
   if (grid < 1) grid = 1;
-  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * hz2::RING_BYTES)) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * hz2::SCRATCH_BYTES)) return HSDS_ERR_DEVICE;
   if (hipMemsetAsync(ctr, 0, 64, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);

@@ -56,35 +56,15 @@ constexpr uint32_t LMAX = 1u << 16;       // segment bits (lane output stays wel
 constexpr uint32_t MCAP_LANE = 256;       // matches per lane per window (ring bound)
 constexpr uint32_t RING = MCAP_LANE * WAVE;   // match ring entries per wave
 constexpr uint32_t RING_BYTES = RING * 8u;
+constexpr uint32_t LCAP_LANE = 1024;      // literals per lane per window (literal stream bound)
+constexpr uint32_t LIT_BYTES = LCAP_LANE * WAVE;
+constexpr uint32_t SCRATCH_BYTES = RING_BYTES + LIT_BYTES;   // per resident wave: match ring, literal stream
 constexpr uint32_t SPAN = 1536;           // resolve batch: output bytes covered by the source map
 constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
 static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
-constexpr uint32_t SVN = (SPAN / 4u + 2u + WAVE - 1u) / WAVE;   // span dwords per lane (plain output)
-#ifndef HZ2_RG
-#define HZ2_RG 8
-#endif
-constexpr uint32_t RG = HZ2_RG;           // resolve (unshuffled output): bytes a lane loads before it stores
-#ifndef HZ2_RGP
-#define HZ2_RGP 24
-#endif
-constexpr uint32_t RGP = HZ2_RGP;         // resolve (plain output): bytes a lane resolves per load round trip
-#ifndef HZ2_DW
-#define HZ2_DW 2
-#endif
-constexpr uint32_t DW = HZ2_DW;           // resolve (plain output): dwords a lane loads before it stores
-#ifndef HZ2_OWIN
-#define HZ2_OWIN 16
-#endif
-constexpr uint32_t OWIN = HZ2_OWIN;       // phase E (plain output): literal window bytes per lane (aligned,
-                                          // written whole: partial cache lines cost an L2 fill + write-back)
-static_assert(OWIN == 16 || OWIN == 32 || OWIN == 64, "OWIN: 16, 32 or 64 bytes (the byte mask is 64 bits)");
-constexpr uint32_t OSH = OWIN == 16 ? 4u : OWIN == 32 ? 5u : 6u;
-#if HZ2_OWIN == 64
-typedef uint64_t OMask;
-#else
-typedef uint32_t OMask;
-#endif
+static_assert(SPL <= 24, "resolve slots per lane");
+constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = lane + 64 i)
 // phase E: match records are staged per lane and stored as whole aligned 32-byte groups
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
 // bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
@@ -113,12 +93,15 @@ constexpr uint32_t SYNC_NONE = 0xfeu;     // predecessor ended (EOB / ERR / CUT)
 constexpr uint32_t SYNC_FAIL = 0xffu;     // predecessor never met this lane's recorded path
 constexpr uint32_t END_NONE = 0, END_EOB = 1, END_ERR = 2, END_CUT = 3;
 
-// record: bits 0-10 token start relative to the segment, 11-23 output bytes, 24-28 matches
-// (cumulative from the lane's first record; K tokens of <= 48 bits / <= 258 bytes fit)
-HZ_HD uint32_t rec_pack(uint32_t rel, uint32_t o, uint32_t m) { return rel | (o << 11) | (m << 24); }
-HZ_HD uint32_t rec_rel(uint32_t r) { return r & 0x7ffu; }
-HZ_HD uint32_t rec_out(uint32_t r) { return (r >> 11) & 0x1fffu; }
-HZ_HD uint32_t rec_mat(uint32_t r) { return r >> 24; }
+// record: bits 0-9 token start relative to the segment, 10-21 output bytes, 22-26 matches,
+// 27-31 literals (cumulative from the lane's first record: the first record lies within 48
+// bits of the segment start, and K - 1 <= 15 tokens of <= 48 bits / <= 258 bytes follow)
+static_assert(K >= 1 && K <= 16, "record fields hold K <= 16 tokens");
+HZ_HD uint32_t rec_pack(uint32_t rel, uint32_t o, uint32_t m, uint32_t l) { return rel | (o << 10) | (m << 22) | (l << 27); }
+HZ_HD uint32_t rec_rel(uint32_t r) { return r & 0x3ffu; }
+HZ_HD uint32_t rec_out(uint32_t r) { return (r >> 10) & 0xfffu; }
+HZ_HD uint32_t rec_mat(uint32_t r) { return (r >> 22) & 31u; }
+HZ_HD uint32_t rec_lit(uint32_t r) { return r >> 27; }
 
 struct alignas(16) Shared {
   uint16_t lut_ll[(1 << LL_ROOT) + LL_SUB];
@@ -143,14 +126,14 @@ struct alignas(16) Shared {
         uint32_t hbits[256];          // dynamic block header: 8192 stream bits from the header's quad
         uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
         struct {                      // phase E
-          alignas(16) uint8_t ostage[WAVE][OWIN];   // plain output: each lane's current literal window
+          alignas(16) uint8_t ostage[WAVE][16];     // each lane's current 16 bytes of the literal stream
           uint64_t rstage[WAVE][RGRP];              // each lane's current group of match records
         };
       };
     };
     struct {                      // phase M
-      uint16_t smap[SPAN];        // batch byte -> distance to its source (0: literal)
-      uint32_t sbuf[SPAN / 4 + 2];   // plain output: the batch's aligned dwords, patched in LDS
+      uint16_t smap[SPAN + 2];    // batch byte -> distance to its source (0: literal); [SPAN] stays 0
+      uint32_t sbuf[SPAN / 4 + 2];   // the batch's aligned dwords, assembled in LDS
     };
   };
   uint32_t syncw[WAVE];           // record index where the predecessor met this lane / SYNC_*
@@ -476,6 +459,7 @@ struct BR {
   uint32_t w0, w1, w2, sh, c;
   uint32_t n0, n1;
   uint32_t wr;
+  uint32_t slot;       // (c + 3) % RS, kept incrementally (no division per token)
 };
 
 HZ_HD uint32_t br_pos(const BR& r) { return r.c * 32u + r.sh; }
@@ -491,7 +475,7 @@ HZ_HD void br_put(Shared& sh, int lane, uint32_t j, uint32_t a0, uint32_t a1, ui
 
 // ring words c+3 and c+4 (slot (c+3) % RS and the next; the mirror covers the wrap)
 HZ_HD void br_next(const Shared& sh, int lane, BR& r) {
-  const uint32_t k = (r.c + 3u) % RS;
+  const uint32_t k = r.slot;
   r.n0 = sh.bring[k][lane];
   r.n1 = sh.bring[k + 1u][lane];
 }
@@ -526,6 +510,7 @@ HZ_HD void br_init(Shared& sh, int lane, const Src& S, BR& r, uint32_t p) {
   r.w2 = i == 0u ? a[2] : i == 1u ? a[3] : i == 2u ? a[4] : a[5];
   r.sh = p & 31u;
   r.c = c;
+  r.slot = (c + 3u) % RS;
   br_put(sh, lane, q, a[0], a[1], a[2], a[3]);
   br_put(sh, lane, q + 4u, a[4], a[5], a[6], a[7]);
   r.wr = q + 8u;
@@ -535,23 +520,21 @@ HZ_HD void br_init(Shared& sh, int lane, const Src& S, BR& r, uint32_t p) {
 HZ_HD void br_tick(Shared& sh, int lane, const Src& S, BR& r) { br_fill(sh, lane, S, r); }
 
 // advance by n <= 48 bits (n0 n1 must hold ring words c+3, c+4).  The window moves by
-// k = 0, 1 or 2 words as masked merges of SSA values: written as selects between fields of
-// the reader, the compiler turns them into an indexed load of the struct (a scratch copy)
+// k = 0, 1 or 2 words: two compares and three pairs of selects (v_cndmask) of SSA values
+// (written as selects between fields of the reader, the compiler turns them into an indexed
+// load of the struct -- a scratch copy)
 HZ_HD void br_adv(BR& r, uint32_t n) {
   const uint32_t a0 = r.w0, a1 = r.w1, a2 = r.w2, a3 = r.n0, a4 = r.n1;
   const uint32_t t = r.sh + n;
   const uint32_t k = t >> 5;
-#if HZ_GPU
-  const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)(k + 1u), 1, 1);   // k >= 1: all ones
-  const uint32_t m2 = (uint32_t)__builtin_amdgcn_sbfe((int)k, 1, 1);          // k >= 2: all ones
-#else
-  const uint32_t m1 = k >= 1u ? ~0u : 0u, m2 = k >= 2u ? ~0u : 0u;
-#endif
-  r.w0 = a0 ^ ((a0 ^ a1) & m1) ^ ((a1 ^ a2) & m2);
-  r.w1 = a1 ^ ((a1 ^ a2) & m1) ^ ((a2 ^ a3) & m2);
-  r.w2 = a2 ^ ((a2 ^ a3) & m1) ^ ((a3 ^ a4) & m2);
+  const bool k1 = t >= 32u, k2 = t >= 64u;
+  r.w0 = k2 ? a2 : k1 ? a1 : a0;
+  r.w1 = k2 ? a3 : k1 ? a2 : a1;
+  r.w2 = k2 ? a4 : k1 ? a3 : a2;
   r.sh = t & 31u;
   r.c += k;
+  const uint32_t s2 = r.slot + k, s3 = s2 - RS;      // (c + 3) % RS without a division
+  r.slot = s3 < s2 ? s3 : s2;
 }
 
 HZ_HD uint32_t bfe32(uint32_t v, uint32_t off, uint32_t w) {
@@ -570,6 +553,11 @@ HZ_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
+#if HZ_GPU && defined(HZ2_MARKS)
+#define HZ2_MARK(s) asm volatile(";@@" s)
+#else
+#define HZ2_MARK(s) do { } while (0)
+#endif
 #if HZ_GPU
 #define HZ2_HM __device__ __forceinline__
 #else
@@ -593,29 +581,32 @@ struct Tok {
 };
 
 // one token at the reader's position, from the rich tables (hz::ent_rich): literal/length
-// symbol, its extra bits, the distance symbol and its extra bits all from the 64-bit window
+// symbol, its extra bits, the distance symbol and its extra bits all from the 64-bit window.
+// Branch-free but for the rare second-level lookups: the distance lookup is made for every
+// token (a literal's is ignored) -- the wave waits for its slowest lane anyway, and a
+// literal/match branch costs both paths plus the exec-mask bookkeeping on every token
 HZ_HD Tok rtok(const Shared* sh, const BR& r) {
   const uint32_t lo = funnel(r.w1, r.w0, r.sh), hi = funnel(r.w2, r.w1, r.sh);
   uint32_t e = sh->lut_ll[lo & ((1u << LL_ROOT) - 1u)];
   if (!(e & 15u)) e = sh->lut_ll[(1u << LL_ROOT) + ((e >> 4) & 511u) + bfe32(lo, LL_ROOT, e >> 13)];
   const uint32_t nb = e & 15u, x = (e >> 4) & 7u, v = e >> 7;
-  Tok t;
-  if (x == 7u) {                                // literal, EOB or an invalid code
-    t.n = nb;
-    t.kind = v < 256u ? TK_LIT : v == 256u ? TK_EOB : TK_ERR;
-    t.len = 1u;
-    t.v = v;
-    return t;
-  }
-  const uint32_t s1 = nb + x;
-  t.len = v + bfe32(lo, nb, x);
+  const bool lit = x == 7u;                     // literal, EOB or an invalid code
+  const uint32_t s1 = nb + x;                   // < 32 for every entry
   const uint32_t dl = funnel(hi, lo, s1);
-  uint32_t ed = sh->lut_d[dl & ((1u << D_ROOT) - 1u)];
+  // a literal looks up distance entry 0 -- the shortest code's, never a second-level pointer
+  // -- so the second-level branch below does not depend on the literal / match split
+  uint32_t ed = sh->lut_d[dl & (lit ? 0u : (1u << D_ROOT) - 1u)];
   if (!(ed & 15u)) ed = sh->lut_d[(1u << D_ROOT) + ((ed >> 4) & 511u) + bfe32(dl, D_ROOT, ed >> 13)];
   const uint32_t nd = ed & 15u, xd = (ed >> 4) & 15u;
-  t.v = (((ed >> 8) & 7u) << xd) + ((ed >> 11) & 1u) + bfe32(dl, nd, xd);
-  t.kind = (ed >> 12) & 1u ? TK_ERR : TK_MATCH;
-  t.n = s1 + ((ed >> 12) & 1u ? nd : nd + xd);
+  const bool derr = (ed >> 12) & 1u;
+  const uint32_t dist = (((ed >> 8) & 7u) << xd) + ((ed >> 11) & 1u) + bfe32(dl, nd, xd);
+  const uint32_t lk = v < 256u ? (uint32_t)TK_LIT : v == 256u ? (uint32_t)TK_EOB : (uint32_t)TK_ERR;
+  const uint32_t mk = derr ? (uint32_t)TK_ERR : (uint32_t)TK_MATCH;
+  Tok t;
+  t.n = lit ? nb : s1 + nd + (derr ? 0u : xd);
+  t.kind = lit ? lk : mk;
+  t.len = lit ? 1u : v + bfe32(lo, nb, x);
+  t.v = lit ? v : dist;
   return t;
 }
 
@@ -669,9 +660,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
 
 namespace hz2 {
 
-// PERM: the job's output map is an unshuffle (F2 chunks, shuffled Blosc blocks); otherwise
-// stream byte x is dst[x] and the resolve stores whole aligned dwords
-template <class StatsT, bool PERM>
+// rank of this lane among the set lanes of a ballot (v_mbcnt)
+HZ_HD uint32_t lane_rank(uint64_t m, int lane) {
+#if HZ_GPU
+  (void)lane;
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+#else
+  return hz::popc64(m & ((1ull << lane) - 1ull));
+#endif
+}
+
+// stream byte x is dst[x] (a shuffled chunk is inflated into staging and unshuffled after);
+// ring_base: the wave's SCRATCH_BYTES (match ring, then the literal stream)
+template <class StatsT>
 #if HZ_GPU
 __device__ __forceinline__
 #else
@@ -691,7 +692,8 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
   typedef uint64_t hz_gu64;
 #endif
   hz_gu64* const ring64 = HZ_GLOBAL(hz_gu64*, ring_base);
-  const Perm P = job.perm;
+  hz_gu8* const lits = HZ_GLOBAL(hz_gu8*, ring_base + RING_BYTES);
+  if (job.perm.n > 1u) return ST_SIZE;      // no output map: shuffled streams are staged
 
   LANE_VAR(uint32_t, s1);     // adler32 partial sums of the bytes this lane wrote: sum b, sum pos*b
   LANE_VAR(uint32_t, s2);
@@ -742,7 +744,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         uint32_t a1 = LV(s1), a2 = LV(s2);
         for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
           const uint32_t b = S.base[sb + i];
-          dst[PERM ? perm_at(P, out + i) : out + i] = (uint8_t)b;
+          dst[out + i] = (uint8_t)b;
           a1 += b;
           a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
         }
@@ -881,6 +883,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       LANE_VAR(BR, rd);
       LANE_VAR(uint32_t, co);      // output bytes since the first record
       LANE_VAR(uint32_t, cm);      // matches since the first record
+      LANE_VAR(uint32_t, cl);      // literals since the first record
       LANE_VAR(uint32_t, ek);      // END_*
       LANE_VAR(uint32_t, ea);      // position after the EOB token
       LANE_LOOP {
@@ -889,28 +892,40 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         BR r;
         br_init(sh, lane, S, r, p0);
         uint32_t steps = 0;
-        uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0;
+        uint32_t nr = 0, o = 0, m = 0, l = 0, e = END_NONE, after = 0;
         // one loop for the warm-up (tokens before ss are decoded and dropped: whatever they
-        // are, even invalid codes, which advance by their table length) and the segment
+        // are, even invalid codes, which advance by their table length) and the segment.
+        // Branch-free body: the only exit is at the top (a token that ends the lane sets e
+        // and does not advance, so the next test fails)
         for (;;) {
+          HZ2_MARK("A_TOP");
           const uint32_t tp = br_pos(r);
-          if (tp >= se) break;
+          if (tp >= se || e != END_NONE) break;
           br_next(sh, lane, r);
           const bool inseg = tp >= ss;
-          if (inseg && nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m); nr++; }
-          const Tok t = rtok(&sh, r);
-          if (inseg) {
-            if (t.kind >= TK_EOB) { e = t.kind == TK_EOB ? END_EOB : END_ERR; after = tp + t.n; break; }
-            if (m >= MCAP_LANE && t.kind == TK_MATCH) { e = END_CUT; break; }
-            o += t.len;
-            m += t.kind;
+          {
+            // a record past the K-th (or in the warm-up) goes to the lane's endp word,
+            // which phase A' overwrites
+            const bool rk = inseg && nr < (uint32_t)K;
+            uint32_t* rp = rk ? &sh.rec[nr < (uint32_t)K ? nr : 0u][lane] : &sh.endp[lane];
+            *rp = rec_pack(tp - ss, o, m, l);
+            nr += rk ? 1u : 0u;
           }
-          br_adv(r, t.n);
+          const Tok t = rtok(&sh, r);
+          const bool ismatch = t.kind == TK_MATCH, islit = t.kind == TK_LIT;
+          const bool stop = inseg && (t.kind >= TK_EOB || (ismatch && m >= MCAP_LANE) || (islit && l >= LCAP_LANE));
+          e = stop ? (t.kind == TK_EOB ? END_EOB : t.kind == TK_ERR ? END_ERR : END_CUT) : e;
+          after = stop ? tp + t.n : after;
+          const bool cnt = inseg && !stop;
+          o += cnt ? t.len : 0u;
+          m += (cnt && ismatch) ? 1u : 0u;
+          l += (cnt && islit) ? 1u : 0u;
+          br_adv(r, stop ? 0u : t.n);
           HZ2_RTICK(steps);
         }
         sh.nrec[lane] = nr;
         sh.syncw[lane] = lane == 0 ? 0u : SYNC_NONE;
-        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;
+        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;
         if (stats) stats->steps_a += steps;
       }
       WAVE_SYNC();
@@ -921,7 +936,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
 #define HZ2_CONTINUE(lane_)                                                                      \
       do {                                                                                       \
         BR r = LV(rd);                                                                           \
-        uint32_t o = LV(co), m = LV(cm), e = LV(ek), after = LV(ea);                             \
+        uint32_t o = LV(co), m = LV(cm), l = LV(cl), e = LV(ek), after = LV(ea);                 \
         uint32_t res = SYNC_NONE;                                                                \
         if (e == END_NONE && (lane_) < 63) {                                                     \
           const uint32_t base = ws + (uint32_t)((lane_) + 1) * L;                                \
@@ -939,16 +954,19 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             if (t.kind >= hz2::TK_EOB) {                                                         \
               e = t.kind == hz2::TK_EOB ? END_EOB : END_ERR; after = tp + t.n; res = SYNC_NONE; break; \
             }                                                                                    \
-            if (m >= MCAP_LANE && t.kind == hz2::TK_MATCH) { e = END_CUT; res = SYNC_NONE; break; } \
+            if ((t.kind == hz2::TK_MATCH && m >= MCAP_LANE) || (t.kind == hz2::TK_LIT && l >= LCAP_LANE)) { \
+              e = END_CUT; res = SYNC_NONE; break;                                               \
+            }                                                                                    \
             o += t.len;                                                                          \
-            m += t.kind;                                                                         \
+            m += t.kind == hz2::TK_MATCH ? 1u : 0u;                                              \
+            l += t.kind == hz2::TK_LIT ? 1u : 0u;                                                \
             hz2::br_adv(r, t.n);                                                                 \
             HZ2_RTICK(ct);                                                                       \
           }                                                                                      \
         }                                                                                        \
         if ((lane_) < 63) sh.syncw[(lane_) + 1] = res;                                           \
         sh.endp[lane_] = hz2::br_pos(r);                                                         \
-        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;                          \
+        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;              \
       } while (0)
       LANE_LOOP { HZ2_CONTINUE(lane); }
       WAVE_SYNC();
@@ -967,23 +985,24 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
             BR r;
             br_init(sh, lane, S, r, sh.endp[lane - 1]);
-            uint32_t nr = 0, o = 0, m = 0, e = END_NONE, after = 0, ct = 0;
+            uint32_t nr = 0, o = 0, m = 0, l = 0, e = END_NONE, after = 0, ct = 0;
             for (;;) {
               const uint32_t tp = br_pos(r);
               if (!(tp < se || nr == 0)) break;
               br_next(sh, lane, r);
-              if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m); nr++; }
+              if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m, l); nr++; }
               const Tok t = rtok(&sh, r);
               if (t.kind >= TK_EOB) { e = t.kind == TK_EOB ? END_EOB : END_ERR; after = tp + t.n; break; }
-              if (m >= MCAP_LANE && t.kind == TK_MATCH) { e = END_CUT; break; }
+              if ((t.kind == TK_MATCH && m >= MCAP_LANE) || (t.kind == TK_LIT && l >= LCAP_LANE)) { e = END_CUT; break; }
               o += t.len;
-              m += t.kind;
+              m += t.kind == TK_MATCH ? 1u : 0u;
+              l += t.kind == TK_LIT ? 1u : 0u;
               br_adv(r, t.n);
               HZ2_RTICK(ct);
             }
             sh.nrec[lane] = nr;
             sh.syncw[lane] = 0;                       // its path starts at record 0
-            LV(rd) = r; LV(co) = o; LV(cm) = m; LV(ek) = e; LV(ea) = after;
+            LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;
           }
         }
         WAVE_SYNC();
@@ -1004,17 +1023,19 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       }
       LANE_VAR(uint32_t, wout);
       LANE_VAR(uint32_t, wmat);
+      LANE_VAR(uint32_t, wlit);
       LANE_VAR(uint32_t, sbit);    // exact start bit of the lane's range
       LANE_LOOP {
-        uint32_t wo = 0, wm = 0, sb = 0;
+        uint32_t wo = 0, wm = 0, wl = 0, sb = 0;
         if ((uint32_t)lane < V) {
           const uint32_t k = sh.syncw[lane];
           const uint32_t rc = sh.rec[k][lane];
           wo = LV(co) - rec_out(rc);
           wm = LV(cm) - rec_mat(rc);
+          wl = LV(cl) - rec_lit(rc);
           sb = ws + (uint32_t)lane * L + rec_rel(rc);
         }
-        LV(wout) = wo; LV(wmat) = wm; LV(sbit) = sb;
+        LV(wout) = wo; LV(wmat) = wm; LV(wlit) = wl; LV(sbit) = sb;
       }
       // the first valid lane that ended (EOB / ERR / CUT) closes the window
       int end_lane = -1;
@@ -1026,7 +1047,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       if (stats) stats->lanes_valid += V;
       uint32_t end_kind = END_NONE, npos = 0;
       LANE_LOOP {
-        if ((uint32_t)lane >= V) { LV(wout) = 0; LV(wmat) = 0; }
+        if ((uint32_t)lane >= V) { LV(wout) = 0; LV(wmat) = 0; LV(wlit) = 0; }
         if (lane == (end_lane >= 0 ? end_lane : (int)V - 1)) {
           sh.u_status = (int32_t)LV(ek);
           sh.u_pos = LV(ek) == END_EOB ? LV(ea) : sh.endp[lane];
@@ -1043,26 +1064,32 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       }
       LANE_VAR(uint32_t, obase);
       LANE_VAR(uint32_t, mbase);
-      uint32_t wtotal = 0, mtotal = 0;
+      LANE_VAR(uint32_t, lbase);
+      uint32_t wtotal = 0, mtotal = 0, ltotal = 0;
 #if HZ_GPU
       obase = wave_excl_scan32(wout);
       mbase = wave_excl_scan32(wmat);
+      lbase = wave_excl_scan32(wlit);
       wtotal = hz::wave_sum(wout);
       mtotal = hz::wave_sum(wmat);
+      ltotal = hz::wave_sum(wlit);
 #else
-      for (int lane = 0; lane < 64; lane++) { obase[lane] = wtotal; mbase[lane] = mtotal; wtotal += wout[lane]; mtotal += wmat[lane]; }
+      for (int lane = 0; lane < 64; lane++) {
+        obase[lane] = wtotal; mbase[lane] = mtotal; lbase[lane] = ltotal;
+        wtotal += wout[lane]; mtotal += wmat[lane]; ltotal += wlit[lane];
+      }
 #endif
+      (void)ltotal;
       if (stats) stats->matches += mtotal;
       if (out + wtotal > dst_len) return ST_SIZE;
       if (npos > limit_bits) return ST_TRUNC;
 
       HZ_T(7);
-      // -------- phase E: exact decode of every valid range; literals to dst, matches to the ring --------
-      // Stores are the cost here (every store is a separate memory request): matches go to
-      // the ring in 16-byte pairs, and on plain output each lane's literals are gathered in
-      // its 32-byte LDS window and written as two 16-byte stores (match bytes in between get
-      // stale bytes that phase M overwrites); windows that reach outside the lane's own range
-      // write their literals byte by byte.
+      // -------- phase E: exact decode of every valid range --------
+      // Nothing goes to dst here: literal bytes go to the window's literal stream (lane i's
+      // literals at lbase[i]..., staged 16 bytes at a time in LDS and stored whole), matches
+      // to the match ring as (position, length, distance) records (staged per lane, stored as
+      // aligned groups).  Phase M then writes every output byte of the window exactly once.
       LANE_VAR(int, lerr);
       LANE_LOOP {
         int err = 0;
@@ -1071,81 +1098,68 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           BR r;
           br_init(sh, lane, S, r, LV(sbit));
           const uint32_t stop = sh.endp[lane];
-          const uint32_t lo_x = out + LV(obase), hi_x = lo_x + LV(wout);
-          uint32_t o = lo_x, mi = LV(mbase);
+          uint32_t o = out + LV(obase), mi = LV(mbase);
+          const uint32_t l0 = LV(lbase);
+          uint32_t lk = l0;
           uint32_t a1 = 0;
           uint64_t a2 = 0;
           const uint32_t m0 = mi;                          // the lane's first record
-          const uint32_t A = (uint32_t)((uintptr_t)job.dst & (OWIN - 1u));
-          uint32_t cw = 0xffffffffu;
-          OMask msk = 0;                                   // bytes of the window written
-          auto flush = [&]() {
-            if (!msk) return;
-            const uint32_t wx = (cw << OSH) - A;        // stream position of the window's byte 0
-            if ((int32_t)wx >= (int32_t)lo_x && wx + OWIN <= hi_x) {
-#if HZ_GPU
-              typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-              typedef __attribute__((address_space(1))) u32x4 gu32x4;
-HZ_UNROLL
-              for (uint32_t k = 0; k < OWIN; k += 16u)
-                *(gu32x4*)(dst + wx + k) = *(const u32x4*)&sh.ostage[lane][k];
-#else
-              memcpy(dst + wx, &sh.ostage[lane][0], OWIN);
-#endif
-            } else {
-              for (uint64_t m = msk; m; m &= m - 1u) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                dst[wx + b] = sh.ostage[lane][b];
-              }
-            }
-          };
-          while (br_pos(r) < stop) {
+          // branch-free body but for the two flushes: a token's literal byte and its match
+          // record are both staged unconditionally -- the one that does not apply sits in the
+          // slot the next literal / match overwrites (lk / mi do not move for it)
+          while (br_pos(r) < stop && !err) {
+            HZ2_MARK("E_TOP");
             br_next(sh, lane, r);
             const Tok tk = rtok(&sh, r);
             br_adv(r, tk.n);
             HZ2_RTICK(steps);
-            if (tk.kind == TK_LIT) {
-              const uint32_t t = tk.v;
-#ifndef HZ2_EXP_NOSTORE
-              if (PERM) {
-                dst[perm_at(P, o)] = (uint8_t)t;
-              } else {
-                const uint32_t ax = A + o, w = ax >> OSH;
-                if (w != cw) { flush(); cw = w; msk = 0; }
-                sh.ostage[lane][ax & (OWIN - 1u)] = (uint8_t)t;
-                msk |= (OMask)1 << (ax & (OWIN - 1u));
-              }
-#endif
-              a1 += t;
-              a2 += (uint64_t)o * t;
-              o++;
-            } else {
-              // a match (E decodes ranges A verified: an EOB / invalid code here is a bug)
-              const uint32_t ln = tk.len, d = tk.v;
-              if (d > o || tk.kind != TK_MATCH) { err = 1; break; }
-              const uint64_t rv = (uint64_t)o | ((uint64_t)((ln << 16) | (d - 1u)) << 32);
+            const bool islit = tk.kind == TK_LIT, ismatch = tk.kind == TK_MATCH;
+            // (E decodes ranges A verified: an EOB / invalid code or a distance past the
+            // output start here is a bug, reported as corrupt data)
+            err |= (!islit && (!ismatch || tk.v > o)) ? 1 : 0;
+            sh.ostage[lane][lk & 15u] = (uint8_t)tk.v;
 #if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
-              sh.rstage[lane][mi & (RGRP - 1u)] = rv;
-              if ((mi & (RGRP - 1u)) == RGRP - 1u) {
-                const uint32_t g = mi & ~(RGRP - 1u);
-                if (g >= m0) {                         // a whole group of this lane: 32 bytes at once
+            sh.rstage[lane][mi & (RGRP - 1u)] = (uint64_t)o | ((uint64_t)((tk.len << 16) | (tk.v - 1u)) << 32);
+#endif
+            lk += islit ? 1u : 0u;
+            a1 += islit ? tk.v : 0u;
+            a2 += islit ? (uint64_t)o * tk.v : 0u;
+#ifndef HZ2_EXP_NOSTORE
+            if (islit && !(lk & 15u)) {                  // 16 bytes of the literal stream complete
+              const uint32_t g = lk - 16u;
+              if (g >= l0) {
 #if HZ_GPU
-                  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-                  typedef __attribute__((address_space(1))) u64x2 gu64x2;
-HZ_UNROLL
-                  for (uint32_t k = 0; k < RGRP; k += 2u)
-                    *(gu64x2*)(ring64 + g + k) = *(const u64x2*)&sh.rstage[lane][k];
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(1))) u32x4 gu32x4;
+                *(gu32x4*)(lits + g) = *(const u32x4*)&sh.ostage[lane][0];
 #else
-                  for (uint32_t k = 0; k < RGRP; k++) ring64[g + k] = sh.rstage[lane][k];
+                memcpy(lits + g, &sh.ostage[lane][0], 16);
 #endif
-                } else {                               // the group starts in the previous lane's records
-                  for (uint32_t k = m0; k <= mi; k++) ring64[k] = sh.rstage[lane][k & (RGRP - 1u)];
-                }
+              } else {                                   // the group starts in the previous lane's literals
+                for (uint32_t k = l0; k < lk; k++) lits[k] = sh.ostage[lane][k & 15u];
               }
-#endif
-              mi++;
-              o += ln;
             }
+#endif
+#if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
+            if (ismatch && (mi & (RGRP - 1u)) == RGRP - 1u) {
+              const uint32_t g = mi & ~(RGRP - 1u);
+              if (g >= m0) {                             // a whole group of this lane: stored at once
+#if HZ_GPU
+                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                typedef __attribute__((address_space(1))) u64x2 gu64x2;
+HZ_UNROLL
+                for (uint32_t k = 0; k < RGRP; k += 2u)
+                  *(gu64x2*)(ring64 + g + k) = *(const u64x2*)&sh.rstage[lane][k];
+#else
+                for (uint32_t k = 0; k < RGRP; k++) ring64[g + k] = sh.rstage[lane][k];
+#endif
+              } else {                                   // the group starts in the previous lane's records
+                for (uint32_t k = m0; k <= mi; k++) ring64[k] = sh.rstage[lane][k & (RGRP - 1u)];
+              }
+            }
+#endif
+            mi += ismatch ? 1u : 0u;
+            o += islit ? 1u : ismatch ? tk.len : 0u;
           }
 #if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
           {                                            // the lane's last, partial group
@@ -1154,7 +1168,10 @@ HZ_UNROLL
           }
 #endif
 #ifndef HZ2_EXP_NOSTORE
-          if (!PERM) flush();
+          {                                            // the lane's last, partial 16 literal bytes
+            const uint32_t g = lk & ~15u;
+            for (uint32_t k = g > l0 ? g : l0; k < lk; k++) lits[k] = sh.ostage[lane][k & 15u];
+          }
 #endif
           LV(s1) = (LV(s1) + a1 % ADLER_MOD) % ADLER_MOD;
           LV(s2) = (uint32_t)((LV(s2) + a2 % ADLER_MOD) % ADLER_MOD);
@@ -1166,19 +1183,25 @@ HZ_UNROLL
       WAVE_SYNC_GLOBAL();
 
       HZ_T(8);
-      // -------- phase M: resolve the window's matches, 64 at a time --------
+      // -------- phase M: write the window's output, one span at a time --------
+      // The window's output [out, out + wtotal) is cut into consecutive spans [F, F + span):
+      // span = the frontier F up to the end of the last of the next <= 256 matches that fit
+      // SPAN bytes (a span of literals only when no match fits).  Per span:
+      //   1. smap[x - F] = distance from match byte x to an equal earlier byte (the periodic
+      //      extension of an overlapping copy), literal bytes 0;
+      //   2. pointer jumping: while a byte's source is a match byte of the span, add that
+      //      byte's distance (rounds over all bytes, one LDS round trip each) -- after it every
+      //      match byte's source is either before F (final in dst) or a literal of the span;
+      //   3. every lane gathers its byte slots q = lane + 64 i at once: literals from the
+      //      literal stream (rank among the span's literals by ballot), sources before F from
+      //      dst; in-span sources (literals) then from LDS;
+      //   4. the span's aligned dwords are stored from LDS, whole where they lie inside the
+      //      span (and the stream), byte by byte at its edges.
+      // Every output byte is written once, coalesced; E stored nothing to dst.
       // match bytes' adler sums: a1 < 2^32 and a2 < 2^64 for any window (< 2^24 bytes)
       LANE_VAR(uint32_t, ra1);
       LANE_VAR(uint64_t, ra2);
       LANE_LOOP { LV(ra1) = 0; LV(ra2) = 0; }
-      // batch = the next <= 256 matches whose output span [F, F + span) fits the source map;
-      // lane l holds matches b0 + l + 64 u (u < MPL: coalesced record loads); the next
-      // batch's records are loaded while this one resolves.
-      //   1. every match byte x gets smap[x - F] = distance to its source (periodic
-      //      extension of an overlapping copy), literal bytes 0;
-      //   2. all lanes walk the span byte-strided, follow smap while the source is inside
-      //      the batch and not a literal, load the byte (before the batch: final; a literal:
-      //      written by E) and store it.
       LANE_ARR(uint32_t, ro, MPL);
       LANE_ARR(uint32_t, rw, MPL);
       LANE_LOOP {
@@ -1189,14 +1212,17 @@ HZ_UNROLL
           LV(rw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
         }
       }
+      LANE_LOOP { if (lane == 0) sh.smap[SPAN] = 0; }
+      const uint32_t wend = out + wtotal;
+      uint32_t F = out, L0 = 0;      // frontier and its rank in the literal stream
 #ifdef HZ2_EXP_NOM
-      for (uint32_t b0 = 0; b0 < 0u;) {
+      for (uint32_t b0 = 0; F < 0u;) {
 #else
-      for (uint32_t b0 = 0; b0 < mtotal;) {
+      for (uint32_t b0 = 0; F < wend;) {
 #endif
         HZ_T(8);
+        HZ2_MARK("M_BATCH");
         if (stats) stats->batches++;
-        const uint32_t F = LVA_AT(ro, 0, 0);
         uint32_t nb = 0, open_ = 1;
 HZ_UNROLL
         for (uint32_t u = 0; u < MPL; u++) {
@@ -1205,27 +1231,33 @@ HZ_UNROLL
           nb += open_ ? k : 0u;
           open_ = open_ && k == 64u;
         }
-        const uint32_t last_o = LVA_AT(ro, (nb - 1u) >> 6, (nb - 1u) & 63u);
-        const uint32_t last_w = LVA_AT(rw, (nb - 1u) >> 6, (nb - 1u) & 63u);
-        const uint32_t span = last_o + (last_w >> 16) - F;
-        // plain output: the span's aligned dwords are loaded first, into registers, so their
-        // round trip overlaps the source-map fill and the record prefetch (issued after them,
-        // so waiting for these does not wait for the prefetch)
-        const uint32_t mis = PERM ? 0u : (uint32_t)((uintptr_t)(job.dst + F) & 3u);
+        uint32_t span;
+        if (nb) {
+          const uint32_t last_o = LVA_AT(ro, (nb - 1u) >> 6, (nb - 1u) & 63u);
+          const uint32_t last_w = LVA_AT(rw, (nb - 1u) >> 6, (nb - 1u) & 63u);
+          span = last_o + (last_w >> 16) - F;
+        } else {
+          const uint32_t nxt = b0 < mtotal ? LVA_AT(ro, 0u, 0u) : wend;
+          span = nxt - F < SPAN ? nxt - F : SPAN;
+        }
+        // the span's first dword holds bytes before F (final): loaded now, merged below
+        const uint32_t mis = (uint32_t)((uintptr_t)(job.dst + F) & 3u);
         const uint32_t xa = F - mis;                           // stream position of dword 0
         const uint32_t ndw = (span + mis + 3u) >> 2;
-        LANE_ARR(uint32_t, sv, SVN);
-        if (!PERM) {
-          LANE_LOOP {
-HZ_UNROLL
-            for (uint32_t k = 0; k < SVN; k++) {
-              const uint32_t kk = (uint32_t)lane + 64u * k, x0 = xa + 4u * kk;
-              LV(sv)[k] = (kk < ndw && x0 + 4u <= dst_len && (int32_t)x0 >= 0) ? *(hz_gu32*)(dst + x0) : 0u;
-            }
-          }
-        }
+        const bool head = mis && (int32_t)xa >= 0 && xa + 4u <= dst_len;   // dword 0 loaded (whole-stored)
+        uint32_t hv = 0;
+        if (head) hv = *(hz_gu32*)(dst + xa);
+        // the whole map is cleared (three 16-byte stores per lane): slots past the span read 0
+        static_assert(SPAN * 2u == 48u * WAVE, "smap clear: 48 bytes per lane");
         LANE_LOOP {
-          for (uint32_t q = (uint32_t)lane * 2u; q < span; q += 128u) *(uint32_t*)&sh.smap[q] = 0u;
+#if HZ_GPU
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4* const zp = (u32x4*)&sh.smap[24u * (uint32_t)lane];
+          const u32x4 z = {0u, 0u, 0u, 0u};
+          zp[0] = z; zp[1] = z; zp[2] = z;
+#else
+          memset(&sh.smap[24u * (uint32_t)lane], 0, 48);
+#endif
         }
         WAVE_SYNC();
         if (stats) {
@@ -1244,11 +1276,20 @@ HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) {
             if ((uint32_t)lane + 64u * u < nb) {
               const uint32_t o0 = LV(ro)[u] - F, ln = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
-              // byte t copies o - d + (t mod d): distance d + d * floor(t / d)
+              // byte t copies o - d + (t mod d): distance d + d * floor(t / d).  Four bytes
+              // per iteration (bytes past the match go to the junk entry SPAN + 1): the wave
+              // runs as many iterations as its longest match needs
               uint32_t dist = d, jj = 0;
-              for (uint32_t t = 0; t < ln; t++) {
-                sh.smap[o0 + t] = (uint16_t)dist;
-                if (++jj == d) { jj = 0; dist += d; }
+              for (uint32_t t0 = 0; t0 < ln; t0 += 4u) {
+HZ_UNROLL
+                for (uint32_t k = 0; k < 4u; k++) {
+                  const uint32_t t = t0 + k;
+                  sh.smap[t < ln ? o0 + t : SPAN + 1u] = (uint16_t)dist;
+                  jj++;
+                  const bool w = jj == d;
+                  jj = w ? 0u : jj;
+                  dist += w ? d : 0u;
+                }
               }
             }
           }
@@ -1266,117 +1307,144 @@ HZ_UNROLL
           }
         }
         HZ_T(11);
-        if (PERM) {
-          HZ_T(12);
-          // unshuffled output: byte-strided over the span
+        HZ2_MARK("M_JUMP");
+        // 2. pointer jumping over the span's match bytes (branch-free per slot: a slot's
+        // source index is min(q - d, SPAN), and smap[SPAN] stays 0, so literal slots (d = 0
+        // reads smap[q] = 0), sources before F (q - d wraps) and slots past the span (d = 0)
+        // never move; every slot's entry is written back each round)
+        LANE_ARR(uint32_t, dq, RGP);
+        LANE_LOOP {
+HZ_UNROLL
+          for (uint32_t i = 0; i < RGP; i++) LV(dq)[i] = sh.smap[(uint32_t)lane + 64u * i];
+        }
+        if (nb) {
+          for (;;) {
+            LANE_VAR(uint32_t, chg);
+            LANE_LOOP {
+              uint32_t d2[RGP];
+HZ_UNROLL
+              for (uint32_t i = 0; i < RGP; i++) {
+                const uint32_t y = (uint32_t)lane + 64u * i - LV(dq)[i];
+                d2[i] = sh.smap[y < SPAN ? y : SPAN];
+              }
+              uint32_t c = 0;
+HZ_UNROLL
+              for (uint32_t i = 0; i < RGP; i++) {
+                c |= d2[i];
+                LV(dq)[i] += d2[i];
+              }
+              LV(chg) = c;
+              if (stats) for (uint32_t i = 0; i < RGP; i++) stats->hops += d2[i] != 0u;
+            }
+            if (stats) stats->tokens++;                // (emulator statistic: pointer-jumping rounds)
+            if (!WAVE_BALLOT(LV(chg) != 0u)) break;
+            WAVE_SYNC();
+            LANE_LOOP {
+HZ_UNROLL
+              for (uint32_t i = 0; i < RGP; i++) sh.smap[(uint32_t)lane + 64u * i] = (uint16_t)LV(dq)[i];
+            }
+            WAVE_SYNC();
+          }
+        }
+        HZ_T(12);
+        HZ2_MARK("M_GATHER");
+        // 3. gather, branch-free per slot: two byte loads each (a literal's from the literal
+        // stream -- its rank among the span's literals by ballot -- and a source before F from
+        // dst; the other load reads a harmless in-range byte) and a select; LDS byte writes of
+        // slots that take no byte go to a junk byte past the span buffer
+        constexpr uint32_t JUNK = (SPAN / 4u + 2u) * 4u - 1u;
+        LANE_VAR(uint32_t, vm);                 // slots inside the span
+        LANE_LOOP {
+          const uint32_t nv = span > (uint32_t)lane ? ((span - 1u - (uint32_t)lane) >> 6) + 1u : 0u;
+          LV(vm) = nv >= 32u ? ~0u : (1u << nv) - 1u;
+        }
+        // per-slot flags live as VGPR bit masks (bit i: slot i), not as per-slot predicates:
+        // the compiler would keep 24 of those in SGPR pairs across the batch and spill them
+        LANE_VAR(uint32_t, lb);                 // literal slots
+        LANE_VAR(uint32_t, fb);                 // match bytes whose source lies before F
+        LANE_LOOP { LV(lb) = 0; LV(fb) = 0; if (lane == 0) sh.sbuf[0] = hv; }
+        WAVE_SYNC();
+        uint32_t lcnt = 0;                      // literals of the span so far (wave-uniform)
+        // two halves of GH slots: GH loaded bytes in flight per lane (all 24 spill)
+        constexpr uint32_t GH = RGP / 2u;
+HZ_UNROLL
+        for (uint32_t h = 0; h < RGP; h += GH) {
+          LANE_ARR(uint32_t, bv, GH);
+HZ_UNROLL
+          for (uint32_t k = 0; k < GH; k++) {
+            const uint32_t i = h + k;
+            const uint64_t bm = WAVE_BALLOT(((LV(vm) >> i) & 1u) && LV(dq)[i] == 0u);
+            LANE_LOOP {
+              const uint32_t q = (uint32_t)lane + 64u * i, d = LV(dq)[i];
+              const uint32_t isl = (LV(vm) >> i) & (d == 0u ? 1u : 0u);
+              const uint32_t far = d > q ? 1u : 0u;      // (never for a slot past the span: d = 0)
+              LV(lb) |= isl << i;
+              LV(fb) |= far << i;
+              // one load: the 64-bit address selected as an integer (a pointer select becomes
+              // a branch), a harmless in-range byte of dst (F) for slots that take no byte
+              const uint64_t la = (uint64_t)(uintptr_t)lits + L0 + lcnt + hz2::lane_rank(bm, lane);
+              const uint64_t da = (uint64_t)(uintptr_t)dst + (far ? F + q - d : F);
+              LV(bv)[k] = *HZ_GLOBAL(hz_gcu8*, (uintptr_t)(isl ? la : da));
+              if (stats && far) stats->src_far[d - q <= 256u ? 0 : d - q <= 1536u ? 1 : d - q <= 4096u ? 2 : 3]++;
+            }
+            lcnt += (uint32_t)hz::popc64(bm);
+          }
           LANE_LOOP {
-            // adler: sum b and the batch-relative sum (x - F) b in 32 bits (a lane's <= SPAN/64
-            // bytes of the batch keep it below 2^32), folded into the 64-bit sum once per batch
-            uint32_t a1 = 0, b2 = 0;
-            for (uint32_t h0 = 0; h0 < span; h0 += RG * 64u) {
-              uint32_t src[RG];
+            uint32_t a1 = 0, b2 = 0;       // match bytes: sum b, batch-relative sum (x - F) b
+            uint8_t* const sb = (uint8_t*)sh.sbuf;
+            const uint32_t tb = LV(lb) | LV(fb);
 HZ_UNROLL
-              for (uint32_t i = 0; i < RG; i++) {
-                const uint32_t q = h0 + (uint32_t)lane + 64u * i;
-                uint32_t y = 0xffffffffu;
-                if (q < span) {
-                  const uint32_t dq = sh.smap[q];
-                  if (dq) {
-                    y = F + q - dq;
-                    while (y >= F) {            // inside the batch: follow an earlier match byte
-                      const uint32_t d2 = sh.smap[y - F];
-                      if (!d2) break;
-                      y -= d2;
-                      if (stats) stats->hops++;
-                    }
-                  }
-                }
-                src[i] = y;
-              }
-              uint32_t bv[RG];
-HZ_UNROLL
-              for (uint32_t i = 0; i < RG; i++) bv[i] = src[i] != 0xffffffffu ? (uint32_t)dst[perm_at(P, src[i])] : 0u;
-HZ_UNROLL
-              for (uint32_t i = 0; i < RG; i++) {
-                if (src[i] != 0xffffffffu) {
-                  const uint32_t x = F + h0 + (uint32_t)lane + 64u * i;
-                  dst[perm_at(P, x)] = (uint8_t)bv[i];
-                  a1 += bv[i];
-                  b2 += (x - F) * bv[i];
-                }
-              }
+            for (uint32_t k = 0; k < GH; k++) {
+              const uint32_t i = h + k;
+              const uint32_t q = (uint32_t)lane + 64u * i, v = LV(bv)[k];
+              const uint32_t far = (LV(fb) >> i) & 1u;
+              sb[((tb >> i) & 1u) ? q + mis : JUNK] = (uint8_t)v;
+              a1 += far * v;
+              b2 += far * (q * v);
             }
             LV(ra1) += a1;
             LV(ra2) += (uint64_t)F * a1 + b2;
           }
-        } else {
-          // plain output: the aligned dwords covering the span are loaded (coalesced) into
-          // LDS, every match byte's source is gathered into them (a source before the batch
-          // from dst, a literal of the batch from LDS), and the dwords are stored back
-          // (coalesced) -- one load round trip and one store drain per batch.  Dwords
-          // reaching outside the stream's output store their match bytes one by one.
-          LANE_LOOP {
+        }
+        WAVE_SYNC();
+        // in-span sources: literals of the span, now in LDS
+        LANE_LOOP {
+          uint32_t a1 = 0, b2 = 0;
+          uint8_t* const sb = (uint8_t*)sh.sbuf;
+          const uint32_t ib = LV(vm) & ~(LV(lb) | LV(fb));
+          uint32_t v[RGP];
 HZ_UNROLL
-            for (uint32_t k = 0; k < SVN; k++) {
-              const uint32_t kk = (uint32_t)lane + 64u * k;
-              if (kk < ndw) sh.sbuf[kk] = LV(sv)[k];
-            }
+          for (uint32_t i = 0; i < RGP; i++) {
+            const uint32_t q = (uint32_t)lane + 64u * i;
+            v[i] = sb[((ib >> i) & 1u) ? q - LV(dq)[i] + mis : JUNK];
           }
-          WAVE_SYNC();
-          HZ_T(12);
-          LANE_LOOP {
-            uint32_t a1 = 0, b2 = 0;                          // as above
-            for (uint32_t h0 = 0; h0 < span; h0 += RGP * 64u) {
-              // each match byte's source is chased through the map and its load issued at
-              // once (a literal of the batch from LDS, anything before the batch from dst);
-              // only the values and a match-byte mask stay live until the loads land
-              uint32_t bv[RGP];
-              uint32_t mb = 0;
 HZ_UNROLL
-              for (uint32_t i = 0; i < RGP; i++) {
-                const uint32_t q = h0 + (uint32_t)lane + 64u * i;
-                bv[i] = 0u;
-                if (q < span) {
-                  const uint32_t dq = sh.smap[q];
-                  if (dq) {
-                    uint32_t y = F + q - dq;
-                    while (y >= F) {
-                      const uint32_t d2 = sh.smap[y - F];
-                      if (!d2) break;
-                      y -= d2;
-                      if (stats) stats->hops++;
-                    }
-                    if (stats) {
-                      if (y >= F) stats->src_in++;
-                      else stats->src_far[F - y <= 256u ? 0 : F - y <= 1536u ? 1 : F - y <= 4096u ? 2 : 3]++;
-                    }
-                    if (y >= F) { const uint32_t by = y - xa; bv[i] = (sh.sbuf[by >> 2] >> (8u * (by & 3u))) & 0xffu; }
-                    else bv[i] = dst[y];
-                    mb |= 1u << i;
-                  }
-                }
-              }
-HZ_UNROLL
-              for (uint32_t i = 0; i < RGP; i++) {
-                if ((mb >> i) & 1u) {
-                  const uint32_t q = h0 + (uint32_t)lane + 64u * i, x = F + q, bx = x - xa;
-                  ((uint8_t*)sh.sbuf)[bx] = (uint8_t)bv[i];
-                  a1 += bv[i];
-                  b2 += (x - F) * bv[i];
-                  const uint32_t x0 = xa + (bx & ~3u);               // its dword, as in the stores below
-                  if (!(x0 + 4u <= dst_len && (int32_t)x0 >= 0)) dst[x] = (uint8_t)bv[i];
-                }
-              }
-            }
-            LV(ra1) += a1;
-            LV(ra2) += (uint64_t)F * a1 + b2;
+          for (uint32_t i = 0; i < RGP; i++) {
+            const uint32_t q = (uint32_t)lane + 64u * i, inb = (ib >> i) & 1u;
+            sb[inb ? q + mis : JUNK] = (uint8_t)v[i];
+            a1 += inb * v[i];
+            b2 += inb * (q * v[i]);
+            if (stats && inb) stats->src_in++;
           }
-          WAVE_SYNC();
-          HZ_T(13);
-          LANE_LOOP {
-            for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
-              const uint32_t x0 = xa + 4u * k;
-              if (x0 + 4u <= dst_len && (int32_t)x0 >= 0) *(hz_gu32*)(dst + x0) = sh.sbuf[k];
+          LV(ra1) += a1;
+          LV(ra2) += (uint64_t)F * a1 + b2;
+        }
+        WAVE_SYNC();
+        HZ_T(13);
+        HZ2_MARK("M_STORE");
+        // 4. store: whole dwords inside the span (dword 0 also when its head was loaded) and
+        // the stream; the span's edge bytes one by one
+        LANE_LOOP {
+          for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
+            const uint32_t x0 = xa + 4u * k;
+            const bool inside = (int32_t)x0 >= 0 && x0 + 4u <= dst_len && x0 + 4u <= F + span && (k > 0u || !mis || head);
+            if (inside) {
+              *(hz_gu32*)(dst + x0) = sh.sbuf[k];
+            } else {
+              for (uint32_t b = 0; b < 4u; b++) {
+                const uint32_t x = x0 + b;
+                if (x >= F && x < F + span && x < dst_len) dst[x] = ((const uint8_t*)sh.sbuf)[4u * k + b];
+              }
             }
           }
         }
@@ -1385,7 +1453,10 @@ HZ_UNROLL
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) { LV(ro)[u] = LV(no)[u]; LV(rw)[u] = LV(nw)[u]; }
         }
+        HZ2_MARK("M_END");
         b0 += nb;
+        F += span;
+        L0 += lcnt;
       }
       LANE_LOOP {
         LV(s1) = (LV(s1) + LV(ra1) % ADLER_MOD) % ADLER_MOD;

@@ -631,6 +631,8 @@ static int blosc_nsplits(int flags, int ts, int64_t blocksize, int leftover) {
   return 1;
 }
 
+static void bshuf_untrans(const uint8_t *in, uint8_t *out, int64_t n, int64_t es);
+
 int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64_t dstcap) {
   if (srclen < 16) return ORC_ERR_FRAME;
   int ver = src[0], verlz = src[1], flags = src[2], ts = src[3];
@@ -646,15 +648,21 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
   int codec = (flags >> 5) & 7;   /* 0 blosclz, 1 lz4/lz4hc, 3 zlib, 4 zstd; 2 snappy unsupported */
   if (codec != 3 && codec != 1 && codec != 0 && codec != 4) return ORC_ERR_UNSUPPORTED;
   if (verlz != 1) return ORC_ERR_FRAME;
-  if (flags & 0x04) return ORC_ERR_UNSUPPORTED; /* bitshuffle inside Blosc */
   if (nbytes == 0) return 0;
   if (bs <= 0 || ts <= 0 || bs > nbytes) return ORC_ERR_FRAME;
   int64_t nblocks = (nbytes + bs - 1) / bs;
   int64_t leftover = nbytes % bs;
   int64_t hdr = 16 + 4 * nblocks;
   if (hdr > cbytes) return ORC_ERR_FRAME;
+  /* c-blosc 1.21 blosc_d: byte unshuffle when 0x01 and typesize > 1, else bit unshuffle
+   * when 0x04 (any typesize) -- bitunshuffle() of format version 2: the block's
+   * bsz / ts elements are untransposed (bshuf_trans_bit_elem inverse) when their count
+   * is a multiple of 8, otherwise the block stays as decoded; tail bytes past the last
+   * whole element stay as decoded.  Pinned against libblosc 1.21.0
+   * (tests/golden/make_blosc_bitshuffle_golden.py). */
   int doshuffle = (flags & 0x01) && ts > 1;
-  uint8_t *tmp = doshuffle ? (uint8_t *)malloc((size_t)bs) : NULL;
+  int dobit = !doshuffle && (flags & 0x04);
+  uint8_t *tmp = (doshuffle || dobit) ? (uint8_t *)malloc((size_t)bs) : NULL;
   int64_t result = nbytes;
   for (int64_t b = 0; b < nblocks; b++) {
     int isleft = (b == nblocks - 1) && leftover;
@@ -663,7 +671,7 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
     int64_t neblock = bsz / nspl;
     int64_t p = (int32_t)rd32(src + 16 + 4 * b);
     if (p < hdr || p >= cbytes) { result = ORC_ERR_FRAME; break; }
-    uint8_t *out = doshuffle ? tmp : dst + b * bs;
+    uint8_t *out = (doshuffle || dobit) ? tmp : dst + b * bs;
     for (int j = 0; j < nspl; j++) {
       if (p + 4 > cbytes) { result = ORC_ERR_FRAME; goto done; }
       int64_t cs = (int32_t)rd32(src + p);
@@ -682,6 +690,15 @@ int64_t orc_blosc_decode(const uint8_t *src, int64_t srclen, uint8_t *dst, int64
       p += cs;
     }
     if (doshuffle) orc_unshuffle(tmp, bsz, ts, dst + b * bs);
+    if (dobit) {
+      const int64_t ne = bsz / ts;
+      if (ne % 8 == 0) {
+        bshuf_untrans(tmp, dst + b * bs, ne, ts);
+        memcpy(dst + b * bs + ne * ts, tmp + ne * ts, (size_t)(bsz - ne * ts));
+      } else {
+        memcpy(dst + b * bs, tmp, (size_t)bsz);
+      }
+    }
   }
 done:
   free(tmp);

@@ -52,3 +52,13 @@ def oracle_lib():
     from oracle import oracle as orc
     orc.lib()
     return orc
+
+
+@pytest.fixture(scope="session")
+def blosc_bit_golden():
+    """Blosc frames with the bitshuffle flag (tests/golden/make_blosc_bitshuffle_golden.py)"""
+    import json
+    import numpy as np
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "blosc_bitshuffle_cases.json")))
+    arrs = np.load(os.path.join(ROOT, "tests", "golden", "blosc_bitshuffle_cases.npz"))
+    return d, arrs

@@ -12,13 +12,23 @@
 extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,
                             int max_rounds, uint32_t over16, uint32_t perm_n, uint32_t dst_off, uint64_t* stats_out) {
   hz2::Shared* sh = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
-  uint8_t* ring = (uint8_t*)malloc(hz2::RING_BYTES);
+  uint8_t* ring = (uint8_t*)malloc(hz2::SCRATCH_BYTES);
   hz2::Stats st = {};
+  // perm_n > 1: the engine's pipeline for shuffled chunks -- inflate into staging, then the
+  // byte unshuffle (unshuffle_kernel) into dst
   const uint32_t n = perm_n < 1 ? 1 : perm_n;
-  hz2::Job job = {src, src_len, dst + dst_off, dst_len, 1u, nullptr, hz2::perm_make(n, dst_len / n, 0)};
+  uint8_t* stage = n > 1 ? (uint8_t*)malloc(dst_len + 16) : nullptr;
+  hz2::Job job = {src, src_len, n > 1 ? stage + (dst_off & 15u) : dst + dst_off, dst_len, 1u, nullptr, hz2::perm_make(1, 1, 0)};
   hz2::Tune tune = {W, max_rounds, over16};
-  int r = n > 1 ? hz2::inflate_stream<hz2::Stats, true>(*sh, job, tune, ring, &st)
-                : hz2::inflate_stream<hz2::Stats, false>(*sh, job, tune, ring, &st);
+  int r = hz2::inflate_stream<hz2::Stats>(*sh, job, tune, ring, &st);
+  if (n > 1) {
+    if (r == 0) {
+      const uint8_t* in = stage + (dst_off & 15u);
+      const uint32_t cnt = dst_len / n, body = cnt * n;
+      for (uint32_t q = 0; q < dst_len; q++) dst[dst_off + q] = q >= body ? in[q] : in[(q % n) * cnt + q / n];
+    }
+    free(stage);
+  }
   if (stats_out) {
     const uint64_t v[] = {st.windows, st.blocks, st.stored, st.tokens, st.matches, st.lanes_valid, st.repairs,
                           st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows, st.fill_max, st.fill_sum, st.span_sum, st.src_in, st.src_far[0], st.src_far[1], st.src_far[2], st.src_far[3]};
