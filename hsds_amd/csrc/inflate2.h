@@ -460,12 +460,13 @@ struct BR {
   uint32_t n0, n1;
   uint32_t wr;
   uint32_t slot;       // (c + 3) % RS, kept incrementally (no division per token)
+  uint32_t wslot;      // wr % RS (a multiple of 4), kept incrementally
 };
 
 HZ_HD uint32_t br_pos(const BR& r) { return r.c * 32u + r.sh; }
 
-HZ_HD void br_put(Shared& sh, int lane, uint32_t j, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
-  const uint32_t k = j % RS;                  // j % 4 == 0 and RS % 4 == 0: the quad never wraps
+// the quad of words at ring slot k (a multiple of 4: with RS % 4 == 0 the quad never wraps)
+HZ_HD void br_put(Shared& sh, int lane, uint32_t k, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
   sh.bring[k][lane] = a0;
   sh.bring[k + 1u][lane] = a1;
   sh.bring[k + 2u][lane] = a2;
@@ -480,22 +481,24 @@ HZ_HD void br_next(const Shared& sh, int lane, BR& r) {
   r.n1 = sh.bring[k + 1u][lane];
 }
 
+HZ_HD uint32_t slot4(uint32_t k) { return k + 4u == RS ? 0u : k + 4u; }
+
 // refill: the quads that fit (their slots hold only words below c+3, i.e. wr <= c + RS - 1),
 // all loads issued before the first write.  Leaves wr in [c + RS, c + RS + 3]: every word a
-// token reads within the next TICKN tokens is in the ring (NEED <= RS).
+// token reads within the next TICKN tokens is in the ring (NEED <= RS).  TICKN tokens read at
+// most 48 TICKN bits, so two quads always restore the ring (and br_init needs two at most)
+static_assert((48u * TICKN + 31u) / 32u <= 8u && RS - 8u + 3u <= 8u, "two quads per refill");
 HZ_HD void br_fill(Shared& sh, int lane, const Src& S, BR& r) {
   if (r.wr + 1u > r.c + RS) return;
-  const uint32_t nq = (r.c + RS + 3u - r.wr) >> 2;     // 1 .. 4
-  uint32_t a[16];
+  const bool two = r.wr + 5u <= r.c + RS;              // room for a second quad
+  uint32_t a[8];
   g_quad(S, r.wr, a[0], a[1], a[2], a[3]);
-  if (nq > 1u) g_quad(S, r.wr + 4u, a[4], a[5], a[6], a[7]);
-  if (nq > 2u) g_quad(S, r.wr + 8u, a[8], a[9], a[10], a[11]);
-  if (nq > 3u) g_quad(S, r.wr + 12u, a[12], a[13], a[14], a[15]);
-  br_put(sh, lane, r.wr, a[0], a[1], a[2], a[3]);
-  if (nq > 1u) br_put(sh, lane, r.wr + 4u, a[4], a[5], a[6], a[7]);
-  if (nq > 2u) br_put(sh, lane, r.wr + 8u, a[8], a[9], a[10], a[11]);
-  if (nq > 3u) br_put(sh, lane, r.wr + 12u, a[12], a[13], a[14], a[15]);
-  r.wr += 4u * nq;
+  if (two) g_quad(S, r.wr + 4u, a[4], a[5], a[6], a[7]);
+  const uint32_t k1 = slot4(r.wslot);
+  br_put(sh, lane, r.wslot, a[0], a[1], a[2], a[3]);
+  if (two) br_put(sh, lane, k1, a[4], a[5], a[6], a[7]);
+  r.wr += two ? 8u : 4u;
+  r.wslot = two ? slot4(k1) : k1;
 }
 
 // position p: the window (words c .. c+2) from two quad loads and a full ring (from quad q)
@@ -511,9 +514,11 @@ HZ_HD void br_init(Shared& sh, int lane, const Src& S, BR& r, uint32_t p) {
   r.sh = p & 31u;
   r.c = c;
   r.slot = (c + 3u) % RS;
-  br_put(sh, lane, q, a[0], a[1], a[2], a[3]);
-  br_put(sh, lane, q + 4u, a[4], a[5], a[6], a[7]);
+  const uint32_t k0 = q % RS, k1 = slot4(k0);
+  br_put(sh, lane, k0, a[0], a[1], a[2], a[3]);
+  br_put(sh, lane, k1, a[4], a[5], a[6], a[7]);
   r.wr = q + 8u;
+  r.wslot = slot4(k1);
   br_fill(sh, lane, S, r);
 }
 
@@ -939,6 +944,8 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         uint32_t o = LV(co), m = LV(cm), l = LV(cl), e = LV(ek), after = LV(ea);                 \
         uint32_t res = SYNC_NONE;                                                                \
         if (e == END_NONE && (lane_) < 63) {                                                     \
+          /* A ticked at most TICKN - 1 tokens ago: refill now, so the tick counter can restart */ \
+          hz2::br_tick(sh, lane, S, r);                                                          \
           const uint32_t base = ws + (uint32_t)((lane_) + 1) * L;                                \
           const uint32_t nrn = sh.nrec[(lane_) + 1];                                             \
           uint32_t k = 0, ct = 0;                                                                \
