@@ -1108,8 +1108,6 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           uint32_t o = out + LV(obase), mi = LV(mbase);
           const uint32_t l0 = LV(lbase);
           uint32_t lk = l0;
-          uint32_t a1 = 0;
-          uint64_t a2 = 0;
           const uint32_t m0 = mi;                          // the lane's first record
           // branch-free body but for the two flushes: a token's literal byte and its match
           // record are both staged unconditionally -- the one that does not apply sits in the
@@ -1129,8 +1127,6 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             sh.rstage[lane][mi & (RGRP - 1u)] = (uint64_t)o | ((uint64_t)((tk.len << 16) | (tk.v - 1u)) << 32);
 #endif
             lk += islit ? 1u : 0u;
-            a1 += islit ? tk.v : 0u;
-            a2 += islit ? (uint64_t)o * tk.v : 0u;
 #ifndef HZ2_EXP_NOSTORE
             if (islit && !(lk & 15u)) {                  // 16 bytes of the literal stream complete
               const uint32_t g = lk - 16u;
@@ -1180,8 +1176,6 @@ HZ_UNROLL
             for (uint32_t k = g > l0 ? g : l0; k < lk; k++) lits[k] = sh.ostage[lane][k & 15u];
           }
 #endif
-          LV(s1) = (LV(s1) + a1 % ADLER_MOD) % ADLER_MOD;
-          LV(s2) = (uint32_t)((LV(s2) + a2 % ADLER_MOD) % ADLER_MOD);
         }
         LV(lerr) = err;
         if (stats) stats->steps_e += steps;
@@ -1397,17 +1391,17 @@ HZ_UNROLL
             lcnt += (uint32_t)hz::popc64(bm);
           }
           LANE_LOOP {
-            uint32_t a1 = 0, b2 = 0;       // match bytes: sum b, batch-relative sum (x - F) b
+            uint32_t a1 = 0, b2 = 0;       // adler: sum b, batch-relative sum (x - F) b
             uint8_t* const sb = (uint8_t*)sh.sbuf;
             const uint32_t tb = LV(lb) | LV(fb);
 HZ_UNROLL
             for (uint32_t k = 0; k < GH; k++) {
               const uint32_t i = h + k;
               const uint32_t q = (uint32_t)lane + 64u * i, v = LV(bv)[k];
-              const uint32_t far = (LV(fb) >> i) & 1u;
-              sb[((tb >> i) & 1u) ? q + mis : JUNK] = (uint8_t)v;
-              a1 += far * v;
-              b2 += far * (q * v);
+              const uint32_t tk = (tb >> i) & 1u;       // a literal or a byte from before F
+              sb[tk ? q + mis : JUNK] = (uint8_t)v;
+              a1 += tk * v;
+              b2 += tk * (q * v);
             }
             LV(ra1) += a1;
             LV(ra2) += (uint64_t)F * a1 + b2;
