@@ -53,7 +53,10 @@ constexpr int LOOK = 4;                     // bytes staged past the segment end
 constexpr uint32_t WIN = SEG - 2 * LOOK;    // farthest match source before the segment
 constexpr uint32_t FARW = 32768;            // zlib window: with a far ring, matches reach this far
                                             // (candidates past the LDS ring come from HBM)
-constexpr int HBITS = 11;
+#ifndef HD_HBITS
+#define HD_HBITS 11
+#endif
+constexpr int HBITS = HD_HBITS;
 constexpr int HSIZE = 1 << HBITS;
 constexpr int LANE_MAX = SEG / WAVE;        // input bytes per lane (a full segment)
 constexpr int TSLOTS = LANE_MAX;            // 16-bit token slots per lane
@@ -69,8 +72,6 @@ struct Tune {
   uint32_t nice;     // stop searching at this match length
   uint32_t too_far;  // length-3 matches farther than this are not taken (zlib TOO_FAR)
   uint32_t stored;   // 1: level 0, stored blocks only
-  uint32_t fast_head; // 1: no exact chains (LZ4 items): prev[p] = the hash head of the
-                      // previous 64-position step, head[h] = any position of this step
   uint32_t far;       // 1: chains continue through the HBM far ring (32 KiB window; zlib
                       // levels >= 6, where ratio outweighs the parse time it costs)
 };
@@ -84,7 +85,6 @@ HZ_HD Tune tune_for_level(int level) {
   Tune t;
   t.too_far = 4096;
   t.stored = level <= 0 ? 1u : 0u;
-  t.fast_head = 0;
   // measured on the cfg5 slab (chain 4, L4): the far ring left the ratio unchanged (1.0018
   // vs libz L4) and cost 45 % more parse time; deeper chains gain ratio only with it
   t.far = far_level(level);
@@ -147,6 +147,19 @@ HZ_HD void lds_add(uint32_t* p, uint32_t v) {
   atomicAdd(p, v);
 #else
   *p += v;
+#endif
+}
+// LDS exchange: returns *p and stores v.  On gfx950 the lanes of one ds_wrxchg_rtn_b32
+// that hit the same address are applied in ascending lane order (measured over 12.8 M
+// lanes at 0..11 hash bits, tools/lds_xchg_order.hip), which is the CPU emulation's
+// sequential lane order.
+HZ_HD uint32_t lds_xchg(uint32_t* p, uint32_t v) {
+#if HZ_GPU
+  return atomicExch(p, v);
+#else
+  const uint32_t o = *p;
+  *p = v;
+  return o;
 #endif
 }
 HZ_HD void lds_or(uint32_t* p, uint32_t v) {
@@ -235,9 +248,15 @@ HZ_HD uint32_t tslot(uint32_t s, int lane) { return ((s >> 1) * (uint32_t)WAVE +
 struct ParseShared {
   uint32_t ring[RWORDS];                 // input bytes, position p at byte p % RING
   uint16_t prev[SEG];                    // (predecessor position) & 0xffff per segment position
-  uint16_t head[HSIZE];                  // (latest position) & 0xffff per hash
-  uint32_t freq[NSYM];
+  // latest position per hash (32-bit: the exchange target).  The greedy parse never reads
+  // the heads, so the symbol counts live in entries [0, NSYM) during it, with those heads
+  // saved in registers (40 KiB in all: 4 parse waves per CU)
+  union {
+    uint32_t head[HSIZE];
+    uint32_t freq[NSYM];
+  };
 };
+static_assert(NSYM <= 5 * WAVE && NSYM <= HSIZE, "head entries saved per lane");
 
 HZ_HD uint32_t rd32(const ParseShared& sh, uint32_t p) {
   const uint32_t w = (p >> 2) & (uint32_t)(RWORDS - 1);
@@ -359,7 +378,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
   LANE_VAR(uint64_t, as2);
   LANE_LOOP {
     LV(as1) = 0; LV(as2) = 0;
-    for (int h = lane; h < HSIZE; h += WAVE) sh.head[h] = 0xffffu;
+    for (int h = lane; h < HSIZE; h += WAVE) sh.head[h] = 0xffffffffu;
   }
   WAVE_SYNC();
 
@@ -388,82 +407,38 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
           }
         }
       }
-      for (int s = lane; s < NSYM; s += WAVE) sh.freq[s] = 0;
     }
     WAVE_SYNC();
 
     const uint32_t lo_pos = s0 > WIN ? s0 - WIN : 0u;   // farthest match source in the LDS ring
-    if (!tune.stored && tune.fast_head) {
-      // ---- approximate chains: every candidate is still an earlier position with the
-      // same hash, so any parse over them is valid; only match quality can differ ----
+    if (!tune.stored) {
+      // ---- exact hash chains, 64 positions per step: one exchange on the head table
+      // gives every position the latest earlier position with its hash (lanes of one
+      // exchange apply in lane order, so a position sees the lower lanes of its step) ----
       HZ_T(2);
       for (uint32_t g = s0; g < s1; g += WAVE) {
-        LANE_VAR(uint32_t, hh);
-        LANE_VAR(uint32_t, hp);
-        LANE_VAR(uint32_t, hn);
         LANE_LOOP {
           const uint32_t p = g + (uint32_t)lane;
-          LV(hh) = KEY_NONE;
-          if (p < s1 && p + 2u < n) LV(hh) = hash3(rd32(sh, p));
+          if (p < s1 && p + 2u < n) sh.prev[p - s0] = (uint16_t)lds_xchg(&sh.head[hash3(rd32(sh, p))], p);
         }
-        HD_NEIGHBOURS(hp, hn, hh);
-        LANE_LOOP {
-          // the position just before, when it has the same hash (runs), else the head
-          const uint32_t p = g + (uint32_t)lane;
-          if (LV(hh) != KEY_NONE)
-            sh.prev[p - s0] = LV(hp) == LV(hh) ? (uint16_t)((p - 1u) & 0xffffu) : sh.head[LV(hh)];
-        }
-        WAVE_SYNC();
-        // the head of a hash is the LAST position of the step with that hash: lanes that
-        // share a hash all store, then any lane above the stored one stores again until the
-        // highest lane holds it (which lane wins one LDS store is not defined on the GPU;
-        // the CPU emulation's lane order gives the same result)
-        LANE_LOOP {
-          if (LV(hh) != KEY_NONE) sh.head[LV(hh)] = (uint16_t)((g + (uint32_t)lane) & 0xffffu);
-        }
-        WAVE_SYNC();
-        for (;;) {
-          const uint64_t redo = WAVE_BALLOT(LV(hh) != KEY_NONE && ((sh.head[LV(hh)] - g) & 0xffffu) < (uint32_t)lane);
-          if (!redo) break;
-          LANE_LOOP {
-            if ((redo >> lane) & 1ull) sh.head[LV(hh)] = (uint16_t)((g + (uint32_t)lane) & 0xffffu);
-          }
-          WAVE_SYNC();
-        }
-      }
-    } else if (!tune.stored) {
-      // ---- exact hash chains, 64 positions per step ----
-      HZ_T(2);
-      for (uint32_t g = s0; g < s1; g += WAVE) {
-        LANE_VAR(uint32_t, key);
-        LANE_VAR(uint32_t, kp);
-        LANE_VAR(uint32_t, kn);
-        LANE_LOOP {
-          const uint32_t p = g + (uint32_t)lane;
-          LV(key) = KEY_NONE;
-          if (p < s1 && p + 2u < n) LV(key) = (hash3(rd32(sh, p)) << 6) | (uint32_t)lane;
-        }
-        HD_SORT64(key);
-        HD_NEIGHBOURS(kp, kn, key);
-        LANE_LOOP {
-          const uint32_t k = LV(key);
-          if (k != KEY_NONE) {
-            const uint32_t h = k >> 6;
-            const uint32_t pos = g + (k & 63u);
-            const uint32_t pk = LV(kp);
-            const uint32_t pv = (pk != KEY_NONE && (pk >> 6) == h) ? ((g + (pk & 63u)) & 0xffffu) : sh.head[h];
-            sh.prev[pos - s0] = (uint16_t)pv;
-          }
-        }
-        WAVE_SYNC();
-        LANE_LOOP {
-          const uint32_t k = LV(key), nk = LV(kn);
-          if (k != KEY_NONE && (nk == KEY_NONE || (nk >> 6) != (k >> 6)))
-            sh.head[k >> 6] = (uint16_t)((g + (k & 63u)) & 0xffffu);
-        }
-        WAVE_SYNC();
       }
     }
+    // the symbol counts take head entries [0, NSYM) for the parse
+    LANE_VAR(uint32_t, hk0);
+    LANE_VAR(uint32_t, hk1);
+    LANE_VAR(uint32_t, hk2);
+    LANE_VAR(uint32_t, hk3);
+    LANE_VAR(uint32_t, hk4);
+    WAVE_SYNC();
+    LANE_LOOP {
+      LV(hk0) = sh.head[lane];
+      LV(hk1) = sh.head[lane + WAVE];
+      LV(hk2) = sh.head[lane + 2 * WAVE];
+      LV(hk3) = sh.head[lane + 3 * WAVE];
+      LV(hk4) = sh.head[lane + 4 * WAVE];
+      for (int k = lane; k < NSYM; k += WAVE) sh.freq[k] = 0;
+    }
+    WAVE_SYNC();
 
     // ---- lane-parallel greedy parse, tokens to HBM ----
     HZ_T(3);
@@ -542,6 +517,11 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     WAVE_SYNC();
     LANE_LOOP {
       for (int s = lane; s < NSYM; s += WAVE) out->freq[s] = sh.freq[s];
+      sh.head[lane] = LV(hk0);
+      sh.head[lane + WAVE] = LV(hk1);
+      sh.head[lane + 2 * WAVE] = LV(hk2);
+      sh.head[lane + 3 * WAVE] = LV(hk3);
+      sh.head[lane + 4 * WAVE] = LV(hk4);
       // the segment's chain links join the far ring once the segment is parsed (written
       // earlier, they would overwrite links FARW back that this parse still follows)
       if (gfar)

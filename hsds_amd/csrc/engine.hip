@@ -811,8 +811,6 @@ __global__ void enc_plan_kernel(const uint8_t* __restrict__ src_base, const hsds
 }
 
 
-constexpr int PARSE_FAST = 100;        // parse_kernel level offset: approximate chains (LZ4 items)
-
 // P: persistent waves, one zlib stream each
 __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ slots,
                                                    const uint32_t* __restrict__ offs,
@@ -827,12 +825,7 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
   uint16_t* const my_far = far ? far + (size_t)blockIdx.x * hd::FARW : nullptr;
   const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   const int lane = threadIdx.x;
-  // level > PARSE_FAST: the LZ4-only approximate-chain parse at level - PARSE_FAST
-  hd::Tune tune = hd::tune_for_level(level > PARSE_FAST ? level - PARSE_FAST : level);
-  if (level > PARSE_FAST) {
-    tune.fast_head = 1;
-    level -= PARSE_FAST;
-  }
+  hd::Tune tune = hd::tune_for_level(level);
   if (chain_ovr) tune.chain = chain_ovr;     // development override (HSDS_DEFLATE_CHAIN)
 #ifdef HZ_PROFILE
   HzProf prof_;
@@ -2098,9 +2091,7 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   hipEventRecord(e->ev2, st);
   hipLaunchKernelGGL(parse_kernel, dim3(pgrid), dim3(64), 0, st, slots,
                      offs, segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap,
-                     // lz4 (the speed codec) parses with approximate chains; zlib, lz4hc and
-                     // blosclz keep the exact chains
-                     cname == HSDS_CNAME_LZ4 && clevel > 0 ? PARSE_FAST + clevel : clevel, 0u, item_cap, far,
+                     clevel, 0u, item_cap, far,
                      e->enc_chain);
   if (cname == HSDS_CNAME_ZSTD) {
     if (grow((void**)&e->ezs, &e->ezs_bytes, (size_t)seg_cap * (hze::ZCAP + hze::LCAP + 8) + 256)) return HSDS_ERR_DEVICE;
@@ -2267,7 +2258,7 @@ int hsds_encode_bitshuffle_batch(hsds_engine* e, const void* d_src, uint64_t src
     return (unsigned)(g < 1 ? 1 : g);
   };
   hipLaunchKernelGGL(parse_kernel, dim3(grid_for(e->parse_blocks_per_cu, slot_cap)), dim3(64), 0, st, slots, offs,
-                     segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, PARSE_FAST + BSHUF_PARSE_LEVEL, 0u,
+                     segoffs, nchunks, ctr, sp, meta, tok, adler, seg_cap, BSHUF_PARSE_LEVEL, 0u,
                      slot_cap, (uint16_t*)nullptr, 0u);
   const unsigned lgrid = grid_for(e->lz4w_blocks_per_cu, slot_cap);
   hipLaunchKernelGGL(lz4_block_kernel, dim3(lgrid), dim3(64), 0, st, slots, offs, segoffs, nchunks, sp, tok, lzsize,

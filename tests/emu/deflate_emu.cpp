@@ -90,9 +90,7 @@ extern "C" int64_t emu_lz4_block(const uint8_t* src, uint32_t n, uint8_t* dst, u
   std::vector<hd::SegParse> sp(nseg);
   std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
   hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
-  // level > 100: the approximate-chain parse of the bitshuffle writer at level - 100
-  hd::Tune tune = hd::tune_for_level(level > 100 ? level - 100 : level);
-  if (level > 100) { tune.fast_head = 1; level -= 100; }
+  hd::Tune tune = hd::tune_for_level(level);
   hd::EncJob job = {src, n, level, 1u, 0u, 0u};
   hd::parse_stream(*ps, job, tune, sp.data(), tok.data());
   free(ps);

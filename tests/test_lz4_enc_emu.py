@@ -52,7 +52,7 @@ def inputs():
 
 
 @pytest.mark.parametrize("name", sorted(inputs()))
-@pytest.mark.parametrize("level", [1, 4, 5, 9, 101, 105])   # 10x: the approximate-chain parse
+@pytest.mark.parametrize("level", [1, 4, 5, 9])
 def test_lz4_blocks_decode(emu, oracle_lib, name, level):
     data = inputs()[name]
     comp = block(emu, data, level)
