@@ -256,7 +256,7 @@ struct ParseShared {
     uint32_t freq[NSYM];
   };
 };
-static_assert(NSYM <= 5 * WAVE && NSYM <= HSIZE, "head entries saved per lane");
+static_assert(NSYM + 1 <= 5 * WAVE && NSYM + 1 <= HSIZE, "head entries saved per lane (counts + dummy)");
 
 HZ_HD uint32_t rd32(const ParseShared& sh, uint32_t p) {
   const uint32_t w = (p >> 2) & (uint32_t)(RWORDS - 1);
@@ -360,6 +360,87 @@ __device__ __forceinline__ uint32_t wave_sort64(uint32_t key, int lane) {
 
 namespace hd {
 
+// branch-free symbol codes for the counts (len 3..258, dist 1..32768)
+HZ_HD uint32_t len_code(uint32_t len) {
+  const uint32_t x = len - 3u;
+  const uint32_t msb = 31u - (uint32_t)__builtin_clz(x | 1u);
+  const uint32_t eb = msb >= 2u ? msb - 2u : 0u;
+  const uint32_t c = x < 8u ? x : 4u * (msb - 1u) + ((x >> eb) & 3u);
+  return len == 258u ? 28u : c;
+}
+HZ_HD uint32_t dist_code(uint32_t dist) {
+  const uint32_t x = dist - 1u;
+  const uint32_t msb = 31u - (uint32_t)__builtin_clz(x | 1u);
+  const uint32_t eb = msb >= 1u ? msb - 1u : 0u;
+  return x < 4u ? x : 2u * msb + ((x >> eb) & 1u);
+}
+
+// One lane's greedy parse of stream bytes [pos, end) (its share of the segment at s0):
+// tokens into its slots of gtok, symbol counts into the head entries [0, NSYM) (and a
+// dummy entry NSYM that literal tokens count their absent distance into).  Returns the
+// number of 16-bit slots written.  FAR: candidates before the LDS ring come from the HBM
+// far ring and the stream in HBM; without it every candidate lies in the ring, and the
+// per-token work is straight-line except the chain walk and the match extension.
+template <bool FAR>
+HZ_HD uint32_t parse_range(ParseShared& sh, const EncJob& job, const Tune& tune, hz_gu16* gfar, hz_gu8* gtok,
+                           int lane, uint32_t s0, uint32_t pos, uint32_t end, uint32_t lo_pos) {
+  uint32_t ns = 0;
+  uint32_t pend = 0, npend = 0;    // slot pairs (2k, 2k + 1) of a lane are stored as one dword
+  while (pos < end) {
+    uint32_t best = 0, bd = 0;
+    const uint32_t maxl = end - pos < 258u ? end - pos : 258u;
+    const uint32_t cur = rd32(sh, pos);
+    uint32_t c16 = sh.prev[pos - s0];
+    const uint32_t maxd = FAR ? (pos < FARW ? pos : FARW) : pos - lo_pos;
+    const uint32_t chain = maxl >= 3u ? tune.chain : 0u;
+    for (uint32_t depth = 0; depth < chain; depth++) {
+      const uint32_t d = (pos - c16) & 0xffffu;
+      if (d == 0u || d > maxd) break;
+      const uint32_t q = pos - d;
+      uint32_t x;
+      bool near = true;
+      if (FAR) {
+        near = q >= lo_pos;
+        // the next candidate's load is independent of this compare: issue it now
+        c16 = q >= s0 ? (uint32_t)sh.prev[q - s0] : (uint32_t)gfar[q & (FARW - 1u)];
+        x = (near ? rd32(sh, q) : load_stream_word(job, q, job.len)) ^ cur;
+      } else {
+        // (d <= maxd keeps q inside the ring; a candidate before the segment ends the chain)
+        const uint32_t pv = sh.prev[q >= s0 ? q - s0 : 0u];
+        x = rd32(sh, q) ^ cur;
+        c16 = q >= s0 ? pv : pos;
+      }
+      const uint32_t L0 = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+      // only a candidate that can beat `best` is measured in full
+      if (L0 >= 3u && (L0 > best || (L0 == 4u && best >= 4u))) {
+        uint32_t L = L0;
+        if (L0 == 4u && maxl > 4u)
+          L = 4u + (near ? match_len(sh, q + 4u, pos + 4u, maxl - 4u)
+                         : match_len_far(sh, job, q + 4u, pos + 4u, maxl - 4u));
+        if (L > maxl) L = maxl;
+        if (L > best) { best = L; bd = d; if (L >= tune.nice || L == maxl) break; }
+      }
+    }
+    if (best == 3u && bd > tune.too_far) best = 0;
+    const bool m = best >= 3u;
+    const uint32_t lit = cur & 0xffu;
+    const uint32_t t0 = m ? (0x8000u | (best - 3u)) : lit;
+    const uint32_t t1 = bd - 1u;
+    // counts (sh.freq aliases sh.head; the dummy entry NSYM is restored with the heads)
+    lds_add(&sh.head[m ? 257u + len_code(best) : lit], 1u);
+    lds_add(&sh.head[m ? (uint32_t)NLL + dist_code(bd) : (uint32_t)NSYM], 1u);
+    pos += m ? best : 1u;
+    // a pending slot pairs with t0; a match without one stores (t0, t1)
+    if (npend || m)
+      *(hz_gu32*)(gtok + (size_t)tslot(ns & ~1u, lane) * 2u) = npend ? (pend | (t0 << 16)) : (t0 | (t1 << 16));
+    pend = npend ? t1 : t0;
+    npend = (npend + (m ? 2u : 1u)) & 1u;
+    ns += m ? 2u : 1u;
+  }
+  if (npend) *(hz_gu32*)(gtok + (size_t)tslot(ns - 1u, lane) * 2u) = pend;
+  return ns;
+}
+
 // Parse one stream into per-segment tokens and frequencies.  sp / tok: this
 // stream's first segment record / token block (SEG_TOK slots per segment).
 // Returns the adler32 of the stream input.
@@ -448,70 +529,9 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
       const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
       uint32_t pos = s0 + a0;
       const uint32_t end = s0 + a1;
-      uint32_t ns = 0;
-      uint32_t pend = 0, npend = 0;    // pairs of slots are stored as one dword
-      if (!tune.stored) {
-        while (pos < end) {
-          uint32_t best = 0, bd = 0;
-          const uint32_t maxl = end - pos < 258u ? end - pos : 258u;
-          if (maxl >= 3u) {
-            const uint32_t cur = rd32(sh, pos);
-            uint32_t c16 = sh.prev[pos - s0];
-            const uint32_t maxd = gfar ? (pos < FARW ? pos : FARW) : pos - lo_pos;
-            for (uint32_t depth = 0; depth < tune.chain; depth++) {
-              const uint32_t d = (pos - c16) & 0xffffu;
-              if (d == 0u || d > maxd) break;
-              const uint32_t q = pos - d;
-              const bool near = q >= lo_pos;
-              // the next candidate's load is independent of this compare: issue it now
-              c16 = q >= s0 ? (uint32_t)sh.prev[q - s0] : gfar ? (uint32_t)gfar[q & (FARW - 1u)] : pos;
-              const uint32_t x = (near ? rd32(sh, q) : load_stream_word(job, q, n)) ^ cur;
-              const uint32_t L0 = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
-              // only a candidate that can beat `best` is measured in full
-              if (L0 >= 3u && (L0 > best || (L0 == 4u && best >= 4u))) {
-                uint32_t L = L0;
-                if (L0 == 4u && maxl > 4u)
-                  L = 4u + (near ? match_len(sh, q + 4u, pos + 4u, maxl - 4u)
-                                 : match_len_far(sh, job, q + 4u, pos + 4u, maxl - 4u));
-                if (L > maxl) L = maxl;
-                if (L > best) { best = L; bd = d; if (L >= tune.nice || L == maxl) break; }
-              }
-            }
-            if (best == 3u && bd > tune.too_far) best = 0;
-          }
-          uint32_t t0, t1 = 0, nt;
-          if (best >= 3u) {
-            uint32_t ls, eb, ev, ds, deb, dev;
-            len_sym(best, ls, eb, ev);
-            dist_sym(bd, ds, deb, dev);
-            t0 = 0x8000u | (best - 3u);
-            t1 = bd - 1u;
-            nt = 2;
-            lds_add(&sh.freq[257u + ls], 1u);
-            lds_add(&sh.freq[NLL + ds], 1u);
-            pos += best;
-          } else {
-            const uint32_t lit = rd8(sh, pos);
-            t0 = lit;
-            nt = 1;
-            lds_add(&sh.freq[lit], 1u);
-            pos++;
-          }
-          // slot pairs (2k, 2k+1) of a lane form one dword: store whole dwords
-          for (uint32_t i = 0; i < nt; i++) {
-            const uint32_t v = i ? t1 : t0;
-            if (npend) {
-              *(hz_gu32*)(gtok + (size_t)tslot(ns - 1u, lane) * 2u) = pend | (v << 16);
-              npend = 0;
-            } else {
-              pend = v;
-              npend = 1;
-            }
-            ns++;
-          }
-        }
-        if (npend) *(hz_gu32*)(gtok + (size_t)tslot(ns - 1u, lane) * 2u) = pend;
-      }
+      const uint32_t ns = tune.stored ? 0u
+                          : gfar ? parse_range<true>(sh, job, tune, gfar, gtok, lane, s0, pos, end, lo_pos)
+                                 : parse_range<false>(sh, job, tune, gfar, gtok, lane, s0, pos, end, lo_pos);
       out->nslot[lane] = (uint16_t)ns;
     }
     WAVE_SYNC();
