@@ -258,12 +258,18 @@ struct ParseShared {
 };
 static_assert(NSYM + 1 <= 5 * WAVE && NSYM + 1 <= HSIZE, "head entries saved per lane (counts + dummy)");
 
-HZ_HD uint32_t rd32(const ParseShared& sh, uint32_t p) {
-  const uint32_t w = (p >> 2) & (uint32_t)(RWORDS - 1);
-  const uint32_t a = sh.ring[w];
-  const uint32_t b = sh.ring[(w + 1u) & (uint32_t)(RWORDS - 1)];
+// bytes [p, p + 4) from the two words a, b they span: {b, a} >> 8 (p & 3) (v_alignbyte)
+HZ_HD uint32_t funnel(uint32_t a, uint32_t b, uint32_t p) {
+#if HZ_GPU
+  return __builtin_amdgcn_alignbyte(b, a, p & 3u);
+#else
   const uint32_t s = (p & 3u) * 8u;
   return s ? (a >> s) | (b << (32u - s)) : a;
+#endif
+}
+HZ_HD uint32_t rd32(const ParseShared& sh, uint32_t p) {
+  const uint32_t w = (p >> 2) & (uint32_t)(RWORDS - 1);
+  return funnel(sh.ring[w], sh.ring[(w + 1u) & (uint32_t)(RWORDS - 1)], p);
 }
 HZ_HD uint32_t rd8(const ParseShared& sh, uint32_t p) {
   return (sh.ring[(p >> 2) & (uint32_t)(RWORDS - 1)] >> ((p & 3u) * 8u)) & 0xffu;
@@ -412,14 +418,16 @@ HZ_HD uint32_t parse_range(ParseShared& sh, const EncJob& job, const Tune& tune,
       }
       const uint32_t L0 = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
       // only a candidate that can beat `best` is measured in full
-      if (L0 >= 3u && (L0 > best || (L0 == 4u && best >= 4u))) {
-        uint32_t L = L0;
-        if (L0 == 4u && maxl > 4u)
-          L = 4u + (near ? match_len(sh, q + 4u, pos + 4u, maxl - 4u)
-                         : match_len_far(sh, job, q + 4u, pos + 4u, maxl - 4u));
-        if (L > maxl) L = maxl;
-        if (L > best) { best = L; bd = d; if (L >= tune.nice || L == maxl) break; }
-      }
+      const bool cand = L0 >= 3u && (L0 > best || (L0 == 4u && best >= 4u));
+      uint32_t L = L0;
+      if (cand && L0 == 4u && maxl > 4u)
+        L = 4u + (near ? match_len(sh, q + 4u, pos + 4u, maxl - 4u)
+                       : match_len_far(sh, job, q + 4u, pos + 4u, maxl - 4u));
+      L = L < maxl ? L : maxl;
+      const bool better = cand && L > best;
+      best = better ? L : best;
+      bd = better ? d : bd;
+      if (better && (L >= tune.nice || L == maxl)) break;
     }
     if (best == 3u && bd > tune.too_far) best = 0;
     const bool m = best >= 3u;
