@@ -366,6 +366,35 @@ __device__ __forceinline__ uint32_t wave_sort64(uint32_t key, int lane) {
 
 namespace hd {
 
+// parse_stream runs as a one-wavefront workgroup, and the LDS executes a wave's
+// instructions in order: a cross-lane LDS hand-off only needs the compiler not to move or
+// cache LDS accesses across it (wavefront-scope fences), not the s_waitcnt vmcnt(0) of
+// __syncthreads, which would also wait for the token stores and the staging prefetch
+#if HZ_GPU
+#define HD_LDS_SYNC()                                           \
+  do {                                                          \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");      \
+    __builtin_amdgcn_wave_barrier();                            \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");      \
+  } while (0)
+#else
+#define HD_LDS_SYNC() do {} while (0)
+#endif
+
+// the ring words of a segment's staging range [s0, hi) a lane prefetches (word k = lane +
+// 64 u), for a contiguous 4-byte aligned stream (job.ts <= 1): whole aligned dwords, the
+// bytes past hi are masked when the words are staged (a dword never crosses a page)
+constexpr uint32_t PF_WORDS = ((uint32_t)SEG + (uint32_t)LOOK + 3u) / 4u / (uint32_t)WAVE + 1u;
+HZ_HD void stage_fetch(const EncJob& job, uint32_t s0, uint32_t hi, int lane, uint32_t* pf) {
+  hz_gcu32* const w = HZ_GLOBAL(hz_gcu32*, job.src);
+  const uint32_t nw = (hi - s0 + 3u) / 4u;
+  HZ_UNROLL
+  for (uint32_t u = 0; u < PF_WORDS; u++) {
+    const uint32_t k = (uint32_t)lane + u * (uint32_t)WAVE;
+    pf[u] = k < nw ? w[(s0 >> 2) + k] : 0u;
+  }
+}
+
 // branch-free symbol codes for the counts (len 3..258, dist 1..32768)
 HZ_HD uint32_t len_code(uint32_t len) {
   const uint32_t x = len - 3u;
@@ -469,8 +498,12 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     LV(as1) = 0; LV(as2) = 0;
     for (int h = lane; h < HSIZE; h += WAVE) sh.head[h] = 0xffffffffu;
   }
-  WAVE_SYNC();
+  HD_LDS_SYNC();
 
+#if HZ_GPU
+  uint32_t pf[PF_WORDS];
+  const bool pf_ok = job.ts <= 1u && ((uintptr_t)job.src & 3u) == 0u;
+#endif
   for (uint32_t seg = 0; seg < nseg; seg++) {
     const uint32_t s0 = seg * (uint32_t)SEG;
     const uint32_t s1 = s0 + (uint32_t)SEG < n ? s0 + (uint32_t)SEG : n;
@@ -483,21 +516,48 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     HZ_T(1);
     LANE_LOOP {
       const uint32_t nw = (stage_hi - s0 + 3u) / 4u;
+      // byte sums of the word at p: S1 += bytes below s1, S2 += their positions * bytes
+#define HD_ADLER_WORD(p, v)                                                    \
+      for (uint32_t b = 0; b < 4u; b++) {                                      \
+        const uint32_t q = (p) + b;                                            \
+        if (q < s1) {                                                          \
+          const uint32_t byte = ((v) >> (8u * b)) & 0xffu;                     \
+          LV(as1) += byte;                                                     \
+          LV(as2) += (uint64_t)q * byte;                                       \
+        }                                                                      \
+      }
+#if HZ_GPU
+      if (pf_ok) {
+        // the words were fetched into registers while the previous segment was parsed
+        if (seg == 0) stage_fetch(job, s0, stage_hi, lane, pf);
+        HZ_UNROLL
+        for (uint32_t u = 0; u < PF_WORDS; u++) {
+          const uint32_t k = (uint32_t)lane + u * (uint32_t)WAVE;
+          const uint32_t p = s0 + 4u * k;           // stream position of ring word
+          if (k < nw) {
+            const uint32_t v = stage_hi - p >= 4u ? pf[u] : pf[u] & ((1u << (8u * (stage_hi - p))) - 1u);
+            sh.ring[(p >> 2) & (uint32_t)(RWORDS - 1)] = v;
+            HD_ADLER_WORD(p, v)
+          }
+        }
+      } else
+#endif
       for (uint32_t k = (uint32_t)lane; k < nw; k += WAVE) {
         const uint32_t p = s0 + 4u * k;             // stream position of ring word
         const uint32_t v = load_stream_word(job, p, stage_hi);
         sh.ring[(p >> 2) & (uint32_t)(RWORDS - 1)] = v;
-        for (uint32_t b = 0; b < 4u; b++) {
-          const uint32_t q = p + b;
-          if (q < s1) {
-            const uint32_t byte = (v >> (8u * b)) & 0xffu;
-            LV(as1) += byte;
-            LV(as2) += (uint64_t)q * byte;
-          }
-        }
+        HD_ADLER_WORD(p, v)
       }
+#undef HD_ADLER_WORD
+#if HZ_GPU
+      // the next segment's words: their loads complete under this segment's chains and parse
+      if (pf_ok && seg + 1u < nseg) {
+        const uint32_t t0 = s1, t1 = t0 + (uint32_t)SEG < n ? t0 + (uint32_t)SEG : n;
+        stage_fetch(job, t0, t1 + (uint32_t)LOOK < n ? t1 + (uint32_t)LOOK : n, lane, pf);
+      }
+#endif
     }
-    WAVE_SYNC();
+    HD_LDS_SYNC();
 
     const uint32_t lo_pos = s0 > WIN ? s0 - WIN : 0u;   // farthest match source in the LDS ring
     if (!tune.stored) {
@@ -518,7 +578,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     LANE_VAR(uint32_t, hk2);
     LANE_VAR(uint32_t, hk3);
     LANE_VAR(uint32_t, hk4);
-    WAVE_SYNC();
+    HD_LDS_SYNC();
     LANE_LOOP {
       LV(hk0) = sh.head[lane];
       LV(hk1) = sh.head[lane + WAVE];
@@ -527,7 +587,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
       LV(hk4) = sh.head[lane + 4 * WAVE];
       for (int k = lane; k < NSYM; k += WAVE) sh.freq[k] = 0;
     }
-    WAVE_SYNC();
+    HD_LDS_SYNC();
 
     // ---- lane-parallel greedy parse, tokens to HBM ----
     HZ_T(3);
@@ -542,7 +602,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
                                  : parse_range<false>(sh, job, tune, gfar, gtok, lane, s0, pos, end, lo_pos);
       out->nslot[lane] = (uint16_t)ns;
     }
-    WAVE_SYNC();
+    HD_LDS_SYNC();
     LANE_LOOP {
       for (int s = lane; s < NSYM; s += WAVE) out->freq[s] = sh.freq[s];
       sh.head[lane] = LV(hk0);
@@ -556,7 +616,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
         for (uint32_t i = (uint32_t)lane; i < seglen; i += WAVE) gfar[(s0 + i) & (FARW - 1u)] = sh.prev[i];
     }
     if (gfar) WAVE_SYNC_GLOBAL();
-    else WAVE_SYNC();
+    else HD_LDS_SYNC();
   }
   HZ_T(9);
   uint64_t S1, S2;
