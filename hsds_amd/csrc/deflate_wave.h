@@ -1036,6 +1036,33 @@ HZ_HD uint32_t tok_bits(const EmitShared& sh, uint32_t t, uint32_t dv) {
   return (sh.tab[257u + ls] & 15u) + eb + (sh.tab[NLL + ds] & 15u) + deb;
 }
 
+// f(t, dv) for each token of one lane's slots in order (t: the first slot, dv: the
+// distance slot of a match, else 0).  The slot dwords are loaded 8 at a time, one memory
+// latency per 16 slots instead of one per dependent load.
+template <class F>
+HZ_HD void walk_tokens(hz_gcu8* gtok, int lane, uint32_t ns, F&& f) {
+  uint32_t mt = 0;                 // a match's first slot waiting for its distance slot
+  const uint32_t nd = (ns + 1u) / 2u;
+  for (uint32_t j0 = 0; j0 < nd; j0 += 8u) {
+    uint32_t d[8];
+    HZ_UNROLL
+    for (uint32_t u = 0; u < 8u; u++) {
+      const uint32_t j = j0 + u;
+      d[u] = j < nd ? *(hz_gcu32*)(gtok + (size_t)(j * (uint32_t)WAVE + (uint32_t)lane) * 4u) : 0u;
+    }
+    HZ_UNROLL
+    for (uint32_t u = 0; u < 16u; u++) {
+      if (2u * j0 + u < ns) {
+        const uint32_t v = (u & 1u) ? d[u >> 1] >> 16 : d[u >> 1] & 0xffffu;
+        const bool call = mt || !(v & 0x8000u);
+        const uint32_t ft = mt ? mt : v, fd = mt ? v : 0u;
+        mt = mt ? 0u : (v & 0x8000u) ? v : 0u;
+        if (call) f(ft, fd);
+      }
+    }
+  }
+}
+
 // dst: the destination buffer as 32-bit words (bit positions are relative to it).
 // The first and the last word touched are shared with neighbours: atomic OR into
 // words the layout phase zeroed; every other word is owned and stored whole.
@@ -1149,29 +1176,7 @@ HZ_HD void emit_segment(EmitShared& sh, const SegOut& so, const SegCode* sc, con
       LV(hb) = lane == 0 ? hbits_all : 0u;
       // pass 1: bits of this lane's tokens
       uint32_t bits = 0;
-      const uint32_t ns = sp->nslot[lane];
-      uint32_t pend = 0;
-      bool have = false;
-      for (uint32_t s = 0; s < ns; s++) {
-        uint32_t t;
-        if (!have) {
-          const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)tslot(s, lane) * 2u);
-          t = pr & 0xffffu; pend = pr >> 16; have = true;
-        } else {
-          t = pend; have = false;
-        }
-        uint32_t dv = 0;
-        if (t & 0x8000u) {
-          s++;
-          if (!have) {
-            const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)tslot(s, lane) * 2u);
-            dv = pr & 0xffffu; pend = pr >> 16; have = true;
-          } else {
-            dv = pend; have = false;
-          }
-        }
-        bits += tok_bits(sh, t, dv);
-      }
+      walk_tokens(gtok, lane, sp->nslot[lane], [&](uint32_t t, uint32_t dv) { bits += tok_bits(sh, t, dv); });
       if (lane == WAVE - 1) bits += sh.tab[256] & 15u;
       LV(nb) = bits;
     }
@@ -1191,39 +1196,20 @@ HZ_HD void emit_segment(EmitShared& sh, const SegOut& so, const SegCode* sc, con
     LANE_LOOP {
       BitW w;
       bw_init(w, off0 + hdr_bits + LV(off));
-      const uint32_t ns = sp->nslot[lane];
-      uint32_t pend = 0;
-      bool have = false;
-      for (uint32_t s = 0; s < ns; s++) {
-        uint32_t t;
-        if (!have) {
-          const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)tslot(s, lane) * 2u);
-          t = pr & 0xffffu; pend = pr >> 16; have = true;
-        } else {
-          t = pend; have = false;
-        }
+      walk_tokens(gtok, lane, sp->nslot[lane], [&](uint32_t t, uint32_t dv) {
         if (t & 0x8000u) {
-          uint32_t dv;
-          s++;
-          if (!have) {
-            const uint32_t pr = *(hz_gcu32*)(gtok + (size_t)tslot(s, lane) * 2u);
-            dv = pr & 0xffffu; pend = pr >> 16; have = true;
-          } else {
-            dv = pend; have = false;
-          }
           uint32_t ls, eb, ev, ds, deb, dev;
           len_sym((t & 0x7fffu) + 3u, ls, eb, ev);
           dist_sym(dv + 1u, ds, deb, dev);
           const uint32_t cl = sh.tab[257u + ls], cd = sh.tab[NLL + ds];
-          bw_put(sh.stage, w, cl >> 4, cl & 15u);
-          if (eb) bw_put(sh.stage, w, ev, eb);
-          bw_put(sh.stage, w, cd >> 4, cd & 15u);
-          if (deb) bw_put(sh.stage, w, dev, deb);
+          // code + extra bits in one put each (<= 20 and <= 28 bits)
+          bw_put(sh.stage, w, (cl >> 4) | (ev << (cl & 15u)), (cl & 15u) + eb);
+          bw_put(sh.stage, w, (cd >> 4) | (dev << (cd & 15u)), (cd & 15u) + deb);
         } else {
           const uint32_t c = sh.tab[t];
           bw_put(sh.stage, w, c >> 4, c & 15u);
         }
-      }
+      });
       if (lane == WAVE - 1) bw_put(sh.stage, w, sh.tab[256] >> 4, sh.tab[256] & 15u);
       bw_flush(sh.stage, w);
     }
