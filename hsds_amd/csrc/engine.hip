@@ -331,6 +331,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) in
   const int lane = threadIdx.x;
   uint8_t* ring = rings + (size_t)blockIdx.x * hz2::SCRATCH_BYTES;
 #ifdef HZ_PROFILE
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_busy = 0;
   HzProf prof_;
   for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
   prof_.last = __builtin_amdgcn_s_memtime();
@@ -354,7 +356,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) in
       hz2::Job job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
                       (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr,
                       item_perm(it)};
+#ifdef HZ_PROFILE
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
       st = hz2::inflate_stream<hz2::Stats>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
+#ifdef HZ_PROFILE
+      t_busy += __builtin_amdgcn_s_memrealtime() - t0;
+      if (lane == 0) atomicMax(&hz_tail[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+#endif
     } else {
       continue;                        // lz_kernel's / zstd_kernel's item
     }
@@ -366,6 +375,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) in
     const uint64_t now = __builtin_amdgcn_s_memtime();
     prof_.acc[prof_.cur] += now - prof_.last;
     if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&hz_prof[i], (unsigned long long)prof_.acc[i]);
+    // tail: wave start / end in the 100 MHz real-time clock, streams' decode time
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      atomicMin(&hz_tail[0], (unsigned long long)t_start);
+      atomicMax(&hz_tail[1], (unsigned long long)t_end);
+      atomicAdd(&hz_tail[2], (unsigned long long)t_end);
+      atomicAdd(&hz_tail[3], 1ull);
+      atomicAdd(&hz_tail[4], (unsigned long long)t_busy);
+      atomicMin(&hz_tail[6], (unsigned long long)t_end);
+    }
   }
 #endif
   (void)prof;
@@ -1727,6 +1746,22 @@ int hsds_decode_batch(hsds_engine* e, const void* d_src, const hsds_chunk_desc* 
                       int itemsize, void* stream) {
   return decode_batch_impl(e, d_src, d_chunks, nchunks, d_dst, dst_extent, d_status, compressor, shuffle, itemsize,
                            stream, 0, nullptr);
+}
+
+// inflate2_kernel wave timing of the HZ_PROFILE build (100 MHz ticks): min start, max end,
+// sum of ends, waves, sum of stream decode time, longest stream, min end
+int hsds_debug_tail(unsigned long long* out8, int reset) {
+#ifdef HZ_PROFILE
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(hz_tail), 8 * sizeof(unsigned long long)) != hipSuccess) return HSDS_ERR_DEVICE;
+  if (reset) {
+    unsigned long long z[8] = {~0ull, 0, 0, 0, 0, 0, ~0ull, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hz_tail), z, sizeof(z)) != hipSuccess) return HSDS_ERR_DEVICE;
+  }
+  return HSDS_OK;
+#else
+  (void)out8; (void)reset;
+  return HSDS_ERR_UNSUPPORTED;
+#endif
 }
 
 int hsds_debug_profile(unsigned long long* out16, int reset) {

@@ -81,6 +81,7 @@ typedef uint16_t hz_gu16;
 
 #if HZ_GPU && defined(HZ_PROFILE)
 __device__ unsigned long long hz_prof[16];
+__device__ unsigned long long hz_tail[8];
 struct HzProf { uint64_t acc[16]; uint64_t last; int cur; };
 #define HZ_T(slot)                                                                          \
   do { if (prof) { const uint64_t _now = __builtin_amdgcn_s_memtime();                      \
