@@ -835,56 +835,142 @@ HZ_HD void huff_counts_serial(HuffShared& sh, int n, int maxbits) {
     }                                                                                           \
   } while (0)
 
-// code-length sequence (RFC 1951 3.2.7) of len_ll[0..hlit) ++ len_d[0..hdist),
-// run-length coded with symbols 16/17/18; lane 0
-HZ_HD void build_rle(HuffShared& sh) {
-  uint32_t hlit = 257, hdist = 1;
-  for (uint32_t s = 257; s < (uint32_t)NLL; s++) if (sh.len_ll[s]) hlit = s + 1;
-  for (uint32_t s = 0; s < (uint32_t)ND; s++) if (sh.len_d[s]) hdist = s + 1;
-  sh.hlit = hlit;
-  sh.hdist = hdist;
-  for (int i = 0; i <= NCL; i++) sh.clf[i] = 0;
-  const uint32_t total = hlit + hdist;
-  uint32_t nr = 0, i = 0;
-  while (i < total) {
-    const uint32_t v = i < hlit ? sh.len_ll[i] : sh.len_d[i - hlit];
-    uint32_t run = 1;
-    while (i + run < total && (i + run < hlit ? sh.len_ll[i + run] : sh.len_d[i + run - hlit]) == v) run++;
-    i += run;
-    if (v == 0) {
-      while (run >= 11u) {
-        const uint32_t r = run > 138u ? 138u : run;
-        sh.rle[nr++] = (uint16_t)(18u | ((r - 11u) << 8)); sh.clf[18]++;
-        run -= r;
-      }
-      if (run >= 3u) { sh.rle[nr++] = (uint16_t)(17u | ((run - 3u) << 8)); sh.clf[17]++; run = 0; }
-      while (run) { sh.rle[nr++] = 0; sh.clf[0]++; run--; }
-    } else {
-      sh.rle[nr++] = (uint16_t)v; sh.clf[v]++;
-      run--;
-      while (run >= 3u) {
-        const uint32_t r = run > 6u ? 6u : run;
-        sh.rle[nr++] = (uint16_t)(16u | ((r - 3u) << 8)); sh.clf[16]++;
-        run -= r;
-      }
-      while (run) { sh.rle[nr++] = (uint16_t)v; sh.clf[v]++; run--; }
-    }
-  }
-  sh.nrle = nr;
-}
 
-// dynamic block header size in bits (after the code-length code is built); lane 0
-HZ_HD uint32_t dyn_header_bits(HuffShared& sh) {
-  uint32_t hclen = 4;
-  for (uint32_t i = 0; i < (uint32_t)NCL; i++) if (sh.len_cl[hz::cl_order(i)]) hclen = i + 1 > 4u ? i + 1 : 4u;
-  sh.hclen = hclen;
-  uint32_t bits = 3u + 5u + 5u + 4u + 3u * hclen;
-  for (uint32_t i = 0; i < sh.nrle; i++) {
-    const uint32_t sym = sh.rle[i] & 0xffu;
-    bits += sh.len_cl[sym] + cl_extra_bits(sym);
-  }
-  return bits;
+// ---- the code-length sequence (RFC 1951 3.2.7) of len_ll[0..hlit) ++ len_d[0..hdist), run-length
+// coded with symbols 16/17/18, built by all lanes (a lane-0 loop through round 3) ----
+// length i of the combined literal/length + distance sequence
+HZ_HD uint32_t rle_len(const HuffShared& sh, uint32_t i, uint32_t hlit) {
+  return i < hlit ? sh.len_ll[i] : sh.len_d[i - hlit];
 }
+// code-length symbols build_rle emits for a run of R copies of v
+HZ_HD uint32_t rle_count(uint32_t v, uint32_t R) {
+  if (v == 0u) {
+    const uint32_t q = R / 138u, rem = R % 138u;
+    return rem >= 11u ? q + 1u : q + (rem >= 3u ? 1u : rem);
+  }
+  const uint32_t rem = R - 1u, q = rem / 6u, rr = rem % 6u;
+  return 1u + q + (rr >= 3u ? 1u : rr);
+}
+// the symbols of that run at rle[nr..], in build_rle's order, counted into clf
+HZ_HD void rle_emit(HuffShared& sh, uint32_t v, uint32_t run, uint32_t nr) {
+  if (v == 0u) {
+    while (run >= 11u) {
+      const uint32_t r = run > 138u ? 138u : run;
+      sh.rle[nr++] = (uint16_t)(18u | ((r - 11u) << 8)); lds_add(&sh.clf[18], 1u);
+      run -= r;
+    }
+    if (run >= 3u) { sh.rle[nr++] = (uint16_t)(17u | ((run - 3u) << 8)); lds_add(&sh.clf[17], 1u); run = 0; }
+    while (run) { sh.rle[nr++] = 0; lds_add(&sh.clf[0], 1u); run--; }
+  } else {
+    sh.rle[nr++] = (uint16_t)v; lds_add(&sh.clf[v], 1u);
+    run--;
+    while (run >= 3u) {
+      const uint32_t r = run > 6u ? 6u : run;
+      sh.rle[nr++] = (uint16_t)(16u | ((r - 3u) << 8)); lds_add(&sh.clf[16], 1u);
+      run -= r;
+    }
+    while (run) { sh.rle[nr++] = (uint16_t)v; lds_add(&sh.clf[v], 1u); run--; }
+  }
+}
+// the first run start after position i (starts: bit i & 63 of sm[i >> 6]), or tot
+HZ_HD uint32_t rle_next_start(const uint64_t* sm, uint32_t i, uint32_t tot) {
+  const uint32_t k = i >> 6;
+  uint64_t w = sm[k] & ~((2ull << (i & 63u)) - 1ull);
+  if (w) return 64u * k + (uint32_t)__builtin_ctzll(w);
+  for (uint32_t j = k + 1u; j < 5u; j++)
+    if (sm[j]) return 64u * j + (uint32_t)__builtin_ctzll(sm[j]);
+  return tot;
+}
+#if HZ_GPU
+#define HD_WAVE_MAX(v, out)                                                                  \
+  do {                                                                                       \
+    uint32_t _m = (v);                                                                       \
+    for (int _o = 32; _o > 0; _o >>= 1) { const uint32_t _y = __shfl_xor(_m, _o, 64); _m = _y > _m ? _y : _m; } \
+    out = _m;                                                                                \
+  } while (0)
+#define HD_WAVE_SCAN(v, off, sum) do { off = hz::wave_excl_scan(v, (int)threadIdx.x); sum = hz::wave_sum(v); } while (0)
+#else
+#define HD_WAVE_MAX(v, out) do { out = 0; for (int _l = 0; _l < 64; _l++) out = (v)[_l] > out ? (v)[_l] : out; } while (0)
+#define HD_WAVE_SCAN(v, off, sum) do { sum = 0; for (int _l = 0; _l < 64; _l++) { (off)[_l] = sum; sum += (v)[_l]; } } while (0)
+#endif
+// hlit / hdist (one past the last nonzero length), the run starts by ballot, each run's
+// symbol count, a wave scan for the offsets, and each run's symbols by its starting lane
+#define HD_BUILD_RLE(sh)                                                                     \
+  do {                                                                                       \
+    LANE_VAR(uint32_t, _hl);                                                                 \
+    LANE_VAR(uint32_t, _hd);                                                                 \
+    LANE_LOOP {                                                                              \
+      uint32_t _a = 257u, _b = 1u;                                                           \
+      for (int _s = lane; _s < NLL; _s += WAVE) if (_s >= 257 && (sh).len_ll[_s]) _a = (uint32_t)_s + 1u; \
+      for (int _s = lane; _s < ND; _s += WAVE) if ((sh).len_d[_s]) _b = (uint32_t)_s + 1u;   \
+      LV(_hl) = _a;                                                                          \
+      LV(_hd) = _b;                                                                          \
+      if (lane <= NCL) (sh).clf[lane] = 0;                                                   \
+    }                                                                                        \
+    uint32_t _hlit, _hdist;                                                                  \
+    HD_WAVE_MAX(_hl, _hlit);                                                                 \
+    HD_WAVE_MAX(_hd, _hdist);                                                                \
+    WAVE_SYNC();                                                                             \
+    const uint32_t _tot = _hlit + _hdist;                                                    \
+    uint64_t _sm[5];                                                                         \
+    for (uint32_t _k = 0; _k < 5u; _k++)                                                     \
+      _sm[_k] = WAVE_BALLOT(64u * _k + (uint32_t)lane < _tot &&                              \
+                            (64u * _k + (uint32_t)lane == 0u ||                              \
+                             hd::rle_len((sh), 64u * _k + (uint32_t)lane, _hlit) !=          \
+                                 hd::rle_len((sh), 64u * _k + (uint32_t)lane - 1u, _hlit))); \
+    uint32_t _base = 0;                                                                      \
+    for (uint32_t _k = 0; _k < 5u; _k++) {                                                   \
+      LANE_VAR(uint32_t, _cn);                                                               \
+      LANE_VAR(uint32_t, _rv);                                                               \
+      LANE_VAR(uint32_t, _rr);                                                               \
+      LANE_VAR(uint32_t, _of);                                                               \
+      uint32_t _sum;                                                                         \
+      LANE_LOOP {                                                                            \
+        const uint32_t _i = 64u * _k + (uint32_t)lane;                                       \
+        uint32_t _c = 0, _v = 0, _r = 0;                                                     \
+        if ((_sm[_k] >> lane) & 1ull) {                                                      \
+          _r = hd::rle_next_start(_sm, _i, _tot) - _i;                                       \
+          _v = hd::rle_len((sh), _i, _hlit);                                                 \
+          _c = hd::rle_count(_v, _r);                                                        \
+        }                                                                                    \
+        LV(_cn) = _c;                                                                        \
+        LV(_rv) = _v;                                                                        \
+        LV(_rr) = _r;                                                                        \
+      }                                                                                      \
+      HD_WAVE_SCAN(_cn, _of, _sum);                                                          \
+      LANE_LOOP { if (LV(_cn)) hd::rle_emit((sh), LV(_rv), LV(_rr), _base + LV(_of)); }      \
+      _base += _sum;                                                                         \
+    }                                                                                        \
+    LANE_LOOP { if (lane == 0) { (sh).nrle = _base; (sh).hlit = _hlit; (sh).hdist = _hdist; } } \
+    WAVE_SYNC();                                                                             \
+  } while (0)
+
+// dynamic block header size in bits (after the code-length code is built): the run-length
+// coded lengths summed by all lanes, HCLEN on lane 0
+#define HD_HEADER_BITS(sh)                                                                   \
+  do {                                                                                       \
+    LANE_VAR(uint32_t, _hb);                                                                 \
+    LANE_LOOP {                                                                              \
+      uint32_t _b = 0;                                                                       \
+      for (uint32_t _i = (uint32_t)lane; _i < (sh).nrle; _i += WAVE) {                       \
+        const uint32_t _sym = (sh).rle[_i] & 0xffu;                                          \
+        _b += (sh).len_cl[_sym] + cl_extra_bits(_sym);                                       \
+      }                                                                                      \
+      LV(_hb) = _b;                                                                          \
+    }                                                                                        \
+    uint32_t _tot;                                                                           \
+    LANE_VAR(uint32_t, _ho);                                                                 \
+    HD_WAVE_SCAN(_hb, _ho, _tot);                                                            \
+    (void)_ho;                                                                               \
+    LANE_LOOP {                                                                              \
+      if (lane == 0) {                                                                       \
+        uint32_t _hc = 4;                                                                    \
+        for (uint32_t _i = 0; _i < (uint32_t)NCL; _i++) if ((sh).len_cl[hz::cl_order(_i)]) _hc = _i + 1 > 4u ? _i + 1 : 4u; \
+        (sh).hclen = _hc;                                                                    \
+        (sh).hdr_bits = 3u + 5u + 5u + 4u + 3u * _hc + _tot;                                 \
+      }                                                                                      \
+    }                                                                                        \
+  } while (0)
 
 // Worst-case bits of a stored block (3-bit header, up to 7 padding bits, LEN/NLEN)
 HZ_HD uint64_t stored_bits_max(uint32_t seglen) { return 3u + 7u + 32u + 8ull * seglen; }
@@ -917,10 +1003,10 @@ HZ_HD void huff_segment(HuffShared& sh, const SegParse* sp, SegCode* sc, uint32_
 #endif
     HD_BUILD_HUFF(sh, sh.freq, NLL, 512, 15, sh.len_ll, sh.code_ll);
     HD_BUILD_HUFF(sh, (sh.freq + NLL), ND, 32, 15, sh.len_d, sh.code_d);
-    LANE_LOOP { if (lane == 0) build_rle(sh); }
+    HD_BUILD_RLE(sh);
     WAVE_SYNC();
     HD_BUILD_HUFF(sh, sh.clf, NCL, 32, 7, sh.len_cl, sh.code_cl);
-    LANE_LOOP { if (lane == 0) sh.hdr_bits = dyn_header_bits(sh); }
+    HD_HEADER_BITS(sh);
     WAVE_SYNC();
     LANE_VAR(uint64_t, db);
     LANE_LOOP {
