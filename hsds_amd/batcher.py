@@ -12,8 +12,14 @@ with one device-to-host copy for all their chunkReadSelection results.  Requests
 same chunk id in a window share one read (the reference's dedupe); requests whose dataset
 parameters differ (dtype, layout, filters, fill value) form separate groups.
 
-The engine is re-entrant (include/hsds_amd.h, "Threading"), so batches run on a worker
-thread off the event loop, as the reference's blosc_nthreads codec work would.
+Batches run on a worker thread off the event loop, as the reference's blosc_nthreads codec
+work would.  A batch holds the store's lock (ChunkStore.lock) from its reads until its
+selections are in host memory, so the DN's own calls on the same store (PUT_Chunk, flush,
+direct reads) wait for it instead of evicting slots the batch is gathering from.  The
+stored objects go up in one asynchronous copy from page-locked staging, the selections
+come back in one asynchronous copy into page-locked memory together with the decode
+statuses, and the batch waits for the device once; responses are views of that host
+buffer.
 """
 import asyncio
 import json
@@ -107,54 +113,119 @@ class ChunkBatcher:
             if read.chunk_id not in index:
                 index[read.chunk_id] = len(order)
                 order.append(read)
-        vals = self.store.get_chunks(order, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
-                                     layout_class=layout_class, hyper_dims=hyper_dims, chunk_init=chunk_init)
+        kw = dict(filter_ops=filter_ops, fill_value=fill_value, layout_class=layout_class, hyper_dims=hyper_dims,
+                  chunk_init=chunk_init)
+        store = self.store
         self.stats["batches"] += 1
         self.stats["reads"] += len(order)
         self.stats["requests"] += len(reqs)
-        items = []
-        for read, slices, _ in reqs:
-            v = vals[index[read.chunk_id]]
-            items.append((v, slices))
-        return _gather(self.store, items, dtype, chunk_dims)
+        if not hasattr(store, "get_chunks_deferred"):
+            vals = store.get_chunks(order, dtype, chunk_dims, **kw)
+            return _gather(None, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
+        import torch
+        # decode, selection gather and both host copies are queued on one stream; the
+        # batch waits for the device once
+        with store.lock:
+            vals, finish = store.get_chunks_deferred(order, dtype, chunk_dims, **kw)
+            items = [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs]
+            plan = _gather_launch(items, dtype, chunk_dims)
+            torch.cuda.current_stream(store.cache.arena.buf.device).synchronize()
+            vals = finish()
+        return _gather_finish(plan, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
 
 
-def _gather(store, items, dtype, chunk_dims):
-    """The selections of one batch: device chunks through ONE copy launch into a packed
-    device buffer and ONE device-to-host copy; host arrays (a CPU store) by numpy."""
+def _sel_shape(slices, chunk_dims):
+    if slices is None:
+        return tuple(chunk_dims)
+    return tuple(len(range(*s.indices(n))) for s, n in zip(slices, chunk_dims))
+
+
+def _gather_launch(items, dtype, chunk_dims):
+    """Queue the device half of a batch's selections: every device chunk's selection
+    (chunkReadSelection, chunkUtil.py:882-929) into one packed device buffer -- one copy
+    launch per source allocation (cache arena, or the per-batch buffer of chunks the
+    cache had no room for) -- and one asynchronous copy of it into page-locked host
+    memory.  Returns the plan _gather_finish reads after the stream has drained."""
+    import torch
+    from .engine import COPY_DESC_DTYPE, ChunkEngine
+    from .selection import copy_desc, _contig_slices
+    dev_items = [k for k, (v, _) in enumerate(items) if isinstance(v, torch.Tensor)]
+    if not dev_items:
+        return None
+    dev = items[dev_items[0]][0].device
+    shapes, offs, total = [], [], 0
+    groups = {}                  # storage pointer -> (uint8 tensor over the storage, [record rows])
+    recs = np.zeros(len(dev_items), COPY_DESC_DTYPE)
+    whole = np.zeros(len(dev_items), bool)
+    for j, k in enumerate(dev_items):
+        v, slices = items[k]
+        shape = _sel_shape(slices, chunk_dims)
+        nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        shapes.append(shape)
+        offs.append(total)
+        st = v.untyped_storage()
+        sp = st.data_ptr()
+        g = groups.get(sp)
+        if g is None:
+            base = torch.empty(0, dtype=torch.uint8, device=dev).set_(st)
+            g = groups[sp] = (base, [])
+        src_off = v.data_ptr() - sp
+        if nbytes:
+            if slices is None:
+                whole[j] = True
+                recs["src_off"][j] = src_off
+                recs["dst_off"][j] = total
+                recs["count"][j, 0] = nbytes
+            else:
+                recs[j] = copy_desc(chunk_dims, slices, shape, _contig_slices(shape), dtype.itemsize,
+                                    src_base=src_off, dst_base=total)[0]
+            g[1].append(j)
+        total += (nbytes + 255) // 256 * 256
+    if whole.any():
+        # whole chunks: one flat record each, in 8-, 4- or 1-byte units
+        so, do, nb = recs["src_off"][whole], recs["dst_off"][whole], recs["count"][whole, 0].astype(np.uint64)
+        a = so | do | nb
+        w = np.where(a % 8 == 0, 8, np.where(a % 4 == 0, 4, 1)).astype(np.int64)
+        recs["src_stride"][whole, 0] = w
+        recs["dst_stride"][whole, 0] = w
+        recs["count"][whole, 0] = nb.astype(np.int64) // w
+        recs["rank"][whole] = 1
+        recs["itemsize"][whole] = w
+    packed = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    eng = ChunkEngine(dev.index)
+    for base, rows in groups.values():
+        if rows:
+            eng.copy(base, packed, recs[np.asarray(rows)])
+    host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+    host.copy_(packed, non_blocking=True)
+    return {"host": host, "dev_items": dev_items, "shapes": shapes, "offs": offs}
+
+
+def _gather_finish(plan, items, dtype, chunk_dims):
+    """The batch's responses once the stream has drained: views of the page-locked
+    host buffer (no further copy), None for 404s, the exception of a failed read."""
     out = [None] * len(items)
-    dev_items = []
     for k, (v, slices) in enumerate(items):
         if v is None or isinstance(v, BaseException):
             out[k] = v
         elif isinstance(v, np.ndarray):
             a = v.reshape(chunk_dims) if v.dtype == dtype else v.view(dtype).reshape(chunk_dims)
             out[k] = np.ascontiguousarray(a if slices is None else a[slices])
-        else:
-            dev_items.append(k)
-    if dev_items:
-        import torch
-        from .engine import ChunkEngine
-        from .selection import copy_desc, _contig_slices
-        abase = store.cache.arena.buf
-        full = tuple(slice(0, n, 1) for n in chunk_dims)
-        recs, shapes, offs, total = [], [], [], 0
-        for k in dev_items:
-            v, slices = items[k]
-            sl = full if slices is None else slices
-            shape = tuple(len(range(*s.indices(n))) for s, n in zip(sl, chunk_dims))
-            nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
-            shapes.append(shape)
-            offs.append(total)
-            if nbytes:
-                recs.append(copy_desc(chunk_dims, sl, shape, _contig_slices(shape), dtype.itemsize,
-                                      src_base=v.data_ptr() - abase.data_ptr(), dst_base=total))
-            total += (nbytes + 255) // 256 * 256
-        packed = torch.empty(max(total, 1), dtype=torch.uint8, device=abase.device)
-        if recs:
-            ChunkEngine(abase.device.index).copy(abase, packed, np.concatenate(recs))
-        host = packed.cpu().numpy()
-        for k, shape, o in zip(dev_items, shapes, offs):
+    if plan is not None:
+        host = plan["host"].numpy()
+        for k, shape, o in zip(plan["dev_items"], plan["shapes"], plan["offs"]):
+            if isinstance(items[k][0], BaseException):
+                continue                                       # the read failed after all
             n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
-            out[k] = host[o:o + n].view(dtype).reshape(shape).copy()
+            out[k] = host[o:o + n].view(dtype).reshape(shape)
     return out
+
+
+def _gather(store, items, dtype, chunk_dims):
+    """The selections of one batch (host arrays, or device chunks through _gather_launch
+    and one synchronisation)."""
+    plan = _gather_launch(items, dtype, chunk_dims)
+    if plan is not None:
+        import torch
+        torch.cuda.current_stream().synchronize()
+    return _gather_finish(plan, items, dtype, chunk_dims)

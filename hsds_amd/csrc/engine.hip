@@ -48,6 +48,9 @@
 #ifndef HZ_ZSTD_WPE
 #define HZ_ZSTD_WPE 3      // zstd_kernel waves per SIMD the compiler must allow (VGPR budget)
 #endif
+#ifndef HZ2_WPE
+#define HZ2_WPE 4          // inflate2_kernel waves per SIMD the compiler must allow (VGPR budget)
+#endif
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
 namespace {
@@ -320,7 +323,7 @@ __device__ __forceinline__ void raw_copy(const Item& it, int lane) {
   }
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) inflate2_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ2_WPE))) inflate2_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
                                                       uint32_t* __restrict__ counter, int32_t* __restrict__ status,
                                                       uint32_t* __restrict__ sizes,
                                                       const uint32_t* __restrict__ kind_counts, hz2::Tune tune,

@@ -151,7 +151,7 @@ class _Node:
     def __init__(self, off, nbytes, shape, dtype):
         self.off, self.nbytes, self.shape, self.dtype = off, int(nbytes), tuple(shape), np.dtype(dtype)
         self.dirty = False
-        self.pinned = False      # slot of a read batch in flight: not evictable
+        self.pinned = 0          # pin count (read batches / writes in flight): not evictable while > 0
         self.last_access = time.time()
 
 
@@ -239,7 +239,7 @@ class DeviceChunkCache:
             if n.nbytes == nbytes:
                 self._lru.move_to_end(key)
                 n.shape, n.dtype, n.last_access = tuple(shape), np.dtype(dtype), time.time()
-                n.pinned = n.pinned or pin
+                n.pinned += 1 if pin else 0
                 return self.arena.view(n.off, n.nbytes)
             dirty = n.dirty
             del self[key]
@@ -251,7 +251,7 @@ class DeviceChunkCache:
         if off is None:
             return None
         node = _Node(off, nbytes, shape, dtype)
-        node.pinned = pin
+        node.pinned = 1 if pin else 0
         self._lru[key] = node
         self._mem += nbytes
         if dirty:
@@ -276,10 +276,14 @@ class DeviceChunkCache:
             raise MemoryError("chunk cache full of dirty chunks")
         slot.copy_(src, non_blocking=False)
 
+    def pin(self, key):
+        """Hold `key`'s slot (a counted pin: every pin() / reserve(pin=True) needs its unpin())."""
+        self._lru[key].pinned += 1
+
     def unpin(self, key):
         n = self._lru.get(key)
-        if n is not None:
-            n.pinned = False
+        if n is not None and n.pinned > 0:
+            n.pinned -= 1
 
     def _evict_one(self, exclude=None):
         for k, n in self._lru.items():          # least recent first
@@ -477,7 +481,8 @@ class ChunkReader:
                     continue
                 if r.length and r.length > 0 and len(data) != r.length:
                     data = bytes(r.length)      # storUtil.py:480-485 (bytearray(length), data not copied)
-                blobs.append(bytes(data))
+                # the staging copy is the only copy of the object (a view is copied now)
+                blobs.append(data if isinstance(data, (bytes, np.ndarray)) else bytes(data))
                 jobs.append((ri, "plain", len(blobs) - 1, None))
                 continue
             # hyper chunk (datanode_lib.py:851-906)
@@ -555,12 +560,17 @@ class ChunkReader:
         return out
 
     def read(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
-             hyper_dims=None):
+             hyper_dims=None, defer=False):
         """Decode a batch of chunks.  Returns a list (one entry per read) of device
         arrays (typed torch views of chunk_dims), or an exception instance:
         HTTPNotFound (object missing), HTTPInternalServerError (codec failure or a
         decoded size that is not the chunk size -- get_chunk's 500), ValueError (a
-        malformed hyper-chunk request)."""
+        malformed hyper-chunk request).
+
+        defer=True returns (results, finish) without waiting for the device: the views
+        are valid once the current stream has drained, and finish() -- called after
+        that -- turns failed decodes into HTTPInternalServerError and returns the final
+        list (the batcher gathers the selections before its single synchronisation)."""
         import torch
         from .engine import COPY_DESC_DTYPE, pack_chunks
         dtype = np.dtype(dtype)
@@ -610,49 +620,130 @@ class ChunkReader:
                     fill_chunk = torch.from_numpy(np.full(chunk_dims, fill_value, dtype=dtype).view(np.uint8)
                                                   .reshape(-1).copy()).to(self.device)
                 view.copy_(fill_chunk)
-        # ONE decode batch into a contiguous buffer (plain objects and HDF5 chunks)
+        # ONE decode batch into a contiguous buffer (plain objects and HDF5 chunks): the
+        # stored objects are packed straight into page-locked staging and go up with one
+        # asynchronous copy; statuses come back with one asynchronous copy as well, and
+        # every chunk is placed whatever its status (a failed chunk's slot is dropped in
+        # finish(), after the one stream synchronisation)
         dec = [j for j in jobs if j[1] in ("plain", "h5")]
+        st_host = None
         if dec:
             sizes = [chunk_size if kind == "plain" else h5_size for _, kind, _, _ in dec]
-            src, descs, ext = pack_chunks([blobs[bi] for _, _, bi, _ in dec], sizes)
-            d_src = torch.from_numpy(src).to(self.device)
+            dblobs = [blobs[bi] for _, _, bi, _ in dec]
+            d_src, descs, ext = _stage_blobs(dblobs, sizes, self.device)
             dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
             status = torch.full((len(dec),), 99, dtype=torch.int32, device=self.device)
-            _decode_batch(self.eng, d_src, descs, dbuf, status, comp, shuffle, isz, [blobs[bi] for _, _, bi, _ in dec])
+            _decode_batch(self.eng, d_src, descs, dbuf, status, comp, shuffle, isz, dblobs)
             self.stats["decode_calls"] += 1
             self.stats["objects"] += sum(1 for _, k, _, _ in dec if k == "plain")
             self.stats["h5_chunks"] += sum(1 for _, k, _, _ in dec if k == "h5")
-            st = status.cpu().numpy()
-            # placement: ONE copy batch per destination tensor
+            st_host = torch.empty(len(dec), dtype=torch.int32, pin_memory=True)
+            st_host.copy_(status, non_blocking=True)
+            # placement: ONE copy batch per destination tensor (whole objects: flat records
+            # built at once; HDF5 chunks: one strided record each)
+            recs = np.zeros(len(dec), COPY_DESC_DTYPE)
             groups = {}
+            flat = np.zeros(len(dec), bool)
             for k, (ri, kind, bi, hidx) in enumerate(dec):
-                if st[k] != nat.OK:
-                    results[ri] = HTTPInternalServerError()
-                    continue
                 base, off = slots[ri]
-                so = int(descs[k]["dst_off"])
                 if kind == "plain":
-                    d = _flat_desc(so, off, chunk_size)
+                    flat[k] = True
+                    recs["dst_off"][k] = off
                 else:
-                    d = _place_desc(so, off, chunk_dims, hyper_dims, hidx, dtype.itemsize)
-                groups.setdefault(id(base), (base, []))[1].append(d)
-            for base, ds in groups.values():
-                arr = np.zeros(len(ds), COPY_DESC_DTYPE)
-                for k, d in enumerate(ds):
-                    arr[k] = d
-                self.eng.copy(dbuf, base, arr)
-        torch.cuda.synchronize(self.device)
-        for cid in pinned:
-            self.cache.unpin(cid)
+                    recs[k] = _place_desc(int(descs[k]["dst_off"]), off, chunk_dims, hyper_dims, hidx, dtype.itemsize)
+                groups.setdefault(id(base), (base, []))[1].append(k)
+            if flat.any():
+                so = descs["dst_off"][flat].astype(np.uint64)
+                do = recs["dst_off"][flat]
+                a = so | do | np.uint64(chunk_size)
+                w = np.where(a % 8 == 0, 8, np.where(a % 4 == 0, 4, 1)).astype(np.int64)
+                recs["src_off"][flat] = so
+                recs["src_stride"][flat, 0] = w
+                recs["dst_stride"][flat, 0] = w
+                recs["count"][flat, 0] = chunk_size // w
+                recs["rank"][flat] = 1
+                recs["itemsize"][flat] = w
+            for base, rows in groups.values():
+                self.eng.copy(dbuf, base, recs[np.asarray(rows)])
         for ri in need:
             base, off = slots[ri]
             if results[ri] is None:
                 results[ri] = device_view(base[off:off + chunk_size], chunk_dims, dtype)
-            elif self.cache is not None and reads[ri].chunk_id in self.cache:
-                del self.cache[reads[ri].chunk_id]     # failed reads are not cached
-        if self.cache is not None and self.cache.memUsed > self.cache.memTarget:
-            self.cache._reduce()
-        return results
+
+        def finish():
+            """after the stream has drained: decode failures become 500s (and leave the
+            cache), the batch's slots are unpinned"""
+            if st_host is not None:
+                st = st_host.numpy()
+                for k, (ri, _, _, _) in enumerate(dec):
+                    if st[k] != nat.OK:
+                        results[ri] = HTTPInternalServerError()
+            for cid in pinned:
+                self.cache.unpin(cid)
+            for ri in need:
+                if isinstance(results[ri], HTTPInternalServerError) and self.cache is not None \
+                        and reads[ri].chunk_id in self.cache:
+                    del self.cache[reads[ri].chunk_id]     # failed reads are not cached
+            if self.cache is not None and self.cache.memUsed > self.cache.memTarget:
+                self.cache._reduce()
+            return results
+
+        if defer:
+            return results, finish
+        torch.cuda.current_stream(self.device).synchronize()
+        return finish()
+
+
+_POOL = None
+
+
+def _stage_pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix="hsds-amd-stage")
+    return _POOL
+
+
+def _stage_blobs(blobs, dst_lens, device, align=256):
+    """pack_chunks into page-locked memory and one asynchronous host-to-device copy:
+    (device uint8 tensor, CHUNK_DESC_DTYPE descriptors, decoded extent).  The staging
+    block returns to torch's pinned-memory cache once the copy has run."""
+    import torch
+    from .engine import CHUNK_DESC_DTYPE
+    n = len(blobs)
+    lens = np.fromiter((len(b) for b in blobs), np.int64, n)
+    descs = np.zeros(n, CHUNK_DESC_DTYPE)
+    pad = (lens + align - 1) // align * align
+    src_off = np.zeros(n, np.int64)
+    if n > 1:
+        np.cumsum(pad[:-1], out=src_off[1:])
+    descs["src_off"] = src_off
+    descs["src_len"] = lens
+    dl = np.asarray(dst_lens, np.int64)
+    dpad = (dl + align - 1) // align * align
+    dst_off = np.zeros(n, np.int64)
+    if n > 1:
+        np.cumsum(dpad[:-1], out=dst_off[1:])
+    descs["dst_off"] = dst_off
+    descs["dst_len"] = dl
+    total = int(pad.sum()) if n else 0
+    host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+    h = host.numpy()
+
+    def put(k0, k1):
+        for o, b in zip(src_off[k0:k1].tolist(), blobs[k0:k1]):
+            h[o:o + len(b)] = np.frombuffer(b, np.uint8) if not isinstance(b, np.ndarray) else b
+    if total >= (32 << 20) and n >= 16:
+        # large batches: the copies into staging run on the host's cores (numpy drops the GIL)
+        parts = min(8, n)
+        cuts = [n * i // parts for i in range(parts + 1)]
+        list(_stage_pool().map(lambda i: put(cuts[i], cuts[i + 1]), range(parts)))
+    else:
+        put(0, n)
+    d_src = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
+    d_src.copy_(host, non_blocking=True)
+    return d_src, descs, int(dpad.sum()) if n else 0
 
 
 def _comp_name(code):
@@ -695,6 +786,17 @@ def _place_desc(src_off, dst_off, chunk_dims, hyper_dims, hidx, itemsize):
     return d
 
 
+def _locked(fn):
+    """run a ChunkStore method under the store's lock"""
+    import functools
+
+    @functools.wraps(fn)
+    def wrap(self, *a, **kw):
+        with self.lock:
+            return fn(self, *a, **kw)
+    return wrap
+
+
 class ChunkStore:
     """get_chunk for many chunks at once (datanode_lib.py:948-1142).  The returned
     device arrays are views of HBM cache slots: valid until the next call that may
@@ -705,37 +807,78 @@ class ChunkStore:
     with chunk_init yields a fill-value (or zero) chunk of the full layout dims."""
 
     def __init__(self, fetch, mem_target=1 << 30, device=None, max_gap=1024):
+        import threading
         import torch
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.cache = DeviceChunkCache(mem_target, dev)
         self.reader = ChunkReader(fetch, cache=self.cache, device=dev, max_gap=max_gap)
+        # every public call holds this lock: the DN event loop and the batcher's worker
+        # thread share one store (the cache's LRU, arena and pins are not thread-safe)
+        self.lock = threading.RLock()
 
     def get_chunks(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
                    hyper_dims=None, chunk_init=False):
+        with self.lock:
+            vals, finish = self.get_chunks_deferred(reads, dtype, chunk_dims, filter_ops=filter_ops,
+                                                    fill_value=fill_value, layout_class=layout_class,
+                                                    hyper_dims=hyper_dims, chunk_init=chunk_init)
+            import torch
+            torch.cuda.current_stream(self.cache.arena.buf.device).synchronize()
+            return finish()
+
+    def get_chunks_deferred(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
+                            hyper_dims=None, chunk_init=False):
+        """get_chunks without waiting for the device: (values, finish).  The values are
+        device views (None for a 404, an exception for a malformed request) whose bytes
+        are ready once the current stream has drained; finish(), called after that,
+        returns the final list with decode failures as HTTPInternalServerError.  Call it
+        under self.lock and keep the lock until the views are consumed (the batcher
+        gathers its selections in between).  Cache hits stay pinned until finish(), so
+        the misses' slot reservations cannot evict them."""
         out = {}
-        todo, seen = [], set()
+        todo, seen, hits = [], set(), []
         for r in reads:
             if r.chunk_id in self.cache:
-                out[r.chunk_id] = self.cache[r.chunk_id]
+                if r.chunk_id not in out:
+                    out[r.chunk_id] = self.cache[r.chunk_id]
+                    self.cache.pin(r.chunk_id)
+                    hits.append(r.chunk_id)
                 self.reader.stats["cache_hits"] += 1
             elif r.chunk_id not in seen:
                 seen.add(r.chunk_id)
                 todo.append(r)
-        if todo:
-            res = self.reader.read(todo, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
-                                   layout_class=layout_class, hyper_dims=hyper_dims)
-            init = [r.chunk_id for r, v in zip(todo, res) if isinstance(v, HTTPNotFound) and chunk_init]
-            if init:
-                self._fill_new(init, dtype, chunk_dims, fill_value)
-            for r, v in zip(todo, res):
-                if isinstance(v, HTTPNotFound) and chunk_init:
-                    v = self.cache[r.chunk_id]
-                elif isinstance(v, HTTPNotFound):
-                    v = None                               # 404: no chunk
-                out[r.chunk_id] = v
+        rfin, init = None, []
+        try:
+            if todo:
+                res, rfin = self.reader.read(todo, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
+                                             layout_class=layout_class, hyper_dims=hyper_dims, defer=True)
+                init = [r.chunk_id for r, v in zip(todo, res) if isinstance(v, HTTPNotFound) and chunk_init]
+                if init:
+                    self._fill_new(init, dtype, chunk_dims, fill_value)
+                for r, v in zip(todo, res):
+                    if isinstance(v, HTTPNotFound) and chunk_init:
+                        v = self.cache[r.chunk_id]
+                    elif isinstance(v, HTTPNotFound):
+                        v = None                               # 404: no chunk
+                    out[r.chunk_id] = v
+        except BaseException:
+            for key in hits:
+                self.cache.unpin(key)
+            raise
+
+        def finish():
+            if rfin is not None:
+                res = rfin()
+                for r, v in zip(todo, res):
+                    if isinstance(v, HTTPInternalServerError):
+                        out[r.chunk_id] = v
             for key in init:
                 self.cache.unpin(key)
-        return [out[r.chunk_id] for r in reads]
+            for key in hits:
+                self.cache.unpin(key)
+            return [out[r.chunk_id] for r in reads]
+
+        return [out[r.chunk_id] for r in reads], finish
 
     def _fill_new(self, keys, dtype, chunk_dims, fill_value):
         """get_chunk's chunk_init for missing objects (datanode_lib.py:1132-1138): a cache
@@ -772,6 +915,7 @@ class ChunkStore:
         self.reader.eng.copy(d_pat, abase, recs)
 
     # ---- write side (PUT_Chunk -> save_chunk -> s3sync / write_s3_obj) ------------
+    @_locked
     def put_selections(self, writes, dtype, chunk_dims, filter_ops=None, fill_value=None, write_zero_chunks=False):
         """PUT_Chunk for many chunks at once (chunk_dn.py:55-314).  `writes` is a list
         of (ChunkRead, slices, data) with data a host ndarray of the selection shape
@@ -808,7 +952,7 @@ class ChunkStore:
             n = self.cache._lru.get(r.chunk_id)
             if n is None:
                 raise MemoryError("chunk cache cannot hold the write batch")
-            n.pinned = True
+            n.pinned += 1
         try:
             abase = self.cache.arena.buf
             data_parts, items, offs = [], [], 0
@@ -839,6 +983,7 @@ class ChunkStore:
         del arrs
         return out
 
+    @_locked
     def put_pieces(self, reads, d_data, make_descs, dtype, chunk_dims, filter_ops=None, fill_value=None,
                    write_zero_chunks=False):
         """PUT_Chunk for many chunks with the request data already in HBM (the sharded
@@ -870,7 +1015,7 @@ class ChunkStore:
             n = self.cache._lru.get(r.chunk_id)
             if n is None:
                 raise MemoryError("chunk cache cannot hold the write batch")
-            n.pinned = True
+            n.pinned += 1
         try:
             abase = self.cache.arena.buf
             offs = [self.cache._lru[r.chunk_id].off for r in reads]
@@ -891,6 +1036,7 @@ class ChunkStore:
         del arrs
         return out
 
+    @_locked
     def encode_dirty(self, filter_ops, stream=None):
         """The device half of flush for a dataset with a Blosc compressor (no bitshuffle):
         ONE asynchronous hsds_encode_batch_codec of every dirty chunk straight from its cache
@@ -920,6 +1066,7 @@ class ChunkStore:
                                    stream=stream)
         return ids, frames, descs, sizes, status
 
+    @_locked
     def flush(self, put, filter_ops=None, keys=None):
         """s3sync for every dirty chunk (datanode_lib.py:1186-1318, 126-311): ONE
         hsds_encode_batch_codec straight from the HBM cache slots (storUtil._compress's

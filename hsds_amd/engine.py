@@ -88,9 +88,14 @@ class HostBuffer:
 
 
 def to_device_bytes(arr, device):
-    """numpy structured / uint8 array -> uint8 tensor on `device`."""
+    """numpy structured / uint8 array -> uint8 tensor on `device`, queued on the current
+    stream: the bytes go through page-locked staging with an asynchronous copy (a pageable
+    copy makes torch synchronise the stream, i.e. wait for every kernel queued before it).
+    The staging block stays reserved by torch's pinned-memory cache until the copy ran."""
     raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
-    return torch.from_numpy(raw.copy()).to(device, non_blocking=False)
+    h = torch.empty(max(raw.size, 1), dtype=torch.uint8, pin_memory=True)
+    h.numpy()[:raw.size] = raw
+    return h[:raw.size].to(device, non_blocking=True)
 
 
 class ChunkEngine:

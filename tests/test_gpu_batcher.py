@@ -51,3 +51,66 @@ def test_batched_get_selection_matches_numpy(oracle_lib):
             assert r is None
         else:
             np.testing.assert_array_equal(r, truth[f"c-b_{i}_0"][sels[j % 3]])
+
+
+def _objs(orc, n, dims, seed):
+    rng = np.random.default_rng(seed)
+    truth, objs = {}, {}
+    for i in range(n):
+        a = np.round(np.cumsum(rng.normal(size=dims[0] * dims[1])), 2).astype("<f4").reshape(dims)
+        truth[f"c-b_{i}_0"] = a
+        objs[f"k{i}"] = orc.blosc_encode(a.tobytes(), typesize=1, clevel=4, shuffle=1)
+    return truth, objs
+
+
+def test_batch_larger_than_cache(oracle_lib):
+    """misses the cache has no room for land in a per-batch buffer, not in the
+    arena; the gather must read them from that buffer (one copy launch per source)"""
+    import torch
+    from hsds_amd.batcher import ChunkBatcher
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    dev = torch.device("cuda", 0)
+    dims = (64, 96)
+    truth, objs = _objs(oracle_lib, 48, dims, 11)
+    chunk_bytes = dims[0] * dims[1] * 4
+    cs = ChunkStore(lambda key, off, ln: objs.get(key), mem_target=5 * chunk_bytes, device=dev)
+    ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
+    b = ChunkBatcher(cs, window_ms=50)
+    sels = [None, (slice(3, 61, 4), slice(1, 96, 5))]
+
+    async def main():
+        return await asyncio.gather(*[b.get_selection(ChunkRead(f"c-b_{j % 48}_0", f"k{j % 48}"), "<f4", dims,
+                                                      sels[j % 2], filter_ops=ops) for j in range(96)])
+
+    res = asyncio.run(main())
+    assert b.stats["batches"] == 1 and b.stats["reads"] == 48
+    assert len(cs.cache) <= 6
+    for j, r in enumerate(res):
+        t = truth[f"c-b_{j % 48}_0"]
+        np.testing.assert_array_equal(r, t if sels[j % 2] is None else t[sels[j % 2]])
+
+
+def test_hits_stay_pinned_while_misses_reserve(oracle_lib):
+    """cache hits of a batch are pinned until it completes, so the misses' slot
+    reservations (which evict clean LRU nodes) cannot reuse a hit's slot mid-batch"""
+    import torch
+    from hsds_amd.batcher import ChunkBatcher
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    dev = torch.device("cuda", 0)
+    dims = (64, 96)
+    truth, objs = _objs(oracle_lib, 30, dims, 12)
+    chunk_bytes = dims[0] * dims[1] * 4
+    cs = ChunkStore(lambda key, off, ln: objs.get(key), mem_target=12 * chunk_bytes, device=dev)
+    ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
+    warm = cs.get_chunks([ChunkRead(f"c-b_{i}_0", f"k{i}") for i in range(10)], "<f4", dims, filter_ops=ops)
+    assert all(v is not None for v in warm) and len(cs.cache) == 10
+    b = ChunkBatcher(cs, window_ms=50)
+
+    async def main():
+        return await asyncio.gather(*[b.get_chunk(ChunkRead(f"c-b_{i}_0", f"k{i}"), "<f4", dims, filter_ops=ops)
+                                      for i in range(30)])
+
+    res = asyncio.run(main())
+    for i, r in enumerate(res):
+        np.testing.assert_array_equal(r, truth[f"c-b_{i}_0"])
+    assert all(n.pinned == 0 for n in cs.cache._lru.values())

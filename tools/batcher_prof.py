@@ -1,0 +1,89 @@
+"""Diagnostic: where the DN micro-batcher's time goes for N concurrent whole-chunk F1
+requests (stage timers around the batch's steps + cProfile's top entries).  GPU box:
+python tools/batcher_prof.py [N]"""
+import asyncio
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from bench import smooth_chunk, CHUNK_BYTES  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+from hsds_amd import batcher as bt, datanode as dn  # noqa: E402
+
+T = {}
+
+
+def timed(mod, name):
+    f = getattr(mod, name)
+
+    def w(*a, **k):
+        t = time.perf_counter()
+        try:
+            return f(*a, **k)
+        finally:
+            T[name] = T.get(name, 0.0) + time.perf_counter() - t
+    setattr(mod, name, w)
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    dev = torch.device("cuda", 0)
+    chunks = [smooth_chunk(777 + i).view(np.uint8).tobytes() for i in range(64)]
+    objs = {f"k{i}": orc.blosc_encode(c, typesize=1, clevel=4, shuffle=1) for i, c in enumerate(chunks)}
+    ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
+    dims = (CHUNK_BYTES // 4,)
+    cs = dn.ChunkStore(lambda key, off, ln: objs.get(key), mem_target=1 << 31, device=dev)
+    for name in ("_stage_blobs", "_decode_batch", "device_view", "_flat_desc"):
+        timed(dn, name)
+    for cls, names in ((dn.ChunkReader, ("_plan", "read")), (dn.DeviceChunkCache, ("reserve", "unpin")),
+                       (dn.ChunkStore, ("get_chunks_deferred",)), (bt.ChunkBatcher, ("_run_batch",))):
+        for name in names:
+            timed(cls, name)
+    from hsds_amd import engine as en
+    for name in ("decode", "copy"):
+        timed(en.ChunkEngine, name)
+    for name in ("_gather_launch", "_gather_finish"):
+        timed(bt, name)
+    sync = torch.cuda.Stream.synchronize
+
+    def tsync(self):
+        t = time.perf_counter()
+        sync(self)
+        T["stream_sync"] = T.get("stream_sync", 0.0) + time.perf_counter() - t
+    torch.cuda.Stream.synchronize = tsync
+
+    def one():
+        cs.cache.clearCache()
+        b = bt.ChunkBatcher(cs, window_ms=0.5)
+
+        async def run():
+            return await asyncio.gather(*[b.get_chunk(dn.ChunkRead(f"c-x_{j}", f"k{j % 64}"), "<f4", dims,
+                                                      filter_ops=ops) for j in range(n)])
+        t = time.perf_counter()
+        got = asyncio.run(run())
+        el = time.perf_counter() - t
+        assert got[-1].tobytes() == chunks[(n - 1) % 64]
+        return el
+    for _ in range(3):
+        one()
+    T.clear()
+    els = [one() for _ in range(5)]
+    print(f"n={n} median {np.median(els)*1e3:.2f} ms  {n * CHUNK_BYTES / np.median(els) / 1e9:.2f} GB/s")
+    for k, v in T.items():
+        print(f"  {k:16s} {v / 5 * 1e3:8.2f} ms per batch")
+    pr = cProfile.Profile()
+    pr.enable()
+    one()
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+
+
+if __name__ == "__main__":
+    main()

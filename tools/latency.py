@@ -65,11 +65,12 @@ def main():
     ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
     dims = (CHUNK_BYTES // 4,)
     res = {}
+    cs = ChunkStore(lambda key, off, ln: store_objs.get(key), mem_target=1 << 31, device=dev)
     for n in (1, 16, 64, 256):
         ts = []
-        for rep in range(3):
-            # a fresh store per trial: every request decodes (no cache hits)
-            cs = ChunkStore(lambda key, off, ln: store_objs.get(key), mem_target=1 << 31, device=dev)
+        for rep in range(5):
+            # an emptied cache per trial: every request decodes (no cache hits)
+            cs.cache.clearCache()
             b = ChunkBatcher(cs, window_ms=0.5)
 
             async def run():
@@ -79,7 +80,7 @@ def main():
             got = asyncio.run(run())
             ts.append(time.perf_counter() - t)
             assert b.stats["batches"] == 1
-            assert got[0].tobytes() == chunks[0]
+            assert got[0].tobytes() == chunks[0] and got[-1].tobytes() == chunks[(n - 1) % 64]
         el = statistics.median(ts)
         res[str(n)] = {"ms": round(el * 1e3, 2), "GBps": round(n * CHUNK_BYTES / el / 1e9, 2)}
     out["batcher_F1_concurrent_requests"] = res
