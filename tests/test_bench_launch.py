@@ -41,3 +41,43 @@ def test_world_size_must_match_gpus():
     p = _run(["--gpus", "2", "--dry-run", "1"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert p.returncode == 2
     assert "WORLD_SIZE" in p.stderr
+
+
+_PARENT = r"""
+import sys, torch
+def _no_gpu(*a, **k):
+    raise RuntimeError("the launching parent touched the GPU runtime")
+for name in ("device_count", "is_available", "init", "_lazy_init", "current_device", "set_device"):
+    setattr(torch.cuda, name, _no_gpu)
+sys.path.insert(0, sys.argv[1])
+import bench
+sys.exit(bench.launch_ranks(int(sys.argv[2]), sys.argv[3:]))
+"""
+
+
+def _fake_topology(tmp_path, gpus):
+    nodes = tmp_path / "nodes"
+    for i, simd in enumerate([0] + [1024] * gpus):        # node 0: the CPU
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if simd else 64}\nsimd_count {simd}\n")
+    return str(nodes)
+
+
+def test_parent_counts_gpus_without_the_gpu_runtime(tmp_path):
+    """the --gpus N parent counts devices from the KFD topology and never
+    calls into torch.cuda; the ranks it starts see the full world"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT",
+                                                             "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                                                             "ROCR_VISIBLE_DEVICES")}
+    env["HSDS_KFD_TOPOLOGY"] = _fake_topology(tmp_path, 2)
+    p = subprocess.run([sys.executable, "-c", _PARENT, ROOT, "2", "--gpus", "2", "--dry-run", "1"], env=env,
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    assert line["n_gpus"] == 2 and line["rccl_world"] == 2
+    # the visibility variables limit the count as the runtime would
+    env["HIP_VISIBLE_DEVICES"] = "1"
+    p = subprocess.run([sys.executable, "-c", _PARENT, ROOT, "2", "--gpus", "2", "--dry-run", "1"], env=env,
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 2 and "1 visible GPU" in p.stderr
