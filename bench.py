@@ -899,17 +899,22 @@ def cpu_model():
 
 def copy_ceiling(dev, nbytes=2 << 30, reps=5):
     """Measured HIP streaming-copy ceilings (BASELINE 4): a device-to-device
-    hipMemcpyAsync (torch copy_) and the engine's copy_kernel on one contiguous record of
-    the same bytes; GB/s of read + write bytes, HIP events on the launch stream."""
+    hipMemcpyAsync (torch copy_) and the engine's copy_kernel over the same bytes as
+    1-byte-element records of 256 MiB each (the contiguous byte runs the kernel's 16-byte
+    slot path streams: a record's bytes must stay below 2^31); GB/s of read + write
+    bytes, HIP events on the launch stream."""
     import torch
     from hsds_amd.engine import ChunkEngine, COPY_DESC_DTYPE, to_device_bytes
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     a.fill_(7)
-    rec = np.zeros(1, COPY_DESC_DTYPE)
-    rec["rank"], rec["itemsize"] = 1, 16
-    rec["count"][0, 0] = nbytes // 16
-    rec["src_stride"][0, 0] = rec["dst_stride"][0, 0] = 16
+    piece = 256 << 20
+    nrec = nbytes // piece
+    rec = np.zeros(nrec, COPY_DESC_DTYPE)
+    rec["rank"], rec["itemsize"] = 1, 1
+    rec["src_off"] = rec["dst_off"] = np.arange(nrec, dtype=np.uint64) * piece
+    rec["count"][:, 0] = piece
+    rec["src_stride"][:, 0] = rec["dst_stride"][:, 0] = 1
     d_rec = to_device_bytes(rec, dev)
     eng = ChunkEngine(dev.index)
     stream = torch.cuda.current_stream()
@@ -926,7 +931,7 @@ def copy_ceiling(dev, nbytes=2 << 30, reps=5):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         out[name] = round(2 * nbytes / (ms / 1e3) / 1e9, 1)
-    assert bool((b[:4096] == 7).all())
+    assert bool((b[:4096] == 7).all()) and bool((b[-4096:] == 7).all())
     del a, b
     torch.cuda.empty_cache()
     return out

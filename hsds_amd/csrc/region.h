@@ -65,6 +65,7 @@ RG_HD int nreg_make(const hsds_copy_desc& d, int fold, NReg& n) {
   for (int k = 0; k < d.rank && k < HSDS_MAX_RANK; k++) {
     const int64_t c = d.count[k];
     if (c <= 0) return 0;
+    if (c >= (1ll << 31)) return 0;     // outside the ABI's range (hsds_copy_desc): the host splits such dims
     if (c == 1) continue;
     n.cnt[r] = (uint32_t)c;
     n.ss[r] = d.src_stride[k];
@@ -161,7 +162,9 @@ RG_HD Plan plan_copy(const NReg& n) {
   p.ids = n.ds[n.r - 1];
   p.isz = n.isz;
   p.run = p.isz == 1 && p.iss == 1 && p.ids == 1;
-  p.gather = !p.run && p.ids == p.isz && (p.isz == 1 || p.isz == 2 || p.isz == 4 || p.isz == 8);
+  // (the 16-byte slot paths count a row's bytes in 32 bits)
+  p.gather = !p.run && p.ids == p.isz && (p.isz == 1 || p.isz == 2 || p.isz == 4 || p.isz == 8) &&
+             (uint64_t)p.C * (uint64_t)p.isz < (1ull << 31);
   const uint32_t units = p.run ? (p.C + 30u) / 16u : p.gather ? (p.C * (uint32_t)p.isz + 30u) / 16u : p.C;
   plan_groups(n, units, p);
   return p;

@@ -181,8 +181,11 @@ class ChunkEngine:
         return self.eng.last_deflate_ms()
 
     def copy(self, src, dst, copy_descs, stream=None, flags=None):
-        """Asynchronous strided region copies (COPY_DESC_DTYPE records)."""
+        """Asynchronous strided region copies (COPY_DESC_DTYPE records).  Dimensions of
+        2^31 elements or more (outside the ABI's range) are split into several records."""
         if isinstance(copy_descs, np.ndarray):
+            if flags is None:
+                copy_descs = split_large_copy_descs(copy_descs)
             n = copy_descs.size
             copy_descs = to_device_bytes(copy_descs, self.device)
         else:
@@ -220,6 +223,36 @@ class ChunkEngine:
                                            _stream_handle(stream))
         if rc != nat.OK:
             raise nat.NativeError(rc, "hsds_shuffle_device")
+
+
+COUNT_LIMIT = 1 << 31       # hsds_copy_desc: every count below 2^31
+
+
+def split_large_copy_descs(recs, limit=COUNT_LIMIT):
+    """Records whose counts reach `limit` split along those dimensions into pieces of
+    limit // 2 elements (offsets advanced by the piece's stride); other records pass
+    through unchanged and in order."""
+    recs = np.ascontiguousarray(recs)
+    if recs.size == 0 or not (recs["count"] >= limit).any():
+        return recs
+    out = []
+    for r in recs:
+        todo = [r.copy()]
+        while todo:
+            x = todo.pop()
+            big = [k for k in range(int(x["rank"])) if x["count"][k] >= limit]
+            if not big:
+                out.append(x)
+                continue
+            k = big[0]
+            c, piece = int(x["count"][k]), limit // 2
+            for start in range(0, c, piece):
+                y = x.copy()
+                y["count"][k] = min(piece, c - start)
+                y["src_off"] = int(x["src_off"]) + start * int(x["src_stride"][k])
+                y["dst_off"] = int(x["dst_off"]) + start * int(x["dst_stride"][k])
+                todo.append(y)
+    return np.array(out, dtype=recs.dtype)
 
 
 def encode_descs(src_lens, align=256, overhead=16):

@@ -84,7 +84,8 @@ typedef struct {
  *   for every index tuple i (0 <= i[k] < count[k]):
  *     dst[dst_off + sum i[k]*dst_stride[k]] <- src[src_off + sum i[k]*src_stride[k]]
  * moving `itemsize` bytes per element.  Strides are in bytes and already include
- * the slice step. */
+ * the slice step.  Every count must be below 2^31 (hsds_amd.engine splits larger
+ * dimensions into several records); a record with a larger count copies nothing. */
 typedef struct {
   uint64_t src_off;
   uint64_t dst_off;

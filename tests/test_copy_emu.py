@@ -134,3 +134,28 @@ def test_long_rows_are_split(emu, n, so, do, isz):
     b[do + n * isz - 2] ^= 1
     emu.emu_compare(b.ctypes.data, a.ctypes.data, rec2.ctypes.data, 1, 0, differs.ctypes.data)
     assert differs[0] == 1
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_split_of_large_counts(emu, seed):
+    """counts of 2^31 or more are split on the host (ChunkEngine.copy); the
+    split is checked here at a small limit against the unsplit records"""
+    from hsds_amd.engine import split_large_copy_descs
+    src, dst0, recs = batch(100 + seed)
+    lim = 8
+    parts = split_large_copy_descs(recs, limit=lim)
+    assert (parts["count"] < lim).all() and len(parts) > len(recs)
+    assert (_copy(emu, src, dst0, parts) == _model(src, dst0, recs)).all()
+
+
+def test_count_beyond_abi_range_copies_nothing(emu):
+    """a record with a count of 2^31 or more (outside hsds_copy_desc's range) is skipped by
+    the kernel, not narrowed to 32 bits"""
+    from hsds_amd.engine import COPY_DESC_DTYPE
+    src = np.arange(64, dtype=np.uint8)
+    dst0 = np.zeros(64, np.uint8)
+    rec = np.zeros(1, COPY_DESC_DTYPE)
+    rec["rank"], rec["itemsize"] = 1, 1
+    rec["count"][0, 0] = (1 << 32) + 4                  # narrowed to 32 bits this would be 4
+    rec["src_stride"][0, 0] = rec["dst_stride"][0, 0] = 1
+    assert (_copy(emu, src, dst0, rec) == dst0).all()
