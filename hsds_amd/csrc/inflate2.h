@@ -75,6 +75,23 @@ constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = 
 #ifndef HZ2_M2
 #define HZ2_M2 0
 #endif
+// HZ2_MLIGHT: the resolve's LDS hand-offs are wavefront-scope (no s_waitcnt vmcnt(0) /
+// s_barrier of __syncthreads), so the next span's records and the head dword stay in
+// flight across them; the span's end keeps the workgroup-scope release (its stores are
+// read back as far sources)
+#ifndef HZ2_MLIGHT
+#define HZ2_MLIGHT 1
+#endif
+#if HZ2_MLIGHT
+#define HZ2_MSYNC() HZ2_LSYNC()
+#else
+#define HZ2_MSYNC() WAVE_SYNC()
+#endif
+// HZ2_FILLB: the resolve's source-map fill writes the first 4 bytes of all of a lane's
+// matches without a loop, then the remainder of longer matches
+#ifndef HZ2_FILLB
+#define HZ2_FILLB 0
+#endif
 constexpr uint32_t RDYW = SPAN / 32u + 2u;  // ready bitmap words
 // phase E: match records are staged per lane and stored as whole aligned 32-byte groups
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
@@ -1302,7 +1319,7 @@ HZ_UNROLL
 #else
       for (uint32_t b0 = 0; F < wend;) {
 #endif
-        HZ_T(8);
+        HZ_T(14);
         HZ2_MARK("M_BATCH");
         if (stats) stats->batches++;
         uint32_t nb = 0, open_ = 1;
@@ -1329,6 +1346,7 @@ HZ_UNROLL
         const bool head = mis && (int32_t)xa >= 0 && xa + 4u <= dst_len;   // dword 0 loaded (whole-stored)
         uint32_t hv = 0;
         if (head) hv = *(hz_gu32*)(dst + xa);
+        HZ_T(8);
         // the whole map is cleared (three 16-byte stores per lane): slots past the span read 0
         static_assert(SPAN % 256u == 0u, "smap clear: whole 8-byte stores per lane");
         LANE_LOOP {
@@ -1348,7 +1366,7 @@ HZ_UNROLL
           memset(&sh.smap[(SPAN / 64u) * (uint32_t)lane], 0, SPAN / 32u);
 #endif
         }
-        WAVE_SYNC();
+        HZ2_MSYNC();
         if (stats) {
           uint64_t mx = 0, sm = 0;
           for (int l = 0; l < 64; l++) {
@@ -1360,6 +1378,45 @@ HZ_UNROLL
           }
           stats->fill_max += mx; stats->fill_sum += sm; stats->span_sum += span;
         }
+#if HZ2_FILLB
+        // the first 4 bytes of every match at once (no loop: matches are >= 3 bytes and
+        // mostly <= 4 here), then the rest of the longer ones
+        LANE_LOOP {
+HZ_UNROLL
+          for (uint32_t u = 0; u < MPL; u++) {
+            const bool in = (uint32_t)lane + 64u * u < nb;
+            const uint32_t o0 = LV(ro)[u] - F, ln = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
+            uint32_t dist = d, jj = 0;
+HZ_UNROLL
+            for (uint32_t t = 0; t < 4u; t++) {
+              sh.smap[t < ln ? o0 + t : SPAN + 1u] = (uint16_t)dist;
+              jj++;
+              const bool w = jj == d;
+              jj = w ? 0u : jj;
+              dist += w ? d : 0u;
+            }
+          }
+HZ_UNROLL
+          for (uint32_t u = 0; u < MPL; u++) {
+            const bool in = (uint32_t)lane + 64u * u < nb;
+            const uint32_t o0 = LV(ro)[u] - F, ln = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
+            if (ln > 4u) {
+              uint32_t jj = mod_small(4u, d), dist = d + 4u - jj;
+              for (uint32_t t0 = 4u; t0 < ln; t0 += 4u) {
+HZ_UNROLL
+                for (uint32_t k = 0; k < 4u; k++) {
+                  const uint32_t t = t0 + k;
+                  sh.smap[t < ln ? o0 + t : SPAN + 1u] = (uint16_t)dist;
+                  jj++;
+                  const bool w = jj == d;
+                  jj = w ? 0u : jj;
+                  dist += w ? d : 0u;
+                }
+              }
+            }
+          }
+        }
+#else
         LANE_LOOP {
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) {
@@ -1383,7 +1440,9 @@ HZ_UNROLL
             }
           }
         }
-        WAVE_SYNC();
+#endif
+        HZ2_MSYNC();
+        HZ_T(15);
         // prefetch the next batch's records
         LANE_ARR(uint32_t, no, MPL);
         LANE_ARR(uint32_t, nw, MPL);
@@ -1427,12 +1486,12 @@ HZ_UNROLL
             }
             if (stats) stats->tokens++;                // (emulator statistic: pointer-jumping rounds)
             if (!WAVE_BALLOT(LV(chg) != 0u)) break;
-            WAVE_SYNC();
+            HZ2_MSYNC();
             LANE_LOOP {
 HZ_UNROLL
               for (uint32_t i = 0; i < RGP; i++) sh.smap[(uint32_t)lane + 64u * i] = (uint16_t)LV(dq)[i];
             }
-            WAVE_SYNC();
+            HZ2_MSYNC();
           }
         }
         HZ_T(12);
@@ -1452,7 +1511,7 @@ HZ_UNROLL
         LANE_VAR(uint32_t, lb);                 // literal slots
         LANE_VAR(uint32_t, fb);                 // match bytes whose source lies before F
         LANE_LOOP { LV(lb) = 0; LV(fb) = 0; if (lane == 0) sh.sbuf[0] = hv; }
-        WAVE_SYNC();
+        HZ2_MSYNC();
         uint32_t lcnt = 0;                      // literals of the span so far (wave-uniform)
         // two halves of GH slots: GH loaded bytes in flight per lane (all 24 spill)
         constexpr uint32_t GH = RGP / 2u;
@@ -1495,7 +1554,7 @@ HZ_UNROLL
             LV(ra2) += (uint64_t)F * a1 + b2;
           }
         }
-        WAVE_SYNC();
+        HZ2_MSYNC();
         // in-span sources: literals of the span, now in LDS
         LANE_LOOP {
           uint32_t a1 = 0, b2 = 0;
@@ -1518,7 +1577,7 @@ HZ_UNROLL
           LV(ra1) += a1;
           LV(ra2) += (uint64_t)F * a1 + b2;
         }
-        WAVE_SYNC();
+        HZ2_MSYNC();
         HZ_T(13);
         HZ2_MARK("M_STORE");
         // 4. store: whole dwords inside the span (dword 0 also when its head was loaded) and

@@ -20,7 +20,7 @@ from bench import make_corpus, CHUNK_BYTES  # noqa: E402
 from hsds_amd.engine import ChunkEngine, pack_chunks  # noqa: E402
 
 NAMES = ["other", "blk-hdr", "tables", "A", "A'", "repair", "valid+scan", "E", "M-fill", "trailer", "win-end",
-         "M-load", "M-resolve", "M-store", "-", "-"]
+         "M-jump", "M-gather", "M-store", "M-setup", "M-prefetch"]
 
 
 LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
