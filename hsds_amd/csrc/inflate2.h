@@ -6,25 +6,31 @@
 // is bit-identical to libz; corrupt / truncated streams and adler32 mismatches fail (the
 // reference's HTTPInternalServerError).
 //
-// Design (DESIGN.md "Inflate"): a Huffman block is cut into 64 segments of L bits, L sized
-// from the previous block so that one window covers the whole block (L is thousands of
-// bits, not hundreds).  Per window:
+// Design (DESIGN.md "The inflate kernel"): a Huffman block is cut into 64 segments of L bits,
+// L sized from the previous block so that one window covers the whole block (L is thousands
+// of bits, not hundreds).  Per window:
 //   A   lane i decodes from W bits before its segment (warm-up: Huffman codes
 //       self-synchronise) to the first token start at or past the next segment, recording
-//       its first K token starts with the output / match counts reached there;
+//       its first K token starts with the output / match / literal counts reached there;
 //   A'  lane i keeps decoding into segment i+1 until it lands on one of lane i+1's recorded
 //       starts ("sync": from there both decodes coincide) -- no token storage at all;
 //   R   a lane its predecessor never met is re-decoded from the predecessor's exit;
-//   P   wave prefix sums of the synced output / match counts give every lane its output
-//       offset and its slot in the wave's match ring;
-//   E   every valid lane decodes its exact range again: literal bytes go straight to their
-//       final address in dst, matches (pos, len, dist) to the match ring in HBM;
-//   M   the ring is resolved in batches of 64 matches: bytes a batch's match copies either
-//       lie before the batch (final) or inside an earlier match of the batch (one LDS owner
-//       map hop each), so all 64 lanes copy at once.
-// The output address of stream byte x goes through an optional byte-unshuffle permutation
-// (HDF5 shuffle of F2 chunks, Blosc typesize > 1 blocks), so unshuffle costs nothing extra.
-// adler32 is accumulated as per-lane (sum b, sum pos*b) pairs by the emit and resolve steps.
+//   P   wave prefix sums of the synced output / match / literal counts give every lane its
+//       output offset, its slots in the wave's match ring and its offset in the window's
+//       literal stream;
+//   E   every valid lane decodes its exact range again.  Nothing goes to dst: literal bytes
+//       go to the literal stream, matches to the match ring as (position, length, distance)
+//       records, both staged per lane in LDS and stored in whole groups;
+//   M   the window's output is written span by span (SPAN bytes / <= 256 matches): a
+//       source map of the span's match bytes (distance to an equal earlier byte, the
+//       periodic extension of overlapping copies), pointer jumping until every match byte's
+//       source is a literal of the span or a final byte before it, one gather per byte slot
+//       (literal stream or dst), in-span sources from LDS, and the span's aligned dwords
+//       stored from LDS.  Every output byte is written once.
+// Shuffled streams (F2, Blosc typesize > 1) are inflated plain into a staging buffer and
+// unshuffled afterwards by unshuffle_kernel (engine.hip); Job.perm must be the identity.
+// adler32 is accumulated as per-lane (sum b, sum pos*b) pairs by M's gather and the
+// stored-block copy.
 //
 // SINGLE SOURCE for the HIP kernel and the CPU emulation (tests/emu/inflate2_emu.cpp), like
 // inflate_wave.h whose helpers (table build, LUT format, load_word) it reuses.
@@ -86,6 +92,11 @@ constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = 
 #define HZ2_MSYNC() HZ2_LSYNC()
 #else
 #define HZ2_MSYNC() WAVE_SYNC()
+#endif
+// HZ2_SPANLIGHT: a span's stores reach the next spans' far loads of the same wavefront by
+// wavefront-scope ordering instead of a workgroup-scope release (which waits for them)
+#ifndef HZ2_SPANLIGHT
+#define HZ2_SPANLIGHT 0
 #endif
 // HZ2_FILLB: the resolve's source-map fill writes the first 4 bytes of all of a lane's
 // matches without a loop, then the remainder of longer matches
@@ -618,6 +629,23 @@ struct HR {
   HZ2_HM void drop(uint32_t n) { p += n; }
   HZ2_HM uint32_t pos() const { return base + p; }
 };
+// the same reader with its current two words in registers and the next one loaded ahead:
+// a symbol's peek is one funnel shift, and the only LDS read on the serial path of the
+// code-length loop is the table lookup (a drop of <= 32 bits crosses at most one word)
+struct HRR {
+  const uint32_t* b;
+  uint32_t p, base, w0, w1, w2, wi;
+  HZ2_HM void init(const uint32_t* bits, uint32_t p0, uint32_t base0) {
+    b = bits; p = p0; base = base0; wi = p0 >> 5;
+    w0 = b[wi]; w1 = b[wi + 1u]; w2 = b[wi + 2u];
+  }
+  HZ2_HM uint32_t peek() const { return funnel(w1, w0, p & 31u); }
+  HZ2_HM void drop(uint32_t n) {
+    p += n;
+    if ((p >> 5) != wi) { wi++; w0 = w1; w1 = w2; w2 = b[wi + 2u]; }
+  }
+  HZ2_HM uint32_t pos() const { return base + p; }
+};
 
 enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_ERR = 3 };
 struct Tok {
@@ -685,10 +713,11 @@ struct Stats {
 namespace hz2 {
 __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wave_excl_scan(v, (int)threadIdx.x); }
 }  // namespace hz2
-// value of lane-variable v in lane i (uniform i); LANE_ARR: a per-lane array
-#define LV_AT(v, i) ((uint32_t)__shfl((int)(v), (int)(i), 64))
+// value of lane-variable v in lane i (uniform i: v_readlane, no LDS round trip as a
+// ds_bpermute shuffle would take); LANE_ARR: a per-lane array
+#define LV_AT(v, i) ((uint32_t)__builtin_amdgcn_readlane((int)(v), (int)(i)))
 #define LANE_ARR(T, name, n) T name[n]
-#define LVA_AT(arr, u, i) ((uint32_t)__shfl((int)hz2::sel4(arr, u), (int)(i), 64))
+#define LVA_AT(arr, u, i) ((uint32_t)__builtin_amdgcn_readlane((int)hz2::sel4(arr, u), (int)(i)))
 // a lane counter made wave-uniform (the first active lane's), for epoch boundaries
 #define HZ2_UNI(v) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(v)))
 // lane-variable v of the lane below (lane 0 reads its own: callers select)
@@ -907,22 +936,28 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             }
           }
           const uint32_t total = hlit + hdist;
-          uint32_t n = 0;
+          uint32_t n = 0, prevl = 0;
+          HRR rr;
+          rr.init(sh.hbits, r.p, r.base);
           while (st == ST_OK && n < total) {
-            if (r.pos() > limit_bits + 64u) { st = ST_TRUNC; break; }
-            const uint32_t e = clut[r.peek() & 127u];
+            if (rr.pos() > limit_bits + 64u) { st = ST_TRUNC; break; }
+            const uint32_t bits = rr.peek();
+            const uint32_t e = clut[bits & 127u];
             const uint32_t sym = e & 0xffu, l = e >> 8;
-            r.drop(l);
-            if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
+            if (sym < 16) { rr.drop(l); sh.lens[n++] = (uint8_t)sym; prevl = sym; continue; }
+            // a repeat: its extra bits follow the code in the same peek (7 + 7 bits)
+            const uint32_t x = bits >> l;
             uint32_t rep, val = 0;
             if (sym == 16) {
               if (n == 0) { st = ST_DATA; break; }
-              val = sh.lens[n - 1]; rep = 3 + (r.peek() & 3u); r.drop(2);
-            } else if (sym == 17) { rep = 3 + (r.peek() & 7u); r.drop(3); }
-            else { rep = 11 + (r.peek() & 127u); r.drop(7); }
+              val = prevl; rep = 3 + (x & 3u); rr.drop(l + 2u);
+            } else if (sym == 17) { rep = 3 + (x & 7u); rr.drop(l + 3u); }
+            else { rep = 11 + (x & 127u); rr.drop(l + 7u); }
             if (n + rep > total) { st = ST_DATA; break; }
             for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
+            prevl = val;
           }
+          r.p = rr.p;
           if (st == ST_OK && r.pos() > limit_bits) st = ST_TRUNC;
           if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;   // missing end-of-block code
           if (st == ST_OK) {
@@ -1314,6 +1349,11 @@ HZ_UNROLL
       LANE_LOOP { if (lane == 0) sh.smap[SPAN] = 0; }
       const uint32_t wend = out + wtotal;
       uint32_t F = out, L0 = 0;      // frontier and its rank in the literal stream
+      // the dword that holds the frontier: the last one the previous span assembled (its
+      // bytes before F are final: that span's own or its head), so only a window's first
+      // span loads it
+      uint32_t hcar = 0;
+      bool hcar_ok = false;
 #ifdef HZ2_EXP_NOM
       for (uint32_t b0 = 0; F < 0u;) {
 #else
@@ -1345,7 +1385,7 @@ HZ_UNROLL
         const uint32_t ndw = (span + mis + 3u) >> 2;
         const bool head = mis && (int32_t)xa >= 0 && xa + 4u <= dst_len;   // dword 0 loaded (whole-stored)
         uint32_t hv = 0;
-        if (head) hv = *(hz_gu32*)(dst + xa);
+        if (head) hv = hcar_ok ? hcar : *(hz_gu32*)(dst + xa);   // the previous span's last dword
         HZ_T(8);
         // the whole map is cleared (three 16-byte stores per lane): slots past the span read 0
         static_assert(SPAN % 256u == 0u, "smap clear: whole 8-byte stores per lane");
@@ -1596,7 +1636,13 @@ HZ_UNROLL
             }
           }
         }
+        hcar = sh.sbuf[ndw - 1u];
+        hcar_ok = true;
+#if HZ2_SPANLIGHT
+        HZ2_LSYNC();      // this wave reads the stored dwords back: wavefront-scope ordering
+#else
         WAVE_SYNC_GLOBAL();
+#endif
         LANE_LOOP {
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) { LV(ro)[u] = LV(no)[u]; LV(rw)[u] = LV(nw)[u]; }
