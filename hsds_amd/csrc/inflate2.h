@@ -74,13 +74,6 @@ static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 static_assert(SPL <= 24, "resolve slots per lane");
 constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = lane + 64 i)
-// HZ2_M2 (default): match-level resolve.  A lane takes 4 consecutive matches of a span; literal
-// runs are copied from an LDS copy of the span's literals, every match byte whose source lies
-// before the frontier is copied from dst at once, and only matches with sources inside the span
-// wait for them in rounds over a ready bitmap.  0: the round-3 byte-slot pointer-jumping resolve.
-#ifndef HZ2_M2
-#define HZ2_M2 0
-#endif
 // HZ2_MLIGHT: the resolve's LDS hand-offs are wavefront-scope (no s_waitcnt vmcnt(0) /
 // s_barrier of __syncthreads), so the next span's records and the head dword stay in
 // flight across them; the span's end keeps the workgroup-scope release (its stores are
@@ -98,12 +91,6 @@ constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = 
 #ifndef HZ2_SPANLIGHT
 #define HZ2_SPANLIGHT 0
 #endif
-// HZ2_FILLB: the resolve's source-map fill writes the first 4 bytes of all of a lane's
-// matches without a loop, then the remainder of longer matches
-#ifndef HZ2_FILLB
-#define HZ2_FILLB 0
-#endif
-constexpr uint32_t RDYW = SPAN / 32u + 2u;  // ready bitmap words
 // phase E: match records are staged per lane and stored as whole aligned 32-byte groups
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
 // bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
@@ -176,18 +163,10 @@ struct alignas(16) Shared {
         };
       };
     };
-#if HZ2_M2
-    struct {                      // phase M (match-level resolve)
-      uint32_t sbuf[SPAN / 4 + 2];   // the span's aligned dwords, assembled in LDS
-      uint32_t lbuf[SPAN / 4 + 4];   // the span's literals: stream dwords from L0 & ~3, at dword 1
-      uint32_t rdy[RDYW];            // bit x: span byte x final (cleared for in-span-sourced matches)
-    };
-#else
     struct {                      // phase M
       uint16_t smap[SPAN + 2];    // batch byte -> distance to its source (0: literal); [SPAN] stays 0
       uint32_t sbuf[SPAN / 4 + 2];   // the batch's aligned dwords, assembled in LDS
     };
-#endif
   };
   uint8_t syncw[WAVE];            // record index where the predecessor met this lane / SYNC_*
   uint32_t endp[WAVE];            // lane's exclusive end (token boundary)
@@ -720,8 +699,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
 #define LVA_AT(arr, u, i) ((uint32_t)__builtin_amdgcn_readlane((int)hz2::sel4(arr, u), (int)(i)))
 // a lane counter made wave-uniform (the first active lane's), for epoch boundaries
 #define HZ2_UNI(v) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(v)))
-// lane-variable v of the lane below (lane 0 reads its own: callers select)
-#define LV_UP1(v) ((uint32_t)__shfl_up((int)(v), 1, 64))
 // LDS hand-off inside one wavefront: the LDS executes a wave's instructions in order, so
 // only the compiler must not move or cache accesses across this point (no s_waitcnt, no
 // s_barrier: loads in flight -- the next span's match records -- stay in flight)
@@ -731,48 +708,14 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
     __builtin_amdgcn_wave_barrier();                             \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       \
   } while (0)
-#define HZ2_LDS_OR(p, m) atomicOr((p), (m))
-#define HZ2_LDS_AND(p, m) atomicAnd((p), (m))
 #else
 #define HZ2_UNI(v) (v)
 #define LV_AT(v, i) ((v)[i])
 #define LANE_ARR(T, name, n) T name[64][n]
 #define LVA_AT(arr, u, i) ((arr)[i][u])
-#define LV_UP1(v) ((lane) > 0 ? (v)[(lane) - 1] : 0u)
 #define HZ2_LSYNC() do { } while (0)
-#define HZ2_LDS_OR(p, m) (*(p) |= (m))
-#define HZ2_LDS_AND(p, m) (*(p) &= (m))
 #endif
 
-namespace hz2 {
-// sum of the byte products of a and b (v_dot4_u32_u8)
-HZ_HD uint32_t dot4(uint32_t a, uint32_t b) {
-#if HZ_GPU
-  return __builtin_amdgcn_udot4(a, b, 0u, false);
-#else
-  uint32_t s = 0;
-  for (int i = 0; i < 4; i++) s += ((a >> (8 * i)) & 0xffu) * ((b >> (8 * i)) & 0xffu);
-  return s;
-#endif
-}
-// k mod d for k <= 4, d >= 1, without a division
-HZ_HD uint32_t mod_small(uint32_t k, uint32_t d) {
-  uint32_t m = k;
-  m = m >= d ? m - d : m;
-  m = m >= d ? m - d : m;
-  m = m >= d ? m - d : m;
-  m = m >= d ? m - d : m;
-  return m;
-}
-// the bits of bitmap word w that lie in [a, b)
-HZ_HD uint32_t bm_word_mask(uint32_t w, uint32_t a, uint32_t b) {
-  const uint32_t w0 = 32u * w;
-  const uint32_t lo = a > w0 ? a - w0 : 0u, hi = b - w0 < 32u ? b - w0 : 32u;
-  const uint32_t mh = hi >= 32u ? ~0u : (1u << hi) - 1u;
-  const uint32_t ml = lo >= 32u ? ~0u : (1u << lo) - 1u;
-  return mh & ~ml;
-}
-}  // namespace hz2
 #if HZ2_EPOCH
 #define HZ2_TICK(it) do { if ((HZ2_UNI(++(it)) % (uint32_t)HZ2_EPOCH) == 0u) hz2::g_epoch(S, r); } while (0)
 #else
@@ -1315,7 +1258,6 @@ HZ_UNROLL
       if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
       WAVE_SYNC_GLOBAL();
 
-#if !HZ2_M2
       HZ_T(8);
       // -------- phase M: write the window's output, one span at a time --------
       // The window's output [out, out + wtotal) is cut into consecutive spans [F, F + span):
@@ -1418,45 +1360,6 @@ HZ_UNROLL
           }
           stats->fill_max += mx; stats->fill_sum += sm; stats->span_sum += span;
         }
-#if HZ2_FILLB
-        // the first 4 bytes of every match at once (no loop: matches are >= 3 bytes and
-        // mostly <= 4 here), then the rest of the longer ones
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            const bool in = (uint32_t)lane + 64u * u < nb;
-            const uint32_t o0 = LV(ro)[u] - F, ln = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
-            uint32_t dist = d, jj = 0;
-HZ_UNROLL
-            for (uint32_t t = 0; t < 4u; t++) {
-              sh.smap[t < ln ? o0 + t : SPAN + 1u] = (uint16_t)dist;
-              jj++;
-              const bool w = jj == d;
-              jj = w ? 0u : jj;
-              dist += w ? d : 0u;
-            }
-          }
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            const bool in = (uint32_t)lane + 64u * u < nb;
-            const uint32_t o0 = LV(ro)[u] - F, ln = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
-            if (ln > 4u) {
-              uint32_t jj = mod_small(4u, d), dist = d + 4u - jj;
-              for (uint32_t t0 = 4u; t0 < ln; t0 += 4u) {
-HZ_UNROLL
-                for (uint32_t k = 0; k < 4u; k++) {
-                  const uint32_t t = t0 + k;
-                  sh.smap[t < ln ? o0 + t : SPAN + 1u] = (uint16_t)dist;
-                  jj++;
-                  const bool w = jj == d;
-                  jj = w ? 0u : jj;
-                  dist += w ? d : 0u;
-                }
-              }
-            }
-          }
-        }
-#else
         LANE_LOOP {
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) {
@@ -1480,7 +1383,6 @@ HZ_UNROLL
             }
           }
         }
-#endif
         HZ2_MSYNC();
         HZ_T(15);
         // prefetch the next batch's records
@@ -1652,368 +1554,6 @@ HZ_UNROLL
         F += span;
         L0 += lcnt;
       }
-#else
-      HZ_T(8);
-      // -------- phase M: write the window's output, one span at a time --------
-      // The window's output [out, out + wtotal) is cut into consecutive spans [F, F + span):
-      // span = the frontier F up to the end of the last of the next <= 256 matches that end
-      // within SPAN bytes (a span of literals only when the next match does not fit).  Every
-      // byte before F is final in dst.  Lane l takes matches b0 + 4 l + u (u < 4) -- a run of
-      // consecutive matches, so a lane-local prefix plus one wave scan places the literal runs
-      // between them.  Per span:
-      //   1. the span's literals (contiguous in the literal stream) are loaded into LDS with
-      //      coalesced dword loads; every span byte is marked ready, then the matches whose
-      //      sources reach into the span ("near") clear the ready bits of their output;
-      //   2. literal runs are copied into the span buffer (a span of literals only: whole
-      //      dwords by funnel shifts); every match byte whose source lies before F is loaded
-      //      from dst (16 loads in flight per lane for the first 4 bytes of its 4 matches);
-      //   3. rounds: a near match whose in-span source bytes are all ready copies them (LDS to
-      //      LDS, the periodic extension t mod d for overlapping copies) and sets its ready
-      //      bits.  Its sources precede it, so the earliest pending match is always ready: the
-      //      rounds end, at most one per near match;
-      //   4. the span's aligned dwords are stored from LDS, whole where they lie inside the
-      //      span (dword 0 merged with the final bytes before F), byte by byte at its edges;
-      //      adler32 sums by v_dot4 over the stored dwords.
-      // Every output byte is written once, coalesced; E stored nothing to dst.
-      // match bytes' adler sums: a1 < 2^32 and a2 < 2^64 for any window (< 2^24 bytes)
-      LANE_VAR(uint32_t, ra1);
-      LANE_VAR(uint64_t, ra2);
-      LANE_LOOP { LV(ra1) = 0; LV(ra2) = 0; }
-      LANE_ARR(uint32_t, ro, MPL);     // match u of the lane: output position (~0u: none)
-      LANE_ARR(uint32_t, rw, MPL);     // len << 16 | (dist - 1)
-      LANE_LOOP {
-HZ_UNROLL
-        for (uint32_t u = 0; u < MPL; u++) {
-          const uint32_t j = 4u * (uint32_t)lane + u;
-          const uint64_t rec = j < mtotal ? ring64[j] : ~0ull;
-          LV(ro)[u] = j < mtotal ? (uint32_t)rec : 0xffffffffu;
-          LV(rw)[u] = (uint32_t)(rec >> 32);
-        }
-      }
-      hz_gcu32* const lits32 = HZ_GLOBAL(hz_gcu32*, lits);
-      constexpr uint32_t JUNK = (SPAN / 4u + 2u) * 4u - 1u;   // sbuf byte no span byte uses
-      const uint32_t wend = out + wtotal;
-      uint32_t F = out, L0 = 0, b0 = 0;      // frontier, its rank in the literal stream, next match
-      while (F < wend) {
-        HZ2_MARK("M_BATCH");
-        if (stats) stats->batches++;
-        uint32_t nb = 0;
-HZ_UNROLL
-        for (uint32_t u = 0; u < MPL; u++)
-          nb += (uint32_t)hz::popc64(WAVE_BALLOT(LV(ro)[u] != 0xffffffffu && LV(ro)[u] + (LV(rw)[u] >> 16) - F <= SPAN));
-        uint32_t span;
-        if (nb) {
-          const uint32_t last_o = LVA_AT(ro, (nb - 1u) & 3u, (nb - 1u) >> 2);
-          const uint32_t last_w = LVA_AT(rw, (nb - 1u) & 3u, (nb - 1u) >> 2);
-          span = last_o + (last_w >> 16) - F;
-        } else {
-          const uint32_t nxt = b0 < mtotal ? LVA_AT(ro, 0u, 0u) : wend;
-          span = nxt - F < SPAN ? nxt - F : SPAN;
-        }
-        // prefetch the next span's records (in flight through steps 1-3)
-        LANE_ARR(uint32_t, no, MPL);
-        LANE_ARR(uint32_t, nw, MPL);
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            const uint32_t j = b0 + nb + 4u * (uint32_t)lane + u;
-            const uint64_t rec = j < mtotal ? ring64[j] : ~0ull;
-            LV(no)[u] = j < mtotal ? (uint32_t)rec : 0xffffffffu;
-            LV(nw)[u] = (uint32_t)(rec >> 32);
-          }
-        }
-        // the span's first dword holds bytes before F (final): loaded now, merged below
-        const uint32_t mis = (uint32_t)((uintptr_t)(job.dst + F) & 3u);
-        const uint32_t xa = F - mis;                           // stream position of dword 0
-        const uint32_t ndw = (span + mis + 3u) >> 2;
-        const bool head = mis && (int32_t)xa >= 0 && xa + 4u <= dst_len;   // dword 0 loaded (whole-stored)
-        uint32_t hv = 0;
-        if (head) hv = *(hz_gu32*)(dst + xa);
-        // literal runs: run u of a lane precedes its match u (the lane's first run starts at
-        // the end of the previous lane's last match, or at F)
-        LANE_VAR(uint32_t, e3);
-        LANE_LOOP { LV(e3) = LV(ro)[3] + (LV(rw)[3] >> 16); }
-        LANE_ARR(uint32_t, rr, MPL);
-        LANE_VAR(uint32_t, rsum);
-        LANE_LOOP {
-          const uint32_t up = LV_UP1(e3);
-          uint32_t prev = lane == 0 ? F : up, s_ = 0;
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            const bool in = 4u * (uint32_t)lane + u < nb;
-            const uint32_t r = in ? LV(ro)[u] - prev : 0u;
-            LV(rr)[u] = r;
-            s_ += r;
-            prev = LV(ro)[u] + (LV(rw)[u] >> 16);
-          }
-          LV(rsum) = s_;
-        }
-        LANE_VAR(uint32_t, rb);      // literals of the span before the lane's first run
-        uint32_t lcnt = 0;
-#if HZ_GPU
-        rb = wave_excl_scan32(rsum);
-        lcnt = hz::wave_sum(rsum);
-#else
-        for (int lane = 0; lane < 64; lane++) { rb[lane] = lcnt; lcnt += rsum[lane]; }
-#endif
-        if (!nb) lcnt = span;
-        // 1. literals into LDS (lbuf byte 4 + (L0 & 3) + k is literal L0 + k), ready bitmap set
-        const uint32_t LB0 = 4u + (L0 & 3u);
-        const uint32_t nlw = ((L0 & 3u) + lcnt + 3u) >> 2;
-        LANE_LOOP {
-          for (uint32_t k = (uint32_t)lane; k < nlw; k += 64u) sh.lbuf[1u + k] = lits32[(L0 >> 2) + k];
-          if ((uint32_t)lane < RDYW) sh.rdy[lane] = ~0u;
-        }
-        HZ2_LSYNC();
-        LANE_VAR(uint32_t, pend);    // bit u: match u has sources inside the span (step 3)
-        uint8_t* const sb = (uint8_t*)sh.sbuf;
-        if (!nb) {
-          // 2. a span of literals: whole dwords from lbuf by funnel shifts
-          LANE_LOOP {
-            for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
-              const uint32_t q = LB0 + 4u * k - mis;
-              uint32_t v = funnel(sh.lbuf[(q >> 2) + 1u], sh.lbuf[q >> 2], (q & 3u) * 8u);
-              if (k == 0u && mis) {
-                const uint32_t hm = (1u << (8u * mis)) - 1u;
-                v = (v & ~hm) | (hv & hm);
-              }
-              sh.sbuf[k] = v;
-            }
-            LV(pend) = 0u;
-          }
-        } else {
-          LANE_LOOP {
-            if (lane == 0) sh.sbuf[0] = hv;
-            uint32_t pe = 0;
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const bool in = 4u * (uint32_t)lane + u < nb;
-              const uint32_t o = LV(ro)[u], len = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
-              const uint32_t se = o - d + (d < len ? d : len);       // end of the source bytes
-              if (in && se > F) {
-                pe |= 1u << u;
-                const uint32_t a = o - F, b = a + len;
-                for (uint32_t w = a >> 5; w <= (b - 1u) >> 5; w++) HZ2_LDS_AND(&sh.rdy[w], ~bm_word_mask(w, a, b));
-              }
-            }
-            LV(pend) = pe;
-          }
-          // 2a. literal runs: the first 4 literals of all 4 runs with their reads together,
-          // then longer runs 16 bytes at a time (wave-uniform trip count: the longest run)
-          LANE_LOOP {
-            const uint8_t* const lb = (const uint8_t*)sh.lbuf;
-            uint32_t v16[4][4], pre = LV(rb);
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const uint32_t r = 4u * (uint32_t)lane + u < nb ? LV(rr)[u] : 0u;
-HZ_UNROLL
-              for (uint32_t k = 0; k < 4u; k++) v16[u][k] = lb[k < r ? LB0 + pre + k : 0u];
-              pre += r;
-            }
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const uint32_t r = 4u * (uint32_t)lane + u < nb ? LV(rr)[u] : 0u;
-              const uint32_t dp = mis + LV(ro)[u] - r - F;         // sbuf byte of the run's first literal
-HZ_UNROLL
-              for (uint32_t k = 0; k < 4u; k++) sb[k < r ? dp + k : JUNK] = (uint8_t)v16[u][k];
-            }
-          }
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            for (uint32_t t0 = 4u; WAVE_BALLOT(4u * (uint32_t)lane + u < nb && LV(rr)[u] > t0); t0 += 16u) {
-              LANE_LOOP {
-                uint32_t pre = LV(rb);
-HZ_UNROLL
-                for (uint32_t v = 0; v < u; v++) pre += LV(rr)[v];
-                const uint32_t r = 4u * (uint32_t)lane + u < nb ? LV(rr)[u] : 0u;
-                const uint32_t dp = mis + LV(ro)[u] - r - F + t0;     // sbuf byte of literal t0
-                const uint32_t sp = LB0 + pre + t0;                     // its lbuf byte
-                const uint8_t* const lb = (const uint8_t*)sh.lbuf;
-                uint32_t v4[16];
-HZ_UNROLL
-                for (uint32_t k = 0; k < 16u; k++) v4[k] = lb[t0 + k < r ? sp + k : 0u];
-HZ_UNROLL
-                for (uint32_t k = 0; k < 16u; k++) sb[t0 + k < r ? dp + k : JUNK] = (uint8_t)v4[k];
-              }
-            }
-          }
-          // 2b. match bytes whose source lies before F: the first 4 bytes of all 4 matches
-          // with their loads in flight together, then longer matches 16 bytes at a time
-          LANE_LOOP {
-            uint32_t v16[4][4];
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const bool in = 4u * (uint32_t)lane + u < nb;
-              const uint32_t o = LV(ro)[u], len = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
-              const uint32_t s = o - d;
-HZ_UNROLL
-              for (uint32_t k = 0; k < 4u; k++) {
-                const uint32_t src = s + mod_small(k, d);
-                const bool ok = k < len && src < F;
-                v16[u][k] = *HZ_GLOBAL(hz_gcu8*, dst + (ok ? src : F));
-              }
-            }
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const bool in = 4u * (uint32_t)lane + u < nb;
-              const uint32_t o = LV(ro)[u], len = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
-              const uint32_t s = o - d;
-HZ_UNROLL
-              for (uint32_t k = 0; k < 4u; k++) {
-                const uint32_t src = s + mod_small(k, d);
-                const bool ok = k < len && src < F;
-                sb[ok ? mis + o - F + k : JUNK] = (uint8_t)v16[u][k];
-              }
-            }
-          }
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            LANE_VAR(uint32_t, jc);      // t0 mod d, carried
-            LANE_LOOP { LV(jc) = mod_small(4u, (LV(rw)[u] & 0xffffu) + 1u); }
-            for (uint32_t t0 = 4u; WAVE_BALLOT(4u * (uint32_t)lane + u < nb && (LV(rw)[u] >> 16) > t0); t0 += 16u) {
-              LANE_LOOP {
-                const bool in = 4u * (uint32_t)lane + u < nb;
-                const uint32_t o = LV(ro)[u], len = in ? LV(rw)[u] >> 16 : 0u, d = (LV(rw)[u] & 0xffffu) + 1u;
-                const uint32_t s = o - d;
-                uint32_t v4[16], dp[16], jj = LV(jc);
-HZ_UNROLL
-                for (uint32_t k = 0; k < 16u; k++) {
-                  const uint32_t t = t0 + k, src = s + jj;
-                  const bool ok = t < len && src < F;
-                  v4[k] = *HZ_GLOBAL(hz_gcu8*, dst + (ok ? src : F));
-                  dp[k] = ok ? mis + o - F + t : JUNK;
-                  jj = jj + 1u == d ? 0u : jj + 1u;
-                }
-HZ_UNROLL
-                for (uint32_t k = 0; k < 16u; k++) sb[dp[k]] = (uint8_t)v4[k];
-                LV(jc) = jj;
-              }
-            }
-          }
-        }
-        HZ2_LSYNC();
-        // 3. rounds over the matches with sources inside the span: every pending match's
-        // ready test reads together, then the ready ones copy (first 4 bytes of all of them
-        // together), then set their ready bits
-        HZ_T(11);
-        HZ2_MARK("M_ROUNDS");
-        for (uint32_t round = 0;; round++) {
-          if (!WAVE_BALLOT(LV(pend) != 0u)) break;
-          if (round > 4u * WAVE) return ST_DATA;     // unreachable: every round completes a match
-          if (stats) stats->hops++;
-          LANE_LOOP {
-            const uint32_t pe = LV(pend);
-            uint32_t rw0[4], rw1[4], ms0[4], ms1[4], wa[4], wb[4];
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const bool p = (pe >> u) & 1u;
-              const uint32_t o = LV(ro)[u], len = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
-              const uint32_t s = o - d, se = s + (d < len ? d : len);
-              const uint32_t a = p ? (s > F ? s - F : 0u) : 0u, b = p ? se - F : 1u;
-              wa[u] = a >> 5; wb[u] = (b - 1u) >> 5;
-              rw0[u] = sh.rdy[wa[u]]; rw1[u] = sh.rdy[wb[u]];
-              ms0[u] = bm_word_mask(wa[u], a, b); ms1[u] = bm_word_mask(wb[u], a, b);
-            }
-            uint32_t rd = 0;
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              bool ok = ((pe >> u) & 1u) && (rw0[u] & ms0[u]) == ms0[u] && (rw1[u] & ms1[u]) == ms1[u];
-              if (ok && wb[u] > wa[u] + 1u)
-                for (uint32_t w = wa[u] + 1u; w < wb[u]; w++) ok = ok && sh.rdy[w] == ~0u;
-              rd |= ok ? 1u << u : 0u;
-            }
-            uint32_t v16[4][4], d16[4][4];
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const bool ok = (rd >> u) & 1u;
-              const uint32_t o = LV(ro)[u], len = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
-              const uint32_t s = o - d;
-HZ_UNROLL
-              for (uint32_t k = 0; k < 4u; k++) {
-                const uint32_t src = s + mod_small(k, d);
-                const bool c = ok && k < len && src >= F;
-                v16[u][k] = sb[c ? mis + src - F : JUNK];
-                d16[u][k] = c ? mis + o - F + k : JUNK;
-              }
-            }
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++)
-HZ_UNROLL
-              for (uint32_t k = 0; k < 4u; k++) sb[d16[u][k]] = (uint8_t)v16[u][k];
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const uint32_t o = LV(ro)[u], len = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
-              if (((rd >> u) & 1u) && len > 4u) {
-                const uint32_t s = o - d;
-                uint32_t jj = mod_small(4u, d);
-                for (uint32_t t0 = 4u; t0 < len; t0 += 16u) {
-                  uint32_t v4[16], dp[16];
-HZ_UNROLL
-                  for (uint32_t k = 0; k < 16u; k++) {
-                    const uint32_t src = s + jj;
-                    const bool c = t0 + k < len && src >= F;
-                    v4[k] = sb[c ? mis + src - F : JUNK];
-                    dp[k] = c ? mis + o - F + t0 + k : JUNK;
-                    jj = jj + 1u == d ? 0u : jj + 1u;
-                  }
-HZ_UNROLL
-                  for (uint32_t k = 0; k < 16u; k++) sb[dp[k]] = (uint8_t)v4[k];
-                }
-              }
-            }
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              if ((rd >> u) & 1u) {
-                const uint32_t oa = LV(ro)[u] - F, ob = oa + (LV(rw)[u] >> 16);
-                for (uint32_t w = oa >> 5; w <= (ob - 1u) >> 5; w++) HZ2_LDS_OR(&sh.rdy[w], bm_word_mask(w, oa, ob));
-              }
-            }
-            LV(pend) = pe & ~rd;
-          }
-          HZ2_LSYNC();
-        }
-        HZ_T(13);
-        HZ2_MARK("M_STORE");
-        // 4. store: whole dwords inside the span (dword 0 also when its head was loaded) and
-        // the stream; the span's edge bytes one by one.  adler32 over the span's bytes.
-        LANE_LOOP {
-          uint32_t a1 = 0, b2 = 0;       // adler: sum b, span-relative sum (x - F) b (mod 2^32)
-          for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
-            const uint32_t x0 = xa + 4u * k;
-            const uint32_t v = sh.sbuf[k];
-            const bool inside = (int32_t)x0 >= 0 && x0 + 4u <= dst_len && x0 + 4u <= F + span && (k > 0u || !mis || head);
-            if (inside) {
-              *(hz_gu32*)(dst + x0) = v;
-            } else {
-              for (uint32_t b = 0; b < 4u; b++) {
-                const uint32_t x = x0 + b;
-                if (x >= F && x < F + span && x < dst_len) dst[x] = (uint8_t)(v >> (8u * b));
-              }
-            }
-            // the span's bytes of this dword: [lo, hi)
-            const uint32_t lo = k == 0u ? mis : 0u;
-            const uint32_t rem = span + mis - 4u * k;          // > 0
-            const uint32_t hi = rem < 4u ? rem : 4u;
-            const uint32_t bm = (hi >= 4u ? ~0u : (1u << (8u * hi)) - 1u) & ~((1u << (8u * lo)) - 1u);
-            const uint32_t vm = v & bm;
-            const uint32_t sv = dot4(vm, 0x01010101u);
-            a1 += sv;
-            b2 += (4u * k - mis) * sv + dot4(vm, 0x03020100u);
-          }
-          LV(ra1) += a1;
-          LV(ra2) += (uint64_t)F * a1 + b2;
-        }
-        WAVE_SYNC_GLOBAL();
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) { LV(ro)[u] = LV(no)[u]; LV(rw)[u] = LV(nw)[u]; }
-        }
-        HZ2_MARK("M_END");
-        b0 += nb;
-        F += span;
-        L0 += lcnt;
-      }
-#endif
       LANE_LOOP {
         LV(s1) = (LV(s1) + LV(ra1) % ADLER_MOD) % ADLER_MOD;
         LV(s2) = (uint32_t)((LV(s2) + LV(ra2) % ADLER_MOD) % ADLER_MOD);
