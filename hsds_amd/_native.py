@@ -154,12 +154,14 @@ class Engine:
         except Exception:
             pass
 
-    def set_tuning(self, seg_over16=None, warmup_bits=None, rounds=None):
+    def set_tuning(self, seg_over16=None, warmup_bits=None, rounds=None, waves_per_stream=None):
         """Inflate tuning; a setting left at None keeps the engine's current value
-        (hsds_engine_create's defaults: the GPU-swept ones)."""
+        (hsds_engine_create's defaults: the GPU-swept ones).  waves_per_stream: 0 by batch
+        size, 1 or 2 wavefronts per zlib stream (None: keep)."""
         keep = 0xFFFFFFFF
         rc = lib().hsds_set_tuning(self.h, keep if seg_over16 is None else seg_over16,
-                                   keep if warmup_bits is None else warmup_bits, 0,
+                                   keep if warmup_bits is None else warmup_bits,
+                                   keep if waves_per_stream is None else waves_per_stream,
                                    -1 if rounds is None else rounds)
         if rc != OK:
             raise NativeError(rc, "hsds_set_tuning")

@@ -51,6 +51,9 @@
 #ifndef HZ2_WPE
 #define HZ2_WPE 4          // inflate2_kernel waves per SIMD the compiler must allow (VGPR budget)
 #endif
+#ifndef HZ2_PIPE_DEFAULT
+#define HZ2_PIPE_DEFAULT 0  // -1: two wavefronts per zlib stream when a batch cannot fill the GPU
+#endif
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
 namespace {
@@ -362,7 +365,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ2_WPE
 #ifdef HZ_PROFILE
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-      st = hz2::inflate_stream<hz2::Stats>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
+      st = hz2::inflate_stream<hz2::Stats, 1>(sh, job, tune, ring, (hz2::Stats*)nullptr, prof);
 #ifdef HZ_PROFILE
       t_busy += __builtin_amdgcn_s_memrealtime() - t0;
       if (lane == 0) atomicMax(&hz_tail[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
@@ -391,6 +394,52 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ2_WPE
   }
 #endif
   (void)prof;
+}
+
+// -------------------------------------------------------------------------
+// inflate, two wavefronts per stream (small batches: fewer zlib streams than resident
+// wavefronts).  Persistent 128-thread workgroups; both wavefronts decode the same item,
+// alternating its windows (inflate2.h, inflate_stream<NW = 2>): one window's header, sync
+// phases and emit run beside the other's resolve, about halving a stream's latency.
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(HZ2_WPE))) inflate2w_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+                                                      uint32_t* __restrict__ counter, int32_t* __restrict__ status,
+                                                      uint32_t* __restrict__ sizes,
+                                                      const uint32_t* __restrict__ kind_counts, hz2::Tune tune,
+                                                      uint8_t* __restrict__ rings) {
+  __shared__ hz2::Shared sh[2];
+  __shared__ hz2::Ctl ctl;
+  if (kind_counts[1] == 0) return;
+  const uint32_t total = *pool_ctr;
+  const uint32_t w = threadIdx.x >> 6;
+  const int lane = (int)(threadIdx.x & 63u);
+  uint8_t* ring = rings + ((size_t)blockIdx.x * 2u + w) * hz2::SCRATCH_BYTES;
+  HzProf* prof = nullptr;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      hz2::ctl_reset(&ctl, atomicAdd(counter, 1u));
+      ctl.bar = 0;
+    }
+    __syncthreads();
+    const uint32_t item = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl.item);
+    if (item >= total) break;
+    const Item it = pool[item];
+    const uint32_t kind = it.kind & 0xff;
+    int st = HSDS_OK;
+    if (kind == ITEM_RAW) {
+      if (w == 0) raw_copy(it, lane);
+    } else if (kind == ITEM_ZLIB) {
+      hz2::Job job = {(const uint8_t*)it.src, it.src_len, (uint8_t*)it.dst, it.dst_len,
+                      (it.kind & ITEM_INEXACT) ? 0u : 1u, (it.kind & ITEM_INEXACT) ? &sizes[it.chunk] : nullptr,
+                      item_perm(it)};
+      // (only wavefront 0 reports the decoded length of an inexact item)
+      if (w != 0) job.out_len = nullptr;
+      st = hz2::inflate_stream<hz2::Stats, 2>(sh[w], job, tune, ring, (hz2::Stats*)nullptr, prof,
+                                              hz2::Pipe{&ctl, &sh[1u - w], w});
+    }
+    if (w == 0 && lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
+    __syncthreads();
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -1411,6 +1460,8 @@ struct hsds_engine {
   int device;
   int num_cus;
   int inflate_blocks_per_cu;   // occupancy of inflate2_kernel
+  int inflate2w_blocks_per_cu; // occupancy of inflate2w_kernel (two wavefronts per workgroup)
+  int inflate_pipe;            // -1: by batch size, 0: one wavefront per stream, 1: two
   int lz_blocks_per_cu;        // occupancy of lz_kernel
   int bshuf_blocks_per_cu;     // occupancy of bshuf_kernel
   int zstd_blocks_per_cu;      // occupancy of zstd_kernel
@@ -1578,6 +1629,12 @@ int hsds_engine_create(int device, hsds_engine** out) {
     if (v >= 1 && v < occ) occ = v;
   }
   e->inflate_blocks_per_cu = occ;
+  int occ2 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, inflate2w_kernel, 128, 0) != hipSuccess || occ2 < 1)
+    occ2 = occ / 2 > 0 ? occ / 2 : 1;
+  e->inflate2w_blocks_per_cu = occ2;
+  e->inflate_pipe = HZ2_PIPE_DEFAULT;
+  if (const char* ev = getenv("HSDS_INFLATE_PIPE")) e->inflate_pipe = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
   int olz = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olz, lz_kernel, 64, 0) != hipSuccess || olz < 1) olz = 8;
   e->lz_blocks_per_cu = olz;
@@ -1648,13 +1705,14 @@ void hsds_engine_destroy(hsds_engine* e) {
   delete e;
 }
 
-int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t unused, int32_t rounds) {
-  (void)unused;
+int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t waves_per_stream,
+                    int32_t rounds) {
   if (!e) return HSDS_ERR_ARG;
   // HSDS_TUNE_KEEP (0xffffffff; -1 for rounds) leaves a setting as it is
   if ((seg_over16 > 16u && seg_over16 != HSDS_TUNE_KEEP) || (warmup_bits > 4096u && warmup_bits != HSDS_TUNE_KEEP) ||
-      rounds < -1 || rounds > 64)
+      (waves_per_stream > 2u && waves_per_stream != HSDS_TUNE_KEEP) || rounds < -1 || rounds > 64)
     return HSDS_ERR_ARG;
+  if (waves_per_stream != HSDS_TUNE_KEEP) e->inflate_pipe = waves_per_stream == 0u ? -1 : waves_per_stream == 2u ? 1 : 0;
   if (seg_over16 != HSDS_TUNE_KEEP) e->tune.over16 = seg_over16;
   if (warmup_bits != HSDS_TUNE_KEEP) e->tune.W = warmup_bits;
   if (rounds >= 0) e->tune.max_rounds = rounds;
@@ -1714,11 +1772,16 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
     if (grow((void**)&e->tmp, &e->tmp_bytes, dst_extent ? dst_extent : 1)) return HSDS_ERR_DEVICE;
     tmp = e->tmp;
   }
-  // one match ring per resident inflate wave
-  int64_t grid = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
+  // one match ring per resident inflate wave.  A batch whose zlib streams (at most 4 per
+  // chunk in HSDS's F1 frames, 1 per F2 chunk) cannot fill half the resident wavefronts
+  // decodes every stream with two wavefronts (inflate2w_kernel)
+  const int64_t waves1 = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
+  const bool pipe = e->inflate_pipe == 1 || (e->inflate_pipe < 0 && nchunks * 4 * 2 <= waves1);
+  int64_t grid = pipe ? (int64_t)e->num_cus * e->inflate2w_blocks_per_cu : waves1;
   if (grid > nchunks * 64) grid = nchunks * 64;
   if (grid < 1) grid = 1;
-  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * hz2::SCRATCH_BYTES)) return HSDS_ERR_DEVICE;
+  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * (pipe ? 2u : 1u) * hz2::SCRATCH_BYTES))
+    return HSDS_ERR_DEVICE;
   if (hipMemsetAsync(ctr, 0, 64, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
   const int nb = (int)((nchunks + tpb - 1) / tpb);
@@ -1726,8 +1789,12 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
                      (uint8_t*)d_dst, tmp, pool, pool_cap, ctr + 8, meta, list, ctr + 1, ctr + 4, d_status,
                      compressor, shuffle, itemsize, inexact);
   hipEventRecord(e->ev0, st);
-  hipLaunchKernelGGL(inflate2_kernel, dim3((unsigned)grid), dim3(64), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
-                     ctr + 4, e->tune, e->rings);
+  if (pipe)
+    hipLaunchKernelGGL(inflate2w_kernel, dim3((unsigned)grid), dim3(128), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
+                       ctr + 4, e->tune, e->rings);
+  else
+    hipLaunchKernelGGL(inflate2_kernel, dim3((unsigned)grid), dim3(64), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
+                       ctr + 4, e->tune, e->rings);
   int64_t lgrid = (int64_t)e->num_cus * e->lz_blocks_per_cu;
   if (lgrid > (nchunks * 64 + lz::GROUP - 1) / lz::GROUP) lgrid = (nchunks * 64 + lz::GROUP - 1) / lz::GROUP;
   if (lgrid < 1) lgrid = 1;

@@ -36,6 +36,13 @@
 // inflate_wave.h whose helpers (table build, LUT format, load_word) it reuses.
 #pragma once
 #include "inflate_wave.h"
+#if !defined(__HIPCC__) && !defined(__HIP__)
+#include <sched.h>
+#endif
+// the table builder's hand-offs are wavefront-scope here (two wavefronts of one workgroup
+// build tables independently)
+#undef HZ_TB_SYNC
+#define HZ_TB_SYNC() HZ2_LSYNC()
 
 namespace hz2 {
 
@@ -74,23 +81,11 @@ static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 static_assert(SPL <= 24, "resolve slots per lane");
 constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = lane + 64 i)
-// HZ2_MLIGHT: the resolve's LDS hand-offs are wavefront-scope (no s_waitcnt vmcnt(0) /
-// s_barrier of __syncthreads), so the next span's records and the head dword stay in
-// flight across them; the span's end keeps the workgroup-scope release (its stores are
-// read back as far sources)
-#ifndef HZ2_MLIGHT
-#define HZ2_MLIGHT 1
-#endif
-#if HZ2_MLIGHT
-#define HZ2_MSYNC() HZ2_LSYNC()
-#else
-#define HZ2_MSYNC() WAVE_SYNC()
-#endif
-// HZ2_SPANLIGHT: a span's stores reach the next spans' far loads of the same wavefront by
-// wavefront-scope ordering instead of a workgroup-scope release (which waits for them)
-#ifndef HZ2_SPANLIGHT
-#define HZ2_SPANLIGHT 0
-#endif
+// Every hand-off inside one stream's decode is wavefront-scope (HZ2_LSYNC for LDS,
+// HZ2_GSYNC for the wave's own global stores read back by its later loads): no s_barrier,
+// no s_waitcnt vmcnt(0) -- loads in flight (the next span's records) stay in flight, and
+// two wavefronts of one workgroup can decode two windows of a stream independently
+// (inflate2w_kernel); their hand-offs are workgroup-scope release / acquire on Ctl.
 // phase E: match records are staged per lane and stored as whole aligned 32-byte groups
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
 // bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
@@ -690,7 +685,7 @@ struct Stats {
 
 #if HZ_GPU
 namespace hz2 {
-__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wave_excl_scan(v, (int)threadIdx.x); }
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wave_excl_scan(v, HZ_LANE_ID()); }
 }  // namespace hz2
 // value of lane-variable v in lane i (uniform i: v_readlane, no LDS round trip as a
 // ds_bpermute shuffle would take); LANE_ARR: a per-lane array
@@ -708,12 +703,34 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) { return hz::wa
     __builtin_amdgcn_wave_barrier();                             \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       \
   } while (0)
+// wavefront-scope ordering of this wavefront's own global stores and later loads (no wait)
+#define HZ2_GSYNC() HZ2_LSYNC()
+#define HZ2_PAUSE() __builtin_amdgcn_s_sleep(2)
+#define HZ2_WGBAR() __syncthreads()
+namespace hz2 {
+__device__ __forceinline__ uint32_t ctl_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ctl_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+}  // namespace hz2
 #else
 #define HZ2_UNI(v) (v)
 #define LV_AT(v, i) ((v)[i])
 #define LANE_ARR(T, name, n) T name[64][n]
 #define LVA_AT(arr, u, i) ((arr)[i][u])
 #define HZ2_LSYNC() do { } while (0)
+#define HZ2_GSYNC() do { } while (0)
+#define HZ2_PAUSE() sched_yield()
+#define HZ2_WGBAR() hz2::emu_wgbar(pipe.ctl)
+namespace hz2 {
+// CPU emulation: the two wavefronts are two threads
+inline uint32_t ctl_ld(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void ctl_st(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+struct Ctl;
+void emu_wgbar(Ctl* c);
+}  // namespace hz2
 #endif
 
 #if HZ2_EPOCH
@@ -736,15 +753,79 @@ HZ_HD uint32_t lane_rank(uint64_t m, int lane) {
 #endif
 }
 
+// ---- the window pipeline of two wavefronts on one stream (inflate2w_kernel) ---------------
+enum : uint32_t { WK_NEWBLOCK = 0, WK_CONT = 1, WK_END = 2 };
+struct WinState {                // a window's start
+  uint32_t pos;                  // bit position (a block header for WK_NEWBLOCK, the trailer's byte for WK_END)
+  uint32_t out;                  // output offset
+  uint32_t kind;                 // WK_*
+  uint32_t block_start, bfinal;  // WK_CONT: the block it continues
+  uint32_t est;                  // WK_CONT: expected bits left in the block
+  uint32_t prev_block_bits;      // the last Huffman block's size (next block's estimate)
+};
+struct Ctl {                     // in LDS, shared by the workgroup's two wavefronts
+  uint32_t synced;               // the window whose start is in `next`
+  uint32_t mdone;                // windows whose output is final
+  uint32_t end_at;               // the WK_END window's index (~0u: not reached)
+  int32_t err;                   // the first error (0: none)
+  uint32_t item;                 // the work item both wavefronts decode
+  uint32_t bar;                  // CPU emulation: barrier generation counter
+  WinState next;
+  uint64_t adler[2][2];          // per wavefront: sum b, sum pos * b
+};
+struct Pipe {
+  Ctl* ctl;
+  const Shared* other;           // the other wavefront's LDS (its block tables)
+  uint32_t w;                    // this wavefront's index in the workgroup
+};
+constexpr uint32_t SPIN_MAX = 1u << 24;   // a wait that never ends fails the stream instead of hanging
+
+HZ_HD void ctl_reset(Ctl* c, uint32_t item) {
+  c->synced = 0; c->mdone = 0; c->end_at = ~0u; c->err = 0; c->item = item;
+}
+HZ_HD void atomic_min_err(Ctl* c, int st) {
+#if HZ_GPU
+  atomicCAS(&c->err, 0, st);
+#else
+  int32_t z = 0;
+  __atomic_compare_exchange_n(&c->err, &z, st, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+#endif
+}
+#if !HZ_GPU
+// both emulated wavefronts meet (generation barrier over Ctl::bar: the low bit counts
+// arrivals, the rest is the generation)
+inline void emu_wgbar(Ctl* c) {
+  const uint32_t g = __atomic_load_n(&c->bar, __ATOMIC_ACQUIRE) & ~1u;
+  uint32_t exp = g;
+  if (__atomic_compare_exchange_n(&c->bar, &exp, g | 1u, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+    while ((__atomic_load_n(&c->bar, __ATOMIC_ACQUIRE) & ~1u) == g) sched_yield();   // first: wait
+  } else {
+    __atomic_store_n(&c->bar, g + 2u, __ATOMIC_RELEASE);                             // second: release
+  }
+}
+#endif
+
 // stream byte x is dst[x] (a shuffled chunk is inflated into staging and unshuffled after);
-// ring_base: the wave's SCRATCH_BYTES (match ring, then the literal stream)
-template <class StatsT>
+// ring_base: the wave's SCRATCH_BYTES (match ring, then the literal stream).
+//
+// The stream is decoded as a sequence of windows (a window = one pass of phases A .. M over
+// one Huffman block or a part of it; a stored block is a window of its own).  A window's
+// start (bit position, output offset, block state) is known once the previous window's
+// sync phases (A, A', R, prefix sums) are done, and its resolve M needs every output byte
+// before it.  NW = 1: one wavefront runs the windows in order.  NW = 2 (inflate2w_kernel):
+// two wavefronts of one workgroup alternate windows -- wavefront w takes windows w, w + 2,
+// ... -- handing the next window's start over as soon as their sync phases end, and
+// waiting for the other's M before their own M, so one window's header, sync phases and
+// emit run beside the other's resolve (pipe.ctl in LDS; a continuation window copies the
+// block's tables from the other wavefront's LDS).
+template <class StatsT, int NW>
 #if HZ_GPU
 __device__ __forceinline__
 #else
 static
 #endif
-int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_base, StatsT* stats, HzProf* prof = nullptr) {
+int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_base, StatsT* stats, HzProf* prof = nullptr,
+                   Pipe pipe = Pipe{nullptr, nullptr, 0u}) {
   (void)prof;
   const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 15u);
   const Src S = {HZ_GLOBAL(hz_gcu8*, job.src - a), a, a + job.src_len, ((a + job.src_len - 1u) >> 2) & ~3u};
@@ -775,175 +856,249 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
     if ((cmf & 0x0f) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0) return ST_DATA;
     if (flg & 0x20) return ST_DATA;   // preset dictionary: Z_NEED_DICT
   }
-  uint32_t pos = S.lo * 8u + 16u;
-  uint32_t out = 0;
-  uint32_t prev_block_bits = 0;
+  (void)pipe;
+  WinState cur;                        // the current window's start
+  cur.pos = S.lo * 8u + 16u;
+  cur.out = 0;
+  cur.kind = WK_NEWBLOCK;
+  cur.block_start = 0;
+  cur.bfinal = 0;
+  cur.est = 0;
+  cur.prev_block_bits = 0;
+  uint32_t k = NW > 1 ? pipe.w : 0u;   // window index
+  WinState nxt = cur;                  // NW == 1: the next window's start
 
-  for (;;) {  // ---- deflate blocks ----
-    HZ_T(1);
-    if (pos + 3u > limit_bits) return ST_TRUNC;
-    uint32_t h3;
-    {
-      GRd r;
-      g_init(S, r, pos);
-      h3 = (uint32_t)(g_peek(r) & 7u);
-    }
-    const uint32_t block_start = pos;
-    pos += 3;
-    const uint32_t bfinal = h3 & 1u, btype = h3 >> 1;
-    if (stats) stats->blocks++;
-    if (btype == 3) return ST_DATA;
-    if (btype == 0) {
-      // ---- stored block: copied through the output map ----
-      pos = (pos + 7u) & ~7u;
-      if (pos + 32u > limit_bits) return ST_TRUNC;
-      GRd r;
-      g_init(S, r, pos);
-      const uint32_t ln = (uint32_t)(g_peek(r) & 0xffffffffu);
-      const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
-      if ((len ^ 0xffffu) != nlen) return ST_DATA;
-      pos += 32u;
-      if (pos + len * 8u > limit_bits) return ST_TRUNC;
-      if (out + len > dst_len) return ST_SIZE;
-      const uint32_t sb = pos >> 3;
-      LANE_LOOP {
-        uint32_t a1 = LV(s1), a2 = LV(s2);
-        for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
-          const uint32_t b = S.base[sb + i];
-          dst[out + i] = (uint8_t)b;
-          a1 += b;
-          a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
-        }
-        LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
-      }
-      out += len;
-      pos += len * 8u;
-      if (stats) stats->stored++;
-      WAVE_SYNC_GLOBAL();
-      if (bfinal) break;
-      continue;
-    }
-    // ---- Huffman code lengths ----
-    uint32_t nlen = 288, ndist = 32;
-    if (btype == 1) {
-      LANE_LOOP {
-        for (int q = lane; q < 320; q += 64) sh.lens[q] = q >= 288 ? 5 : q < 144 ? 8 : q < 256 ? 9 : q < 280 ? 7 : 8;
-      }
-      WAVE_SYNC();
+  // the next window's start to whoever decodes it
+  auto publish = [&](const WinState& nx) {
+    if (NW > 1) {
+      Ctl* c = pipe.ctl;
+      c->next = nx;
+      if (nx.kind == WK_END) ctl_st(&c->end_at, k + 1u);
+      ctl_st(&c->synced, k + 1u);
     } else {
-      // dynamic header (RFC 1951 3.2.7): the wave loads the 8192 stream bits from the header's
-      // quad into LDS at once (a header is at most 14 + 19 x 3 + 320 x 14 bits), then lane 0
-      // decodes it serially from LDS -- no global load latency per refill
-      const uint32_t hq = (pos >> 5) & ~3u;
-      LANE_LOOP {
-        uint32_t a0, a1, a2, a3;
-        g_quad(S, hq + 4u * (uint32_t)lane, a0, a1, a2, a3);
-        sh.hbits[4 * lane] = a0; sh.hbits[4 * lane + 1] = a1; sh.hbits[4 * lane + 2] = a2; sh.hbits[4 * lane + 3] = a3;
-      }
-      WAVE_SYNC();
-      LANE_LOOP {
-        if (lane == 0) {
-          int st = ST_OK;
-          HR r = {sh.hbits, pos - hq * 32u, hq * 32u};
-          const uint32_t hlit = (r.peek() & 31u) + 257u, hdist = ((r.peek() >> 5) & 31u) + 1u;
-          const uint32_t hclen = ((r.peek() >> 10) & 15u) + 4u;
-          r.drop(14);
-          if (hlit > 286 || hdist > 30) st = ST_DATA;
-          uint16_t* cl = sh.sorted_cl;
-          for (int i = 0; i < 19; i++) cl[i] = 0;
-          for (uint32_t i = 0; i < hclen; i++) {
-            cl[hz::cl_order(i)] = (uint16_t)(r.peek() & 7u);
-            r.drop(3);
-          }
-          uint16_t* cnt = sh.cnt_cl;
-          for (int l = 0; l < 16; l++) cnt[l] = 0;
-          for (int i = 0; i < 19; i++) cnt[cl[i]]++;
-          cnt[0] = 0;
-          int left = 1, maxl = 0;
-          for (int l = 1; l <= 7; l++) {
-            left <<= 1; left -= cnt[l];
-            if (cnt[l]) maxl = l;
-            if (left < 0) st = ST_DATA;
-          }
-          if (left > 0 || maxl == 0) st = ST_DATA;   // code-length code must be complete
-          uint16_t* clut = sh.lut_d;                   // 7-bit LUT (sym | len << 8), rebuilt below
-          if (st == ST_OK) {
-            uint16_t* next = sh.tb_next;                 // next code per length (LDS: no scratch)
-            uint32_t code = 0;
-            for (int l = 1; l <= 7; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; next[l] = (uint16_t)code; }
-            for (int i = 0; i < 19; i++) {
-              const uint32_t l = cl[i];
-              if (!l) continue;
-              const uint32_t rc = hz::rev_bits(next[l]++, (int)l);
-              for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint16_t)(i | (l << 8));
-            }
-          }
-          const uint32_t total = hlit + hdist;
-          uint32_t n = 0, prevl = 0;
-          HRR rr;
-          rr.init(sh.hbits, r.p, r.base);
-          while (st == ST_OK && n < total) {
-            if (rr.pos() > limit_bits + 64u) { st = ST_TRUNC; break; }
-            const uint32_t bits = rr.peek();
-            const uint32_t e = clut[bits & 127u];
-            const uint32_t sym = e & 0xffu, l = e >> 8;
-            if (sym < 16) { rr.drop(l); sh.lens[n++] = (uint8_t)sym; prevl = sym; continue; }
-            // a repeat: its extra bits follow the code in the same peek (7 + 7 bits)
-            const uint32_t x = bits >> l;
-            uint32_t rep, val = 0;
-            if (sym == 16) {
-              if (n == 0) { st = ST_DATA; break; }
-              val = prevl; rep = 3 + (x & 3u); rr.drop(l + 2u);
-            } else if (sym == 17) { rep = 3 + (x & 7u); rr.drop(l + 3u); }
-            else { rep = 11 + (x & 127u); rr.drop(l + 7u); }
-            if (n + rep > total) { st = ST_DATA; break; }
-            for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
-            prevl = val;
-          }
-          r.p = rr.p;
-          if (st == ST_OK && r.pos() > limit_bits) st = ST_TRUNC;
-          if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;   // missing end-of-block code
-          if (st == ST_OK) {
-            for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
-            for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
-            for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
-          }
-          sh.u_status = st;
-          sh.u_pos = r.pos();
-          sh.u_nlen = hlit;
-          sh.u_ndist = hdist;
-        }
-      }
-      WAVE_SYNC();
-      const int hst = sh.u_status;
-      if (hst != ST_OK) return hst;
-      pos = sh.u_pos;
-      nlen = sh.u_nlen;
-      ndist = sh.u_ndist;
+      nxt = nx;
     }
-    HZ_T(2);
-    {
-      int bst = ST_OK;
-      hz::TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB, 1};
-      HZ_BUILD_TABLE(sh, tll, bst);
-      if (bst != ST_OK) return bst;
-      hz::TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB, 1};
-      HZ_BUILD_TABLE(sh, td, bst);
-      if (bst != ST_OK) return bst;
+  };
+  // wait until every output byte before this window is final (the other wavefront's M)
+  auto wait_output = [&]() -> int {
+    if (NW > 1) {
+      Ctl* c = pipe.ctl;
+      for (uint32_t spin = 0;; spin++) {
+        if (ctl_ld(&c->mdone) == k) return ST_OK;
+        const int32_t e = (int32_t)ctl_ld((const uint32_t*)&c->err);
+        if (e) return e;
+        if (spin > SPIN_MAX) return ST_DATA;
+        HZ2_PAUSE();
+      }
     }
-    WAVE_SYNC();
+    return ST_OK;
+  };
+  auto output_done = [&]() {
+    if (NW > 1) ctl_st(&pipe.ctl->mdone, k + 1u);
+  };
 
-    // ---- windows over the Huffman block ----
-    // expected block size: the previous block's (zlib closes blocks at a fixed symbol count),
-    // else up to 200 kbit; over-provisioned so that one window usually reaches the EOB
-    uint32_t est = prev_block_bits ? prev_block_bits : 200000u;
-    {
-      const uint32_t rem = limit_bits > pos ? limit_bits - pos : 0u;
-      if (est > rem + 64u) est = rem + 64u;
+  int fail = ST_OK;
+  for (;; k += NW) {
+    if (NW > 1) {
+      // window k's start: published by the other wavefront's sync phases of window k - 1
+      Ctl* c = pipe.ctl;
+      int got = 0;
+      for (uint32_t spin = 0;; spin++) {
+        if (k == 0u) { got = 1; break; }             // window 0 starts at the stream's first block
+        if (ctl_ld(&c->synced) == k) { cur = c->next; got = 1; break; }
+        if (ctl_ld(&c->end_at) <= k) break;          // the stream ended before window k
+        const int32_t e = (int32_t)ctl_ld((const uint32_t*)&c->err);
+        if (e) { fail = e; break; }
+        if (spin > SPIN_MAX) { fail = ST_DATA; break; }
+        HZ2_PAUSE();
+      }
+      if (!got) break;
+    } else if (k > 0) {
+      cur = nxt;
     }
-    est += (uint32_t)(((uint64_t)est * tune.over16) >> 4);
-    int first_window = 1;
-    for (;;) {
+    if (cur.kind == WK_END) break;
+    const int wst = [&]() -> int {
+      uint32_t pos = cur.pos, out = cur.out;
+      uint32_t block_start = cur.block_start, bfinal = cur.bfinal, est = cur.est;
+      int first_window = 0;
+      if (cur.kind == WK_NEWBLOCK) {
+      HZ_T(1);
+      if (pos + 3u > limit_bits) return ST_TRUNC;
+      uint32_t h3;
+      {
+        GRd r;
+        g_init(S, r, pos);
+        h3 = (uint32_t)(g_peek(r) & 7u);
+      }
+      block_start = pos;
+      pos += 3;
+      bfinal = h3 & 1u;
+      const uint32_t btype = h3 >> 1;
+      if (stats) stats->blocks++;
+      if (btype == 3) return ST_DATA;
+        if (btype == 0) {
+        // ---- stored block: copied through the output map ----
+        pos = (pos + 7u) & ~7u;
+        if (pos + 32u > limit_bits) return ST_TRUNC;
+        GRd r;
+        g_init(S, r, pos);
+        const uint32_t ln = (uint32_t)(g_peek(r) & 0xffffffffu);
+        const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
+        if ((len ^ 0xffffu) != nlen) return ST_DATA;
+        pos += 32u;
+        if (pos + len * 8u > limit_bits) return ST_TRUNC;
+        if (out + len > dst_len) return ST_SIZE;
+        {
+          WinState nx = cur;
+          nx.pos = pos + len * 8u;
+          nx.out = out + len;
+          nx.kind = bfinal ? WK_END : WK_NEWBLOCK;
+          publish(nx);
+          const int wr = wait_output();
+          if (wr != ST_OK) return wr;
+        }
+        const uint32_t sb = pos >> 3;
+        LANE_LOOP {
+          uint32_t a1 = LV(s1), a2 = LV(s2);
+          for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
+            const uint32_t b = S.base[sb + i];
+            dst[out + i] = (uint8_t)b;
+            a1 += b;
+            a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
+          }
+          LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
+        }
+        if (stats) stats->stored++;
+        HZ2_GSYNC();
+        output_done();
+        return ST_OK;
+        }
+      // ---- Huffman code lengths ----
+      uint32_t nlen = 288, ndist = 32;
+      if (btype == 1) {
+        LANE_LOOP {
+          for (int q = lane; q < 320; q += 64) sh.lens[q] = q >= 288 ? 5 : q < 144 ? 8 : q < 256 ? 9 : q < 280 ? 7 : 8;
+        }
+        HZ2_LSYNC();
+      } else {
+        // dynamic header (RFC 1951 3.2.7): the wave loads the 8192 stream bits from the header's
+        // quad into LDS at once (a header is at most 14 + 19 x 3 + 320 x 14 bits), then lane 0
+        // decodes it serially from LDS -- no global load latency per refill
+        const uint32_t hq = (pos >> 5) & ~3u;
+        LANE_LOOP {
+          uint32_t a0, a1, a2, a3;
+          g_quad(S, hq + 4u * (uint32_t)lane, a0, a1, a2, a3);
+          sh.hbits[4 * lane] = a0; sh.hbits[4 * lane + 1] = a1; sh.hbits[4 * lane + 2] = a2; sh.hbits[4 * lane + 3] = a3;
+        }
+        HZ2_LSYNC();
+        LANE_LOOP {
+          if (lane == 0) {
+            int st = ST_OK;
+            HR r = {sh.hbits, pos - hq * 32u, hq * 32u};
+            const uint32_t hlit = (r.peek() & 31u) + 257u, hdist = ((r.peek() >> 5) & 31u) + 1u;
+            const uint32_t hclen = ((r.peek() >> 10) & 15u) + 4u;
+            r.drop(14);
+            if (hlit > 286 || hdist > 30) st = ST_DATA;
+            uint16_t* cl = sh.sorted_cl;
+            for (int i = 0; i < 19; i++) cl[i] = 0;
+            for (uint32_t i = 0; i < hclen; i++) {
+              cl[hz::cl_order(i)] = (uint16_t)(r.peek() & 7u);
+              r.drop(3);
+            }
+            uint16_t* cnt = sh.cnt_cl;
+            for (int l = 0; l < 16; l++) cnt[l] = 0;
+            for (int i = 0; i < 19; i++) cnt[cl[i]]++;
+            cnt[0] = 0;
+            int left = 1, maxl = 0;
+            for (int l = 1; l <= 7; l++) {
+              left <<= 1; left -= cnt[l];
+              if (cnt[l]) maxl = l;
+              if (left < 0) st = ST_DATA;
+            }
+            if (left > 0 || maxl == 0) st = ST_DATA;   // code-length code must be complete
+            uint16_t* clut = sh.lut_d;                   // 7-bit LUT (sym | len << 8), rebuilt below
+            if (st == ST_OK) {
+              uint16_t* next = sh.tb_next;                 // next code per length (LDS: no scratch)
+              uint32_t code = 0;
+              for (int l = 1; l <= 7; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; next[l] = (uint16_t)code; }
+              for (int i = 0; i < 19; i++) {
+                const uint32_t l = cl[i];
+                if (!l) continue;
+                const uint32_t rc = hz::rev_bits(next[l]++, (int)l);
+                for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint16_t)(i | (l << 8));
+              }
+            }
+            const uint32_t total = hlit + hdist;
+            uint32_t n = 0, prevl = 0;
+            HRR rr;
+            rr.init(sh.hbits, r.p, r.base);
+            while (st == ST_OK && n < total) {
+              if (rr.pos() > limit_bits + 64u) { st = ST_TRUNC; break; }
+              const uint32_t bits = rr.peek();
+              const uint32_t e = clut[bits & 127u];
+              const uint32_t sym = e & 0xffu, l = e >> 8;
+              if (sym < 16) { rr.drop(l); sh.lens[n++] = (uint8_t)sym; prevl = sym; continue; }
+              // a repeat: its extra bits follow the code in the same peek (7 + 7 bits)
+              const uint32_t x = bits >> l;
+              uint32_t rep, val = 0;
+              if (sym == 16) {
+                if (n == 0) { st = ST_DATA; break; }
+                val = prevl; rep = 3 + (x & 3u); rr.drop(l + 2u);
+              } else if (sym == 17) { rep = 3 + (x & 7u); rr.drop(l + 3u); }
+              else { rep = 11 + (x & 127u); rr.drop(l + 7u); }
+              if (n + rep > total) { st = ST_DATA; break; }
+              for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
+              prevl = val;
+            }
+            r.p = rr.p;
+            if (st == ST_OK && r.pos() > limit_bits) st = ST_TRUNC;
+            if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;   // missing end-of-block code
+            if (st == ST_OK) {
+              for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
+              for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
+              for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
+            }
+            sh.u_status = st;
+            sh.u_pos = r.pos();
+            sh.u_nlen = hlit;
+            sh.u_ndist = hdist;
+          }
+        }
+        HZ2_LSYNC();
+        const int hst = sh.u_status;
+        if (hst != ST_OK) return hst;
+        pos = sh.u_pos;
+        nlen = sh.u_nlen;
+        ndist = sh.u_ndist;
+      }
+      HZ_T(2);
+      {
+        int bst = ST_OK;
+        hz::TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB, 1};
+        HZ_BUILD_TABLE(sh, tll, bst);
+        if (bst != ST_OK) return bst;
+        hz::TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB, 1};
+        HZ_BUILD_TABLE(sh, td, bst);
+        if (bst != ST_OK) return bst;
+      }
+      HZ2_LSYNC();
+
+      est = cur.prev_block_bits ? cur.prev_block_bits : 200000u;
+      {
+        const uint32_t rem = limit_bits > pos ? limit_bits - pos : 0u;
+        if (est > rem + 64u) est = rem + 64u;
+      }
+      est += (uint32_t)(((uint64_t)est * tune.over16) >> 4);
+        first_window = 1;
+      } else if (NW > 1) {
+        // a continuation window: the block's tables are the other wavefront's
+        const Shared& o = *pipe.other;
+        LANE_LOOP {
+          for (uint32_t i = (uint32_t)lane; i < (uint32_t)((1 << LL_ROOT) + LL_SUB); i += 64u) sh.lut_ll[i] = o.lut_ll[i];
+          for (uint32_t i = (uint32_t)lane; i < (uint32_t)((1 << D_ROOT) + D_SUB); i += 64u) sh.lut_d[i] = o.lut_d[i];
+        }
+        HZ2_LSYNC();
+      }
       if (stats) { stats->windows++; if (!first_window) stats->extra_windows++; }
       const uint32_t ws = pos;
       uint32_t L = (est + 63u) >> 6;
@@ -1000,7 +1155,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;
         if (stats) stats->steps_a += steps;
       }
-      WAVE_SYNC();
+      HZ2_LSYNC();
 
       HZ_T(4);
       // -------- phase A': continuation until lane+1's recorded path is met --------
@@ -1043,7 +1198,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;              \
       } while (0)
       LANE_LOOP { HZ2_CONTINUE(lane); }
-      WAVE_SYNC();
+      HZ2_LSYNC();
 
       HZ_T(5);
       // -------- repair rounds --------
@@ -1079,11 +1234,11 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;
           }
         }
-        WAVE_SYNC();
+        HZ2_LSYNC();
         LANE_LOOP {
           if ((redo_m >> lane) & 1ull) HZ2_CONTINUE(lane);
         }
-        WAVE_SYNC();
+        HZ2_LSYNC();
       }
 #undef HZ2_CONTINUE
 
@@ -1128,7 +1283,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           sh.u_nlen = sh.endp[lane];
         }
       }
-      WAVE_SYNC();
+      HZ2_LSYNC();
       end_kind = (uint32_t)sh.u_status;
       npos = sh.u_pos;
       if (end_kind == END_ERR) {
@@ -1157,6 +1312,31 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       if (stats) stats->matches += mtotal;
       if (out + wtotal > dst_len) return ST_SIZE;
       if (npos > limit_bits) return ST_TRUNC;
+
+      {  // the next window's start: the other wavefront may begin its sync phases now
+        WinState nx;
+        nx.pos = npos;
+        nx.out = out + wtotal;
+        nx.prev_block_bits = cur.prev_block_bits;
+        nx.block_start = block_start;
+        nx.bfinal = bfinal;
+        nx.est = 0;
+        if (end_kind == END_EOB) {
+          nx.kind = bfinal ? WK_END : WK_NEWBLOCK;
+          nx.prev_block_bits = npos - block_start;
+        } else {
+          nx.kind = WK_CONT;
+          // the block goes on: the rest is estimated from what is left of the estimate
+          const uint32_t used = npos - ws;
+          uint32_t e2 = est > used ? est - used : 0u;
+          const uint32_t floor_est = ((npos - block_start) >> 3) + 64u * LMIN;
+          e2 = e2 < floor_est ? floor_est : e2;
+          const uint32_t rem = limit_bits > npos ? limit_bits - npos : 0u;
+          if (e2 > rem + 64u) e2 = rem + 64u;
+          nx.est = e2;
+        }
+        publish(nx);
+      }
 
       HZ_T(7);
       // -------- phase E: exact decode of every valid range --------
@@ -1256,8 +1436,12 @@ HZ_UNROLL
         if (stats) stats->steps_e += steps;
       }
       if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
-      WAVE_SYNC_GLOBAL();
+      HZ2_GSYNC();
 
+      {
+        const int wr = wait_output();    // every byte before `out` final (the other wavefront's M)
+        if (wr != ST_OK) return wr;
+      }
       HZ_T(8);
       // -------- phase M: write the window's output, one span at a time --------
       // The window's output [out, out + wtotal) is cut into consecutive spans [F, F + span):
@@ -1348,7 +1532,7 @@ HZ_UNROLL
           memset(&sh.smap[(SPAN / 64u) * (uint32_t)lane], 0, SPAN / 32u);
 #endif
         }
-        HZ2_MSYNC();
+        HZ2_LSYNC();
         if (stats) {
           uint64_t mx = 0, sm = 0;
           for (int l = 0; l < 64; l++) {
@@ -1383,7 +1567,7 @@ HZ_UNROLL
             }
           }
         }
-        HZ2_MSYNC();
+        HZ2_LSYNC();
         HZ_T(15);
         // prefetch the next batch's records
         LANE_ARR(uint32_t, no, MPL);
@@ -1428,12 +1612,12 @@ HZ_UNROLL
             }
             if (stats) stats->tokens++;                // (emulator statistic: pointer-jumping rounds)
             if (!WAVE_BALLOT(LV(chg) != 0u)) break;
-            HZ2_MSYNC();
+            HZ2_LSYNC();
             LANE_LOOP {
 HZ_UNROLL
               for (uint32_t i = 0; i < RGP; i++) sh.smap[(uint32_t)lane + 64u * i] = (uint16_t)LV(dq)[i];
             }
-            HZ2_MSYNC();
+            HZ2_LSYNC();
           }
         }
         HZ_T(12);
@@ -1453,7 +1637,7 @@ HZ_UNROLL
         LANE_VAR(uint32_t, lb);                 // literal slots
         LANE_VAR(uint32_t, fb);                 // match bytes whose source lies before F
         LANE_LOOP { LV(lb) = 0; LV(fb) = 0; if (lane == 0) sh.sbuf[0] = hv; }
-        HZ2_MSYNC();
+        HZ2_LSYNC();
         uint32_t lcnt = 0;                      // literals of the span so far (wave-uniform)
         // two halves of GH slots: GH loaded bytes in flight per lane (all 24 spill)
         constexpr uint32_t GH = RGP / 2u;
@@ -1496,7 +1680,7 @@ HZ_UNROLL
             LV(ra2) += (uint64_t)F * a1 + b2;
           }
         }
-        HZ2_MSYNC();
+        HZ2_LSYNC();
         // in-span sources: literals of the span, now in LDS
         LANE_LOOP {
           uint32_t a1 = 0, b2 = 0;
@@ -1519,7 +1703,7 @@ HZ_UNROLL
           LV(ra1) += a1;
           LV(ra2) += (uint64_t)F * a1 + b2;
         }
-        HZ2_MSYNC();
+        HZ2_LSYNC();
         HZ_T(13);
         HZ2_MARK("M_STORE");
         // 4. store: whole dwords inside the span (dword 0 also when its head was loaded) and
@@ -1540,11 +1724,7 @@ HZ_UNROLL
         }
         hcar = sh.sbuf[ndw - 1u];
         hcar_ok = true;
-#if HZ2_SPANLIGHT
-        HZ2_LSYNC();      // this wave reads the stored dwords back: wavefront-scope ordering
-#else
-        WAVE_SYNC_GLOBAL();
-#endif
+        HZ2_GSYNC();      // this wave reads the stored dwords back as far sources
         LANE_LOOP {
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) { LV(ro)[u] = LV(no)[u]; LV(rw)[u] = LV(nw)[u]; }
@@ -1560,23 +1740,27 @@ HZ_UNROLL
       }
 
       HZ_T(10);
-      out += wtotal;
-      pos = npos;
-      first_window = 0;
-      if (end_kind == END_EOB) break;
-      // the block goes on: the rest is estimated from what is left of the estimate
-      const uint32_t used = npos - ws;
-      est = est > used ? est - used : 0u;
-      const uint32_t floor_est = ((npos - block_start) >> 3) + 64u * LMIN;
-      est = est < floor_est ? floor_est : est;
-      {
-        const uint32_t rem = limit_bits > pos ? limit_bits - pos : 0u;
-        if (est > rem + 64u) est = rem + 64u;
-      }
+      output_done();
+      return ST_OK;
+    }();
+    if (wst != ST_OK) {
+      fail = wst;
+      if (NW > 1) atomic_min_err(pipe.ctl, wst);
+      break;
     }
-    prev_block_bits = pos - block_start;
-    if (bfinal) break;
   }
+  if (NW > 1) {
+    // both wavefronts: every window done (or failed); the adler sums of both
+    if (fail != ST_OK) atomic_min_err(pipe.ctl, fail);
+    HZ2_WGBAR();
+    const int32_t e = (int32_t)ctl_ld((const uint32_t*)&pipe.ctl->err);
+    if (e) return e;
+    cur = pipe.ctl->next;                 // the END state: trailer position and total output
+  } else if (fail != ST_OK) {
+    return fail;
+  }
+  uint32_t pos = cur.pos;
+  const uint32_t out = cur.out;
   // ---- trailer: adler32 (big-endian) after byte alignment ----
   HZ_T(9);
   pos = (pos + 7u) & ~7u;
@@ -1595,6 +1779,15 @@ HZ_UNROLL
 #else
   for (int lane = 0; lane < 64; lane++) { S1 += s1[lane]; S2 += s2[lane]; }
 #endif
+  if (NW > 1) {
+    // the two wavefronts' partial sums, added up through LDS
+    Ctl* c = pipe.ctl;
+    c->adler[pipe.w][0] = S1;
+    c->adler[pipe.w][1] = S2;
+    HZ2_WGBAR();
+    S1 = c->adler[0][0] + c->adler[1][0];
+    S2 = c->adler[0][1] + c->adler[1][1];
+  }
   const uint32_t A = (uint32_t)((1u + S1) % ADLER_MOD);
   const uint32_t B = (uint32_t)(((uint64_t)(out % ADLER_MOD) * A + ADLER_MOD - (S2 % ADLER_MOD)) % ADLER_MOD);
   if (((B << 16) | A) != want) return ST_DATA;

@@ -42,7 +42,9 @@ typedef __attribute__((address_space(1))) uint16_t hz_gu16;
 #define HZ_UNROLL _Pragma("unroll")
 #define LANE_VAR(T, name) T name
 #define LV(name) name
-#define LANE_LOOP for (int lane = (int)threadIdx.x, _once = 1; _once; _once = 0)
+// the lane index within the wavefront (a workgroup may hold two: inflate2w_kernel)
+#define HZ_LANE_ID() ((int)(threadIdx.x & 63u))
+#define LANE_LOOP for (int lane = HZ_LANE_ID(), _once = 1; _once; _once = 0)
 #if defined(HZ_LIGHT_SYNC)
 // one-wavefront workgroups: the LDS executes a wave's instructions in order, so
 // cross-lane LDS hand-offs only need the compiler not to move or cache memory
@@ -424,7 +426,7 @@ HZ_HD uint32_t load_word(hz_gcu8* base, uint32_t k, uint32_t lo, uint32_t hi) {
 // ---- wave-collective helpers (the only places the two drivers differ) -------
 #if HZ_GPU
 #define WAVE_BALLOT(expr) \
-  ([&]() { const int lane = (int)threadIdx.x; (void)lane; return (uint64_t)__ballot((expr) ? 1 : 0); }())
+  ([&]() { const int lane = HZ_LANE_ID(); (void)lane; return (uint64_t)__ballot((expr) ? 1 : 0); }())
 namespace hz {
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
   uint32_t x = v;
@@ -488,7 +490,7 @@ struct TableArgs {
 // exclusive scan of the low 24 bits of lane variable v into o, total into t
 #define HZ_SCAN_LOW24(v, o, t)                                \
   do {                                                        \
-    o = hz::wave_excl_scan((v) & 0xffffffu, (int)threadIdx.x); \
+    o = hz::wave_excl_scan((v) & 0xffffffu, HZ_LANE_ID()); \
     t = hz::wave_sum((v) & 0xffffffu);                        \
   } while (0)
 #else
@@ -500,20 +502,23 @@ struct TableArgs {
   } while (0)
 #endif
 
+#ifndef HZ_TB_SYNC
+#define HZ_TB_SYNC() WAVE_SYNC()
+#endif
 // Table build as a macro-free function per driver is awkward because it needs
 // ballots; it is written once in the SIMT style below.
 #define HZ_BUILD_TABLE(sh, A, status_out)                                               \
   do {                                                                                  \
     /* counts: LDS atomics over all lanes */                                          \
     LANE_LOOP { if (lane < 16) (A).cnt[lane] = 0; }                                     \
-    WAVE_SYNC();                                                                        \
+    HZ_TB_SYNC();                                                                        \
     LANE_LOOP {                                                                         \
       for (int s = lane; s < (A).n; s += 64) {                                          \
         const int l = (A).lens[s];                                                      \
         if (l) hz::atomicAdd_lds(&(A).cnt[l], 1);                                       \
       }                                                                                 \
     }                                                                                   \
-    WAVE_SYNC();                                                                        \
+    HZ_TB_SYNC();                                                                        \
     /* validity (zlib inflate_table rules), first code and offset per length */        \
     LANE_LOOP {                                                                         \
       if (lane == 0) {                                                                  \
@@ -537,7 +542,7 @@ struct TableArgs {
         (sh).u_status = bad ? hz::ST_DATA : hz::ST_OK;                                  \
       }                                                                                 \
     }                                                                                   \
-    WAVE_SYNC();                                                                        \
+    HZ_TB_SYNC();                                                                        \
     /* per-length counts, first codes and offsets, read once into wave-uniform registers */ \
     uint32_t _cn[16], _fc[16], _of[16];                                                 \
     _Pragma("unroll") for (int _q = 0; _q < 16; _q++) {                                 \
@@ -567,7 +572,7 @@ struct TableArgs {
         }                                                                               \
       }                                                                                 \
     }                                                                                   \
-    WAVE_SYNC();                                                                        \
+    HZ_TB_SYNC();                                                                        \
     /* LUT fill: every root index tested against each length's canonical range (no   \
        loop-carried chain: a prefix-free code matches at most one length) */           \
     LANE_LOOP {                                                                         \
@@ -583,7 +588,7 @@ struct TableArgs {
         (A).lut[idx] = (uint16_t)e;                                                     \
       }                                                                                 \
     }                                                                                   \
-    WAVE_SYNC();                                                                        \
+    HZ_TB_SYNC();                                                                        \
     /* second level: one subtable per root prefix of longer codes.  Codes with the     \
        same prefix are contiguous in canonical order; the last of a run (the longest)  \
        sizes its subtable, and a scan over the runs places them */                      \
@@ -623,7 +628,7 @@ struct TableArgs {
       /* <= nsub for every complete code (see LL_SUB/D_SUB); a table that would not    \
          fit is rejected before any subtable entry is written */                        \
       LANE_LOOP { if (lane == 0 && _used > (uint32_t)(A).nsub) (sh).u_status = hz::ST_DATA; } \
-      WAVE_SYNC();                                                                      \
+      HZ_TB_SYNC();                                                                      \
       /* fill subtables by symbol (zlib-style replication) */                           \
       LANE_LOOP {                                                                       \
         for (int k = _k0 + lane; k < _k1 && (sh).u_status == hz::ST_OK; k += 64) {      \
@@ -640,7 +645,7 @@ struct TableArgs {
           for (int m = 0; m < (1 << (sb - tl)); m++) (A).lut[off + (j0 | (m << tl))] = e; \
         }                                                                               \
       }                                                                                 \
-      WAVE_SYNC();                                                                      \
+      HZ_TB_SYNC();                                                                      \
     }                                                                                   \
     status_out = (sh).u_status;                                                         \
   } while (0)
@@ -1193,7 +1198,7 @@ int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* sta
       // output offsets; the window keeps only what fits the LDS reference map
       LANE_VAR(uint32_t, obase);
 #if HZ_GPU
-      obase = wave_excl_scan(olen, (int)threadIdx.x);
+      obase = wave_excl_scan(olen, HZ_LANE_ID());
 #else
       { uint32_t acc = 0; for (int lane = 0; lane < 64; lane++) { obase[lane] = acc; acc += olen[lane]; } }
 #endif

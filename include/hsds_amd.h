@@ -111,12 +111,14 @@ const char* hsds_version(void);
 const char* hsds_strerror(int status);
 
 /* Tuning of the inflate kernel: segment over-provisioning against the previous
- * deflate block in 16ths (0..16), warm-up bits before a segment (0..4096), an unused
- * argument (0), repair rounds per window (0..64).  Any setting decodes the same bytes;
- * it only moves work between the phases.  Defaults are set by hsds_engine_create;
- * HSDS_TUNE_KEEP (rounds: -1) leaves a setting unchanged. */
+ * deflate block in 16ths (0..16), warm-up bits before a segment (0..4096), wavefronts
+ * per zlib stream (0: by batch size -- two when the batch's streams cannot fill half the
+ * resident wavefronts --, 1, or 2), repair rounds per window (0..64).  Any setting
+ * decodes the same bytes; it only moves work between the phases and wavefronts.
+ * Defaults are set by hsds_engine_create; HSDS_TUNE_KEEP (rounds: -1) leaves a setting
+ * unchanged. */
 #define HSDS_TUNE_KEEP 0xffffffffu
-int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t unused,
+int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, uint32_t waves_per_stream,
                     int32_t repair_rounds);
 
 /* ---- partition ------------------------------------------------------------- */

@@ -3,14 +3,42 @@
 // order, so its orchestration (segments, sync, repairs, emit, match-ring resolve, fused
 // unshuffle) is checked against libz on CPU.  Never used by the product.
 #include <stdlib.h>
+#include <string.h>
+#include <thread>
 #include "../../hsds_amd/csrc/inflate2.h"
 
 // perm_n > 1: the output is written through the byte-unshuffle map of perm_n-byte elements
 // (dst holds the unshuffled bytes), as the engine does for F2 chunks.
 // dst_off: the stream's output starts dst_off bytes into dst (dst has dst_len + dst_off + 8
 // bytes; the bytes around the output must stay untouched)
-extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,
-                            int max_rounds, uint32_t over16, uint32_t perm_n, uint32_t dst_off, uint64_t* stats_out) {
+// nwaves == 2: the window pipeline of inflate2w_kernel -- two threads, one per emulated
+// wavefront, sharing a hz2::Ctl and each other's LDS tables; both must return the same status
+static int run_stream(hz2::Shared* sh, const hz2::Job& job, const hz2::Tune& tune, uint8_t* ring, hz2::Stats& st,
+                      int nwaves) {
+  if (nwaves < 2) return hz2::inflate_stream<hz2::Stats, 1>(*sh, job, tune, ring, &st);
+  hz2::Shared* sh2 = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
+  uint8_t* ring2 = (uint8_t*)malloc(hz2::SCRATCH_BYTES);
+  hz2::Ctl ctl;
+  memset(&ctl, 0, sizeof(ctl));
+  hz2::ctl_reset(&ctl, 0);
+  hz2::Stats st2 = {};
+  int r2 = 0;
+  std::thread t([&]() {
+    r2 = hz2::inflate_stream<hz2::Stats, 2>(*sh2, job, tune, ring2, &st2, nullptr, hz2::Pipe{&ctl, sh, 1u});
+  });
+  const int r = hz2::inflate_stream<hz2::Stats, 2>(*sh, job, tune, ring, &st, nullptr, hz2::Pipe{&ctl, sh2, 0u});
+  t.join();
+  uint64_t* a = (uint64_t*)&st;
+  const uint64_t* b = (const uint64_t*)&st2;
+  for (size_t i = 0; i < sizeof(st) / 8; i++) a[i] += b[i];
+  free(ring2);
+  free(sh2);
+  return r == r2 ? r : -100;          // the two wavefronts disagree: a pipeline bug
+}
+
+extern "C" int emu_inflate2_nw(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,
+                               int max_rounds, uint32_t over16, uint32_t perm_n, uint32_t dst_off, uint64_t* stats_out,
+                               int nwaves) {
   hz2::Shared* sh = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
   uint8_t* ring = (uint8_t*)malloc(hz2::SCRATCH_BYTES);
   hz2::Stats st = {};
@@ -20,7 +48,7 @@ extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, 
   uint8_t* stage = n > 1 ? (uint8_t*)malloc(dst_len + 16) : nullptr;
   hz2::Job job = {src, src_len, n > 1 ? stage + (dst_off & 15u) : dst + dst_off, dst_len, 1u, nullptr, hz2::perm_make(1, 1, 0)};
   hz2::Tune tune = {W, max_rounds, over16};
-  int r = hz2::inflate_stream<hz2::Stats>(*sh, job, tune, ring, &st);
+  int r = run_stream(sh, job, tune, ring, st, nwaves);
   if (n > 1) {
     if (r == 0) {
       const uint8_t* in = stage + (dst_off & 15u);
@@ -37,6 +65,11 @@ extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, 
   free(ring);
   free(sh);
   return r;
+}
+
+extern "C" int emu_inflate2(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,
+                            int max_rounds, uint32_t over16, uint32_t perm_n, uint32_t dst_off, uint64_t* stats_out) {
+  return emu_inflate2_nw(src, src_len, dst, dst_len, W, max_rounds, over16, perm_n, dst_off, stats_out, 1);
 }
 
 extern "C" int emu2_shared_bytes() { return (int)sizeof(hz2::Shared); }

@@ -21,22 +21,23 @@ STATS = ("windows blocks stored tokens matches lanes_valid repairs repair_lanes 
 def emu():
     hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("inflate2.h", "inflate_wave.h")]
     if not os.path.exists(EMU) or os.path.getmtime(EMU) < max(os.path.getmtime(p) for p in [SRC] + hdrs):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", EMU, SRC])
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", EMU, SRC])
     L = ctypes.CDLL(EMU)
     L.emu_inflate2.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    L.emu_inflate2_nw.argtypes = L.emu_inflate2.argtypes + [ctypes.c_int]
     return L
 
 
-def run(L, comp, n, W=384, rounds=4, over16=1, perm_n=1, dst_off=0):
+def run(L, comp, n, W=384, rounds=4, over16=1, perm_n=1, dst_off=0, nwaves=1):
     src = np.frombuffer(comp, np.uint8).copy()
     if src.size == 0:
         src = np.zeros(1, np.uint8)
     guard = 0xA5
     dst = np.full(max(n, 1) + dst_off + 8, guard, np.uint8)
     st = np.zeros(len(STATS), np.uint64)
-    r = L.emu_inflate2(src.ctypes.data, len(comp), dst.ctypes.data, n, W, rounds, over16, perm_n, dst_off,
-                       st.ctypes.data)
+    r = L.emu_inflate2_nw(src.ctypes.data, len(comp), dst.ctypes.data, n, W, rounds, over16, perm_n, dst_off,
+                          st.ctypes.data, nwaves)
     assert (dst[:dst_off] == guard).all() and (dst[dst_off + n:] == guard).all(), "write outside the output"
     return r, dst[dst_off:dst_off + n].tobytes(), dict(zip(STATS, st.tolist()))
 
@@ -221,3 +222,92 @@ def test_long_overlapping_matches_and_far_distances(emu):
         c = zlib.compress(data, level)
         r, out, _ = run(emu, c, len(data))
         assert r == 0 and out == data, level
+
+
+# ---- two wavefronts per stream (inflate2w_kernel's window pipeline, emulated by two threads) ----
+@pytest.mark.parametrize("level", [0, 1, 4, 9])
+def test_two_wavefronts_match_zlib(emu, level):
+    for name, data in corpus().items():
+        c = zlib.compress(data, level)
+        r, out, st = run(emu, c, len(data), nwaves=2)
+        assert r == 0, (name, level, r)
+        assert out == data, (name, level)
+
+
+def test_two_wavefronts_strategies_and_stored_blocks(emu):
+    for strategy in (zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED):
+        for name in ("smooth_f32", "text", "random", "runs"):
+            data = corpus()[name]
+            co = zlib.compressobj(5, zlib.DEFLATED, 15, 8, strategy)
+            c = co.compress(data) + co.flush()
+            r, out, _ = run(emu, c, len(data), nwaves=2)
+            assert r == 0 and out == data, (name, strategy, r)
+    # many small blocks of each type: a full flush after every piece
+    rng = np.random.default_rng(4)
+    co = zlib.compressobj(6)
+    data, c = b"", b""
+    for i in range(60):
+        piece = rng.integers(0, 256 if i % 3 == 0 else 4, int(rng.integers(1, 3000)), dtype=np.uint8).tobytes()
+        data += piece
+        c += co.compress(piece) + co.flush(zlib.Z_FULL_FLUSH)
+    c += co.flush()
+    for nw in (1, 2):
+        r, out, st = run(emu, c, len(data), nwaves=nw)
+        assert r == 0 and out == data, nw
+    assert st["stored"] > 0
+
+
+def test_two_wavefronts_continuation_windows_and_f1_stream(emu):
+    """one block over several windows (the continuation copies the other wavefront's tables),
+    and a 256 KiB split of the bench chunk (7 blocks: both wavefronts alternate)"""
+    import sys
+    sys.path.insert(0, ROOT)
+    from bench import smooth_chunk
+    raw = smooth_chunk(20261015).view(np.uint8)[:262144].tobytes()
+    r, out, st = run(emu, zlib.compress(raw, 4), len(raw), nwaves=2)
+    assert r == 0 and out == raw and st["windows"] >= st["blocks"]
+    z = bytes(1 << 20)
+    r, out, st = run(emu, zlib.compress(z, 9), len(z), nwaves=2)
+    assert r == 0 and out == z
+    data = corpus()["smooth_f32"]
+    r, out, st = run(emu, zlib.compress(data, 4), len(data), over16=0, W=64, nwaves=2)
+    assert r == 0 and out == data
+
+
+@pytest.mark.parametrize("off", [1, 3])
+def test_two_wavefronts_unaligned_output(emu, off):
+    data = corpus()["smooth_f32"][:50001]
+    r, out, _ = run(emu, zlib.compress(data, 4), len(data), dst_off=off, nwaves=2)
+    assert r == 0 and out == data
+
+
+def test_two_wavefronts_corruptions_fail_like_libz(emu):
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+    rng = np.random.default_rng(19)
+    base = corpus()["smooth_f32"][:60000]
+    good = zlib.compress(base, 4)
+    for t in range(120):
+        b = bytearray(good)
+        k = t % 4
+        if k == 0:
+            b = b[:int(rng.integers(1, len(b)))]
+        elif k == 1:
+            i = int(rng.integers(0, len(b)))
+            b[i] ^= 1 << int(rng.integers(0, 8))
+        elif k == 2:
+            b[-1 - int(rng.integers(0, 4))] ^= 0x40
+        else:
+            b = b + bytes(rng.integers(0, 256, 5, dtype=np.uint8))
+        n = len(base)
+        ref = orc.uncompress(bytes(b), "zlib", 0, 1, n)
+        r, out, _ = run(emu, bytes(b), n, nwaves=2)
+        if isinstance(ref, int):
+            assert r < 0 and r != -100, (t, k, ref, r)
+        else:
+            assert r == 0 and out == ref, (t, k, r)
+    data = corpus()["text"]
+    c = zlib.compress(data, 4)
+    assert run(emu, c, len(data) - 1, nwaves=2)[0] not in (0, -100)
+    assert run(emu, c, len(data) + 1, nwaves=2)[0] not in (0, -100)

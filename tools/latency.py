@@ -49,13 +49,18 @@ def main():
         d_src = torch.from_numpy(src).to(dev)
         d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
         d_st = torch.zeros(1, dtype=torch.int32, device=dev)
-        ks = []
-        for _ in range(10):
-            eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
-            torch.cuda.synchronize()
-            ks.append(eng.last_inflate_ms())
-        assert int(d_st[0]) == 0
-        r["device_one_chunk_kernel_ms"] = round(statistics.median(ks), 3)
+        for mode, key in ((0, "device_one_chunk_kernel_ms"), (1, "device_one_chunk_kernel_ms_1wave"),
+                          (2, "device_one_chunk_kernel_ms_2wave")):
+            eng.set_tuning(waves_per_stream=mode)
+            ks = []
+            for _ in range(10):
+                d_dst.zero_()
+                eng.decode(d_src, descs, d_dst, d_st, compressor="zlib", shuffle=1, itemsize=4)
+                torch.cuda.synchronize()
+                ks.append(eng.last_inflate_ms())
+            assert int(d_st[0]) == 0 and d_dst[:CHUNK_BYTES].cpu().numpy().tobytes() == raw
+            r[key] = round(statistics.median(ks), 3)
+        eng.set_tuning(waves_per_stream=0)
         out[fmt] = r
     # micro-batcher: N concurrent whole-chunk requests of distinct F1 chunks
     from hsds_amd.batcher import ChunkBatcher
