@@ -586,40 +586,43 @@ class ChunkReader:
         results = [None] * len(reads)
         for ri, e in errors.items():
             results[ri] = e
-        # destination slots (base tensor, byte offset): cache arena, else a batch tensor
         need = [ri for ri in range(len(reads)) if ri not in errors]
         slots = {}
         pinned = []
-        if self.cache is not None:
-            abase = self.cache.arena.buf
-            for ri in need:
-                cid = reads[ri].chunk_id
-                # get_chunk caches when `chunk_id in cache or memFree >= size` (:1094-1103)
-                if cid not in self.cache and self.cache.memFree < chunk_size:
+
+        def reserve_slots():
+            # destination slots (base tensor, byte offset): cache arena, else a batch tensor
+            if self.cache is not None:
+                abase = self.cache.arena.buf
+                for ri in need:
+                    cid = reads[ri].chunk_id
+                    # get_chunk caches when `chunk_id in cache or memFree >= size` (:1094-1103)
+                    if cid not in self.cache and self.cache.memFree < chunk_size:
+                        continue
+                    v = self.cache.reserve(cid, chunk_dims, dtype, pin=True)
+                    if v is not None:
+                        slots[ri] = (abase, v.data_ptr() - abase.data_ptr())
+                        pinned.append(cid)
+            rest = [ri for ri in need if ri not in slots]
+            if rest:
+                tmp = torch.empty(len(rest) * chunk_size, dtype=torch.uint8, device=self.device)
+                for k, ri in enumerate(rest):
+                    slots[ri] = (tmp, k * chunk_size)
+            # prefill hyper chunks with the fill value or zeros (datanode_lib.py:884-888)
+            fill_chunk = None
+            for ri, kind, _, _ in jobs:
+                if kind != "hyper_init":
                     continue
-                v = self.cache.reserve(cid, chunk_dims, dtype, pin=True)
-                if v is not None:
-                    slots[ri] = (abase, v.data_ptr() - abase.data_ptr())
-                    pinned.append(cid)
-        rest = [ri for ri in need if ri not in slots]
-        if rest:
-            tmp = torch.empty(len(rest) * chunk_size, dtype=torch.uint8, device=self.device)
-            for k, ri in enumerate(rest):
-                slots[ri] = (tmp, k * chunk_size)
-        # prefill hyper chunks with the fill value or zeros (datanode_lib.py:884-888)
-        fill_chunk = None
-        for ri, kind, _, _ in jobs:
-            if kind != "hyper_init":
-                continue
-            base, off = slots[ri]
-            view = base[off:off + chunk_size]
-            if fill_value is None or not np.array(fill_value, dtype=dtype).reshape(1).view(np.uint8).any():
-                view.zero_()
-            else:
-                if fill_chunk is None:
-                    fill_chunk = torch.from_numpy(np.full(chunk_dims, fill_value, dtype=dtype).view(np.uint8)
-                                                  .reshape(-1).copy()).to(self.device)
-                view.copy_(fill_chunk)
+                base, off = slots[ri]
+                view = base[off:off + chunk_size]
+                if fill_value is None or not np.array(fill_value, dtype=dtype).reshape(1).view(np.uint8).any():
+                    view.zero_()
+                else:
+                    if fill_chunk is None:
+                        fill_chunk = torch.from_numpy(np.full(chunk_dims, fill_value, dtype=dtype).view(np.uint8)
+                                                      .reshape(-1).copy()).to(self.device)
+                    view.copy_(fill_chunk)
+
         # ONE decode batch into a contiguous buffer (plain objects and HDF5 chunks): the
         # stored objects are packed straight into page-locked staging and go up with one
         # asynchronous copy; statuses come back with one asynchronous copy as well, and
@@ -639,6 +642,7 @@ class ChunkReader:
             self.stats["h5_chunks"] += sum(1 for _, k, _, _ in dec if k == "h5")
             st_host = torch.empty(len(dec), dtype=torch.int32, pin_memory=True)
             st_host.copy_(status, non_blocking=True)
+            reserve_slots()      # while the device copies and decodes
             # placement: ONE copy batch per destination tensor (whole objects: flat records
             # built at once; HDF5 chunks: one strided record each)
             recs = np.zeros(len(dec), COPY_DESC_DTYPE)
@@ -665,6 +669,8 @@ class ChunkReader:
                 recs["itemsize"][flat] = w
             for base, rows in groups.values():
                 self.eng.copy(dbuf, base, recs[np.asarray(rows)])
+        else:
+            reserve_slots()
         for ri in need:
             base, off = slots[ri]
             if results[ri] is None:
@@ -734,15 +740,23 @@ def _stage_blobs(blobs, dst_lens, device, align=256):
     def put(k0, k1):
         for o, b in zip(src_off[k0:k1].tolist(), blobs[k0:k1]):
             h[o:o + len(b)] = np.frombuffer(b, np.uint8) if not isinstance(b, np.ndarray) else b
-    if total >= (32 << 20) and n >= 16:
+    d_src = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
+    if total >= (32 << 20) and n >= 32:
         # large batches: the copies into staging run on the host's cores (numpy drops the GIL)
-        parts = min(8, n)
+        # in 32 pieces, and each piece goes up as soon as it is staged, so the link works
+        # while the later pieces are still being copied
+        parts = 32
         cuts = [n * i // parts for i in range(parts + 1)]
-        list(_stage_pool().map(lambda i: put(cuts[i], cuts[i + 1]), range(parts)))
+        futs = [_stage_pool().submit(put, cuts[i], cuts[i + 1]) for i in range(parts)]
+        for i, f in enumerate(futs):
+            f.result()
+            lo = int(src_off[cuts[i]])
+            hi = int(src_off[cuts[i + 1]]) if cuts[i + 1] < n else total
+            if hi > lo:
+                d_src[lo:hi].copy_(host[lo:hi], non_blocking=True)
     else:
         put(0, n)
-    d_src = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
-    d_src.copy_(host, non_blocking=True)
+        d_src.copy_(host, non_blocking=True)
     return d_src, descs, int(dpad.sum()) if n else 0
 
 
