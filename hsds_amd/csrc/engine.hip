@@ -52,7 +52,7 @@
 #define HZ2_WPE 4          // inflate2_kernel waves per SIMD the compiler must allow (VGPR budget)
 #endif
 #ifndef HZ2_PIPE_DEFAULT
-#define HZ2_PIPE_DEFAULT 0  // -1: two wavefronts per zlib stream when a batch cannot fill the GPU
+#define HZ2_PIPE_DEFAULT -1  // two wavefronts per zlib stream when a batch cannot fill the GPU (0: never)
 #endif
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 

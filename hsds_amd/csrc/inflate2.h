@@ -163,6 +163,7 @@ struct alignas(16) Shared {
       uint32_t sbuf[SPAN / 4 + 2];   // the batch's aligned dwords, assembled in LDS
     };
   };
+  uint32_t wnext[8];              // NW == 1: the next window's start (WinState), kept in LDS across E and M
   uint8_t syncw[WAVE];            // record index where the predecessor met this lane / SYNC_*
   uint32_t endp[WAVE];            // lane's exclusive end (token boundary)
   uint8_t nrec[WAVE];
@@ -866,7 +867,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
   cur.est = 0;
   cur.prev_block_bits = 0;
   uint32_t k = NW > 1 ? pipe.w : 0u;   // window index
-  WinState nxt = cur;                  // NW == 1: the next window's start
+  static_assert(sizeof(WinState) <= sizeof(sh.wnext), "WinState in Shared::wnext");
 
   // the next window's start to whoever decodes it
   auto publish = [&](const WinState& nx) {
@@ -876,7 +877,8 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       if (nx.kind == WK_END) ctl_st(&c->end_at, k + 1u);
       ctl_st(&c->synced, k + 1u);
     } else {
-      nxt = nx;
+      // (in LDS: no register holds it across phases E and M)
+      LANE_LOOP { if (lane == 0) memcpy(sh.wnext, &nx, sizeof(nx)); }
     }
   };
   // wait until every output byte before this window is final (the other wavefront's M)
@@ -914,7 +916,8 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       }
       if (!got) break;
     } else if (k > 0) {
-      cur = nxt;
+      HZ2_LSYNC();
+      memcpy(&cur, sh.wnext, sizeof(cur));
     }
     if (cur.kind == WK_END) break;
     const int wst = [&]() -> int {
