@@ -140,7 +140,9 @@ __device__
 #else
 static
 #endif
-inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_t wb, uint32_t we, uint32_t nseq) {
+inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_t wb, uint32_t we, uint32_t nseq,
+                    HzProf* prof) {
+  (void)prof;
   const uint32_t g0 = (wb + dmis) >> 4, g1 = (we + dmis + 15u) >> 4;
   for (uint32_t it = g0; it < g1; it += 64u) {
     const uint32_t ia = it * 16u;
@@ -178,12 +180,14 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_
           }
           hv |= 1u << k;
         }
+        HZ_T(6);
         HZ_UNROLL
         for (uint32_t k = 0; k < 16u; k++) ww[k >> 2] |= (uint32_t)*sp[k] << (8u * (k & 3u));
       }
       LV(have) = hv;
       LV(w0) = ww[0]; LV(w1) = ww[1]; LV(w2) = ww[2]; LV(w3) = ww[3];
     }
+    HZ_T(7);
     WAVE_SYNC_GLOBAL();       // every load of the iteration before any store
     LANE_LOOP {
       const uint32_t g = it + (uint32_t)lane;
@@ -200,6 +204,7 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_
       }
     }
     WAVE_SYNC_GLOBAL();
+    HZ_T(3);
   }
 }
 
@@ -248,6 +253,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     if (q + csz > n) return zs::E_TRUNC;
     int64_t tsz = 0;
     if (lt == 2) {
+      HZ_T(4);
       WAVE_SYNC();
       tsz = (int64_t)(int32_t)uni((uint32_t)zs::huf_tree(t, in, at + q, csz));
       WAVE_SYNC();
@@ -256,6 +262,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       return zs::E_DATA;
     }
     const uint32_t s0 = at + q + (uint32_t)tsz, ssz = csz - (uint32_t)tsz;
+    HZ_T(1);
     if (ns == 1) {
       LANE_LOOP { if (lane == 0) ls.u_err = zs::huf_stream(t, in, s0, ssz, lit, rsz); }
     } else {
@@ -298,6 +305,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     if (q >= n) return zs::E_TRUNC;
     const uint32_t modes = ub8(in, at + q++);
     if (modes & 3) return zs::E_DATA;
+    HZ_T(5);
     WAVE_SYNC();
     int64_t u = (int32_t)uni((uint32_t)zs::seq_table(t, t.ll, t.ll_al, (modes >> 6) & 3, in, at + q, n - q, 0, 35, 9));
     if (u < 0) return zs::E_DATA;
@@ -378,7 +386,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     }
     WAVE_SYNC();
     HZ_T(3);
-    if (ns_w) resolve(ls, dst, dmis, lit, wb, op, ns_w);
+    if (ns_w) resolve(ls, dst, dmis, lit, wb, op, ns_w, prof);
     if (last) break;
   }
   HZ_T(0);
