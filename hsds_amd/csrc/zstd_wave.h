@@ -28,13 +28,16 @@ namespace zw {
 
 constexpr int NSEQ = 128;
 constexpr int STG = 1024;                 // staged sequence-bitstream bytes
+constexpr int32_t SB_NONE = -(1 << 30);
+
+// one window sequence.  The FSE walk stores {LL entry, OF entry, ML entry, bit position}
+// (packed entries, below); the lane pass turns it into {out, lit, src, off}.
+enum : uint32_t { SQ_OUT = 0, SQ_LIT = 1, SQ_SRC = 2, SQ_OFF = 3 };
 
 struct Shared {
   zs::Tables t;
-  uint32_t s_out[NSEQ + 1];               // output offset of each window sequence; [n] = window end
-  uint32_t s_lit[NSEQ];                   // literal bytes
-  uint32_t s_src[NSEQ];                   // literal-area index of the first literal
-  uint32_t s_off[NSEQ];                   // match distance (0: none)
+  uint32_t seq[NSEQ + 1][4];              // out: output offset; lit: literal bytes; src: literal-area
+                                          // index of the first literal; off: match distance (0: none)
   uint32_t stage[STG / 4 + 4];
   int32_t u_err;
 };
@@ -48,9 +51,31 @@ HZ_HD uint32_t uni(uint32_t v) {
   return v;
 #endif
 }
+HZ_HD uint64_t uni64(uint64_t v) { return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v); }
 HZ_HD uint32_t ub8(const zs::In& in, uint32_t i) { return uni(zs::b8(in, i)); }
-// an FSE entry {sym, nb, base} as one word: sym | nb << 8 | base << 16
-HZ_HD uint32_t fse_word(const zs::Fse& e) { return uni((uint32_t)e.sym | ((uint32_t)e.nb << 8) | ((uint32_t)e.base << 16)); }
+// A sequence-table entry, repacked in place once its table is built:
+//   bits 0..15 state baseline, 16..19 state bits, 20..24 extra bits of the code, 25..31 code
+// so the serial FSE walk learns everything it needs from one LDS dword per table.
+static_assert(sizeof(zs::Fse) == 4, "an FSE entry is one dword");
+HZ_HD uint32_t sq_pack(const zs::Fse& e, uint32_t which) {
+  const uint32_t c = e.sym;
+  const uint32_t eb = which == 0 ? zs::ll_bits(c) : which == 1 ? c : zs::ml_bits(c);
+  return (uint32_t)e.base | ((uint32_t)e.nb << 16) | (eb << 20) | (c << 25);
+}
+HZ_HD uint32_t sq_base(uint32_t e) { return e & 0xffffu; }
+HZ_HD uint32_t sq_nb(uint32_t e) { return (e >> 16) & 15u; }
+HZ_HD uint32_t sq_eb(uint32_t e) { return (e >> 20) & 31u; }
+HZ_HD uint32_t sq_code(uint32_t e) { return e >> 25; }
+
+HZ_HD uint32_t fse_word(const zs::Fse* tab, uint32_t i) {
+#if HZ_GPU
+  return uni(((const uint32_t*)tab)[i]);     // one LDS dword read
+#else
+  uint32_t v;
+  memcpy(&v, tab + i, 4);
+  return v;
+#endif
+}
 
 // staged backward bitstream of the sequences (uniform): the input bytes are staged into
 // LDS STG bytes at a time, and the bits are read from a 64-bit register window over
@@ -60,7 +85,7 @@ struct SBits {
   zs::In in;
   uint32_t lo, n;     // stream = input bytes [lo, lo + n)
   int32_t pos;        // bits left (negative after reading past the start: an error)
-  int32_t sb;         // first stream byte in the stage (-1: none)
+  int32_t sb;         // stream byte of stage byte 0 (SB_NONE: nothing staged)
   int32_t wbit;       // stream bit of window bit 0 (a byte boundary; -1: none)
   uint64_t win;
 };
@@ -72,19 +97,49 @@ static
 #endif
 inline void sb_stage(Shared& ls, SBits& b, int32_t first) {
   WAVE_SYNC();
+  // the stage starts at the dword-aligned address at or below stream byte `first`;
+  // stage byte 0 is stream byte s0 (up to 3 bytes before `first`, possibly before the
+  // stream's start).  Bytes outside the stream read as 0.
+  const int32_t s0 = first - (int32_t)(((uintptr_t)b.in.p + b.lo + (uint32_t)first) & 3u);
   LANE_LOOP {
-    for (uint32_t k0 = 0; k0 < (uint32_t)STG / 4u + 4u; k0 += 64u) {   // uniform trip count
-      const uint32_t k = k0 + (uint32_t)lane;
-      uint32_t v = 0;
-      for (uint32_t i = 0; i < 4u; i++) {
-        const int32_t bi = first + 4 * (int32_t)k + (int32_t)i;
-        v |= (bi >= 0 && bi < (int32_t)b.n ? zs::b8(b.in, b.lo + (uint32_t)bi) : 0u) << (8 * i);
+    constexpr uint32_t NWD = (uint32_t)STG / 4u + 4u, NJ = (NWD + 63u) / 64u;
+    uint32_t v[NJ];
+#if HZ_GPU
+    // one aligned dword load per word, all issued before any is used (a word outside
+    // the stream loads the word holding `first`), so a lane's loads share one latency
+    hz_gcu8* bp = HZ_GLOBAL(hz_gcu8*, b.in.p) + b.lo;
+    HZ_UNROLL
+    for (uint32_t j = 0; j < NJ; j++) {
+      const int32_t sk = s0 + 4 * (int32_t)(j * 64u + (uint32_t)lane);
+      v[j] = *(hz_gcu32*)(bp + (sk + 4 > 0 && sk < (int32_t)b.n ? sk : s0));
+    }
+    HZ_UNROLL
+    for (uint32_t j = 0; j < NJ; j++) {
+      const int32_t sk = s0 + 4 * (int32_t)(j * 64u + (uint32_t)lane);     // stream byte of word k
+      uint32_t w = v[j];
+      if (sk < 0) w &= ~hz::bmask((uint32_t)(-sk) * 8u);
+      if (sk + 4 > (int32_t)b.n) w &= hz::bmask((uint32_t)((int32_t)b.n - sk) * 8u);
+      v[j] = sk + 4 > 0 && sk < (int32_t)b.n ? w : 0u;
+    }
+#else
+    for (uint32_t j = 0; j < NJ; j++) {
+      const int32_t sk = s0 + 4 * (int32_t)(j * 64u + (uint32_t)lane);     // stream byte of word k
+      uint32_t w = 0;
+      for (int32_t i = 0; i < 4; i++) {
+        const int32_t bi = sk + i;
+        if (bi >= 0 && bi < (int32_t)b.n) w |= zs::b8(b.in, b.lo + (uint32_t)bi) << (8 * i);
       }
-      if (k < (uint32_t)STG / 4u + 4u) ls.stage[k] = v;
+      v[j] = w;
+    }
+#endif
+    HZ_UNROLL
+    for (uint32_t j = 0; j < NJ; j++) {
+      const uint32_t k = j * 64u + (uint32_t)lane;
+      if (k < NWD) ls.stage[k] = v[j];
     }
   }
   WAVE_SYNC();
-  b.sb = (int32_t)uni((uint32_t)first);
+  b.sb = (int32_t)uni((uint32_t)s0);
 }
 
 #if HZ_GPU
@@ -95,7 +150,7 @@ static
 inline void sb_refill(Shared& ls, SBits& b) {
   int32_t by = (b.pos - 57) >> 3;            // window bytes [by, by + 8) hold >= 57 bits below pos
   if (by < 0) by = 0;
-  if (b.sb < 0 || by < b.sb || by + 8 > b.sb + STG) {
+  if (by < b.sb || by + 8 > b.sb + STG) {                 // (SB_NONE fails the second test)
     const int32_t f = by + 8 - STG;
     sb_stage(ls, b, f < 0 ? 0 : f);
   }
@@ -124,12 +179,12 @@ inline uint32_t sb_read(Shared& ls, SBits& b, uint32_t k) {
   return v;
 }
 
-// largest k <= hi with s_out[k] <= p
+// largest k <= hi with seq[k].out <= p
 HZ_HD uint32_t find_seq(const Shared& ls, uint32_t hi, uint32_t p) {
   uint32_t lo = 0;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1u) >> 1;
-    if (ls.s_out[mid] <= p) lo = mid; else hi = mid - 1u;
+    if (ls.seq[mid][SQ_OUT] <= p) lo = mid; else hi = mid - 1u;
   }
   return lo;
 }
@@ -159,7 +214,7 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_
         const uint32_t a0 = g * 16u;
         const uint32_t pb = a0 > wb + dmis ? a0 - dmis : wb;
         uint32_t t = find_seq(ls, nseq - 1u, pb);
-        uint32_t t_end = t + 1u < nseq ? ls.s_out[t + 1u] : we;
+        uint32_t t_end = t + 1u < nseq ? ls.seq[t + 1u][SQ_OUT] : we;
         hz_gu8* sp[16];
         HZ_UNROLL
         for (uint32_t k = 0; k < 16u; k++) {
@@ -167,12 +222,12 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_
           sp[k] = dst;
           if (ak < wb + dmis || ak >= we + dmis) continue;
           const uint32_t p = ak - dmis;
-          while (p >= t_end) { t++; t_end = t + 1u < nseq ? ls.s_out[t + 1u] : we; }
+          while (p >= t_end) { t++; t_end = t + 1u < nseq ? ls.seq[t + 1u][SQ_OUT] : we; }
           uint32_t q = p, u = t;
           for (;;) {
-            const uint32_t ub = ls.s_out[u], rel = q - ub, nl = ls.s_lit[u];
-            if (rel < nl) { sp[k] = lit + ls.s_src[u] + rel; break; }
-            const uint32_t m = ub + nl, d = ls.s_off[u], kk = q - m;
+            const uint32_t ub = ls.seq[u][SQ_OUT], rel = q - ub, nl = ls.seq[u][SQ_LIT];
+            if (rel < nl) { sp[k] = lit + ls.seq[u][SQ_SRC] + rel; break; }
+            const uint32_t m = ub + nl, d = ls.seq[u][SQ_OFF], kk = q - m;
             const uint32_t q2 = m - d + (kk < d ? kk : kk % d);
             if (q2 < it_lo) { sp[k] = dst + q2; break; }     // final output (earlier window / iteration)
             u = find_seq(ls, u, q2);
@@ -206,6 +261,191 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_
     WAVE_SYNC_GLOBAL();
     HZ_T(3);
   }
+}
+
+// ---- the lane pass over a window's sequences ----------------------------------------
+// Repeat offsets (RFC 8878 3.1.1.5) as functions of the previous three offsets R: slot s
+// of the result is R[src_s] + v_s (src_s < 3) or the constant v_s (src_s == 3).  The
+// offset a sequence uses is slot 0 after its own step, so a window's offsets are an
+// inclusive prefix composition of the steps, a log-depth scan across the lanes.
+struct RepFn { uint32_t src, v0, v1, v2; };   // src: 2 bits per slot
+HZ_HD RepFn rep_id() { return RepFn{0u | 1u << 2 | 2u << 4, 0u, 0u, 0u}; }
+HZ_HD RepFn rep_step(uint32_t ofv, uint32_t ll) {
+  if (ofv > 3u) return RepFn{3u | 0u << 2 | 1u << 4, ofv - 3u, 0u, 0u};        // new offset pushed
+  const uint32_t idx = ofv - 1u + (ll == 0u ? 1u : 0u);
+  if (idx == 0u) return rep_id();                                             // R0, history unchanged
+  if (idx == 1u) return RepFn{1u | 0u << 2 | 2u << 4, 0u, 0u, 0u};            // R1 to the front
+  if (idx == 2u) return RepFn{2u | 0u << 2 | 1u << 4, 0u, 0u, 0u};            // R2 to the front
+  return RepFn{0u | 0u << 2 | 1u << 4, 0xffffffffu, 0u, 0u};                  // R0 - 1 pushed
+}
+HZ_HD uint32_t rep_sel(const RepFn& f, uint32_t s) { return s == 0u ? f.v0 : s == 1u ? f.v1 : f.v2; }
+// f after g
+HZ_HD RepFn rep_compose(const RepFn& f, const RepFn& g) {
+  RepFn h;
+  uint32_t src = 0, hv[3];
+  HZ_UNROLL
+  for (uint32_t s = 0; s < 3u; s++) {
+    const uint32_t fs = (f.src >> (2u * s)) & 3u;
+    const uint32_t gs = fs == 3u ? 3u : (g.src >> (2u * fs)) & 3u;
+    hv[s] = fs == 3u ? rep_sel(f, s) : rep_sel(g, fs) + rep_sel(f, s);
+    src |= gs << (2u * s);
+  }
+  h.src = src; h.v0 = hv[0]; h.v1 = hv[1]; h.v2 = hv[2];
+  return h;
+}
+HZ_HD uint32_t rep_apply(const RepFn& f, uint32_t s, uint32_t r0, uint32_t r1, uint32_t r2) {
+  const uint32_t fs = (f.src >> (2u * s)) & 3u;
+  return (fs == 3u ? 0u : fs == 0u ? r0 : fs == 1u ? r1 : r2) + rep_sel(f, s);
+}
+
+// aligned dword j of the sequence stream (stream byte x is in dword (x + aoff) >> 2);
+// bytes outside the stream read as 0, and j is clamped into the stream's words
+HZ_HD uint32_t stream_word(const SBits& b, uint32_t aoff, int32_t j) {
+  const int32_t sk = 4 * j - (int32_t)aoff;                // stream byte of the dword's byte 0
+  const bool any = sk + 4 > 0 && sk < (int32_t)b.n;
+#if HZ_GPU
+  const int32_t jc = any ? j : 0;                          // word 0 holds stream byte 0
+  uint32_t w = *(hz_gcu32*)(HZ_GLOBAL(hz_gcu8*, b.in.p) + b.lo - aoff + 4 * jc);
+  if (sk < 0) w &= ~hz::bmask((uint32_t)(-sk) * 8u);
+  if (sk + 4 > (int32_t)b.n) w &= hz::bmask((uint32_t)((int32_t)b.n - sk) * 8u);
+  return any ? w : 0u;
+#else
+  uint32_t w = 0;
+  for (int32_t i = 0; i < 4; i++)
+    if (sk + i >= 0 && sk + i < (int32_t)b.n) w |= zs::b8(b.in, b.lo + (uint32_t)(sk + i)) << (8 * i);
+  (void)any;
+  return w;
+#endif
+}
+
+struct SeqLane { uint32_t ll, ml; RepFn f; };
+// one sequence from its walk record {LL entry, OF entry, ML entry, bit position}: the
+// extra bits lie below the position (offset on top, then match length, then literal
+// length) and are read straight from the input
+HZ_HD SeqLane seq_decode(const uint32_t* rec, const SBits& b, uint32_t aoff) {
+  const uint32_t eL = rec[0], eO = rec[1], eM = rec[2];
+  const uint32_t llc = sq_code(eL), ofc = sq_code(eO), mlc = sq_code(eM);
+  const uint32_t llb = sq_eb(eL), mlb = sq_eb(eM), ofb = sq_eb(eO);
+  const int32_t q = (int32_t)rec[3] - (int32_t)(llb + mlb + ofb) + 8 * (int32_t)aoff;
+  const int32_t j = q >> 5;
+  const uint32_t r = (uint32_t)(q - 32 * j);
+  const uint32_t w0 = stream_word(b, aoff, j), w1 = stream_word(b, aoff, j + 1), w2 = stream_word(b, aoff, j + 2);
+  const uint64_t lo64 = (uint64_t)w0 | ((uint64_t)w1 << 32);
+  auto field = [&](uint32_t o, uint32_t w) -> uint32_t {
+    const uint64_t v = o >= 64u ? (uint64_t)(w2 >> (o - 64u)) : o ? (lo64 >> o) | ((uint64_t)w2 << (64u - o)) : lo64;
+    return (uint32_t)v & hz::bmask(w);
+  };
+  SeqLane d;
+  d.ll = zs::ll_base(llc) + field(r, llb);
+  d.ml = zs::ml_base(mlc) + field(r + llb, mlb);
+  d.f = rep_step((1u << ofc) + field(r + llb + mlb, ofb), d.ll);
+  return d;
+}
+
+// the window's n walk records -> {out, lit, src, off}; op, lp and the offset history
+// advance past them.  Returns 0 or the status of the first failing sequence (uniform).
+#if HZ_GPU
+__device__
+#else
+static
+#endif
+inline int seq_lanes(Shared& ls, const SBits& b, uint32_t n, uint32_t rsz, uint32_t cap, uint32_t& op, uint32_t& lp,
+                     uint32_t& r0, uint32_t& r1, uint32_t& r2) {
+  const uint32_t aoff = (uint32_t)(((uintptr_t)b.in.p + b.lo) & 3u);
+  for (uint32_t c = 0; c < n; c += 64u) {
+#if HZ_GPU
+    const int lane = HZ_LANE_ID();
+    const uint32_t i = c + (uint32_t)lane;
+    const bool valid = i < n;
+    SeqLane d;
+    if (valid) {
+      uint32_t rec[4] = {ls.seq[i][0], ls.seq[i][1], ls.seq[i][2], ls.seq[i][3]};
+      d = seq_decode(rec, b, aoff);
+    } else {
+      d.ll = 0; d.ml = 0; d.f = rep_id();
+    }
+    RepFn F = d.f;
+    HZ_UNROLL
+    for (int o = 1; o < 64; o <<= 1) {
+      RepFn g;
+      g.src = __shfl_up(F.src, o, 64); g.v0 = __shfl_up(F.v0, o, 64);
+      g.v1 = __shfl_up(F.v1, o, 64); g.v2 = __shfl_up(F.v2, o, 64);
+      if (lane >= o) F = rep_compose(F, g);
+    }
+    const uint32_t off = rep_apply(F, 0u, r0, r1, r2);
+    const uint32_t tot = d.ll + d.ml;
+    const uint32_t ox = hz::wave_excl_scan(tot, lane), lx = hz::wave_excl_scan(d.ll, lane);
+    const uint32_t opi = op + ox, lpi = lp + lx;
+    const int code = !valid ? 0
+                     : d.ll > rsz - lpi ? zs::E_DATA
+                     : (uint64_t)opi + d.ml + (rsz - lpi) > cap ? zs::E_SIZE
+                     : off == 0u || (uint64_t)off > (uint64_t)opi + d.ll ? zs::E_DATA : 0;
+    const uint64_t bad = (uint64_t)__ballot(code != 0);
+    if (bad) return __builtin_amdgcn_readlane(code, (int)__builtin_ctzll(bad));
+    if (valid) {
+      ls.seq[i][SQ_OUT] = opi; ls.seq[i][SQ_LIT] = d.ll; ls.seq[i][SQ_SRC] = lpi; ls.seq[i][SQ_OFF] = off;
+    }
+    RepFn L;                                    // the whole chunk's composition (lane 63)
+    L.src = uni(__builtin_amdgcn_readlane(F.src, 63)); L.v0 = uni(__builtin_amdgcn_readlane(F.v0, 63));
+    L.v1 = uni(__builtin_amdgcn_readlane(F.v1, 63)); L.v2 = uni(__builtin_amdgcn_readlane(F.v2, 63));
+    const uint32_t n0 = rep_apply(L, 0u, r0, r1, r2), n1 = rep_apply(L, 1u, r0, r1, r2), n2 = rep_apply(L, 2u, r0, r1, r2);
+    r0 = uni(n0); r1 = uni(n1); r2 = uni(n2);
+    op = uni(op + (uint32_t)__builtin_amdgcn_readlane(ox + tot, 63));
+    lp = uni(lp + (uint32_t)__builtin_amdgcn_readlane(lx + d.ll, 63));
+#else
+    SeqLane d[64];
+    RepFn F[64];
+    for (int lane = 0; lane < 64; lane++) {
+      const uint32_t i = c + (uint32_t)lane;
+      if (i < n) d[lane] = seq_decode(ls.seq[i], b, aoff);
+      else { d[lane].ll = 0; d[lane].ml = 0; d[lane].f = rep_id(); }
+      F[lane] = d[lane].f;
+    }
+    for (int o = 1; o < 64; o <<= 1) {         // the same log-depth scan as the wavefront's
+      RepFn g[64];
+      for (int lane = 0; lane < 64; lane++) g[lane] = F[lane];
+      for (int lane = o; lane < 64; lane++) F[lane] = rep_compose(g[lane], g[lane - o]);
+    }
+    uint32_t ox = 0, lx = 0;
+    for (int lane = 0; lane < 64; lane++) {
+      const uint32_t i = c + (uint32_t)lane;
+      if (i >= n) break;
+      const uint32_t off = rep_apply(F[lane], 0u, r0, r1, r2);
+      const uint32_t opi = op + ox, lpi = lp + lx;
+      if (d[lane].ll > rsz - lpi) return zs::E_DATA;
+      if ((uint64_t)opi + d[lane].ml + (rsz - lpi) > cap) return zs::E_SIZE;
+      if (off == 0u || (uint64_t)off > (uint64_t)opi + d[lane].ll) return zs::E_DATA;
+      ls.seq[i][SQ_OUT] = opi; ls.seq[i][SQ_LIT] = d[lane].ll; ls.seq[i][SQ_SRC] = lpi; ls.seq[i][SQ_OFF] = off;
+      ox += d[lane].ll + d[lane].ml; lx += d[lane].ll;
+    }
+    const RepFn& L = F[63];
+    const uint32_t n0 = rep_apply(L, 0u, r0, r1, r2), n1 = rep_apply(L, 1u, r0, r1, r2), n2 = rep_apply(L, 2u, r0, r1, r2);
+    r0 = n0; r1 = n1; r2 = n2;
+    op += ox; lp += lx;
+#endif
+  }
+  return 0;
+}
+
+// repack a freshly built sequence table (sq_pack): every lane converts its own entries
+#if HZ_GPU
+__device__
+#else
+static
+#endif
+inline void sq_convert(zs::Fse* tab, uint32_t al, uint32_t which) {
+  WAVE_SYNC();
+  LANE_LOOP {
+    for (uint32_t u = (uint32_t)lane; u < (1u << al); u += 64u) {
+      const uint32_t w = sq_pack(tab[u], which);
+#if HZ_GPU
+      *(uint32_t*)(tab + u) = w;
+#else
+      memcpy(tab + u, &w, 4);
+#endif
+    }
+  }
+  WAVE_SYNC();
 }
 
 // one compressed block at input [at, at + n); output from op; returns the new op or < 0 (uniform)
@@ -316,10 +556,14 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     u = (int32_t)uni((uint32_t)zs::seq_table(t, t.ml, t.ml_al, (modes >> 2) & 3, in, at + q, n - q, 2, 52, 9));
     if (u < 0) return zs::E_DATA;
     q += (uint32_t)u;
+    // fresh tables (not mode 3, "repeat": those were repacked when built) -> packed words
+    if (((modes >> 6) & 3) != 3u) sq_convert(t.ll, uni(t.ll_al), 0u);
+    if (((modes >> 4) & 3) != 3u) sq_convert(t.of, uni(t.of_al), 1u);
+    if (((modes >> 2) & 3) != 3u) sq_convert(t.ml, uni(t.ml_al), 2u);
     t.have_seq = 1;
     WAVE_SYNC();
     if (n - q == 0 || ub8(in, at + n - 1) == 0) return zs::E_DATA;
-    b.in = in; b.lo = at + q; b.n = n - q; b.sb = -1; b.wbit = -1; b.win = 0;
+    b.in = in; b.lo = at + q; b.n = n - q; b.sb = SB_NONE; b.wbit = -1; b.win = 0;
     b.pos = 8 * (int32_t)(b.n - 1) + (int32_t)zs::hib(ub8(in, at + n - 1));
     const uint32_t lal = uni(t.ll_al), oal = uni(t.of_al), mal = uni(t.ml_al);
     const uint32_t v = sb_read(ls, b, lal + oal + mal);      // LL, OF, ML initial states
@@ -328,49 +572,55 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
   uint32_t k = 0;
   for (;;) {
     HZ_T(2);
-    // ---- decode up to NSEQ sequences (uniform, scalar) ----
     const uint32_t wb = op;
+    // ---- (1) the serial FSE walk (uniform): per sequence, one LDS dword from each table
+    // and four stage words; it records the three entries and the bit position of the
+    // sequence's extra bits, skips the extra bits and takes the next states ----
     uint32_t ns_w = 0;
-    while (k < nseq && ns_w < (uint32_t)NSEQ - 1u) {
-      const uint32_t ell = fse_word(t.ll[sll]), eof = fse_word(t.of[sof]), eml = fse_word(t.ml[sml]);
-      const uint32_t llc = ell & 255u, ofc = eof & 255u, mlc = eml & 255u;
-      if (llc > 35 || mlc > 52 || ofc > 31) return zs::E_DATA;
-      // extra bits: offset, then match length, then literal length
-      const uint32_t ofv = (1u << ofc) + sb_read(ls, b, ofc);
-      const uint32_t mlb = zs::ml_bits(mlc), llb = zs::ll_bits(llc);
-      const uint32_t vx = sb_read(ls, b, mlb + llb);
-      const uint32_t ml = zs::ml_base(mlc) + (vx >> llb);
-      const uint32_t ll = zs::ll_base(llc) + (vx & ((1u << llb) - 1u));
-      uint32_t off;
-      if (ofv > 3) {
-        off = ofv - 3;
-        rep2 = rep1; rep1 = rep0; rep0 = off;
-      } else {
-        const uint32_t idx = ofv - 1u + (ll == 0 ? 1u : 0u);
-        if (idx == 0) off = rep0;
-        else {
-          off = idx == 3 ? rep0 - 1u : idx == 1 ? rep1 : rep2;
-          if (idx != 1) rep2 = rep1;
-          rep1 = rep0; rep0 = off;
-        }
+    for (;;) {
+      // the walk's state is uniform; re-asserting it each sequence keeps the loop on the
+      // scalar unit (the enclosing loops' divergent lane work would otherwise make the
+      // compiler carry it in vector registers under exec masks)
+      k = uni(k); ns_w = uni(ns_w);
+      sll = uni(sll); sof = uni(sof); sml = uni(sml);
+      b.pos = (int32_t)uni((uint32_t)b.pos); b.sb = (int32_t)uni((uint32_t)b.sb);
+      if (!(k < nseq && ns_w < (uint32_t)NSEQ - 1u)) break;
+      int32_t P = b.pos - 8 * b.sb;                   // stage bit of the current position
+      if (P < 128 && b.sb > 0) {                      // the next 96 bits below P leave the stage
+        int32_t f = ((b.pos + 7) >> 3) - STG;
+        sb_stage(ls, b, f < 0 ? 0 : f);
+        P = b.pos - 8 * b.sb;
       }
-      if (k + 1 < nseq) {       // state updates: LL, then ML, then OF
-        const uint32_t nl = (ell >> 8) & 255u, nm = (eml >> 8) & 255u, no = (eof >> 8) & 255u;
-        const uint32_t vs = sb_read(ls, b, nl + nm + no);
-        sll = (ell >> 16) + (vs >> (nm + no));
-        sml = (eml >> 16) + ((vs >> no) & ((1u << nm) - 1u));
-        sof = (eof >> 16) + (vs & ((1u << no) - 1u));
-      }
-      if (ll > rsz - lp) return zs::E_DATA;
-      if ((uint64_t)op + ml + (rsz - lp) > cap) return zs::E_SIZE;
-      if (off == 0 || (uint64_t)off > (uint64_t)op + ll) return zs::E_DATA;
-      // every lane stores the same words: a lane-0 branch would make the loop divergent
-      // and push its uniform state into vector registers
-      ls.s_out[ns_w] = op; ls.s_lit[ns_w] = ll; ls.s_src[ns_w] = lp; ls.s_off[ns_w] = off;
+      int32_t j0 = (P - 96) >> 5;
+      j0 = j0 < 0 ? 0 : j0 > STG / 4 ? STG / 4 : j0;
+      const uint32_t eL = fse_word(t.ll, sll), eO = fse_word(t.of, sof), eM = fse_word(t.ml, sml);
+      const uint32_t w0 = uni(ls.stage[j0]), w1 = uni(ls.stage[j0 + 1]), w2 = uni(ls.stage[j0 + 2]),
+                     w3 = uni(ls.stage[j0 + 3]);
+      const uint32_t xb = sq_eb(eL) + sq_eb(eO) + sq_eb(eM);
+      const uint32_t nL = sq_nb(eL), nM = sq_nb(eM), nO = sq_nb(eO);
+      const uint32_t nsb = k + 1u < nseq ? nL + nM + nO : 0u;   // state updates: LL, ML, OF
+      int32_t r = P - (int32_t)(xb + nsb) - 32 * j0;            // the state bits in w0..w3
+      r = r < 0 ? 0 : r > 127 ? 127 : r;                      // (127 - nsb at most on valid input)
+      const uint64_t lo64 = (uint64_t)w0 | ((uint64_t)w1 << 32), hi64 = (uint64_t)w2 | ((uint64_t)w3 << 32);
+      const uint64_t f64 = r >= 64 ? hi64 >> (uint32_t)(r - 64) : r ? (lo64 >> (uint32_t)r) | (hi64 << (uint32_t)(64 - r)) : lo64;
+      const uint32_t fld = (uint32_t)f64 & hz::bmask(nsb);
+      ls.seq[ns_w][0] = eL; ls.seq[ns_w][1] = eO; ls.seq[ns_w][2] = eM; ls.seq[ns_w][3] = (uint32_t)b.pos;
+      sll = sq_base(eL) + (fld >> (nM + nO));
+      sml = sq_base(eM) + ((fld >> nO) & hz::bmask(nM));
+      sof = sq_base(eO) + (fld & hz::bmask(nO));
+      b.pos -= (int32_t)(xb + nsb);
       ns_w++;
-      op += ll + ml; lp += ll;
       k++;
     }
+    HZ_T(8);
+    WAVE_SYNC();
+    // ---- (2) the lanes: extra bits, lengths, repeat offsets and positions of the window's
+    // sequences, 64 at a time (the offset history is a prefix composition) ----
+    {
+      const int st = seq_lanes(ls, b, ns_w, rsz, cap, op, lp, rep0, rep1, rep2);
+      if (st) return st;
+    }
+    HZ_T(2);
     const int last = k >= nseq;
     if (last) {
       if (nseq > 0 && b.pos != 0) return zs::E_DATA;
@@ -379,7 +629,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       const uint32_t rest = rsz - lp;
       if ((uint64_t)op + rest > cap) return zs::E_SIZE;
       if (rest) {
-        LZ_LANE0_ZW { ls.s_out[ns_w] = op; ls.s_lit[ns_w] = rest; ls.s_src[ns_w] = lp; ls.s_off[ns_w] = 0; }
+        LZ_LANE0_ZW { ls.seq[ns_w][SQ_OUT] = op; ls.seq[ns_w][SQ_LIT] = rest; ls.seq[ns_w][SQ_SRC] = lp; ls.seq[ns_w][SQ_OFF] = 0; }
         ns_w++;
         op += rest; lp += rest;
       }

@@ -24,7 +24,7 @@ NAMES = ["other", "blk-hdr", "tables", "A", "A'", "repair", "valid+scan", "E", "
 
 
 LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
-ZSTD_NAMES = ["other", "lit-stream", "seq-decode", "res-walk", "huf-tree", "seq-tables", "res-load", "res-store"]
+ZSTD_NAMES = ["other", "lit-stream", "seq-walk", "res-walk", "huf-tree", "seq-tables", "res-load", "res-store", "seq-lanes"]
 
 
 def run(fmt, n, unique, tune=None):
