@@ -46,7 +46,7 @@
 #include "region.h"
 
 #ifndef HZ_ZSTD_WPE
-#define HZ_ZSTD_WPE 3      // zstd_kernel waves per SIMD the compiler must allow (VGPR budget)
+#define HZ_ZSTD_WPE 4      // zstd_kernel waves per SIMD the compiler must allow (VGPR budget)
 #endif
 #ifndef HZ2_WPE
 #define HZ2_WPE 4          // inflate2_kernel waves per SIMD the compiler must allow (VGPR budget)

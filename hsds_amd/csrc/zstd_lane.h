@@ -24,7 +24,7 @@ struct Tables {            // one per lane, in global memory
   Fse ll[512], of[256], ml[512];
   Fse hw[64];              // Huffman weights table (accuracy <= 6)
   Huf huf[1 << 11];
-  uint32_t ll_al, of_al, ml_al, have_seq, huf_bits, have_huf;
+  uint32_t ll_al, of_al, ml_al, have_seq, huf_bits, have_huf, huf_nw;
   uint32_t rep[3];
   int16_t norm[256];       // scratch for table descriptions
   uint16_t next[256];
@@ -34,7 +34,8 @@ constexpr size_t ZTAB_BYTES = (sizeof(Tables) + 255) & ~(size_t)255;
 
 constexpr int OK = 0, E_DATA = -2, E_TRUNC = -3, E_SIZE = -4, E_UNSUP = -5;
 
-HZ_HD uint32_t hib(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v | 1u); }
+// constexpr (host and device): also used to build the predefined tables at compile time
+constexpr uint32_t hib(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v | 1u); }
 
 // input bytes of the split (bounded)
 struct In { const uint8_t* p; uint32_t n; };
@@ -70,7 +71,8 @@ HZ_HD uint32_t bits_read(Bits& b, uint32_t k) {
 }
 
 // FSE table description (forward little-endian bits); returns bytes used or -1
-HZ_HD int64_t ncount(Tables& t, const In& in, uint32_t at, uint32_t n, uint32_t& maxsym, uint32_t& al,
+template <class TT>
+HZ_HD int64_t ncount(TT& t, const In& in, uint32_t at, uint32_t n, uint32_t& maxsym, uint32_t& al,
                      uint32_t maxal) {
   if (n < 1) return -1;
   uint64_t bp = 0;
@@ -122,7 +124,8 @@ HZ_HD int64_t ncount(Tables& t, const In& in, uint32_t at, uint32_t n, uint32_t&
   return (int64_t)((bp + 7) >> 3);
 }
 
-HZ_HD int build_fse(Tables& t, Fse* tab, uint32_t maxsym, uint32_t al) {
+template <class TT>
+HZ_HD int build_fse(TT& t, Fse* tab, uint32_t maxsym, uint32_t al) {
   const uint32_t size = 1u << al;
   int32_t high = (int32_t)size - 1;
   for (uint32_t s = 0; s <= maxsym; s++) {
@@ -147,7 +150,7 @@ HZ_HD int build_fse(Tables& t, Fse* tab, uint32_t maxsym, uint32_t al) {
 }
 
 // predefined distributions (RFC 8878 3.1.1.3.2.2) and code baselines
-HZ_HD int16_t def_norm(uint32_t which, uint32_t s) {
+constexpr int16_t def_norm(uint32_t which, uint32_t s) {
   // which: 0 LL (36 codes), 1 OF (29), 2 ML (53)
   if (which == 0) {
     const int16_t v[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1,
@@ -162,7 +165,7 @@ HZ_HD int16_t def_norm(uint32_t which, uint32_t s) {
 }
 // code -> baseline / extra bits (RFC 8878 3.1.1.3.2.1.1), from packed immediates: a
 // local table would be read from memory on every sequence
-HZ_HD uint32_t ll_bits(uint32_t c) {
+constexpr uint32_t ll_bits(uint32_t c) {
   if (c < 16) return 0;
   if (c >= 25) return c - 19;                                   // 25: 6 bits ... 35: 16 bits
   return (uint32_t)((0x433221111ull >> (4 * (c - 16))) & 15u);   // 16..24: 1 1 1 1 2 2 3 3 4
@@ -175,7 +178,7 @@ HZ_HD uint32_t ll_base(uint32_t c) {
                      40ull << 42 | 48ull << 48;
   return (uint32_t)((v >> (6 * (c - 16))) & 63u);
 }
-HZ_HD uint32_t ml_bits(uint32_t c) {
+constexpr uint32_t ml_bits(uint32_t c) {
   if (c < 32) return 0;
   if (c >= 43) return c - 36;                                   // 43: 7 bits ... 52: 16 bits
   // 32..42: 1 1 1 1 2 2 3 3 4 4 5, 3 bits each
@@ -196,7 +199,8 @@ HZ_HD uint32_t ml_base(uint32_t c) {
 }
 
 // LL / OF / ML table: mode 0 predefined, 1 RLE, 2 FSE description, 3 repeat
-HZ_HD int64_t seq_table(Tables& t, Fse* tab, uint32_t& al, uint32_t mode, const In& in, uint32_t at, uint32_t n,
+template <class TT>
+HZ_HD int64_t seq_table(TT& t, Fse* tab, uint32_t& al, uint32_t mode, const In& in, uint32_t at, uint32_t n,
                         uint32_t which, uint32_t maxsym, uint32_t maxal) {
   if (mode == 0) {
     const uint32_t defmax = which == 0 ? 35u : which == 1 ? 28u : 52u;
@@ -220,8 +224,12 @@ HZ_HD int64_t seq_table(Tables& t, Fse* tab, uint32_t& al, uint32_t mode, const 
   return t.have_seq ? 0 : -1;
 }
 
+template <class TT>
+HZ_HD void huf_fill(TT& t, uint32_t nw, uint32_t maxb);
+
 // Huffman tree description at `at`; returns bytes used or -1
-HZ_HD int64_t huf_tree(Tables& t, const In& in, uint32_t at, uint32_t n) {
+template <class TT>
+HZ_HD int64_t huf_tree(TT& t, const In& in, uint32_t at, uint32_t n) {
   if (n < 1) return -1;
   uint32_t nw = 0;
   int64_t used;
@@ -268,6 +276,15 @@ HZ_HD int64_t huf_tree(Tables& t, const In& in, uint32_t at, uint32_t n) {
   if (rest & (rest - 1)) return -1;
   t.w[nw++] = (uint8_t)(hib(rest) + 1);
   if (maxb > 11) return -1;
+  t.huf_nw = nw;
+  huf_fill(t, nw, maxb);
+  return used;
+}
+
+// the decode table of weights w[0, nw) (max code length maxb): entries of symbol i fill
+// 2^(w-1) consecutive slots in weight order
+template <class TT>
+HZ_HD void huf_fill(TT& t, uint32_t nw, uint32_t maxb) {
   uint32_t start[13];
   {
     uint32_t rank[13];
@@ -285,13 +302,13 @@ HZ_HD int64_t huf_tree(Tables& t, const In& in, uint32_t at, uint32_t n) {
   }
   t.huf_bits = maxb;
   t.have_huf = 1;
-  return used;
 }
 
 // one Huffman literal stream (backward bitstream of n bytes at `at`) -> cnt symbols.
 // The bits come through a 64-bit register window refilled with two aligned dword
 // loads, so a refill costs one memory latency per ~4 symbols.
-HZ_HD int huf_stream(const Tables& t, const In& in, uint32_t at, uint32_t n, hz_gu8* out, uint32_t cnt) {
+template <class TT>
+HZ_HD int huf_stream(const TT& t, const In& in, uint32_t at, uint32_t n, hz_gu8* out, uint32_t cnt) {
   if (n == 0 || at + n > in.n) return -1;
   const uint32_t last = b8(in, at + n - 1);
   if (!last) return -1;

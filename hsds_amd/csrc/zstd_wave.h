@@ -34,11 +34,31 @@ constexpr int32_t SB_NONE = -(1 << 30);
 // (packed entries, below); the lane pass turns it into {out, lit, src, off}.
 enum : uint32_t { SQ_OUT = 0, SQ_LIT = 1, SQ_SRC = 2, SQ_OFF = 3 };
 
+// The wavefront's tables.  Same members as zs::Tables (the builders are shared), but the
+// Huffman table, the table-description scratch and the sequence window share one LDS
+// region: the Huffman table is dead once the literals are decoded (a treeless literals
+// section rebuilds it from the kept weights), the scratch once the tables are built.
+// 9.8 KB of LDS: four one-wavefront workgroups per SIMD.
+struct WTables {
+  zs::Fse ll[512], of[256], ml[512];
+  zs::Fse hw[64];                          // Huffman weights table (accuracy <= 6)
+  uint32_t ll_al, of_al, ml_al, have_seq, huf_bits, have_huf, huf_nw;
+  uint32_t rep[3];
+  uint8_t w[256];                          // Huffman weights (kept for treeless sections)
+  union {
+    zs::Huf huf[1 << 11];                  // the literals section
+    struct { int16_t norm[256]; uint16_t next[256]; };        // table descriptions
+    struct {                               // the sequences section
+      alignas(16) uint32_t seq[NSEQ + 1][4];   // out: output offset; lit: literal bytes; src:
+                                               // literal-area index of the first literal; off:
+                                               // match distance (0: none)
+      uint32_t stage[STG / 4 + 4];
+    };
+  };
+};
+
 struct Shared {
-  zs::Tables t;
-  uint32_t seq[NSEQ + 1][4];              // out: output offset; lit: literal bytes; src: literal-area
-                                          // index of the first literal; off: match distance (0: none)
-  uint32_t stage[STG / 4 + 4];
+  WTables t;
   int32_t u_err;
 };
 
@@ -67,9 +87,46 @@ HZ_HD uint32_t sq_nb(uint32_t e) { return (e >> 16) & 15u; }
 HZ_HD uint32_t sq_eb(uint32_t e) { return (e >> 20) & 31u; }
 HZ_HD uint32_t sq_code(uint32_t e) { return e >> 25; }
 
+// The predefined distributions' tables (RFC 8878 3.1.1.3.2.2), built at compile time in
+// the packed form and copied into LDS when a block selects them: built at run time, the
+// compiler folds the whole construction into constants that then occupy vector
+// registers for the kernel's lifetime.
+struct PreTab { uint32_t e[64]; };
+constexpr PreTab pre_build(uint32_t which) {
+  PreTab r{};
+  const uint32_t al = which == 1u ? 5u : 6u, size = 1u << al, maxsym = which == 0u ? 35u : which == 1u ? 28u : 52u;
+  uint8_t sym[64] = {};
+  uint32_t next[53] = {};
+  int32_t high = (int32_t)size - 1;
+  for (uint32_t s = 0; s <= maxsym; s++) {
+    const int16_t nv = zs::def_norm(which, s);
+    if (nv == -1) { sym[high--] = (uint8_t)s; next[s] = 1u; }
+    else next[s] = (uint32_t)nv;
+  }
+  const uint32_t step = (size >> 1) + (size >> 3) + 3u, mask = size - 1u;
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s <= maxsym; s++)
+    for (int32_t i = 0; i < zs::def_norm(which, s); i++) {
+      sym[pos] = (uint8_t)s;
+      do pos = (pos + step) & mask; while ((int32_t)pos > high);
+    }
+  for (uint32_t u = 0; u < size; u++) {
+    const uint32_t c = sym[u], ns = next[c]++;
+    const uint32_t nb = al - zs::hib(ns), base = (ns << nb) - size;
+    const uint32_t eb = which == 0u ? zs::ll_bits(c) : which == 1u ? c : zs::ml_bits(c);
+    r.e[u] = base | (nb << 16) | (eb << 20) | (c << 25);
+  }
+  return r;
+}
+#if HZ_GPU
+__constant__ PreTab zw_pre[3] = {pre_build(0u), pre_build(1u), pre_build(2u)};
+#else
+static constexpr PreTab zw_pre[3] = {pre_build(0u), pre_build(1u), pre_build(2u)};
+#endif
+
 HZ_HD uint32_t fse_word(const zs::Fse* tab, uint32_t i) {
 #if HZ_GPU
-  return uni(((const uint32_t*)tab)[i]);     // one LDS dword read
+  return ((const uint32_t*)tab)[i];          // one LDS dword read (callers make it uniform)
 #else
   uint32_t v;
   memcpy(&v, tab + i, 4);
@@ -135,7 +192,7 @@ inline void sb_stage(Shared& ls, SBits& b, int32_t first) {
     HZ_UNROLL
     for (uint32_t j = 0; j < NJ; j++) {
       const uint32_t k = j * 64u + (uint32_t)lane;
-      if (k < NWD) ls.stage[k] = v[j];
+      if (k < NWD) ls.t.stage[k] = v[j];
     }
   }
   WAVE_SYNC();
@@ -155,8 +212,8 @@ inline void sb_refill(Shared& ls, SBits& b) {
     sb_stage(ls, b, f < 0 ? 0 : f);
   }
   const uint32_t r = (uint32_t)(by - b.sb), wi = r >> 2, sh = (r & 3u) * 8u;
-  const uint64_t lo = (uint64_t)uni(ls.stage[wi]) | ((uint64_t)uni(ls.stage[wi + 1]) << 32);
-  const uint64_t hi = uni(ls.stage[wi + 2]);
+  const uint64_t lo = (uint64_t)uni(ls.t.stage[wi]) | ((uint64_t)uni(ls.t.stage[wi + 1]) << 32);
+  const uint64_t hi = uni(ls.t.stage[wi + 2]);
   b.win = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
   b.wbit = (int32_t)uni((uint32_t)(by * 8));
 }
@@ -184,18 +241,27 @@ HZ_HD uint32_t find_seq(const Shared& ls, uint32_t hi, uint32_t p) {
   uint32_t lo = 0;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1u) >> 1;
-    if (ls.seq[mid][SQ_OUT] <= p) lo = mid; else hi = mid - 1u;
+    if (ls.t.seq[mid][SQ_OUT] <= p) lo = mid; else hi = mid - 1u;
   }
   return lo;
 }
+// the same for a match source p below sequence u's start: sources are mostly near, so
+// the two sequences below u are tried before the binary search
+HZ_HD uint32_t find_back(const Shared& ls, uint32_t u, uint32_t p) {
+  if (ls.t.seq[u][SQ_OUT] <= p) return u;
+  if (u >= 1u && ls.t.seq[u - 1u][SQ_OUT] <= p) return u - 1u;
+  if (u >= 2u && ls.t.seq[u - 2u][SQ_OUT] <= p) return u - 2u;
+  return u >= 3u ? find_seq(ls, u - 3u, p) : 0u;
+}
 
-// resolve and store the window's output [wb, we) (nseq sequences in the LDS table)
+// resolve and store the window's output [wb, we) (nseq sequences in the LDS table);
+// literals are at dst + lbase
 #if HZ_GPU
 __device__
 #else
 static
 #endif
-inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_t wb, uint32_t we, uint32_t nseq,
+inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, uint32_t lbase, uint32_t wb, uint32_t we, uint32_t nseq,
                     HzProf* prof) {
   (void)prof;
   const uint32_t g0 = (wb + dmis) >> 4, g1 = (we + dmis + 15u) >> 4;
@@ -213,31 +279,55 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, hz_gu8* lit, uint32_
       if (g < g1) {
         const uint32_t a0 = g * 16u;
         const uint32_t pb = a0 > wb + dmis ? a0 - dmis : wb;
+        // the lane's current sequence t, its record in registers
         uint32_t t = find_seq(ls, nseq - 1u, pb);
-        uint32_t t_end = t + 1u < nseq ? ls.seq[t + 1u][SQ_OUT] : we;
-        hz_gu8* sp[16];
+        uint32_t r_out = ls.t.seq[t][SQ_OUT], r_lit = ls.t.seq[t][SQ_LIT], r_src = ls.t.seq[t][SQ_SRC], r_off = ls.t.seq[t][SQ_OFF];
+        uint32_t t_end = t + 1u < nseq ? ls.t.seq[t + 1u][SQ_OUT] : we;
+        uint32_t mq = ~0u;            // the previous byte's match source (same sequence), else ~0
+        uint32_t so[16];              // source of each byte, from dst
         HZ_UNROLL
         for (uint32_t k = 0; k < 16u; k++) {
           const uint32_t ak = a0 + k;
-          sp[k] = dst;
+          so[k] = 0;
           if (ak < wb + dmis || ak >= we + dmis) continue;
           const uint32_t p = ak - dmis;
-          while (p >= t_end) { t++; t_end = t + 1u < nseq ? ls.seq[t + 1u][SQ_OUT] : we; }
-          uint32_t q = p, u = t;
-          for (;;) {
-            const uint32_t ub = ls.seq[u][SQ_OUT], rel = q - ub, nl = ls.seq[u][SQ_LIT];
-            if (rel < nl) { sp[k] = lit + ls.seq[u][SQ_SRC] + rel; break; }
-            const uint32_t m = ub + nl, d = ls.seq[u][SQ_OFF], kk = q - m;
-            const uint32_t q2 = m - d + (kk < d ? kk : kk % d);
-            if (q2 < it_lo) { sp[k] = dst + q2; break; }     // final output (earlier window / iteration)
-            u = find_seq(ls, u, q2);
-            q = q2;
+          if (p >= t_end) {
+            do { t++; t_end = t + 1u < nseq ? ls.t.seq[t + 1u][SQ_OUT] : we; } while (p >= t_end);
+            r_out = ls.t.seq[t][SQ_OUT]; r_lit = ls.t.seq[t][SQ_LIT]; r_src = ls.t.seq[t][SQ_SRC]; r_off = ls.t.seq[t][SQ_OFF];
+            mq = ~0u;
+          }
+          const uint32_t rel = p - r_out;
+          if (rel < r_lit) {
+            so[k] = lbase + r_src + rel;
+            mq = ~0u;
+          } else {
+            // match byte: the periodic extension m - d + (k mod d), stepped from the
+            // previous byte's source when there is one (no division)
+            const uint32_t m = r_out + r_lit, kk = p - m;
+            const uint32_t q2 = mq != ~0u ? (mq + 1u == m ? m - r_off : mq + 1u)
+                                          : m - r_off + (kk < r_off ? kk : kk % r_off);
+            mq = q2;
+            if (q2 < it_lo) {
+              so[k] = q2;                 // final output (an earlier window / iteration)
+            } else {
+              // a source inside this iteration: follow the chain through the table
+              uint32_t q = q2, u = find_back(ls, t, q2);
+              for (;;) {
+                const uint32_t ub = ls.t.seq[u][SQ_OUT], nl = ls.t.seq[u][SQ_LIT], rl = q - ub;
+                if (rl < nl) { so[k] = lbase + ls.t.seq[u][SQ_SRC] + rl; break; }
+                const uint32_t mu = ub + nl, d = ls.t.seq[u][SQ_OFF], ku = q - mu;
+                const uint32_t q3 = mu - d + (ku < d ? ku : ku % d);
+                if (q3 < it_lo) { so[k] = q3; break; }
+                u = find_back(ls, u, q3);
+                q = q3;
+              }
+            }
           }
           hv |= 1u << k;
         }
         HZ_T(6);
         HZ_UNROLL
-        for (uint32_t k = 0; k < 16u; k++) ww[k >> 2] |= (uint32_t)*sp[k] << (8u * (k & 3u));
+        for (uint32_t k = 0; k < 16u; k++) ww[k >> 2] |= (uint32_t)dst[so[k]] << (8u * (k & 3u));
       }
       LV(have) = hv;
       LV(w0) = ww[0]; LV(w1) = ww[1]; LV(w2) = ww[2]; LV(w3) = ww[3];
@@ -278,24 +368,27 @@ HZ_HD RepFn rep_step(uint32_t ofv, uint32_t ll) {
   if (idx == 2u) return RepFn{2u | 0u << 2 | 1u << 4, 0u, 0u, 0u};            // R2 to the front
   return RepFn{0u | 0u << 2 | 1u << 4, 0xffffffffu, 0u, 0u};                  // R0 - 1 pushed
 }
-HZ_HD uint32_t rep_sel(const RepFn& f, uint32_t s) { return s == 0u ? f.v0 : s == 1u ? f.v1 : f.v2; }
+// slot s of f's values, by masks (a select chain on the index becomes a scratch array)
+HZ_HD uint32_t rep_sel(const RepFn& f, uint32_t s) {
+  return (f.v0 & (0u - (uint32_t)(s == 0u))) | (f.v1 & (0u - (uint32_t)(s == 1u))) | (f.v2 & (0u - (uint32_t)(s == 2u)));
+}
 // f after g
 HZ_HD RepFn rep_compose(const RepFn& f, const RepFn& g) {
+  const uint32_t f0 = f.src & 3u, f1 = (f.src >> 2) & 3u, f2 = (f.src >> 4) & 3u;
+  const uint32_t g0 = f0 == 3u ? 3u : (g.src >> (2u * f0)) & 3u;
+  const uint32_t g1 = f1 == 3u ? 3u : (g.src >> (2u * f1)) & 3u;
+  const uint32_t g2 = f2 == 3u ? 3u : (g.src >> (2u * f2)) & 3u;
   RepFn h;
-  uint32_t src = 0, hv[3];
-  HZ_UNROLL
-  for (uint32_t s = 0; s < 3u; s++) {
-    const uint32_t fs = (f.src >> (2u * s)) & 3u;
-    const uint32_t gs = fs == 3u ? 3u : (g.src >> (2u * fs)) & 3u;
-    hv[s] = fs == 3u ? rep_sel(f, s) : rep_sel(g, fs) + rep_sel(f, s);
-    src |= gs << (2u * s);
-  }
-  h.src = src; h.v0 = hv[0]; h.v1 = hv[1]; h.v2 = hv[2];
+  h.src = g0 | (g1 << 2) | (g2 << 4);
+  h.v0 = f.v0 + (f0 == 3u ? 0u : rep_sel(g, f0));
+  h.v1 = f.v1 + (f1 == 3u ? 0u : rep_sel(g, f1));
+  h.v2 = f.v2 + (f2 == 3u ? 0u : rep_sel(g, f2));
   return h;
 }
 HZ_HD uint32_t rep_apply(const RepFn& f, uint32_t s, uint32_t r0, uint32_t r1, uint32_t r2) {
   const uint32_t fs = (f.src >> (2u * s)) & 3u;
-  return (fs == 3u ? 0u : fs == 0u ? r0 : fs == 1u ? r1 : r2) + rep_sel(f, s);
+  const uint32_t rv = (r0 & (0u - (uint32_t)(fs == 0u))) | (r1 & (0u - (uint32_t)(fs == 1u))) | (r2 & (0u - (uint32_t)(fs == 2u)));
+  return rv + rep_sel(f, s);
 }
 
 // aligned dword j of the sequence stream (stream byte x is in dword (x + aoff) >> 2);
@@ -359,7 +452,7 @@ inline int seq_lanes(Shared& ls, const SBits& b, uint32_t n, uint32_t rsz, uint3
     const bool valid = i < n;
     SeqLane d;
     if (valid) {
-      uint32_t rec[4] = {ls.seq[i][0], ls.seq[i][1], ls.seq[i][2], ls.seq[i][3]};
+      uint32_t rec[4] = {ls.t.seq[i][0], ls.t.seq[i][1], ls.t.seq[i][2], ls.t.seq[i][3]};
       d = seq_decode(rec, b, aoff);
     } else {
       d.ll = 0; d.ml = 0; d.f = rep_id();
@@ -383,7 +476,7 @@ inline int seq_lanes(Shared& ls, const SBits& b, uint32_t n, uint32_t rsz, uint3
     const uint64_t bad = (uint64_t)__ballot(code != 0);
     if (bad) return __builtin_amdgcn_readlane(code, (int)__builtin_ctzll(bad));
     if (valid) {
-      ls.seq[i][SQ_OUT] = opi; ls.seq[i][SQ_LIT] = d.ll; ls.seq[i][SQ_SRC] = lpi; ls.seq[i][SQ_OFF] = off;
+      ls.t.seq[i][SQ_OUT] = opi; ls.t.seq[i][SQ_LIT] = d.ll; ls.t.seq[i][SQ_SRC] = lpi; ls.t.seq[i][SQ_OFF] = off;
     }
     RepFn L;                                    // the whole chunk's composition (lane 63)
     L.src = uni(__builtin_amdgcn_readlane(F.src, 63)); L.v0 = uni(__builtin_amdgcn_readlane(F.v0, 63));
@@ -397,7 +490,7 @@ inline int seq_lanes(Shared& ls, const SBits& b, uint32_t n, uint32_t rsz, uint3
     RepFn F[64];
     for (int lane = 0; lane < 64; lane++) {
       const uint32_t i = c + (uint32_t)lane;
-      if (i < n) d[lane] = seq_decode(ls.seq[i], b, aoff);
+      if (i < n) d[lane] = seq_decode(ls.t.seq[i], b, aoff);
       else { d[lane].ll = 0; d[lane].ml = 0; d[lane].f = rep_id(); }
       F[lane] = d[lane].f;
     }
@@ -415,7 +508,7 @@ inline int seq_lanes(Shared& ls, const SBits& b, uint32_t n, uint32_t rsz, uint3
       if (d[lane].ll > rsz - lpi) return zs::E_DATA;
       if ((uint64_t)opi + d[lane].ml + (rsz - lpi) > cap) return zs::E_SIZE;
       if (off == 0u || (uint64_t)off > (uint64_t)opi + d[lane].ll) return zs::E_DATA;
-      ls.seq[i][SQ_OUT] = opi; ls.seq[i][SQ_LIT] = d[lane].ll; ls.seq[i][SQ_SRC] = lpi; ls.seq[i][SQ_OFF] = off;
+      ls.t.seq[i][SQ_OUT] = opi; ls.t.seq[i][SQ_LIT] = d[lane].ll; ls.t.seq[i][SQ_SRC] = lpi; ls.t.seq[i][SQ_OFF] = off;
       ox += d[lane].ll + d[lane].ml; lx += d[lane].ll;
     }
     const RepFn& L = F[63];
@@ -448,6 +541,40 @@ inline void sq_convert(zs::Fse* tab, uint32_t al, uint32_t which) {
   WAVE_SYNC();
 }
 
+// one sequence table of the block header: bytes used or < 0 (uniform)
+#if HZ_GPU
+__device__
+#else
+static
+#endif
+inline int64_t seq_table_w(Shared& ls, zs::Fse* tab, uint32_t& al, uint32_t mode, const zs::In& in, uint32_t at,
+                           uint32_t n, uint32_t which, uint32_t maxsym, uint32_t maxal) {
+  WTables& t = ls.t;
+  if (mode == 0u) {
+    WAVE_SYNC();
+    LANE_LOOP {
+      const uint32_t size = which == 1u ? 32u : 64u;
+      if ((uint32_t)lane < size) {
+        const uint32_t w = zw_pre[which].e[lane];
+#if HZ_GPU
+        *(uint32_t*)(tab + lane) = w;
+#else
+        memcpy(tab + lane, &w, 4);
+#endif
+      }
+    }
+    WAVE_SYNC();
+    LZ_LANE0_ZW { al = which == 1u ? 5u : 6u; }
+    WAVE_SYNC();
+    return 0;
+  }
+  WAVE_SYNC();
+  const int64_t u = (int32_t)uni((uint32_t)zs::seq_table(t, tab, al, mode, in, at, n, which, maxsym, maxal));
+  if (u < 0) return u;
+  if (mode != 3u) sq_convert(tab, uni(al), which);
+  return u;
+}
+
 // one compressed block at input [at, at + n); output from op; returns the new op or < 0 (uniform)
 #if HZ_GPU
 __device__
@@ -457,7 +584,7 @@ static
 inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_gu8* dst, uint32_t dmis, uint32_t op,
                      uint32_t cap, HzProf* prof) {
   (void)prof;
-  zs::Tables& t = ls.t;
+  WTables& t = ls.t;
   HZ_T(1);
   if (n < 1) return zs::E_DATA;
   const uint32_t h0 = ub8(in, at), lt = h0 & 3u, sf = (h0 >> 2) & 3u;
@@ -498,8 +625,13 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       tsz = (int64_t)(int32_t)uni((uint32_t)zs::huf_tree(t, in, at + q, csz));
       WAVE_SYNC();
       if (tsz < 0) return zs::E_DATA;
-    } else if (!uni(t.have_huf)) {
-      return zs::E_DATA;
+    } else {
+      // treeless: the previous table, rebuilt from its weights (the sequences section
+      // reused its LDS)
+      if (!uni(t.have_huf)) return zs::E_DATA;
+      WAVE_SYNC();
+      zs::huf_fill(t, uni(t.huf_nw), uni(t.huf_bits));
+      WAVE_SYNC();
     }
     const uint32_t s0 = at + q + (uint32_t)tsz, ssz = csz - (uint32_t)tsz;
     HZ_T(1);
@@ -530,6 +662,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     q += csz;
   }
   WAVE_SYNC_GLOBAL();         // literals visible to every lane
+  q = uni(q);
   // ---- sequences ----
   if (q >= n) return zs::E_TRUNC;
   uint32_t nseq = ub8(in, at + q++);
@@ -547,19 +680,18 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     if (modes & 3) return zs::E_DATA;
     HZ_T(5);
     WAVE_SYNC();
-    int64_t u = (int32_t)uni((uint32_t)zs::seq_table(t, t.ll, t.ll_al, (modes >> 6) & 3, in, at + q, n - q, 0, 35, 9));
-    if (u < 0) return zs::E_DATA;
-    q += (uint32_t)u;
-    u = (int32_t)uni((uint32_t)zs::seq_table(t, t.of, t.of_al, (modes >> 4) & 3, in, at + q, n - q, 1, 31, 8));
-    if (u < 0) return zs::E_DATA;
-    q += (uint32_t)u;
-    u = (int32_t)uni((uint32_t)zs::seq_table(t, t.ml, t.ml_al, (modes >> 2) & 3, in, at + q, n - q, 2, 52, 9));
-    if (u < 0) return zs::E_DATA;
-    q += (uint32_t)u;
-    // fresh tables (not mode 3, "repeat": those were repacked when built) -> packed words
-    if (((modes >> 6) & 3) != 3u) sq_convert(t.ll, uni(t.ll_al), 0u);
-    if (((modes >> 4) & 3) != 3u) sq_convert(t.of, uni(t.of_al), 1u);
-    if (((modes >> 2) & 3) != 3u) sq_convert(t.ml, uni(t.ml_al), 2u);
+    // per table: mode 0 copies the compile-time predefined table; modes 1 (RLE) and 2
+    // (FSE description) build it and repack it; mode 3 (repeat) keeps the packed table
+    const int64_t ul = seq_table_w(ls, t.ll, t.ll_al, (modes >> 6) & 3u, in, at + q, n - q, 0u, 35u, 9u);
+    if (ul < 0) return zs::E_DATA;
+    q += (uint32_t)ul;
+    const int64_t uo = seq_table_w(ls, t.of, t.of_al, (modes >> 4) & 3u, in, at + q, n - q, 1u, 31u, 8u);
+    if (uo < 0) return zs::E_DATA;
+    q += (uint32_t)uo;
+    const int64_t um = seq_table_w(ls, t.ml, t.ml_al, (modes >> 2) & 3u, in, at + q, n - q, 2u, 52u, 9u);
+    if (um < 0) return zs::E_DATA;
+    q += (uint32_t)um;
+    q = uni(q);
     t.have_seq = 1;
     WAVE_SYNC();
     if (n - q == 0 || ub8(in, at + n - 1) == 0) return zs::E_DATA;
@@ -572,6 +704,8 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
   uint32_t k = 0;
   for (;;) {
     HZ_T(2);
+    op = uni(op); lp = uni(lp); k = uni(k);
+    rep0 = uni(rep0); rep1 = uni(rep1); rep2 = uni(rep2);
     const uint32_t wb = op;
     // ---- (1) the serial FSE walk (uniform): per sequence, one LDS dword from each table
     // and four stage words; it records the three entries and the bit position of the
@@ -593,9 +727,11 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       }
       int32_t j0 = (P - 96) >> 5;
       j0 = j0 < 0 ? 0 : j0 > STG / 4 ? STG / 4 : j0;
-      const uint32_t eL = fse_word(t.ll, sll), eO = fse_word(t.of, sof), eM = fse_word(t.ml, sml);
-      const uint32_t w0 = uni(ls.stage[j0]), w1 = uni(ls.stage[j0 + 1]), w2 = uni(ls.stage[j0 + 2]),
-                     w3 = uni(ls.stage[j0 + 3]);
+      // the seven LDS reads of a sequence are issued together, then moved to scalars
+      uint32_t eL = fse_word(t.ll, sll), eO = fse_word(t.of, sof), eM = fse_word(t.ml, sml);
+      uint32_t w0 = ls.t.stage[j0], w1 = ls.t.stage[j0 + 1], w2 = ls.t.stage[j0 + 2], w3 = ls.t.stage[j0 + 3];
+      w0 = uni(w0); w1 = uni(w1); w2 = uni(w2); w3 = uni(w3);
+      eL = uni(eL); eO = uni(eO); eM = uni(eM);
       const uint32_t xb = sq_eb(eL) + sq_eb(eO) + sq_eb(eM);
       const uint32_t nL = sq_nb(eL), nM = sq_nb(eM), nO = sq_nb(eO);
       const uint32_t nsb = k + 1u < nseq ? nL + nM + nO : 0u;   // state updates: LL, ML, OF
@@ -604,7 +740,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       const uint64_t lo64 = (uint64_t)w0 | ((uint64_t)w1 << 32), hi64 = (uint64_t)w2 | ((uint64_t)w3 << 32);
       const uint64_t f64 = r >= 64 ? hi64 >> (uint32_t)(r - 64) : r ? (lo64 >> (uint32_t)r) | (hi64 << (uint32_t)(64 - r)) : lo64;
       const uint32_t fld = (uint32_t)f64 & hz::bmask(nsb);
-      ls.seq[ns_w][0] = eL; ls.seq[ns_w][1] = eO; ls.seq[ns_w][2] = eM; ls.seq[ns_w][3] = (uint32_t)b.pos;
+      ls.t.seq[ns_w][0] = eL; ls.t.seq[ns_w][1] = eO; ls.t.seq[ns_w][2] = eM; ls.t.seq[ns_w][3] = (uint32_t)b.pos;
       sll = sq_base(eL) + (fld >> (nM + nO));
       sml = sq_base(eM) + ((fld >> nO) & hz::bmask(nM));
       sof = sq_base(eO) + (fld & hz::bmask(nO));
@@ -629,14 +765,14 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       const uint32_t rest = rsz - lp;
       if ((uint64_t)op + rest > cap) return zs::E_SIZE;
       if (rest) {
-        LZ_LANE0_ZW { ls.seq[ns_w][SQ_OUT] = op; ls.seq[ns_w][SQ_LIT] = rest; ls.seq[ns_w][SQ_SRC] = lp; ls.seq[ns_w][SQ_OFF] = 0; }
+        LZ_LANE0_ZW { ls.t.seq[ns_w][SQ_OUT] = op; ls.t.seq[ns_w][SQ_LIT] = rest; ls.t.seq[ns_w][SQ_SRC] = lp; ls.t.seq[ns_w][SQ_OFF] = 0; }
         ns_w++;
         op += rest; lp += rest;
       }
     }
     WAVE_SYNC();
     HZ_T(3);
-    if (ns_w) resolve(ls, dst, dmis, lit, wb, op, ns_w, prof);
+    if (ns_w) resolve(ls, dst, dmis, lbase, wb, op, ns_w, prof);
     if (last) break;
   }
   HZ_T(0);
@@ -653,7 +789,7 @@ inline int frame(Shared& ls, const uint8_t* src, uint32_t n, uint8_t* dstp, uint
   zs::In in = {src, n};
   hz_gu8* dst = HZ_GLOBAL(hz_gu8*, dstp);
   const uint32_t dmis = (uint32_t)(((uintptr_t)dstp) & 3u);
-  zs::Tables& t = ls.t;
+  WTables& t = ls.t;
   if (n < 5) return zs::E_TRUNC;
   if ((ub8(in, 0) | ub8(in, 1) << 8 | ub8(in, 2) << 16 | ub8(in, 3) << 24) != 0xFD2FB528u) return zs::E_DATA;
   const uint32_t fhd = ub8(in, 4);
@@ -678,6 +814,9 @@ inline int frame(Shared& ls, const uint8_t* src, uint32_t n, uint8_t* dstp, uint
   WAVE_SYNC();
   uint32_t op = 0;
   for (;;) {
+    // the frame walk is uniform: re-assert it at each block (a lane loop's exit value can
+    // otherwise make the compiler treat the loop-carried state as divergent)
+    q = uni(q); op = uni(op);
     if (q + 3 > n) return zs::E_TRUNC;
     const uint32_t bh = ub8(in, q) | (ub8(in, q + 1) << 8) | (ub8(in, q + 2) << 16);
     q += 3;
