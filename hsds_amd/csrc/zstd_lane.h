@@ -305,8 +305,9 @@ HZ_HD void huf_fill(TT& t, uint32_t nw, uint32_t maxb) {
 }
 
 // one Huffman literal stream (backward bitstream of n bytes at `at`) -> cnt symbols.
-// The bits come through a 64-bit register window refilled with two aligned dword
-// loads, so a refill costs one memory latency per ~4 symbols.
+// The bits come from four aligned dwords held in registers (W0 the highest); when the
+// top one is used up the others move up and the next lower dword is loaded, three
+// dwords (~10 symbols) before it is needed, so the loads' latency is hidden.
 template <class TT>
 HZ_HD int huf_stream(const TT& t, const In& in, uint32_t at, uint32_t n, hz_gu8* out, uint32_t cnt) {
   if (n == 0 || at + n > in.n) return -1;
@@ -314,33 +315,34 @@ HZ_HD int huf_stream(const TT& t, const In& in, uint32_t at, uint32_t n, hz_gu8*
   if (!last) return -1;
   const uint32_t a = (uint32_t)(((uintptr_t)in.p + at) & 3u);
   hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, in.p + at - a);     // stream byte i is base[a + i]
-  int64_t pos = 8 * (int64_t)(n - 1) + hib(last);          // bits left
-  int64_t wlo = 0;                                         // window holds stream bits [wlo, wlo + 64)
-  bool loaded = false, at_start = false;                   // at_start: the window reaches bit 0
-  uint64_t w = 0;
+  // positions in base bits (stream bit s is base bit s + 8a); bits below the stream
+  // start read as 0.  Dword k > 0 lies wholly in the stream (up to the top dword, whose
+  // bytes above the stream are never peeked): its load is unconditional, so its use --
+  // three dwords later -- is where the wait lands.
+  auto dw = [&](int32_t k) -> uint32_t {
+    if (k > 0) return *(hz_gcu32*)(base + 4 * k);
+    if (k < 0) return 0u;
+    return *(hz_gcu32*)base & ~hz::bmask(8u * a);
+  };
+  int32_t pos = 8 * (int32_t)(n - 1) + (int32_t)hib(last) + 8 * (int32_t)a;   // bits left, exclusive top
+  int32_t top = (pos - 1) >> 5;                            // the dword holding bit pos - 1 (W0)
+  uint32_t W0 = dw(top), W1 = dw(top - 1), W2 = dw(top - 2), W3 = dw(top - 3);
   const uint32_t hb = t.huf_bits;
-  const uint64_t mask = (1ull << hb) - 1ull;
-  uint32_t i = 0;
-  for (; i < cnt; i++) {
-    const int64_t np = pos - (int64_t)hb;
-    if (!loaded || (np < wlo && !at_start)) {
-      // window [wl, wl + 64) with wl dword-aligned in base coordinates, wl <= np
-      int64_t wl = pos - 64 + 8 * (int64_t)a;                // in base bit coordinates
-      wl = wl < 0 ? 0 : ((wl + 31) & ~(int64_t)31);
-      const uint32_t k = (uint32_t)(wl >> 5);
-      w = (uint64_t)hz::load_word(base, k, a, a + n) | ((uint64_t)hz::load_word(base, k + 1u, a, a + n) << 32);
-      wlo = wl - 8 * (int64_t)a;                             // stream bit of w's bit 0 (may be < 0)
-      loaded = true;
-      at_start = wl == 0;
-    }
-    uint32_t peek;
-    if (np >= wlo) peek = (uint32_t)((w >> (np - wlo)) & mask);
-    else peek = (uint32_t)((w << (wlo - np)) & mask);      // bits below the stream start read as 0
-    const Huf e = t.huf[peek];
+  const uint32_t mask = (1u << hb) - 1u;
+  for (uint32_t i = 0; i < cnt; i++) {
+    // 32 top < pos <= 32 top + 32, so the hb <= 11 bits below pos are in W0:W1
+    const uint64_t win = ((uint64_t)W0 << 32) | W1;      // base bits [32 (top - 1), 32 (top + 1))
+    const uint32_t rel = (uint32_t)(pos - (int32_t)hb - 32 * (top - 1));
+    const Huf e = t.huf[(uint32_t)(win >> rel) & mask];
     pos -= e.nb;
     out[i] = e.sym;
+    if (pos <= 32 * top) {
+      W0 = W1; W1 = W2; W2 = W3;
+      W3 = dw(top - 4);
+      top--;
+    }
   }
-  return pos == 0 ? 0 : -1;
+  return pos == 8 * (int32_t)a ? 0 : -1;
 }
 
 // n bytes from s to d with d <= s (possibly overlapping): 16 loads issued together,
