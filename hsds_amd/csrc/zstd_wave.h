@@ -27,7 +27,7 @@
 namespace zw {
 
 constexpr int NSEQ = 128;
-constexpr int STG = 1024;                 // staged sequence-bitstream bytes
+constexpr int STG = 864;                  // staged sequence-bitstream bytes
 constexpr int32_t SB_NONE = -(1 << 30);
 
 // one window sequence.  The FSE walk stores {LL entry, OF entry, ML entry, bit position}
@@ -52,6 +52,8 @@ struct WTables {
       alignas(16) uint32_t seq[NSEQ + 1][4];   // out: output offset; lit: literal bytes; src:
                                                // literal-area index of the first literal; off:
                                                // match distance (0: none)
+      alignas(16) uint8_t ib[1024];            // resolve: the iteration's output bytes
+      uint16_t pm[64];                         // resolve: each lane's bytes still pending
       uint32_t stage[STG / 4 + 4];
     };
   };
@@ -245,17 +247,16 @@ HZ_HD uint32_t find_seq(const Shared& ls, uint32_t hi, uint32_t p) {
   }
   return lo;
 }
-// the same for a match source p below sequence u's start: sources are mostly near, so
-// the two sequences below u are tried before the binary search
-HZ_HD uint32_t find_back(const Shared& ls, uint32_t u, uint32_t p) {
-  if (ls.t.seq[u][SQ_OUT] <= p) return u;
-  if (u >= 1u && ls.t.seq[u - 1u][SQ_OUT] <= p) return u - 1u;
-  if (u >= 2u && ls.t.seq[u - 2u][SQ_OUT] <= p) return u - 2u;
-  return u >= 3u ? find_seq(ls, u - 3u, p) : 0u;
-}
-
 // resolve and store the window's output [wb, we) (nseq sequences in the LDS table);
-// literals are at dst + lbase
+// literals are at dst + lbase.  An iteration covers 64 x 16 output bytes:
+//   (1) every lane finds its 16 bytes' sources: a literal, a byte of the final output
+//       (an earlier window or iteration), or -- a match source inside the iteration -- a
+//       pending byte; the first two are loaded (all loads of a lane together) into the
+//       LDS byte buffer;
+//   (2) rounds: a pending byte whose source is no longer pending copies it (the lowest
+//       pending byte's source always precedes it, so every round makes progress; a
+//       chain of in-iteration matches takes one round per link);
+//   (3) the buffer is stored.
 #if HZ_GPU
 __device__
 #else
@@ -264,41 +265,42 @@ static
 inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, uint32_t lbase, uint32_t wb, uint32_t we, uint32_t nseq,
                     HzProf* prof) {
   (void)prof;
+  WTables& T = ls.t;
+  struct Src { uint32_t v[16]; };
   const uint32_t g0 = (wb + dmis) >> 4, g1 = (we + dmis + 15u) >> 4;
   for (uint32_t it = g0; it < g1; it += 64u) {
     const uint32_t ia = it * 16u;
     const uint32_t it_lo = ia > wb + dmis ? ia - dmis : wb;     // first window byte of the iteration
     LANE_VAR(uint32_t, have);
-    LANE_VAR(uint32_t, w0);
-    LANE_VAR(uint32_t, w1);
-    LANE_VAR(uint32_t, w2);
-    LANE_VAR(uint32_t, w3);
+    LANE_VAR(uint32_t, pend);
+    LANE_VAR(Src, so);
     LANE_LOOP {
       const uint32_t g = it + (uint32_t)lane;
-      uint32_t hv = 0, ww[4] = {0u, 0u, 0u, 0u};
+      uint32_t hv = 0, pv = 0, ww[4] = {0u, 0u, 0u, 0u};
+      Src& S = LV(so);
       if (g < g1) {
         const uint32_t a0 = g * 16u;
         const uint32_t pb = a0 > wb + dmis ? a0 - dmis : wb;
         // the lane's current sequence t, its record in registers
         uint32_t t = find_seq(ls, nseq - 1u, pb);
-        uint32_t r_out = ls.t.seq[t][SQ_OUT], r_lit = ls.t.seq[t][SQ_LIT], r_src = ls.t.seq[t][SQ_SRC], r_off = ls.t.seq[t][SQ_OFF];
-        uint32_t t_end = t + 1u < nseq ? ls.t.seq[t + 1u][SQ_OUT] : we;
+        uint32_t r_out = T.seq[t][SQ_OUT], r_lit = T.seq[t][SQ_LIT], r_src = T.seq[t][SQ_SRC], r_off = T.seq[t][SQ_OFF];
+        uint32_t t_end = t + 1u < nseq ? T.seq[t + 1u][SQ_OUT] : we;
         uint32_t mq = ~0u;            // the previous byte's match source (same sequence), else ~0
-        uint32_t so[16];              // source of each byte, from dst
         HZ_UNROLL
         for (uint32_t k = 0; k < 16u; k++) {
           const uint32_t ak = a0 + k;
-          so[k] = 0;
+          S.v[k] = 0;
           if (ak < wb + dmis || ak >= we + dmis) continue;
           const uint32_t p = ak - dmis;
           if (p >= t_end) {
-            do { t++; t_end = t + 1u < nseq ? ls.t.seq[t + 1u][SQ_OUT] : we; } while (p >= t_end);
-            r_out = ls.t.seq[t][SQ_OUT]; r_lit = ls.t.seq[t][SQ_LIT]; r_src = ls.t.seq[t][SQ_SRC]; r_off = ls.t.seq[t][SQ_OFF];
+            do { t++; t_end = t + 1u < nseq ? T.seq[t + 1u][SQ_OUT] : we; } while (p >= t_end);
+            r_out = T.seq[t][SQ_OUT]; r_lit = T.seq[t][SQ_LIT]; r_src = T.seq[t][SQ_SRC]; r_off = T.seq[t][SQ_OFF];
             mq = ~0u;
           }
           const uint32_t rel = p - r_out;
+          hv |= 1u << k;
           if (rel < r_lit) {
-            so[k] = lbase + r_src + rel;
+            S.v[k] = lbase + r_src + rel;
             mq = ~0u;
           } else {
             // match byte: the periodic extension m - d + (k mod d), stepped from the
@@ -307,38 +309,78 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, uint32_t lbase, uint
             const uint32_t q2 = mq != ~0u ? (mq + 1u == m ? m - r_off : mq + 1u)
                                           : m - r_off + (kk < r_off ? kk : kk % r_off);
             mq = q2;
-            if (q2 < it_lo) {
-              so[k] = q2;                 // final output (an earlier window / iteration)
-            } else {
-              // a source inside this iteration: follow the chain through the table
-              uint32_t q = q2, u = find_back(ls, t, q2);
-              for (;;) {
-                const uint32_t ub = ls.t.seq[u][SQ_OUT], nl = ls.t.seq[u][SQ_LIT], rl = q - ub;
-                if (rl < nl) { so[k] = lbase + ls.t.seq[u][SQ_SRC] + rl; break; }
-                const uint32_t mu = ub + nl, d = ls.t.seq[u][SQ_OFF], ku = q - mu;
-                const uint32_t q3 = mu - d + (ku < d ? ku : ku % d);
-                if (q3 < it_lo) { so[k] = q3; break; }
-                u = find_back(ls, u, q3);
-                q = q3;
-              }
-            }
+            if (q2 < it_lo) S.v[k] = q2;                         // final output
+            else { S.v[k] = q2 + dmis - ia; pv |= 1u << k; }     // a byte of this iteration
           }
-          hv |= 1u << k;
         }
         HZ_T(6);
+        const uint32_t ld = hv & ~pv;
         HZ_UNROLL
-        for (uint32_t k = 0; k < 16u; k++) ww[k >> 2] |= (uint32_t)dst[so[k]] << (8u * (k & 3u));
+        for (uint32_t k = 0; k < 16u; k++) {
+          const uint32_t v = dst[(ld >> k) & 1u ? S.v[k] : 0u];
+          ww[k >> 2] |= ((ld >> k) & 1u ? v : 0u) << (8u * (k & 3u));
+        }
       }
+      uint32_t* ibw = (uint32_t*)(T.ib + 16u * (uint32_t)lane);
+      ibw[0] = ww[0]; ibw[1] = ww[1]; ibw[2] = ww[2]; ibw[3] = ww[3];
+      T.pm[lane] = (uint16_t)pv;
       LV(have) = hv;
-      LV(w0) = ww[0]; LV(w1) = ww[1]; LV(w2) = ww[2]; LV(w3) = ww[3];
+      LV(pend) = pv;
     }
     HZ_T(7);
-    WAVE_SYNC_GLOBAL();       // every load of the iteration before any store
+    WAVE_SYNC();
+    for (;;) {
+      if (!WAVE_BALLOT(LV(pend) != 0u)) break;
+      LANE_VAR(uint32_t, done);
+      LANE_VAR(uint32_t, v0);
+      LANE_VAR(uint32_t, v1);
+      LANE_VAR(uint32_t, v2);
+      LANE_VAR(uint32_t, v3);
+      LANE_LOOP {
+        const uint32_t pv = LV(pend);
+        uint32_t dn = 0, vv[4] = {0u, 0u, 0u, 0u};
+        const Src& S = LV(so);
+        HZ_UNROLL
+        for (uint32_t k = 0; k < 16u; k++) {
+          if ((pv >> k) & 1u) {
+            const uint32_t sx = S.v[k];
+            if (!((T.pm[sx >> 4] >> (sx & 15u)) & 1u)) {
+              dn |= 1u << k;
+              vv[k >> 2] |= (uint32_t)T.ib[sx] << (8u * (k & 3u));
+            }
+          }
+        }
+        LV(done) = dn;
+        LV(v0) = vv[0]; LV(v1) = vv[1]; LV(v2) = vv[2]; LV(v3) = vv[3];
+      }
+      WAVE_SYNC();
+      LANE_LOOP {
+        const uint32_t dn = LV(done);
+        if (dn) {
+          const uint32_t vv[4] = {LV(v0), LV(v1), LV(v2), LV(v3)};
+          uint32_t* ibw = (uint32_t*)(T.ib + 16u * (uint32_t)lane);
+          HZ_UNROLL
+          for (uint32_t i = 0; i < 4u; i++) {
+            const uint32_t bm = (dn >> (4u * i)) & 15u;
+            if (bm) {
+              const uint32_t m = ((bm & 1u) ? 0xffu : 0u) | ((bm & 2u) ? 0xff00u : 0u) | ((bm & 4u) ? 0xff0000u : 0u) |
+                                 ((bm & 8u) ? 0xff000000u : 0u);
+              ibw[i] = (ibw[i] & ~m) | (vv[i] & m);
+            }
+          }
+          LV(pend) &= ~dn;
+          T.pm[lane] = (uint16_t)LV(pend);
+        }
+      }
+      WAVE_SYNC();
+    }
+    HZ_T(3);
     LANE_LOOP {
       const uint32_t g = it + (uint32_t)lane;
       if (g < g1) {
         const uint32_t a0 = g * 16u;
-        const uint32_t ww[4] = {LV(w0), LV(w1), LV(w2), LV(w3)};
+        const uint32_t* ibw = (const uint32_t*)(T.ib + 16u * (uint32_t)lane);
+        const uint32_t ww[4] = {ibw[0], ibw[1], ibw[2], ibw[3]};
         for (uint32_t i = 0; i < 4u; i++) {
           const uint32_t hm = (LV(have) >> (4u * i)) & 15u;
           if (hm == 15u) *(hz_gu32*)(dst + (a0 + 4u * i - dmis)) = ww[i];
@@ -348,8 +390,8 @@ inline void resolve(Shared& ls, hz_gu8* dst, uint32_t dmis, uint32_t lbase, uint
         }
       }
     }
-    WAVE_SYNC_GLOBAL();
-    HZ_T(3);
+    WAVE_SYNC_GLOBAL();       // this iteration's output final before the next one reads it
+    HZ_T(9);
   }
 }
 
@@ -771,7 +813,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
       }
     }
     WAVE_SYNC();
-    HZ_T(3);
+    HZ_T(9);
     if (ns_w) resolve(ls, dst, dmis, lbase, wb, op, ns_w, prof);
     if (last) break;
   }

@@ -24,7 +24,7 @@ NAMES = ["other", "blk-hdr", "tables", "A", "A'", "repair", "valid+scan", "E", "
 
 
 LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
-ZSTD_NAMES = ["other", "lit-stream", "seq-walk", "res-walk", "huf-tree", "seq-tables", "res-load", "res-store", "seq-lanes"]
+ZSTD_NAMES = ["other", "lit-stream", "seq-walk", "res-store", "huf-tree", "seq-tables", "res-load", "res-rounds", "seq-lanes", "res-walk"]
 
 
 def run(fmt, n, unique, tune=None):
