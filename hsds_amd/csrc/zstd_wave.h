@@ -126,6 +126,34 @@ __constant__ PreTab zw_pre[3] = {pre_build(0u), pre_build(1u), pre_build(2u)};
 static constexpr PreTab zw_pre[3] = {pre_build(0u), pre_build(1u), pre_build(2u)};
 #endif
 
+// a lane-uniform value kept in a vector register (the compiler would otherwise move each
+// LDS result to a scalar register before using it)
+HZ_HD uint32_t vdiv(uint32_t v) {
+#if HZ_GPU
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+#else
+  return v;
+#endif
+}
+// bits [o, o + w) of x (w < 32)
+HZ_HD uint32_t ubfe(uint32_t x, uint32_t o, uint32_t w) {
+#if HZ_GPU
+  return __builtin_amdgcn_ubfe(x, o, w);
+#else
+  return w ? (x >> o) & ((1u << w) - 1u) : 0u;
+#endif
+}
+// the low 32 bits of (hi:lo) >> s, s < 32
+HZ_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+#if HZ_GPU
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+
 HZ_HD uint32_t fse_word(const zs::Fse* tab, uint32_t i) {
 #if HZ_GPU
   return ((const uint32_t*)tab)[i];          // one LDS dword read (callers make it uniform)
@@ -749,46 +777,43 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     op = uni(op); lp = uni(lp); k = uni(k);
     rep0 = uni(rep0); rep1 = uni(rep1); rep2 = uni(rep2);
     const uint32_t wb = op;
-    // ---- (1) the serial FSE walk (uniform): per sequence, one LDS dword from each table
-    // and four stage words; it records the three entries and the bit position of the
-    // sequence's extra bits, skips the extra bits and takes the next states ----
     uint32_t ns_w = 0;
-    for (;;) {
-      // the walk's state is uniform; re-asserting it each sequence keeps the loop on the
-      // scalar unit (the enclosing loops' divergent lane work would otherwise make the
-      // compiler carry it in vector registers under exec masks)
-      k = uni(k); ns_w = uni(ns_w);
-      sll = uni(sll); sof = uni(sof); sml = uni(sml);
-      b.pos = (int32_t)uni((uint32_t)b.pos); b.sb = (int32_t)uni((uint32_t)b.sb);
-      if (!(k < nseq && ns_w < (uint32_t)NSEQ - 1u)) break;
-      int32_t P = b.pos - 8 * b.sb;                   // stage bit of the current position
-      if (P < 128 && b.sb > 0) {                      // the next 96 bits below P leave the stage
-        int32_t f = ((b.pos + 7) >> 3) - STG;
-        sb_stage(ls, b, f < 0 ? 0 : f);
-        P = b.pos - 8 * b.sb;
+    // ---- (1) the serial FSE walk, in vector registers (lane-uniform values: LDS results
+    // feed the next addresses with no scalar moves): per sequence one LDS dword from each
+    // table, then the two stage dwords holding the state bits.  It records the three
+    // entries and the bit position of the sequence's extra bits, skips those bits and
+    // takes the next states ----
+    {
+      const uint32_t kend = uni(nseq - k < (uint32_t)NSEQ - 1u ? nseq : k + (uint32_t)NSEQ - 1u);
+      uint32_t vl = vdiv(sll), vo = vdiv(sof), vm = vdiv(sml);
+      int32_t vpos = (int32_t)vdiv((uint32_t)b.pos);
+      while (k < kend) {
+        int32_t sb = b.sb;
+        if ((int32_t)uni((uint32_t)vpos) - 8 * sb < 128 && sb > 0) {   // the state bits may leave the stage
+          b.pos = (int32_t)uni((uint32_t)vpos);
+          const int32_t f = ((b.pos + 7) >> 3) - STG;
+          sb_stage(ls, b, f < 0 ? 0 : f);
+          sb = b.sb;
+        }
+        const uint32_t eL = fse_word(t.ll, vl), eO = fse_word(t.of, vo), eM = fse_word(t.ml, vm);
+        const uint32_t xb = sq_eb(eL) + sq_eb(eO) + sq_eb(eM);
+        const uint32_t nL = sq_nb(eL), nM = sq_nb(eM), nO = sq_nb(eO);
+        const uint32_t nsb = k + 1u < nseq ? nL + nM + nO : 0u;   // state updates: LL, ML, OF
+        int32_t lo = vpos - 8 * sb - (int32_t)(xb + nsb);           // stage bit of the state bits
+        lo = lo < 0 ? 0 : lo;                                        // (< 0 only past the stream start)
+        const uint32_t j = (uint32_t)lo >> 5;
+        const uint32_t fld = ubfe(funnel(ls.t.stage[j + 1u], ls.t.stage[j], (uint32_t)lo & 31u), 0u, nsb);
+        ls.t.seq[ns_w][0] = eL; ls.t.seq[ns_w][1] = eO; ls.t.seq[ns_w][2] = eM; ls.t.seq[ns_w][3] = (uint32_t)vpos;
+        vl = sq_base(eL) + (fld >> (nM + nO));
+        vm = sq_base(eM) + ubfe(fld, nO, nM);
+        vo = sq_base(eO) + ubfe(fld, 0u, nO);
+        vpos -= (int32_t)(xb + nsb);
+        ns_w++;
+        k++;
       }
-      int32_t j0 = (P - 96) >> 5;
-      j0 = j0 < 0 ? 0 : j0 > STG / 4 ? STG / 4 : j0;
-      // the seven LDS reads of a sequence are issued together, then moved to scalars
-      uint32_t eL = fse_word(t.ll, sll), eO = fse_word(t.of, sof), eM = fse_word(t.ml, sml);
-      uint32_t w0 = ls.t.stage[j0], w1 = ls.t.stage[j0 + 1], w2 = ls.t.stage[j0 + 2], w3 = ls.t.stage[j0 + 3];
-      w0 = uni(w0); w1 = uni(w1); w2 = uni(w2); w3 = uni(w3);
-      eL = uni(eL); eO = uni(eO); eM = uni(eM);
-      const uint32_t xb = sq_eb(eL) + sq_eb(eO) + sq_eb(eM);
-      const uint32_t nL = sq_nb(eL), nM = sq_nb(eM), nO = sq_nb(eO);
-      const uint32_t nsb = k + 1u < nseq ? nL + nM + nO : 0u;   // state updates: LL, ML, OF
-      int32_t r = P - (int32_t)(xb + nsb) - 32 * j0;            // the state bits in w0..w3
-      r = r < 0 ? 0 : r > 127 ? 127 : r;                      // (127 - nsb at most on valid input)
-      const uint64_t lo64 = (uint64_t)w0 | ((uint64_t)w1 << 32), hi64 = (uint64_t)w2 | ((uint64_t)w3 << 32);
-      const uint64_t f64 = r >= 64 ? hi64 >> (uint32_t)(r - 64) : r ? (lo64 >> (uint32_t)r) | (hi64 << (uint32_t)(64 - r)) : lo64;
-      const uint32_t fld = (uint32_t)f64 & hz::bmask(nsb);
-      ls.t.seq[ns_w][0] = eL; ls.t.seq[ns_w][1] = eO; ls.t.seq[ns_w][2] = eM; ls.t.seq[ns_w][3] = (uint32_t)b.pos;
-      sll = sq_base(eL) + (fld >> (nM + nO));
-      sml = sq_base(eM) + ((fld >> nO) & hz::bmask(nM));
-      sof = sq_base(eO) + (fld & hz::bmask(nO));
-      b.pos -= (int32_t)(xb + nsb);
-      ns_w++;
-      k++;
+      sll = uni(vl); sof = uni(vo); sml = uni(vm);
+      b.pos = (int32_t)uni((uint32_t)vpos);
+      ns_w = uni(ns_w); k = uni(k);
     }
     HZ_T(8);
     WAVE_SYNC();
