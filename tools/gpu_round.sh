@@ -3,7 +3,7 @@
 # (each step time-limited; the script stops at the first failing step)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
 if [ "${HZ_PHASE:-1}" = "1" ]; then
