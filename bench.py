@@ -789,7 +789,7 @@ def run_cfg4(args, dev, rank, world):
     return out
 
 
-TRAFFIC_ROUND = "r3"
+TRAFFIC_ROUND = "r4"
 
 
 def run_cfg4_full(args, dev, rank, world):
