@@ -58,6 +58,8 @@ struct Shared {
   uint32_t m_lo[GROUP], m_hi[GROUP], m_nk[GROUP];   // round output [lo, hi) and sequence count
   int32_t m_st[GROUP];                               // per-split status
   uint32_t gpre[GROUP + 1];                          // exclusive prefix of 16-byte groups per split
+  alignas(16) uint8_t ib[1024];                      // resolve: the iteration's output bytes
+  uint16_t pm[64];                                   // resolve: each lane's bytes still pending
 };
 
 // per-lane input window: 8 bytes at a dword-aligned position of the split
@@ -254,58 +256,156 @@ inline void lz_group(Shared& ls, HzProf* prof = nullptr) {
     }
     WAVE_SYNC();
     const uint32_t total = ls.gpre[GROUP];
-    // ---- resolve: 16-byte destination groups shared by all lanes ----
-    LANE_LOOP {
-      for (uint32_t g = (uint32_t)lane; g < total; g += 64u) {
-        const uint32_t s = find_split(ls, g);
-        const LaneJob j = ls.job[s];
-        hz_gcu8* src = HZ_GLOBAL(hz_gcu8*, j.src);
-        hz_gu8* dst = HZ_GLOBAL(hz_gu8*, j.dst);
-        const uint32_t dmis = (uint32_t)(((uintptr_t)j.dst) & 3u);
-        const uint32_t wb = ls.m_lo[s], we = ls.m_hi[s], nk = ls.m_nk[s];
-        const uint32_t a0 = (((wb + dmis) >> 4) + (g - ls.gpre[s])) * 16u;   // dst - dmis offset of the group
-        const uint32_t pb = a0 > wb + dmis ? a0 - dmis : wb;                  // first window byte in it
-        uint32_t t = find_seq(ls, s, nk - 1u, pb);
-        uint32_t t_beg = ls.t_out[t][s], t_end = t + 1u < nk ? ls.t_out[t + 1u][s] : we;
-        // pass 1: the source address of every byte (no loads: no waits inside chains)
-        hz_gcu8* sp[16];
-        uint32_t have = 0;
-        HZ_UNROLL
-        for (uint32_t k = 0; k < 16u; k++) {
-          const uint32_t ak = a0 + k;
-          sp[k] = src;
-          if (ak < wb + dmis || ak >= we + dmis) continue;
-          const uint32_t p = ak - dmis;
-          while (p >= t_end) { t++; t_beg = t_end; t_end = t + 1u < nk ? ls.t_out[t + 1u][s] : we; }
-          uint32_t q = p, u = t, ub = t_beg;
-          for (;;) {
-            const uint32_t rel = q - ub, nl = ls.t_lit[u][s];
-            if (rel < nl) { sp[k] = src + ls.t_src[u][s] + rel; break; }
-            const uint32_t m = ub + nl, d = ls.t_off[u][s], kk = q - m;
-            const uint32_t q2 = m - d + (kk < d ? kk : kk % d);
-            if (q2 < wb) { sp[k] = (hz_gcu8*)dst + q2; break; }
-            u = find_seq(ls, s, u, q2);                // an earlier (or this) sequence
-            q = q2; ub = ls.t_out[u][s];
+    // ---- resolve: 16-byte destination groups shared by all lanes, 64 per iteration ----
+    // (1) each byte's source: a literal of the input, a byte stored before this iteration
+    //     (an earlier round or iteration: final), or a byte of this iteration (pending);
+    //     the first two are loaded, together, into the LDS byte buffer;
+    // (2) rounds: a pending byte copies its source once that is no longer pending (the
+    //     lowest pending byte's source always precedes it, so every round makes progress);
+    // (3) the buffer is stored, and the iteration's bytes are final for the next one.
+    struct Src { uint32_t v[16]; };          // bit 31: from the input, else from dst / the buffer
+    for (uint32_t it = 0; it < total; it += 64u) {
+      LANE_VAR(uint32_t, have);
+      LANE_VAR(uint32_t, pend);
+      LANE_VAR(uint32_t, gsplit);
+      LANE_VAR(Src, so);
+      LANE_LOOP {
+        const uint32_t g = it + (uint32_t)lane;
+        uint32_t hv = 0, pv = 0, ww[4] = {0u, 0u, 0u, 0u}, s = 0;
+        Src& S = LV(so);
+        if (g < total) {
+          s = find_split(ls, g);
+          const LaneJob j = ls.job[s];
+          hz_gcu8* src = HZ_GLOBAL(hz_gcu8*, j.src);
+          hz_gcu8* dst = HZ_GLOBAL(hz_gcu8*, j.dst);
+          const uint32_t dmis = (uint32_t)(((uintptr_t)j.dst) & 3u);
+          const uint32_t wb = ls.m_lo[s], we = ls.m_hi[s], nk = ls.m_nk[s], gp = ls.gpre[s];
+          const uint32_t gw = (wb + dmis) >> 4;                        // the round's first group of the split
+          const uint32_t a0 = (gw + (g - gp)) * 16u;                   // dst - dmis offset of the group
+          const uint32_t pb = a0 > wb + dmis ? a0 - dmis : wb;         // first window byte in it
+          // the split's first byte in this iteration: sources below it are final
+          const uint32_t it_lo = gp >= it ? wb : (gw + (it - gp)) * 16u - dmis;
+          uint32_t t = find_seq(ls, s, nk - 1u, pb);
+          uint32_t r_out = ls.t_out[t][s], r_lit = ls.t_lit[t][s], r_src = ls.t_src[t][s], r_off = ls.t_off[t][s];
+          uint32_t t_end = t + 1u < nk ? ls.t_out[t + 1u][s] : we;
+          uint32_t mq = ~0u;            // the previous byte's match source (same sequence), else ~0
+          HZ_UNROLL
+          for (uint32_t k = 0; k < 16u; k++) {
+            const uint32_t ak = a0 + k;
+            S.v[k] = 0;
+            if (ak < wb + dmis || ak >= we + dmis) continue;
+            const uint32_t p = ak - dmis;
+            if (p >= t_end) {
+              do { t++; t_end = t + 1u < nk ? ls.t_out[t + 1u][s] : we; } while (p >= t_end);
+              r_out = ls.t_out[t][s]; r_lit = ls.t_lit[t][s]; r_src = ls.t_src[t][s]; r_off = ls.t_off[t][s];
+              mq = ~0u;
+            }
+            hv |= 1u << k;
+            const uint32_t rel = p - r_out;
+            if (rel < r_lit) {
+              S.v[k] = 0x80000000u | (r_src + rel);
+              mq = ~0u;
+            } else {
+              // the periodic extension m - d + (k mod d), stepped from the previous byte's
+              // source when there is one (no division)
+              const uint32_t m = r_out + r_lit, kk = p - m;
+              const uint32_t q2 = mq != ~0u ? (mq + 1u == m ? m - r_off : mq + 1u)
+                                            : m - r_off + (kk < r_off ? kk : kk % r_off);
+              mq = q2;
+              if (q2 < it_lo) {
+                S.v[k] = q2;
+              } else {                  // its group, relative to the iteration
+                S.v[k] = (gp + ((q2 + dmis) >> 4) - gw - it) * 16u + ((q2 + dmis) & 15u);
+                pv |= 1u << k;
+              }
+            }
           }
-          have |= 1u << k;
+          const uint32_t ld = hv & ~pv;
+          HZ_UNROLL
+          for (uint32_t k = 0; k < 16u; k++) {
+            const uint32_t x = S.v[k];
+            const uint64_t la = (uint64_t)(uintptr_t)src + (x & 0x7fffffffu), da = (uint64_t)(uintptr_t)dst + x;
+            const uint32_t v = *HZ_GLOBAL(hz_gcu8*, (uintptr_t)((ld >> k) & 1u ? ((x >> 31) ? la : da)
+                                                                            : (uint64_t)(uintptr_t)dst));
+            ww[k >> 2] |= ((ld >> k) & 1u ? v : 0u) << (8u * (k & 3u));
+          }
         }
-        // pass 2: 16 independent byte loads in flight together
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        HZ_UNROLL
-        for (uint32_t k = 0; k < 16u; k++) w[k >> 2] |= (uint32_t)*sp[k] << (8u * (k & 3u));
-        for (uint32_t i = 0; i < 4u; i++) {
-          const uint32_t hm = (have >> (4u * i)) & 15u;
-          if (hm == 15u) {
-            *(hz_gu32*)(dst + (a0 + 4u * i - dmis)) = w[i];
-          } else if (hm) {
-            for (uint32_t k = 0; k < 4u; k++)
-              if (hm & (1u << k)) dst[a0 + 4u * i + k - dmis] = (uint8_t)(w[i] >> (8u * k));
+        uint32_t* ibw = (uint32_t*)(ls.ib + 16u * (uint32_t)lane);
+        ibw[0] = ww[0]; ibw[1] = ww[1]; ibw[2] = ww[2]; ibw[3] = ww[3];
+        ls.pm[lane] = (uint16_t)pv;
+        LV(have) = hv;
+        LV(pend) = pv;
+        LV(gsplit) = s;
+      }
+      WAVE_SYNC();
+      for (;;) {
+        if (!WAVE_BALLOT(LV(pend) != 0u)) break;
+        LANE_VAR(uint32_t, done);
+        LANE_VAR(uint32_t, v0);
+        LANE_VAR(uint32_t, v1);
+        LANE_VAR(uint32_t, v2);
+        LANE_VAR(uint32_t, v3);
+        LANE_LOOP {
+          const uint32_t pv = LV(pend);
+          uint32_t dn = 0, vv[4] = {0u, 0u, 0u, 0u};
+          const Src& S = LV(so);
+          HZ_UNROLL
+          for (uint32_t k = 0; k < 16u; k++) {
+            if ((pv >> k) & 1u) {
+              const uint32_t sx = S.v[k];
+              if (!((ls.pm[sx >> 4] >> (sx & 15u)) & 1u)) {
+                dn |= 1u << k;
+                vv[k >> 2] |= (uint32_t)ls.ib[sx] << (8u * (k & 3u));
+              }
+            }
+          }
+          LV(done) = dn;
+          LV(v0) = vv[0]; LV(v1) = vv[1]; LV(v2) = vv[2]; LV(v3) = vv[3];
+        }
+        WAVE_SYNC();
+        LANE_LOOP {
+          const uint32_t dn = LV(done);
+          if (dn) {
+            const uint32_t vv[4] = {LV(v0), LV(v1), LV(v2), LV(v3)};
+            uint32_t* ibw = (uint32_t*)(ls.ib + 16u * (uint32_t)lane);
+            HZ_UNROLL
+            for (uint32_t i = 0; i < 4u; i++) {
+              const uint32_t bm = (dn >> (4u * i)) & 15u;
+              if (bm) {
+                const uint32_t m = ((bm & 1u) ? 0xffu : 0u) | ((bm & 2u) ? 0xff00u : 0u) | ((bm & 4u) ? 0xff0000u : 0u) |
+                                   ((bm & 8u) ? 0xff000000u : 0u);
+                ibw[i] = (ibw[i] & ~m) | (vv[i] & m);
+              }
+            }
+            LV(pend) &= ~dn;
+            ls.pm[lane] = (uint16_t)LV(pend);
+          }
+        }
+        WAVE_SYNC();
+      }
+      LANE_LOOP {
+        const uint32_t g = it + (uint32_t)lane;
+        if (g < total && LV(have)) {
+          const uint32_t s = LV(gsplit);
+          const LaneJob j = ls.job[s];
+          hz_gu8* dst = HZ_GLOBAL(hz_gu8*, j.dst);
+          const uint32_t dmis = (uint32_t)(((uintptr_t)j.dst) & 3u);
+          const uint32_t a0 = (((ls.m_lo[s] + dmis) >> 4) + (g - ls.gpre[s])) * 16u;
+          const uint32_t* ibw = (const uint32_t*)(ls.ib + 16u * (uint32_t)lane);
+          for (uint32_t i = 0; i < 4u; i++) {
+            const uint32_t w = ibw[i];
+            const uint32_t hm = (LV(have) >> (4u * i)) & 15u;
+            if (hm == 15u) {
+              *(hz_gu32*)(dst + (a0 + 4u * i - dmis)) = w;
+            } else if (hm) {
+              for (uint32_t k = 0; k < 4u; k++)
+                if (hm & (1u << k)) dst[a0 + 4u * i + k - dmis] = (uint8_t)(w >> (8u * k));
+            }
           }
         }
       }
+      WAVE_SYNC_GLOBAL();       // this iteration's output final before the next one reads it
     }
-    HZ_T(3);
-    WAVE_SYNC_GLOBAL();
     HZ_T(0);
     LANE_LOOP {
       if (lane < GROUP && LV(active) && LV(ps).done) {

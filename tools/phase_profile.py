@@ -23,7 +23,7 @@ NAMES = ["other", "blk-hdr", "tables", "A", "A'", "repair", "valid+scan", "E", "
          "M-jump", "M-gather", "M-store", "M-setup", "M-prefetch"]
 
 
-LZ_NAMES = ["other", "stage", "parse", "resolve", "sync"]
+LZ_NAMES = ["other", "parse", "resolve"]
 ZSTD_NAMES = ["other", "lit-stream", "seq-walk", "res-store", "huf-tree", "seq-tables", "res-load", "res-rounds", "seq-lanes", "res-walk"]
 
 
