@@ -175,7 +175,7 @@ inline int chunk(Shared& sh, const uint8_t* srcp, uint32_t n, uint8_t* dstp, uin
       }
     }
     WAVE_SYNC();
-    lz::lz_group(sh.lz);
+    lz::lz_group<false>(sh.lz, nullptr);
     WAVE_SYNC_GLOBAL();        // the group's staged blocks visible to every lane
     for (int g = 0; g < lz::GROUP; g++)
       if (sh.blk_n[g] && sh.lz.m_st[g] != hz::ST_OK) return sh.lz.m_st[g];

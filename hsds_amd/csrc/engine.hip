@@ -452,6 +452,7 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ pool, c
                                                 int32_t* __restrict__ status,
                                                 const uint32_t* __restrict__ kind_counts) {
   __shared__ lz::Shared ls;
+  __shared__ lz::Stage stg;
   if (kind_counts[0] == 0) return;
   const uint32_t total = *pool_ctr;
   const int lane = threadIdx.x;
@@ -483,7 +484,7 @@ __global__ void __launch_bounds__(64) lz_kernel(const Item* __restrict__ pool, c
     }
     if (lane < lz::GROUP) ls.job[lane] = j;
     __syncthreads();
-    lz::lz_group(ls, prof);
+    lz::lz_group<true>(ls, &stg, prof);
     if (j.valid && ls.m_st[lane] != HSDS_OK) atomicMin(&status[chunk], ls.m_st[lane]);
     __syncthreads();
   }

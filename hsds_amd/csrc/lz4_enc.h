@@ -48,6 +48,8 @@ HZ_HD void in_init(InRd& in, const hd::EncJob& job) {
   in.r.lo = a;
   in.r.hi = a + (job.ts > 1u ? job.off + job.len : job.len);
   in.r.bpos = 0x80000000u;
+  in.r.stg = nullptr;
+  in.r.sb = 0x80000000u;                    // no LDS stage: every refill from global memory
   in.r.buf = 0;
   in.blk = HZ_GLOBAL(hz_gcu8*, job.src);
   in.ts = job.ts; in.neb = job.neb; in.off = job.off;

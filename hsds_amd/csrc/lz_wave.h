@@ -40,6 +40,10 @@ constexpr int GK = LZ_GK;                           // sequences per split per r
 // GROUP 64 / 16 / 8 / 4 -> 23 / 62 / 79 / 67 GB/s; GK 16 / 32 / 64 -> 77 / 79 / 79).
 constexpr int GROUP = LZ_GROUP;
 constexpr uint32_t FMT_BLOSCLZ = 0, FMT_LZ4 = 1;    // Blosc1 codec numbers (flags >> 5)
+#ifndef LZ_SW
+#define LZ_SW 128
+#endif
+constexpr uint32_t SW = LZ_SW;                      // staged input dwords per split per round
 
 // one split per lane
 struct LaneJob {
@@ -62,20 +66,37 @@ struct Shared {
   uint16_t pm[64];                                   // resolve: each lane's bytes still pending
 };
 
+// the parse's LDS stage (lz_kernel; the bitshuffle decoder's small blocks run without:
+// its 4 KB would cost that kernel a wave per SIMD)
+struct Stage {
+  uint32_t stg[GROUP][SW];                           // staged input of each split
+  uint32_t sbeg[GROUP];                              // its base offset (~0: none)
+};
+
 // per-lane input window: 8 bytes at a dword-aligned position of the split
+// Each round the wave stages SW dwords of every split's input from its parse position
+// into LDS (all 64 lanes, one memory latency); the header walk refills its window from
+// there (an LDS latency) and from global memory only past the staged bytes.
 struct ByteRd {
   hz_gcu8* base;      // split start rounded down to 4 bytes
   uint32_t lo, hi;    // valid byte range in base coordinates
   uint32_t bpos;      // base offset of buf
   uint64_t buf;
+  const uint32_t* stg;  // this split's stage (LDS): dwords at base offsets sb + 4k, k < SW
+  uint32_t sb;
 };
 
 HZ_HD uint32_t rd_byte(ByteRd& r, uint32_t pos) {
   const uint32_t ap = pos + r.lo;
   if (ap - r.bpos >= 8u) {
     r.bpos = ap & ~3u;
-    r.buf = (uint64_t)hz::load_word(r.base, r.bpos >> 2, r.lo, r.hi) |
-            ((uint64_t)hz::load_word(r.base, (r.bpos >> 2) + 1u, r.lo, r.hi) << 32);
+    const uint32_t rel = r.bpos - r.sb;
+    if (rel + 8u <= 4u * SW) {
+      r.buf = (uint64_t)r.stg[rel >> 2] | ((uint64_t)r.stg[(rel >> 2) + 1u] << 32);
+    } else {
+      r.buf = (uint64_t)hz::load_word(r.base, r.bpos >> 2, r.lo, r.hi) |
+              ((uint64_t)hz::load_word(r.base, (r.bpos >> 2) + 1u, r.lo, r.hi) << 32);
+    }
   }
   return (uint32_t)(r.buf >> (8u * (ap - r.bpos))) & 0xffu;
 }
@@ -185,12 +206,13 @@ HZ_HD uint32_t find_split(const Shared& ls, uint32_t g) {
 // Decode the splits in ls.job[0..GROUP) (valid ones); statuses land in ls.m_st.
 // Forced inline: lz_kernel and bshuf_kernel both call it, and an outlined call costs
 // lz_kernel 92 -> 165 VGPRs (5 -> 3 waves/SIMD) and a scratch spill.
+template <bool STAGE>
 #if HZ_GPU
 __device__ __attribute__((always_inline))
 #else
 static
 #endif
-inline void lz_group(Shared& ls, HzProf* prof = nullptr) {
+inline void lz_group(Shared& ls, Stage* stage, HzProf* prof = nullptr) {
   (void)prof;
   LANE_VAR(PState, ps);
   LANE_VAR(ByteRd, rd);
@@ -206,6 +228,7 @@ inline void lz_group(Shared& ls, HzProf* prof = nullptr) {
     LV(rd).base = HZ_GLOBAL(hz_gcu8*, j.src - a);
     LV(rd).lo = a; LV(rd).hi = a + j.src_len;
     LV(rd).bpos = 0x80000000u; LV(rd).buf = 0;
+    LV(rd).stg = STAGE ? stage->stg[lane] : nullptr; LV(rd).sb = 0x80000000u;
     LV(active) = j.valid != 0;
     ls.m_st[lane] = hz::ST_OK;
     if (j.valid && j.src_len == 0) { ls.m_st[lane] = hz::ST_TRUNC; LV(active) = 0; }
@@ -214,8 +237,37 @@ inline void lz_group(Shared& ls, HzProf* prof = nullptr) {
   for (;;) {
     if (!WAVE_BALLOT(LV(active))) break;
     HZ_T(1);
+    // ---- stage: SW dwords of every active split's input from its parse position ----
+    if constexpr (STAGE) {
+    LANE_LOOP {
+      if (lane < GROUP) stage->sbeg[lane] = LV(active) ? ((LV(ps).ip + LV(rd).lo) & ~3u) : ~0u;
+    }
+    WAVE_SYNC();
+    LANE_LOOP {
+      const uint32_t s = (uint32_t)lane >> 3, part = (uint32_t)lane & 7u, b0 = stage->sbeg[s];
+      if (b0 != ~0u) {
+        const LaneJob j = ls.job[s];
+        const uint32_t a = (uint32_t)(((uintptr_t)j.src) & 3u), hi = a + j.src_len;
+        hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, j.src - a);
+        uint32_t v[SW / 8u];
+        HZ_UNROLL
+        for (uint32_t i = 0; i < SW / 8u; i++) {       // every load issued before any is used
+          const uint32_t o = b0 + 4u * (part + 8u * i);
+#if HZ_GPU
+          v[i] = *(hz_gcu32*)(base + (o < hi ? o : b0));
+#else
+          v[i] = hz::load_word(base, o >> 2, a, hi);
+#endif
+        }
+        HZ_UNROLL
+        for (uint32_t i = 0; i < SW / 8u; i++) stage->stg[s][part + 8u * i] = b0 + 4u * (part + 8u * i) < hi ? v[i] : 0u;
+      }
+    }
+    WAVE_SYNC();
+    }
     // ---- parse: every lane walks up to GK sequence headers of its own split ----
     LANE_LOOP {
+      if (STAGE && lane < GROUP) LV(rd).sb = stage->sbeg[lane];
       if (lane >= GROUP) continue;
       const LaneJob j = ls.job[lane];
       const uint32_t op0 = LV(ps).op;

@@ -10,16 +10,18 @@ extern "C" int emu_lz_group(const uint8_t* const* src, const uint32_t* src_len, 
                             const uint32_t* dst_len, const uint32_t* fmt, int n, int32_t* status) {
   if (n < 0 || n > 64) return -6;
   lz::Shared* ls = (lz::Shared*)calloc(1, sizeof(lz::Shared));
+  lz::Stage* st_ = (lz::Stage*)calloc(1, sizeof(lz::Stage));
   for (int b = 0; b < n; b += lz::GROUP) {       // one wavefront per GROUP splits
     for (int i = 0; i < lz::GROUP; i++) {
       lz::LaneJob j = {nullptr, nullptr, 0u, 0u, 0u, 0u};
       if (b + i < n) j = {src[b + i], dst[b + i], src_len[b + i], dst_len[b + i], fmt[b + i], 1u};
       ls->job[i] = j;
     }
-    lz::lz_group(*ls);
+    lz::lz_group<true>(*ls, st_);
     for (int i = 0; i < lz::GROUP && b + i < n; i++) status[b + i] = ls->m_st[i];
   }
   free(ls);
+  free(st_);
   return 0;
 }
 
