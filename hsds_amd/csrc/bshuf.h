@@ -113,8 +113,11 @@ HZ_HD void trans_group(hz_gcu8* blk, hz_gu8* out, uint32_t q, uint32_t row, uint
 
 HZ_HD uint32_t be32(hz_gcu8* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
+#ifndef BS_GK
+#define BS_GK 16
+#endif
 struct Shared {
-  lz::Shared lz;
+  lz::SharedT<BS_GK> lz;      // 8 KiB LZ4 blocks: 16 sequences per round (A/B: 272 vs 255 GB/s at 32)
   uint32_t blk_e[lz::GROUP];      // first element of each block of the group
   uint32_t blk_n[lz::GROUP];      // elements
   uint32_t next_p, next_e;        // walk position after the group

@@ -53,11 +53,15 @@ struct LaneJob {
   uint32_t fmt, valid;
 };
 
-struct Shared {
-  uint32_t t_out[GK][GROUP];   // [k][split]: output offset of the split's k-th sequence this round
-  uint32_t t_lit[GK][GROUP];   // literal bytes
-  uint32_t t_src[GK][GROUP];   // input offset of the literals
-  uint32_t t_off[GK][GROUP];   // match distance (0: literals only)
+// KR: sequences per split per round (lz_kernel GK; the bitshuffle decoder's 8 KiB blocks
+// take fewer)
+template <int KR>
+struct SharedT {
+  static constexpr int K = KR;
+  uint32_t t_out[KR][GROUP];   // [k][split]: output offset of the split's k-th sequence this round
+  uint32_t t_lit[KR][GROUP];   // literal bytes
+  uint32_t t_src[KR][GROUP];   // input offset of the literals
+  uint32_t t_off[KR][GROUP];   // match distance (0: literals only)
   LaneJob job[GROUP];
   uint32_t m_lo[GROUP], m_hi[GROUP], m_nk[GROUP];   // round output [lo, hi) and sequence count
   int32_t m_st[GROUP];                               // per-split status
@@ -65,6 +69,7 @@ struct Shared {
   alignas(16) uint8_t ib[1024];                      // resolve: the iteration's output bytes
   uint16_t pm[64];                                   // resolve: each lane's bytes still pending
 };
+using Shared = SharedT<GK>;
 
 // the parse's LDS stage (lz_kernel; the bitshuffle decoder's small blocks run without:
 // its 4 KB would cost that kernel a wave per SIMD)
@@ -184,7 +189,8 @@ HZ_HD int parse_blosclz(ByteRd& r, PState& ps, uint32_t iend, uint32_t oend, uin
 #undef LZ_NEED
 
 // largest k <= hi with t_out[k][s] <= p (non-decreasing in k, t_out[0][s] <= p)
-HZ_HD uint32_t find_seq(const Shared& ls, uint32_t s, uint32_t hi, uint32_t p) {
+template <class SH>
+HZ_HD uint32_t find_seq(const SH& ls, uint32_t s, uint32_t hi, uint32_t p) {
   uint32_t lo = 0;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1u) >> 1;
@@ -194,7 +200,8 @@ HZ_HD uint32_t find_seq(const Shared& ls, uint32_t s, uint32_t hi, uint32_t p) {
 }
 
 // largest s < GROUP with gpre[s] <= g
-HZ_HD uint32_t find_split(const Shared& ls, uint32_t g) {
+template <class SH>
+HZ_HD uint32_t find_split(const SH& ls, uint32_t g) {
   uint32_t lo = 0, hi = GROUP - 1;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1u) >> 1;
@@ -206,13 +213,13 @@ HZ_HD uint32_t find_split(const Shared& ls, uint32_t g) {
 // Decode the splits in ls.job[0..GROUP) (valid ones); statuses land in ls.m_st.
 // Forced inline: lz_kernel and bshuf_kernel both call it, and an outlined call costs
 // lz_kernel 92 -> 165 VGPRs (5 -> 3 waves/SIMD) and a scratch spill.
-template <bool STAGE>
+template <bool STAGE, class SH>
 #if HZ_GPU
 __device__ __attribute__((always_inline))
 #else
 static
 #endif
-inline void lz_group(Shared& ls, Stage* stage, HzProf* prof = nullptr) {
+inline void lz_group(SH& ls, Stage* stage, HzProf* prof = nullptr) {
   (void)prof;
   LANE_VAR(PState, ps);
   LANE_VAR(ByteRd, rd);
@@ -244,15 +251,17 @@ inline void lz_group(Shared& ls, Stage* stage, HzProf* prof = nullptr) {
     }
     WAVE_SYNC();
     LANE_LOOP {
-      const uint32_t s = (uint32_t)lane >> 3, part = (uint32_t)lane & 7u, b0 = stage->sbeg[s];
+      constexpr uint32_t LPS = 64u / GROUP;          // lanes per split
+      static_assert(64 % GROUP == 0 && SW % (64u / GROUP) == 0, "stage: whole dwords per lane");
+      const uint32_t s = (uint32_t)lane / LPS, part = (uint32_t)lane % LPS, b0 = stage->sbeg[s];
       if (b0 != ~0u) {
         const LaneJob j = ls.job[s];
         const uint32_t a = (uint32_t)(((uintptr_t)j.src) & 3u), hi = a + j.src_len;
         hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, j.src - a);
-        uint32_t v[SW / 8u];
+        uint32_t v[SW / LPS];
         HZ_UNROLL
-        for (uint32_t i = 0; i < SW / 8u; i++) {       // every load issued before any is used
-          const uint32_t o = b0 + 4u * (part + 8u * i);
+        for (uint32_t i = 0; i < SW / LPS; i++) {      // every load issued before any is used
+          const uint32_t o = b0 + 4u * (part + LPS * i);
 #if HZ_GPU
           v[i] = *(hz_gcu32*)(base + (o < hi ? o : b0));
 #else
@@ -260,7 +269,8 @@ inline void lz_group(Shared& ls, Stage* stage, HzProf* prof = nullptr) {
 #endif
         }
         HZ_UNROLL
-        for (uint32_t i = 0; i < SW / 8u; i++) stage->stg[s][part + 8u * i] = b0 + 4u * (part + 8u * i) < hi ? v[i] : 0u;
+        for (uint32_t i = 0; i < SW / LPS; i++)
+          stage->stg[s][part + LPS * i] = b0 + 4u * (part + LPS * i) < hi ? v[i] : 0u;
       }
     }
     WAVE_SYNC();
@@ -273,7 +283,7 @@ inline void lz_group(Shared& ls, Stage* stage, HzProf* prof = nullptr) {
       const uint32_t op0 = LV(ps).op;
       uint32_t k = 0;
       if (LV(active)) {
-        for (; k < (uint32_t)GK && !LV(ps).done; k++) {
+        for (; k < (uint32_t)SH::K && !LV(ps).done; k++) {
           uint32_t lit, lsrc, off, ml;
           const int r = j.fmt == FMT_LZ4 ? parse_lz4(LV(rd), LV(ps), j.src_len, j.dst_len, lit, lsrc, off, ml)
                                          : parse_blosclz(LV(rd), LV(ps), j.src_len, j.dst_len, lit, lsrc, off, ml);
