@@ -52,7 +52,7 @@
 #define HZ2_WPE 4          // inflate2_kernel waves per SIMD the compiler must allow (VGPR budget)
 #endif
 #ifndef HZ2_PIPE_DEFAULT
-#define HZ2_PIPE_DEFAULT -1  // two wavefronts per zlib stream when a batch cannot fill the GPU (0: never)
+#define HZ2_PIPE_DEFAULT 0   // wavefronts per zlib stream: 0 by batch size (4 or 2 when a batch cannot fill the GPU), or 1, 2, 4
 #endif
 #define HSDS_VERSION "hsds_amd 0.1.0 (gfx950)"
 
@@ -402,18 +402,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ2_WPE
 // alternating its windows (inflate2.h, inflate_stream<NW = 2>): one window's header, sync
 // phases and emit run beside the other's resolve, about halving a stream's latency.
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(HZ2_WPE))) inflate2w_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(HZ2_WPE))) inflate2w_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
                                                       uint32_t* __restrict__ counter, int32_t* __restrict__ status,
                                                       uint32_t* __restrict__ sizes,
                                                       const uint32_t* __restrict__ kind_counts, hz2::Tune tune,
                                                       uint8_t* __restrict__ rings) {
-  __shared__ hz2::Shared sh[2];
+  __shared__ hz2::Shared sh[NW];
   __shared__ hz2::Ctl ctl;
   if (kind_counts[1] == 0) return;
   const uint32_t total = *pool_ctr;
   const uint32_t w = threadIdx.x >> 6;
   const int lane = (int)(threadIdx.x & 63u);
-  uint8_t* ring = rings + ((size_t)blockIdx.x * 2u + w) * hz2::SCRATCH_BYTES;
+  uint8_t* ring = rings + ((size_t)blockIdx.x * NW + w) * hz2::SCRATCH_BYTES;
   HzProf* prof = nullptr;
   for (;;) {
     if (threadIdx.x == 0) {
@@ -434,8 +435,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(HZ2_WP
                       item_perm(it)};
       // (only wavefront 0 reports the decoded length of an inexact item)
       if (w != 0) job.out_len = nullptr;
-      st = hz2::inflate_stream<hz2::Stats, 2>(sh[w], job, tune, ring, (hz2::Stats*)nullptr, prof,
-                                              hz2::Pipe{&ctl, &sh[1u - w], w});
+      st = hz2::inflate_stream<hz2::Stats, NW>(sh[w], job, tune, ring, (hz2::Stats*)nullptr, prof,
+                                               hz2::Pipe{&ctl, &sh[(w + NW - 1u) % NW], w});
     }
     if (w == 0 && lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
     __syncthreads();
@@ -1461,8 +1462,9 @@ struct hsds_engine {
   int device;
   int num_cus;
   int inflate_blocks_per_cu;   // occupancy of inflate2_kernel
-  int inflate2w_blocks_per_cu; // occupancy of inflate2w_kernel (two wavefronts per workgroup)
-  int inflate_pipe;            // -1: by batch size, 0: one wavefront per stream, 1: two
+  int inflate2w_blocks_per_cu; // occupancy of inflate2w_kernel<2> (two wavefronts per workgroup)
+  int inflate4w_blocks_per_cu; // occupancy of inflate2w_kernel<4>
+  int inflate_pipe;            // wavefronts per stream: 0 by batch size, else 1, 2 or 4
   int lz_blocks_per_cu;        // occupancy of lz_kernel
   int bshuf_blocks_per_cu;     // occupancy of bshuf_kernel
   int zstd_blocks_per_cu;      // occupancy of zstd_kernel
@@ -1630,12 +1632,18 @@ int hsds_engine_create(int device, hsds_engine** out) {
     if (v >= 1 && v < occ) occ = v;
   }
   e->inflate_blocks_per_cu = occ;
-  int occ2 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, inflate2w_kernel, 128, 0) != hipSuccess || occ2 < 1)
+  int occ2 = 0, occ4 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, inflate2w_kernel<2>, 128, 0) != hipSuccess || occ2 < 1)
     occ2 = occ / 2 > 0 ? occ / 2 : 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, inflate2w_kernel<4>, 256, 0) != hipSuccess || occ4 < 1)
+    occ4 = occ / 4 > 0 ? occ / 4 : 1;
   e->inflate2w_blocks_per_cu = occ2;
+  e->inflate4w_blocks_per_cu = occ4;
   e->inflate_pipe = HZ2_PIPE_DEFAULT;
-  if (const char* ev = getenv("HSDS_INFLATE_PIPE")) e->inflate_pipe = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
+  if (const char* ev = getenv("HSDS_INFLATE_PIPE")) {       // 0 (or < 0): by batch size; 1, 2, 4 wavefronts
+    const int v = atoi(ev);
+    e->inflate_pipe = v == 1 || v == 2 || v == 4 ? v : 0;
+  }
   int olz = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olz, lz_kernel, 64, 0) != hipSuccess || olz < 1) olz = 8;
   e->lz_blocks_per_cu = olz;
@@ -1711,9 +1719,10 @@ int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, u
   if (!e) return HSDS_ERR_ARG;
   // HSDS_TUNE_KEEP (0xffffffff; -1 for rounds) leaves a setting as it is
   if ((seg_over16 > 16u && seg_over16 != HSDS_TUNE_KEEP) || (warmup_bits > 4096u && warmup_bits != HSDS_TUNE_KEEP) ||
-      (waves_per_stream > 2u && waves_per_stream != HSDS_TUNE_KEEP) || rounds < -1 || rounds > 64)
+      (waves_per_stream > 4u && waves_per_stream != HSDS_TUNE_KEEP) || waves_per_stream == 3u || rounds < -1 ||
+      rounds > 64)
     return HSDS_ERR_ARG;
-  if (waves_per_stream != HSDS_TUNE_KEEP) e->inflate_pipe = waves_per_stream == 0u ? -1 : waves_per_stream == 2u ? 1 : 0;
+  if (waves_per_stream != HSDS_TUNE_KEEP) e->inflate_pipe = (int)waves_per_stream;
   if (seg_over16 != HSDS_TUNE_KEEP) e->tune.over16 = seg_over16;
   if (warmup_bits != HSDS_TUNE_KEEP) e->tune.W = warmup_bits;
   if (rounds >= 0) e->tune.max_rounds = rounds;
@@ -1777,11 +1786,16 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   // chunk in HSDS's F1 frames, 1 per F2 chunk) cannot fill half the resident wavefronts
   // decodes every stream with two wavefronts (inflate2w_kernel)
   const int64_t waves1 = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
-  const bool pipe = e->inflate_pipe == 1 || (e->inflate_pipe < 0 && nchunks * 4 * 2 <= waves1);
-  int64_t grid = pipe ? (int64_t)e->num_cus * e->inflate2w_blocks_per_cu : waves1;
+  // wavefronts per stream: by batch size, the most whose streams (at most 4 per chunk) all
+  // fit in half the resident wavefronts
+  int nw = e->inflate_pipe;
+  if (nw == 0) nw = nchunks * 4 * 4 * 2 <= waves1 ? 4 : nchunks * 4 * 2 <= waves1 ? 2 : 1;
+  const bool pipe = nw > 1;
+  int64_t grid = nw == 4 ? (int64_t)e->num_cus * e->inflate4w_blocks_per_cu
+                 : nw == 2 ? (int64_t)e->num_cus * e->inflate2w_blocks_per_cu : waves1;
   if (grid > nchunks * 64) grid = nchunks * 64;
   if (grid < 1) grid = 1;
-  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * (pipe ? 2u : 1u) * hz2::SCRATCH_BYTES))
+  if (grow((void**)&e->rings, &e->rings_bytes, (size_t)grid * (size_t)nw * hz2::SCRATCH_BYTES))
     return HSDS_ERR_DEVICE;
   if (hipMemsetAsync(ctr, 0, 64, st) != hipSuccess) return HSDS_ERR_DEVICE;
   const int tpb = 256;
@@ -1790,9 +1804,12 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
                      (uint8_t*)d_dst, tmp, pool, pool_cap, ctr + 8, meta, list, ctr + 1, ctr + 4, d_status,
                      compressor, shuffle, itemsize, inexact);
   hipEventRecord(e->ev0, st);
-  if (pipe)
-    hipLaunchKernelGGL(inflate2w_kernel, dim3((unsigned)grid), dim3(128), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
-                       ctr + 4, e->tune, e->rings);
+  if (nw == 4)
+    hipLaunchKernelGGL(inflate2w_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, pool, ctr + 8, ctr, d_status,
+                       ctr + 2, ctr + 4, e->tune, e->rings);
+  else if (pipe)
+    hipLaunchKernelGGL(inflate2w_kernel<2>, dim3((unsigned)grid), dim3(128), 0, st, pool, ctr + 8, ctr, d_status,
+                       ctr + 2, ctr + 4, e->tune, e->rings);
   else
     hipLaunchKernelGGL(inflate2_kernel, dim3((unsigned)grid), dim3(64), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
                        ctr + 4, e->tune, e->rings);

@@ -724,13 +724,13 @@ __device__ __forceinline__ void ctl_st(uint32_t* p, uint32_t v) {
 #define HZ2_LSYNC() do { } while (0)
 #define HZ2_GSYNC() do { } while (0)
 #define HZ2_PAUSE() sched_yield()
-#define HZ2_WGBAR() hz2::emu_wgbar(pipe.ctl)
+#define HZ2_WGBAR() hz2::emu_wgbar(pipe.ctl, NW)
 namespace hz2 {
 // CPU emulation: the two wavefronts are two threads
 inline uint32_t ctl_ld(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 inline void ctl_st(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 struct Ctl;
-void emu_wgbar(Ctl* c);
+void emu_wgbar(Ctl* c, int n);
 }  // namespace hz2
 #endif
 
@@ -764,7 +764,8 @@ struct WinState {                // a window's start
   uint32_t est;                  // WK_CONT: expected bits left in the block
   uint32_t prev_block_bits;      // the last Huffman block's size (next block's estimate)
 };
-struct Ctl {                     // in LDS, shared by the workgroup's two wavefronts
+constexpr int NW_MAX = 4;        // wavefronts per stream in the window pipeline
+struct Ctl {                     // in LDS, shared by the workgroup's wavefronts
   uint32_t synced;               // the window whose start is in `next`
   uint32_t mdone;                // windows whose output is final
   uint32_t end_at;               // the WK_END window's index (~0u: not reached)
@@ -772,11 +773,11 @@ struct Ctl {                     // in LDS, shared by the workgroup's two wavefr
   uint32_t item;                 // the work item both wavefronts decode
   uint32_t bar;                  // CPU emulation: barrier generation counter
   WinState next;
-  uint64_t adler[2][2];          // per wavefront: sum b, sum pos * b
+  uint64_t adler[NW_MAX][2];     // per wavefront: sum b, sum pos * b
 };
 struct Pipe {
   Ctl* ctl;
-  const Shared* other;           // the other wavefront's LDS (its block tables)
+  const Shared* other;           // the previous window's wavefront's LDS (its block tables)
   uint32_t w;                    // this wavefront's index in the workgroup
 };
 constexpr uint32_t SPIN_MAX = 1u << 24;   // a wait that never ends fails the stream instead of hanging
@@ -793,15 +794,15 @@ HZ_HD void atomic_min_err(Ctl* c, int st) {
 #endif
 }
 #if !HZ_GPU
-// both emulated wavefronts meet (generation barrier over Ctl::bar: the low bit counts
+// the emulated wavefronts meet (generation barrier over Ctl::bar: the low 8 bits count
 // arrivals, the rest is the generation)
-inline void emu_wgbar(Ctl* c) {
-  const uint32_t g = __atomic_load_n(&c->bar, __ATOMIC_ACQUIRE) & ~1u;
-  uint32_t exp = g;
-  if (__atomic_compare_exchange_n(&c->bar, &exp, g | 1u, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
-    while ((__atomic_load_n(&c->bar, __ATOMIC_ACQUIRE) & ~1u) == g) sched_yield();   // first: wait
+inline void emu_wgbar(Ctl* c, int n) {
+  const uint32_t v = __atomic_add_fetch(&c->bar, 1u, __ATOMIC_ACQ_REL);
+  const uint32_t g = v & ~0xffu;
+  if ((v & 0xffu) == (uint32_t)n) {
+    __atomic_store_n(&c->bar, g + 0x100u, __ATOMIC_RELEASE);                          // the last: release
   } else {
-    __atomic_store_n(&c->bar, g + 2u, __ATOMIC_RELEASE);                             // second: release
+    while ((__atomic_load_n(&c->bar, __ATOMIC_ACQUIRE) & ~0xffu) == g) sched_yield();  // wait
   }
 }
 #endif
@@ -866,6 +867,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
   cur.bfinal = 0;
   cur.est = 0;
   cur.prev_block_bits = 0;
+  static_assert(NW >= 1 && NW <= NW_MAX, "wavefronts per stream");
   uint32_t k = NW > 1 ? pipe.w : 0u;   // window index
   static_assert(sizeof(WinState) <= sizeof(sh.wnext), "WinState in Shared::wnext");
 
@@ -1094,7 +1096,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       est += (uint32_t)(((uint64_t)est * tune.over16) >> 4);
         first_window = 1;
       } else if (NW > 1) {
-        // a continuation window: the block's tables are the other wavefront's
+        // a continuation window: the block's tables are the previous window's wavefront's
         const Shared& o = *pipe.other;
         LANE_LOOP {
           for (uint32_t i = (uint32_t)lane; i < (uint32_t)((1 << LL_ROOT) + LL_SUB); i += 64u) sh.lut_ll[i] = o.lut_ll[i];
@@ -1753,7 +1755,7 @@ HZ_UNROLL
     }
   }
   if (NW > 1) {
-    // both wavefronts: every window done (or failed); the adler sums of both
+    // all wavefronts: every window done (or failed); the adler sums of all
     if (fail != ST_OK) atomic_min_err(pipe.ctl, fail);
     HZ2_WGBAR();
     const int32_t e = (int32_t)ctl_ld((const uint32_t*)&pipe.ctl->err);
@@ -1783,13 +1785,13 @@ HZ_UNROLL
   for (int lane = 0; lane < 64; lane++) { S1 += s1[lane]; S2 += s2[lane]; }
 #endif
   if (NW > 1) {
-    // the two wavefronts' partial sums, added up through LDS
+    // the wavefronts' partial sums, added up through LDS
     Ctl* c = pipe.ctl;
     c->adler[pipe.w][0] = S1;
     c->adler[pipe.w][1] = S2;
     HZ2_WGBAR();
-    S1 = c->adler[0][0] + c->adler[1][0];
-    S2 = c->adler[0][1] + c->adler[1][1];
+    S1 = 0; S2 = 0;
+    for (int i = 0; i < NW; i++) { S1 += c->adler[i][0]; S2 += c->adler[i][1]; }
   }
   const uint32_t A = (uint32_t)((1u + S1) % ADLER_MOD);
   const uint32_t B = (uint32_t)(((uint64_t)(out % ADLER_MOD) * A + ADLER_MOD - (S2 % ADLER_MOD)) % ADLER_MOD);

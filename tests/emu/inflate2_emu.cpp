@@ -11,29 +11,53 @@
 // (dst holds the unshuffled bytes), as the engine does for F2 chunks.
 // dst_off: the stream's output starts dst_off bytes into dst (dst has dst_len + dst_off + 8
 // bytes; the bytes around the output must stay untouched)
-// nwaves == 2: the window pipeline of inflate2w_kernel -- two threads, one per emulated
-// wavefront, sharing a hz2::Ctl and each other's LDS tables; both must return the same status
-static int run_stream(hz2::Shared* sh, const hz2::Job& job, const hz2::Tune& tune, uint8_t* ring, hz2::Stats& st,
-                      int nwaves) {
-  if (nwaves < 2) return hz2::inflate_stream<hz2::Stats, 1>(*sh, job, tune, ring, &st);
-  hz2::Shared* sh2 = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
-  uint8_t* ring2 = (uint8_t*)malloc(hz2::SCRATCH_BYTES);
+// nwaves == 2 or 4: the window pipeline of inflate2w_kernel -- one thread per emulated
+// wavefront, sharing a hz2::Ctl and the previous window's wavefront's LDS tables; all must
+// return the same status
+template <int NW>
+static int run_pipe(hz2::Shared* sh0, const hz2::Job& job, const hz2::Tune& tune, uint8_t* ring0, hz2::Stats& st) {
+  hz2::Shared* sh[NW];
+  uint8_t* ring[NW];
+  hz2::Stats sts[NW] = {};
+  int rs[NW] = {};
+  sh[0] = sh0; ring[0] = ring0;
+  for (int w = 1; w < NW; w++) {
+    sh[w] = (hz2::Shared*)calloc(1, sizeof(hz2::Shared));
+    ring[w] = (uint8_t*)malloc(hz2::SCRATCH_BYTES);
+  }
   hz2::Ctl ctl;
   memset(&ctl, 0, sizeof(ctl));
   hz2::ctl_reset(&ctl, 0);
-  hz2::Stats st2 = {};
-  int r2 = 0;
-  std::thread t([&]() {
-    r2 = hz2::inflate_stream<hz2::Stats, 2>(*sh2, job, tune, ring2, &st2, nullptr, hz2::Pipe{&ctl, sh, 1u});
-  });
-  const int r = hz2::inflate_stream<hz2::Stats, 2>(*sh, job, tune, ring, &st, nullptr, hz2::Pipe{&ctl, sh2, 0u});
-  t.join();
-  uint64_t* a = (uint64_t*)&st;
-  const uint64_t* b = (const uint64_t*)&st2;
-  for (size_t i = 0; i < sizeof(st) / 8; i++) a[i] += b[i];
-  free(ring2);
-  free(sh2);
-  return r == r2 ? r : -100;          // the two wavefronts disagree: a pipeline bug
+  std::thread t[NW];
+  for (int w = 1; w < NW; w++)
+    t[w] = std::thread([&, w]() {
+      rs[w] = hz2::inflate_stream<hz2::Stats, NW>(*sh[w], job, tune, ring[w], &sts[w], nullptr,
+                                                  hz2::Pipe{&ctl, sh[(w + NW - 1) % NW], (uint32_t)w});
+    });
+  rs[0] = hz2::inflate_stream<hz2::Stats, NW>(*sh[0], job, tune, ring[0], &sts[0], nullptr,
+                                              hz2::Pipe{&ctl, sh[NW - 1], 0u});
+  int r = rs[0];
+  for (int w = 1; w < NW; w++) {
+    t[w].join();
+    if (rs[w] != r) r = -100;          // the wavefronts disagree: a pipeline bug
+  }
+  for (int w = 0; w < NW; w++) {
+    uint64_t* a = (uint64_t*)&st;
+    const uint64_t* b = (const uint64_t*)&sts[w];
+    for (size_t i = 0; i < sizeof(st) / 8; i++) a[i] += b[i];
+  }
+  for (int w = 1; w < NW; w++) {
+    free(ring[w]);
+    free(sh[w]);
+  }
+  return r;
+}
+
+static int run_stream(hz2::Shared* sh, const hz2::Job& job, const hz2::Tune& tune, uint8_t* ring, hz2::Stats& st,
+                      int nwaves) {
+  if (nwaves >= 4) return run_pipe<4>(sh, job, tune, ring, st);
+  if (nwaves == 2) return run_pipe<2>(sh, job, tune, ring, st);
+  return hz2::inflate_stream<hz2::Stats, 1>(*sh, job, tune, ring, &st);
 }
 
 extern "C" int emu_inflate2_nw(const uint8_t* src, uint32_t src_len, uint8_t* dst, uint32_t dst_len, uint32_t W,

@@ -224,23 +224,25 @@ def test_long_overlapping_matches_and_far_distances(emu):
         assert r == 0 and out == data, level
 
 
-# ---- two wavefronts per stream (inflate2w_kernel's window pipeline, emulated by two threads) ----
+# ---- two and four wavefronts per stream (inflate2w_kernel's window pipeline, one thread each) ----
+@pytest.mark.parametrize("nw", [2, 4])
 @pytest.mark.parametrize("level", [0, 1, 4, 9])
-def test_two_wavefronts_match_zlib(emu, level):
+def test_two_wavefronts_match_zlib(emu, level, nw):
     for name, data in corpus().items():
         c = zlib.compress(data, level)
-        r, out, st = run(emu, c, len(data), nwaves=2)
+        r, out, st = run(emu, c, len(data), nwaves=nw)
         assert r == 0, (name, level, r)
         assert out == data, (name, level)
 
 
-def test_two_wavefronts_strategies_and_stored_blocks(emu):
+@pytest.mark.parametrize("nw", [2, 4])
+def test_two_wavefronts_strategies_and_stored_blocks(emu, nw):
     for strategy in (zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED):
         for name in ("smooth_f32", "text", "random", "runs"):
             data = corpus()[name]
             co = zlib.compressobj(5, zlib.DEFLATED, 15, 8, strategy)
             c = co.compress(data) + co.flush()
-            r, out, _ = run(emu, c, len(data), nwaves=2)
+            r, out, _ = run(emu, c, len(data), nwaves=nw)
             assert r == 0 and out == data, (name, strategy, r)
     # many small blocks of each type: a full flush after every piece
     rng = np.random.default_rng(4)
@@ -251,37 +253,40 @@ def test_two_wavefronts_strategies_and_stored_blocks(emu):
         data += piece
         c += co.compress(piece) + co.flush(zlib.Z_FULL_FLUSH)
     c += co.flush()
-    for nw in (1, 2):
-        r, out, st = run(emu, c, len(data), nwaves=nw)
-        assert r == 0 and out == data, nw
+    for n in (1, nw):
+        r, out, st = run(emu, c, len(data), nwaves=n)
+        assert r == 0 and out == data, n
     assert st["stored"] > 0
 
 
-def test_two_wavefronts_continuation_windows_and_f1_stream(emu):
+@pytest.mark.parametrize("nw", [2, 4])
+def test_two_wavefronts_continuation_windows_and_f1_stream(emu, nw):
     """one block over several windows (the continuation copies the other wavefront's tables),
     and a 256 KiB split of the bench chunk (7 blocks: both wavefronts alternate)"""
     import sys
     sys.path.insert(0, ROOT)
     from bench import smooth_chunk
     raw = smooth_chunk(20261015).view(np.uint8)[:262144].tobytes()
-    r, out, st = run(emu, zlib.compress(raw, 4), len(raw), nwaves=2)
+    r, out, st = run(emu, zlib.compress(raw, 4), len(raw), nwaves=nw)
     assert r == 0 and out == raw and st["windows"] >= st["blocks"]
     z = bytes(1 << 20)
-    r, out, st = run(emu, zlib.compress(z, 9), len(z), nwaves=2)
+    r, out, st = run(emu, zlib.compress(z, 9), len(z), nwaves=nw)
     assert r == 0 and out == z
     data = corpus()["smooth_f32"]
-    r, out, st = run(emu, zlib.compress(data, 4), len(data), over16=0, W=64, nwaves=2)
+    r, out, st = run(emu, zlib.compress(data, 4), len(data), over16=0, W=64, nwaves=nw)
     assert r == 0 and out == data
 
 
+@pytest.mark.parametrize("nw", [2, 4])
 @pytest.mark.parametrize("off", [1, 3])
-def test_two_wavefronts_unaligned_output(emu, off):
+def test_two_wavefronts_unaligned_output(emu, off, nw):
     data = corpus()["smooth_f32"][:50001]
-    r, out, _ = run(emu, zlib.compress(data, 4), len(data), dst_off=off, nwaves=2)
+    r, out, _ = run(emu, zlib.compress(data, 4), len(data), dst_off=off, nwaves=nw)
     assert r == 0 and out == data
 
 
-def test_two_wavefronts_corruptions_fail_like_libz(emu):
+@pytest.mark.parametrize("nw", [2, 4])
+def test_two_wavefronts_corruptions_fail_like_libz(emu, nw):
     import sys
     sys.path.insert(0, ROOT)
     from oracle import oracle as orc
@@ -302,12 +307,12 @@ def test_two_wavefronts_corruptions_fail_like_libz(emu):
             b = b + bytes(rng.integers(0, 256, 5, dtype=np.uint8))
         n = len(base)
         ref = orc.uncompress(bytes(b), "zlib", 0, 1, n)
-        r, out, _ = run(emu, bytes(b), n, nwaves=2)
+        r, out, _ = run(emu, bytes(b), n, nwaves=nw)
         if isinstance(ref, int):
             assert r < 0 and r != -100, (t, k, ref, r)
         else:
             assert r == 0 and out == ref, (t, k, r)
     data = corpus()["text"]
     c = zlib.compress(data, 4)
-    assert run(emu, c, len(data) - 1, nwaves=2)[0] not in (0, -100)
-    assert run(emu, c, len(data) + 1, nwaves=2)[0] not in (0, -100)
+    assert run(emu, c, len(data) - 1, nwaves=nw)[0] not in (0, -100)
+    assert run(emu, c, len(data) + 1, nwaves=nw)[0] not in (0, -100)

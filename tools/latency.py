@@ -50,7 +50,7 @@ def main():
         d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
         d_st = torch.zeros(1, dtype=torch.int32, device=dev)
         for mode, key in ((0, "device_one_chunk_kernel_ms"), (1, "device_one_chunk_kernel_ms_1wave"),
-                          (2, "device_one_chunk_kernel_ms_2wave")):
+                          (2, "device_one_chunk_kernel_ms_2wave"), (4, "device_one_chunk_kernel_ms_4wave")):
             eng.set_tuning(waves_per_stream=mode)
             ks = []
             for _ in range(10):
