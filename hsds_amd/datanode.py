@@ -155,17 +155,28 @@ class _Node:
         self.last_access = time.time()
 
 
+_TORCH_DT = {}
+
+
+def _torch_dtype(dtype):
+    """torch dtype of a numpy dtype (None: no equivalent, e.g. compound types); cached, as
+    a read batch asks once per chunk"""
+    dt = np.dtype(dtype)
+    if dt not in _TORCH_DT:
+        import torch
+        m = {np.dtype(k): v for k, v in ((np.float32, torch.float32), (np.float64, torch.float64),
+                                         (np.float16, torch.float16), (np.int8, torch.int8), (np.uint8, torch.uint8),
+                                         (np.int16, torch.int16), (np.int32, torch.int32), (np.int64, torch.int64),
+                                         (np.uint16, torch.uint16), (np.uint32, torch.uint32),
+                                         (np.uint64, torch.uint64), (np.bool_, torch.bool))}
+        _TORCH_DT[dt] = m.get(dt.newbyteorder("=")) if dt.isnative or dt.itemsize == 1 else None
+    return _TORCH_DT[dt]
+
+
 def device_view(u8, shape, dtype):
     """Typed torch view of a uint8 device slice (falls back to the uint8 bytes for
     numpy dtypes torch has no equivalent of, e.g. compound types)."""
-    import torch
-    m = {np.dtype(k): v for k, v in ((np.float32, torch.float32), (np.float64, torch.float64),
-                                     (np.float16, torch.float16), (np.int8, torch.int8), (np.uint8, torch.uint8),
-                                     (np.int16, torch.int16), (np.int32, torch.int32), (np.int64, torch.int64),
-                                     (np.uint16, torch.uint16), (np.uint32, torch.uint32),
-                                     (np.uint64, torch.uint64), (np.bool_, torch.bool))}
-    dt = np.dtype(dtype)
-    td = m.get(dt.newbyteorder("=")) if dt.isnative or dt.itemsize == 1 else None
+    td = _torch_dtype(dtype)
     if td is None:
         return u8
     return u8.view(td).reshape(shape)

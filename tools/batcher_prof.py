@@ -78,11 +78,20 @@ def main():
     print(f"n={n} median {np.median(els)*1e3:.2f} ms  {n * CHUNK_BYTES / np.median(els) / 1e9:.2f} GB/s")
     for k, v in T.items():
         print(f"  {k:16s} {v / 5 * 1e3:8.2f} ms per batch")
+    # the batch runs on the batcher's worker thread: profile inside _run_batch
     pr = cProfile.Profile()
-    pr.enable()
+    orig = bt.ChunkBatcher._run_batch
+
+    def prof_run(self, *a, **k):
+        pr.enable()
+        try:
+            return orig(self, *a, **k)
+        finally:
+            pr.disable()
+    bt.ChunkBatcher._run_batch = prof_run
     one()
-    pr.disable()
-    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+    bt.ChunkBatcher._run_batch = orig
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
 
 
 if __name__ == "__main__":
