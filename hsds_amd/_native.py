@@ -105,6 +105,7 @@ def lib():
         "hsds_plan_descs": (I, [P, P, P, P, P, P, I64, P, P]),
         "hsds_host_map": (I, [P, P, U64, ctypes.POINTER(ctypes.c_void_p)]),
         "hsds_host_unmap": (I, [P, P]),
+        "hsds_stage_upload": (I, [P, P, P, P, I64, P, P, U64, I, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

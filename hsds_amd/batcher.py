@@ -31,6 +31,20 @@ __all__ = ["ChunkBatcher"]
 
 
 def _freeze(x):
+    """hashable, value-equal key of a request parameter (per request, so the common
+    cases -- None, scalars, a flat dict of hashable values such as getFilterOps' -- stay
+    off the JSON encoder)"""
+    if x is None or isinstance(x, (bool, int, str, bytes)):
+        return x
+    if isinstance(x, float):
+        return x if x == x else "nan"       # every NaN fill value is one group
+    if isinstance(x, dict):
+        try:
+            items = tuple(sorted(x.items()))
+            hash(items)
+            return ("dict", items)
+        except TypeError:
+            pass
     try:
         return json.dumps(x, sort_keys=True, default=str)
     except TypeError:

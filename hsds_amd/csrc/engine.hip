@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -2105,6 +2106,58 @@ int hsds_host_unmap(hsds_engine* e, void* p) {
   if (!e || !p) return HSDS_ERR_ARG;
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
   return hipHostUnregister(p) == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
+}
+
+// Staging of a read batch's stored objects: `threads` host threads copy the objects into
+// the page-locked buffer, piece by piece in ascending order of offset (pieces of about
+// total / 32 bytes, whole objects each), and the calling thread queues each piece's
+// host-to-device copy as soon as every object below its end is staged, so the link
+// works while later pieces are still being copied.  The calling thread copies pieces
+// too while it waits.
+int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* lens, const uint64_t* offs,
+                      int64_t n, void* h_stage, void* d_dst, uint64_t total, int threads, void* stream) {
+  if (!e || n < 0 || (n && (!srcs || !lens || !offs || !h_stage || !d_dst))) return HSDS_ERR_ARG;
+  if (n == 0 || total == 0) return HSDS_OK;
+  for (int64_t k = 0; k < n; k++)
+    if ((lens[k] && !srcs[k]) || offs[k] > total || lens[k] > total - offs[k] || (k && offs[k] < offs[k - 1]))
+      return HSDS_ERR_ARG;
+  if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
+  uint8_t* const host = (uint8_t*)h_stage;
+  // piece p = objects [cut[p], cut[p + 1]); the last piece's upload runs to `total`
+  const int64_t parts = n < 32 ? n : 32;
+  std::vector<int64_t> cut(parts + 1);
+  for (int64_t p = 0; p <= parts; p++) cut[p] = n * p / parts;
+  std::vector<std::atomic<int>> done(parts);
+  for (auto& d : done) d.store(0, std::memory_order_relaxed);
+  std::atomic<int64_t> next{0};
+  auto copy_piece = [&](int64_t p) {
+    for (int64_t k = cut[p]; k < cut[p + 1]; k++)
+      if (lens[k]) memcpy(host + offs[k], srcs[k], (size_t)lens[k]);
+    done[p].store(1, std::memory_order_release);
+  };
+  auto worker = [&]() {
+    for (int64_t p; (p = next.fetch_add(1, std::memory_order_relaxed)) < parts;) copy_piece(p);
+  };
+  const int nt = threads < 1 ? 0 : (threads > 64 ? 63 : threads - 1);
+  std::vector<std::thread> pool;
+  pool.reserve(nt);
+  for (int t = 0; t < nt && t + 1 < parts; t++) pool.emplace_back(worker);
+  int rc = HSDS_OK;
+  for (int64_t p = 0; p < parts; p++) {
+    while (!done[p].load(std::memory_order_acquire)) {
+      const int64_t q = next.fetch_add(1, std::memory_order_relaxed);
+      if (q < parts) copy_piece(q);
+      else std::this_thread::yield();
+    }
+    const uint64_t lo = offs[cut[p]];
+    const uint64_t hi = p + 1 < parts ? offs[cut[p + 1]] : total;
+    if (rc == HSDS_OK && hi > lo &&
+        hipMemcpyAsync((uint8_t*)d_dst + lo, host + lo, (size_t)(hi - lo), hipMemcpyHostToDevice,
+                       (hipStream_t)stream) != hipSuccess)
+      rc = HSDS_ERR_DEVICE;
+  }
+  for (auto& t : pool) t.join();
+  return rc;
 }
 
 int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d_tabs, const int64_t* d_piece,

@@ -21,6 +21,8 @@ into their slots of an HBM-resident cache arena (DeviceChunkCache).  The
 storage read itself (POSIX / S3 / Azure drivers) stays outside this engine: callers
 pass `fetch(key, offset, length) -> bytes | None` (None = object not found).
 """
+import ctypes
+import os
 import time
 from collections import OrderedDict, namedtuple
 from operator import attrgetter
@@ -711,15 +713,9 @@ class ChunkReader:
         return finish()
 
 
-_POOL = None
-
-
-def _stage_pool():
-    global _POOL
-    if _POOL is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix="hsds-amd-stage")
-    return _POOL
+# host threads copying a large batch into page-locked staging (the GPU box's CPU share is
+# 16 cores; the DN's event loop and the batch worker keep theirs)
+_STAGE_THREADS = int(os.environ.get("HSDS_STAGE_THREADS", "8"))
 
 
 def _stage_blobs(blobs, dst_lens, device, align=256):
@@ -746,28 +742,30 @@ def _stage_blobs(blobs, dst_lens, device, align=256):
     descs["dst_len"] = dl
     total = int(pad.sum()) if n else 0
     host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
-    h = host.numpy()
-
-    def put(k0, k1):
-        for o, b in zip(src_off[k0:k1].tolist(), blobs[k0:k1]):
-            h[o:o + len(b)] = np.frombuffer(b, np.uint8) if not isinstance(b, np.ndarray) else b
     d_src = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
-    if total >= (32 << 20) and n >= 32:
-        # large batches: the copies into staging run on the host's cores (numpy drops the GIL)
-        # in 32 pieces, and each piece goes up as soon as it is staged, so the link works
-        # while the later pieces are still being copied
-        parts = 32
-        cuts = [n * i // parts for i in range(parts + 1)]
-        futs = [_stage_pool().submit(put, cuts[i], cuts[i + 1]) for i in range(parts)]
-        for i, f in enumerate(futs):
-            f.result()
-            lo = int(src_off[cuts[i]])
-            hi = int(src_off[cuts[i + 1]]) if cuts[i + 1] < n else total
-            if hi > lo:
-                d_src[lo:hi].copy_(host[lo:hi], non_blocking=True)
-    else:
-        put(0, n)
-        d_src.copy_(host, non_blocking=True)
+    if total:
+        # hsds_stage_upload: the copies into staging run on native threads (no GIL), in
+        # pieces that go up as soon as they are staged, so the link works while the later
+        # pieces are still being copied
+        keep, ptrs = [], np.empty(n, np.uint64)
+        for k, b in enumerate(blobs):
+            if isinstance(b, np.ndarray):
+                b = np.ascontiguousarray(b).reshape(-1).view(np.uint8)
+                keep.append(b)
+                ptrs[k] = b.__array_interface__["data"][0]
+            else:
+                ptrs[k] = ctypes.cast(b, ctypes.c_void_p).value or 0
+        lens_u = lens.astype(np.uint64)
+        offs_u = src_off.astype(np.uint64)
+        threads = _STAGE_THREADS if total >= (8 << 20) else 1
+        rc = nat.lib().hsds_stage_upload(nat.engine(d_src.device.index).h, ptrs.ctypes.data, lens_u.ctypes.data,
+                                         offs_u.ctypes.data, n, host.data_ptr(), d_src.data_ptr(), total, threads,
+                                         torch.cuda.current_stream(d_src.device).cuda_stream)
+        if rc != nat.OK:
+            raise nat.NativeError(rc, "hsds_stage_upload")
+        # one byte through torch's copy on the same stream, after the staged copies: the
+        # pinned-memory cache records its event and keeps `host` reserved until they ran
+        d_src[:1].copy_(host[:1], non_blocking=True)
     return d_src, descs, int(dpad.sum()) if n else 0
 
 

@@ -216,6 +216,17 @@ int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d
 int hsds_host_map(hsds_engine* e, void* p, uint64_t n, void** d_ptr);
 int hsds_host_unmap(hsds_engine* e, void* p);
 
+/* ---- read-batch staging (the DN's get_chunk batch, datanode_lib.py:948-1142) -----
+ * The stored objects a batch fetched (storUtil.getStorBytes' bytes, storUtil.py:450-522)
+ * are host buffers srcs[k] of lens[k] bytes.  hsds_stage_upload copies object k to
+ * h_stage + offs[k] (page-locked, offs ascending, every object inside [0, total)) with
+ * `threads` host threads, and queues the host-to-device copy of h_stage[0, total) to
+ * d_dst on `stream` in pieces, each as soon as the objects below its end are staged.
+ * Returns once every copy is queued; h_stage must stay allocated until the stream has
+ * run them. */
+int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* lens, const uint64_t* offs,
+                      int64_t n, void* h_stage, void* d_dst, uint64_t total, int threads, void* stream);
+
 /* ---- encode (write path) ---------------------------------------------------- */
 /* Batched, device-resident encode into HSDS F1 objects: chunk k (d_chunks[k].src_off /
  * src_len in d_src) becomes a Blosc1 frame with the zlib codec at level `clevel`

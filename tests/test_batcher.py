@@ -88,3 +88,25 @@ def test_max_batch_dispatches_early():
     assert [len(c) for c in store.calls] == [5, 5]
     for i in range(10):
         np.testing.assert_array_equal(res[i], chunks[f"c-{i}"])
+
+
+def test_group_keys():
+    """equal parameters share a group whatever the dict object or key order; different
+    values, unhashable values (JSON fallback) and NaN fill values behave as values"""
+    from hsds_amd.batcher import _freeze
+    a = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
+    b = {"dtype": np.dtype("<f4"), "level": 4, "shuffle": 1, "compressor": "zlib"}
+    assert _freeze(a) == _freeze(b) and hash(_freeze(a)) == hash(_freeze(b))
+    assert _freeze(a) != _freeze(dict(a, level=5))
+    assert _freeze({"x": [1, 2]}) == _freeze({"x": [1, 2]}) != _freeze({"x": [1, 3]})
+    assert _freeze(float("nan")) == _freeze(np.nan) and _freeze(None) is None
+    assert _freeze([1.5, 2]) == _freeze([1.5, 2])
+    chunks = _chunks(2)
+    store = FakeStore(chunks)
+    bt = ChunkBatcher(store, window_ms=20)
+
+    async def main():
+        return await asyncio.gather(*[bt.get_chunk(ChunkRead(f"c-{i}", "k"), np.float32, (8, 16),
+                                                   filter_ops=dict(a) if i else dict(b)) for i in range(2)])
+    asyncio.run(main())
+    assert len(store.calls) == 1
