@@ -1784,13 +1784,14 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
     tmp = e->tmp;
   }
   // one match ring per resident inflate wave.  A batch whose zlib streams (at most 4 per
-  // chunk in HSDS's F1 frames, 1 per F2 chunk) cannot fill half the resident wavefronts
-  // decodes every stream with two wavefronts (inflate2w_kernel)
+  // chunk in HSDS's F1 frames, 1 per F2 chunk) cannot fill the resident wavefronts decodes
+  // every stream with two or four wavefronts (inflate2w_kernel)
   const int64_t waves1 = (int64_t)e->num_cus * e->inflate_blocks_per_cu;
   // wavefronts per stream: by batch size, the most whose streams (at most 4 per chunk) all
-  // fit in half the resident wavefronts
+  // fit in the resident wavefronts (256 F1 chunks, DN micro-batcher: 4 wavefronts decode
+  // in 3.9 ms, 2 in 5.1, 1 in 5.6; tools/batcher_prof.py)
   int nw = e->inflate_pipe;
-  if (nw == 0) nw = nchunks * 4 * 4 * 2 <= waves1 ? 4 : nchunks * 4 * 2 <= waves1 ? 2 : 1;
+  if (nw == 0) nw = nchunks * 4 * 4 <= waves1 ? 4 : nchunks * 4 * 2 <= waves1 ? 2 : 1;
   const bool pipe = nw > 1;
   int64_t grid = nw == 4 ? (int64_t)e->num_cus * e->inflate4w_blocks_per_cu
                  : nw == 2 ? (int64_t)e->num_cus * e->inflate2w_blocks_per_cu : waves1;
@@ -2108,12 +2109,12 @@ int hsds_host_unmap(hsds_engine* e, void* p) {
   return hipHostUnregister(p) == hipSuccess ? HSDS_OK : HSDS_ERR_DEVICE;
 }
 
-// Staging of a read batch's stored objects: `threads` host threads copy the objects into
-// the page-locked buffer, piece by piece in ascending order of offset (pieces of about
-// total / 32 bytes, whole objects each), and the calling thread queues each piece's
-// host-to-device copy as soon as every object below its end is staged, so the link
-// works while later pieces are still being copied.  The calling thread copies pieces
-// too while it waits.
+// Staging of a read batch's stored objects: `threads` host threads (the calling one among
+// them) take pieces of whole objects in ascending order, copy them into the page-locked
+// buffer and queue each piece's host-to-device copy as soon as it is staged, so the link
+// starts after the first pieces instead of after the last.  At most 16 pieces of at least
+// 2 MiB: 150 MiB goes up at 57 GB/s in one copy, 54 in 16, 46 in 64 and 29 in 256
+// (tools/pcie_bw.py).
 int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* lens, const uint64_t* offs,
                       int64_t n, void* h_stage, void* d_dst, uint64_t total, int threads, void* stream) {
   if (!e || n < 0 || (n && (!srcs || !lens || !offs || !h_stage || !d_dst))) return HSDS_ERR_ARG;
@@ -2124,40 +2125,33 @@ int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* l
   if (hipSetDevice(e->device) != hipSuccess) return HSDS_ERR_DEVICE;
   uint8_t* const host = (uint8_t*)h_stage;
   // piece p = objects [cut[p], cut[p + 1]); the last piece's upload runs to `total`
-  const int64_t parts = n < 32 ? n : 32;
+  int64_t parts = (int64_t)(total >> 21);
+  parts = parts < 1 ? 1 : parts > 16 ? 16 : parts;
+  if (parts > n) parts = n;
   std::vector<int64_t> cut(parts + 1);
   for (int64_t p = 0; p <= parts; p++) cut[p] = n * p / parts;
-  std::vector<std::atomic<int>> done(parts);
-  for (auto& d : done) d.store(0, std::memory_order_relaxed);
   std::atomic<int64_t> next{0};
-  auto copy_piece = [&](int64_t p) {
-    for (int64_t k = cut[p]; k < cut[p + 1]; k++)
-      if (lens[k]) memcpy(host + offs[k], srcs[k], (size_t)lens[k]);
-    done[p].store(1, std::memory_order_release);
-  };
+  std::atomic<int> rc{HSDS_OK};
+  const int dev = e->device;
   auto worker = [&]() {
-    for (int64_t p; (p = next.fetch_add(1, std::memory_order_relaxed)) < parts;) copy_piece(p);
+    if (hipSetDevice(dev) != hipSuccess) { rc.store(HSDS_ERR_DEVICE); return; }
+    for (int64_t p; (p = next.fetch_add(1, std::memory_order_relaxed)) < parts;) {
+      for (int64_t k = cut[p]; k < cut[p + 1]; k++)
+        if (lens[k]) memcpy(host + offs[k], srcs[k], (size_t)lens[k]);
+      const uint64_t lo = offs[cut[p]];
+      const uint64_t hi = p + 1 < parts ? offs[cut[p + 1]] : total;
+      if (hi > lo && hipMemcpyAsync((uint8_t*)d_dst + lo, host + lo, (size_t)(hi - lo), hipMemcpyHostToDevice,
+                                    (hipStream_t)stream) != hipSuccess)
+        rc.store(HSDS_ERR_DEVICE);
+    }
   };
   const int nt = threads < 1 ? 0 : (threads > 64 ? 63 : threads - 1);
   std::vector<std::thread> pool;
   pool.reserve(nt);
   for (int t = 0; t < nt && t + 1 < parts; t++) pool.emplace_back(worker);
-  int rc = HSDS_OK;
-  for (int64_t p = 0; p < parts; p++) {
-    while (!done[p].load(std::memory_order_acquire)) {
-      const int64_t q = next.fetch_add(1, std::memory_order_relaxed);
-      if (q < parts) copy_piece(q);
-      else std::this_thread::yield();
-    }
-    const uint64_t lo = offs[cut[p]];
-    const uint64_t hi = p + 1 < parts ? offs[cut[p + 1]] : total;
-    if (rc == HSDS_OK && hi > lo &&
-        hipMemcpyAsync((uint8_t*)d_dst + lo, host + lo, (size_t)(hi - lo), hipMemcpyHostToDevice,
-                       (hipStream_t)stream) != hipSuccess)
-      rc = HSDS_ERR_DEVICE;
-  }
+  worker();
   for (auto& t : pool) t.join();
-  return rc;
+  return rc.load();
 }
 
 int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d_tabs, const int64_t* d_piece,

@@ -113,7 +113,7 @@ const char* hsds_strerror(int status);
 /* Tuning of the inflate kernel: segment over-provisioning against the previous
  * deflate block in 16ths (0..16), warm-up bits before a segment (0..4096), wavefronts
  * per zlib stream (0: by batch size -- four or two when the batch's streams times that
- * fit in half the resident wavefronts --, 1, 2 or 4), repair rounds per window (0..64).  Any setting
+ * fit in the resident wavefronts --, 1, 2 or 4), repair rounds per window (0..64).  Any setting
  * decodes the same bytes; it only moves work between the phases and wavefronts.
  * Defaults are set by hsds_engine_create; HSDS_TUNE_KEEP (rounds: -1) leaves a setting
  * unchanged. */
@@ -221,7 +221,7 @@ int hsds_host_unmap(hsds_engine* e, void* p);
  * are host buffers srcs[k] of lens[k] bytes.  hsds_stage_upload copies object k to
  * h_stage + offs[k] (page-locked, offs ascending, every object inside [0, total)) with
  * `threads` host threads, and queues the host-to-device copy of h_stage[0, total) to
- * d_dst on `stream` in pieces, each as soon as the objects below its end are staged.
+ * d_dst on `stream` in pieces of whole objects, each as soon as it is staged.
  * Returns once every copy is queued; h_stage must stay allocated until the stream has
  * run them. */
 int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* lens, const uint64_t* offs,

@@ -34,6 +34,17 @@ def main():
                 h2.copy_(d2, non_blocking=True)
         bi = rate(both, 2 * n)
         print(f"{mb:4d} MiB  H2D {h2d:6.1f} GB/s  D2H {d2h:6.1f} GB/s  both {bi:6.1f} GB/s (sum)")
+    # 150 MB host-to-device in pieces (the read batch's staged upload)
+    n = 150 << 20
+    h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    for parts in (1, 4, 16, 64, 256):
+        cuts = [n * i // parts for i in range(parts + 1)]
+
+        def pieces():
+            for i in range(parts):
+                d[cuts[i]:cuts[i + 1]].copy_(h[cuts[i]:cuts[i + 1]], non_blocking=True)
+        print(f"150 MiB H2D in {parts:3d} pieces: {rate(pieces, n):6.1f} GB/s")
 
 
 if __name__ == "__main__":
