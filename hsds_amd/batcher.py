@@ -140,8 +140,8 @@ class ChunkBatcher:
             return _gather(None, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
         import torch
         # decode, selection gather and both host copies of a group are queued on one stream;
-        # a large batch is two groups on two streams, so the first group's download runs
-        # under the second group's upload and decode (the engine orders the two decodes);
+        # a large batch is two groups on two streams with an engine (workspace) each, so the
+        # second group's upload and decode run beside the first group's decode and download;
         # the batch waits for the device once
         dev = store.cache.arena.buf.device
         ng = 2 if len(order) >= SPLIT_READS else 1
@@ -157,7 +157,8 @@ class ChunkBatcher:
                     mine = [k for k, (r, _, _) in enumerate(reqs) if group[r.chunk_id] == g]
                     gi = {r.chunk_id: j for j, r in enumerate(order[cuts[g]:cuts[g + 1]])}
                     with torch.cuda.stream(streams[g]):
-                        vals, finish = store.get_chunks_deferred(order[cuts[g]:cuts[g + 1]], dtype, chunk_dims, **kw)
+                        vals, finish = store.get_chunks_deferred(order[cuts[g]:cuts[g + 1]], dtype, chunk_dims,
+                                                                 engine_slot=g, **kw)
                         parts.append([mine, gi, finish, None])
                         items = [(vals[gi[reqs[k][0].chunk_id]], reqs[k][1]) for k in mine]
                         parts[-1][3] = _gather_launch(items, dtype, chunk_dims)

@@ -900,7 +900,9 @@ __global__ void __launch_bounds__(64) parse_kernel(const EncItem* __restrict__ s
   const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
   const int lane = threadIdx.x;
   hd::Tune tune = hd::tune_for_level(level);
-  if (chain_ovr) tune.chain = chain_ovr;     // development override (HSDS_DEFLATE_CHAIN)
+  // development overrides (HSDS_DEFLATE_CHAIN, HSDS_DEFLATE_FAR): chain depth, far ring
+  if (chain_ovr & 0xffffu) tune.chain = chain_ovr & 0xffffu;
+  if (chain_ovr >> 16) tune.far = 1u;
 #ifdef HZ_PROFILE
   HzProf prof_;
   for (int i = 0; i < 16; i++) prof_.acc[i] = 0;
@@ -1500,7 +1502,8 @@ struct hsds_engine {
   size_t efar_bytes = 0;
   uint8_t* ezs = nullptr;      // encode: zstd block scratch (one ZCAP slot + size per segment)
   size_t ezs_bytes = 0;
-  uint32_t enc_chain = 0;      // development override of the parse chain depth (0: the level's)
+  uint32_t enc_chain = 0;      // development overrides: parse chain depth (bits 0-15, 0: the level's),
+                               // far ring at any level (bit 16)
   hipEvent_t ev2, ev3;
   int ev_enc_valid = 0;
   // re-entrancy (SURVEY 8b "Threading"): every entry point that uses the workspace holds mu
@@ -1670,6 +1673,9 @@ int hsds_engine_create(int device, hsds_engine** out) {
   if (const char* ev = getenv("HSDS_DEFLATE_CHAIN")) {   // development override (A/B experiments)
     const int v = atoi(ev);
     if (v >= 1 && v <= 4096) e->enc_chain = (uint32_t)v;
+  }
+  if (const char* ev = getenv("HSDS_DEFLATE_FAR")) {     // development override: far ring at any level
+    if (atoi(ev) == 1) e->enc_chain |= 1u << 16;
   }
   e->huff_blocks_per_cu = o2;
   e->emit_blocks_per_cu = o3;
@@ -2253,7 +2259,7 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
   };
   const unsigned pgrid = grid_for(e->parse_blocks_per_cu, item_cap);
   uint16_t* far = nullptr;
-  if ((cname == HSDS_CNAME_ZLIB || cname == HSDS_CNAME_ZSTD) && hd::far_level(clevel)) {
+  if ((cname == HSDS_CNAME_ZLIB || cname == HSDS_CNAME_ZSTD) && (hd::far_level(clevel) || (e->enc_chain >> 16))) {
     // levels >= 6: matches reach 32 KiB back, the chains beyond the LDS ring live in HBM
     if (grow((void**)&e->efar, &e->efar_bytes, (size_t)pgrid * hd::FARW * 2)) return HSDS_ERR_DEVICE;
     far = (uint16_t*)e->efar;
