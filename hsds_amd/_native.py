@@ -182,17 +182,15 @@ class Engine:
         return v.value
 
 
-def engine(device=None, slot=0):
-    """Process-wide engine for `device` (default: torch's current device).  slot > 0: a
-    further engine of that device with its own workspace, so that its decodes need not
-    wait for slot 0's (the DN batcher's second read group on a second stream)."""
+def engine(device=None):
+    """Process-wide engine for `device` (default: torch's current device)."""
     if device is None:
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("hsds_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
         device = torch.cuda.current_device()
-    e = _engines.get((device, slot))
+    e = _engines.get(device)
     if e is None:
         e = Engine(device)
-        _engines[(device, slot)] = e
+        _engines[device] = e
     return e

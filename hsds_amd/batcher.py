@@ -8,9 +8,7 @@ chunk id wait on the first (pending_s3_read, datanode_lib.py:1041-1065).  One st
 request is 1-4 zlib streams on a GPU that needs thousands to be busy, so the DN side
 gathers the requests that arrive within a short window (or up to max_batch of them) into
 ONE ChunkStore.get_chunks batch -- one decode launch -- and ONE selection-gather launch
-with one device-to-host copy for all their chunkReadSelection results (a batch of
-SPLIT_READS or more chunks: two such groups on two streams, so that one group's
-download overlaps the other's upload and decode).  Requests for the
+with one device-to-host copy for all their chunkReadSelection results.  Requests for the
 same chunk id in a window share one read (the reference's dedupe); requests whose dataset
 parameters differ (dtype, layout, filters, fill value) form separate groups.
 
@@ -139,58 +137,15 @@ class ChunkBatcher:
             vals = store.get_chunks(order, dtype, chunk_dims, **kw)
             return _gather(None, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
         import torch
-        # decode, selection gather and both host copies of a group are queued on one stream;
-        # a large batch is two groups on two streams with an engine (workspace) each, so the
-        # second group's upload and decode run beside the first group's decode and download;
-        # the batch waits for the device once
-        dev = store.cache.arena.buf.device
-        ng = 2 if len(order) >= SPLIT_READS else 1
-        cuts = [len(order) * g // ng for g in range(ng + 1)]
-        streams = [torch.cuda.current_stream(dev)] + [_side_stream(dev, g) for g in range(1, ng)]
-        group = {r.chunk_id: g for g in range(ng) for r in order[cuts[g]:cuts[g + 1]]}
-        for s in streams[1:]:
-            s.wait_stream(streams[0])          # device work queued before the batch
+        # decode, selection gather and both host copies are queued on one stream; the
+        # batch waits for the device once
         with store.lock:
-            parts, launched = [], False
-            try:
-                for g in range(ng):
-                    mine = [k for k, (r, _, _) in enumerate(reqs) if group[r.chunk_id] == g]
-                    gi = {r.chunk_id: j for j, r in enumerate(order[cuts[g]:cuts[g + 1]])}
-                    with torch.cuda.stream(streams[g]):
-                        vals, finish = store.get_chunks_deferred(order[cuts[g]:cuts[g + 1]], dtype, chunk_dims,
-                                                                 engine_slot=g, **kw)
-                        parts.append([mine, gi, finish, None])
-                        items = [(vals[gi[reqs[k][0].chunk_id]], reqs[k][1]) for k in mine]
-                        parts[-1][3] = _gather_launch(items, dtype, chunk_dims)
-                launched = True
-            finally:
-                for s in streams[1:]:
-                    streams[0].wait_stream(s)
-                streams[0].synchronize()
-                if not launched:
-                    for p in parts:           # a group failed to launch: release every group's pins
-                        p[2]()
-            out = [None] * len(reqs)
-            for mine, gi, finish, plan in parts:
-                vals = finish()
-                res = _gather_finish(plan, [(vals[gi[reqs[k][0].chunk_id]], reqs[k][1]) for k in mine], dtype,
-                                     chunk_dims)
-                for k, v in zip(mine, res):
-                    out[k] = v
-        return out
-
-
-# a batch of at least this many distinct chunk reads is decoded as two groups on two streams
-SPLIT_READS = 128
-_SIDE = {}
-
-
-def _side_stream(dev, g):
-    import torch
-    key = (dev.index, g)
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=dev)
-    return _SIDE[key]
+            vals, finish = store.get_chunks_deferred(order, dtype, chunk_dims, **kw)
+            items = [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs]
+            plan = _gather_launch(items, dtype, chunk_dims)
+            torch.cuda.current_stream(store.cache.arena.buf.device).synchronize()
+            vals = finish()
+        return _gather_finish(plan, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
 
 
 def _sel_shape(slices, chunk_dims):

@@ -573,7 +573,7 @@ class ChunkReader:
         return out
 
     def read(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
-             hyper_dims=None, defer=False, engine_slot=0):
+             hyper_dims=None, defer=False):
         """Decode a batch of chunks.  Returns a list (one entry per read) of device
         arrays (typed torch views of chunk_dims), or an exception instance:
         HTTPNotFound (object missing), HTTPInternalServerError (codec failure or a
@@ -583,12 +583,9 @@ class ChunkReader:
         defer=True returns (results, finish) without waiting for the device: the views
         are valid once the current stream has drained, and finish() -- called after
         that -- turns failed decodes into HTTPInternalServerError and returns the final
-        list (the batcher gathers the selections before its single synchronisation).
-        engine_slot > 0 decodes with a further engine of the device (its own workspace), so
-        a batch on another stream need not wait for this reader's other decodes."""
+        list (the batcher gathers the selections before its single synchronisation)."""
         import torch
-        from .engine import COPY_DESC_DTYPE, ChunkEngine, pack_chunks
-        eng = self.eng if not engine_slot else ChunkEngine(self.device.index, engine_slot)
+        from .engine import COPY_DESC_DTYPE, pack_chunks
         dtype = np.dtype(dtype)
         chunk_dims = tuple(int(c) for c in chunk_dims)
         comp, shuffle, isz = _filter_args(filter_ops, dtype)
@@ -652,7 +649,7 @@ class ChunkReader:
             d_src, descs, ext = _stage_blobs(dblobs, sizes, self.device)
             dbuf = torch.empty(max(ext, 1), dtype=torch.uint8, device=self.device)
             status = torch.full((len(dec),), 99, dtype=torch.int32, device=self.device)
-            _decode_batch(eng, d_src, descs, dbuf, status, comp, shuffle, isz, dblobs)
+            _decode_batch(self.eng, d_src, descs, dbuf, status, comp, shuffle, isz, dblobs)
             self.stats["decode_calls"] += 1
             self.stats["objects"] += sum(1 for _, k, _, _ in dec if k == "plain")
             self.stats["h5_chunks"] += sum(1 for _, k, _, _ in dec if k == "h5")
@@ -684,7 +681,7 @@ class ChunkReader:
                 recs["rank"][flat] = 1
                 recs["itemsize"][flat] = w
             for base, rows in groups.values():
-                eng.copy(dbuf, base, recs[np.asarray(rows)])
+                self.eng.copy(dbuf, base, recs[np.asarray(rows)])
         else:
             reserve_slots()
         for ri in need:
@@ -853,7 +850,7 @@ class ChunkStore:
             return finish()
 
     def get_chunks_deferred(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
-                            hyper_dims=None, chunk_init=False, engine_slot=0):
+                            hyper_dims=None, chunk_init=False):
         """get_chunks without waiting for the device: (values, finish).  The values are
         device views (None for a 404, an exception for a malformed request) whose bytes
         are ready once the current stream has drained; finish(), called after that,
@@ -877,8 +874,7 @@ class ChunkStore:
         try:
             if todo:
                 res, rfin = self.reader.read(todo, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
-                                             layout_class=layout_class, hyper_dims=hyper_dims, defer=True,
-                                             engine_slot=engine_slot)
+                                             layout_class=layout_class, hyper_dims=hyper_dims, defer=True)
                 init = [r.chunk_id for r, v in zip(todo, res) if isinstance(v, HTTPNotFound) and chunk_init]
                 if init:
                     self._fill_new(init, dtype, chunk_dims, fill_value)

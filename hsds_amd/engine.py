@@ -102,11 +102,11 @@ class ChunkEngine:
     """Batched decode of HSDS chunk objects (F1 Blosc-zlib frames, F2 zlib+shuffle
     streams, raw chunks) resident in device memory."""
 
-    def __init__(self, device=None, slot=0):
+    def __init__(self, device=None):
         if device is None:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-        self.eng = nat.engine(self.device.index, slot)
+        self.eng = nat.engine(self.device.index)
 
     def set_tuning(self, **kw):
         self.eng.set_tuning(**kw)

@@ -115,39 +115,3 @@ def test_hits_stay_pinned_while_misses_reserve(oracle_lib):
         np.testing.assert_array_equal(r, truth[f"c-b_{i}_0"])
     assert all(n.pinned == 0 for n in cs.cache._lru.values())
 
-
-@pytest.mark.parametrize("split", [16, 128])
-def test_split_batch_two_streams(oracle_lib, monkeypatch, split):
-    """a batch of SPLIT_READS+ distinct reads is decoded as two groups on two streams:
-    duplicates, 404s, cache hits from an earlier batch, strided selections and a cache
-    too small for the batch all come back bit-exact, and no cache node stays pinned"""
-    import torch
-    from hsds_amd import batcher as bt
-    from hsds_amd.datanode import ChunkRead, ChunkStore
-    monkeypatch.setattr(bt, "SPLIT_READS", split)
-    dev = torch.device("cuda", 0)
-    dims = (32, 48)
-    truth, objs = _objs(oracle_lib, 150, dims, 13)
-    chunk_bytes = dims[0] * dims[1] * 4
-    cs = ChunkStore(lambda key, off, ln: objs.get(key), mem_target=100 * chunk_bytes, device=dev)
-    ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
-    cs.get_chunks([ChunkRead(f"c-b_{i}_0", f"k{i}") for i in range(0, 150, 7)], "<f4", dims, filter_ops=ops)
-    b = bt.ChunkBatcher(cs, window_ms=50)
-    sels = [None, (slice(3, 31, 4), slice(1, 48, 5)), (slice(10, 11, 1), slice(0, 48, 2))]
-
-    def key(j):
-        return 150 + j % 3 if j % 41 == 0 else j % 150         # some objects do not exist
-
-    async def main():
-        return await asyncio.gather(*[b.get_selection(ChunkRead(f"c-b_{key(j)}_0", f"k{key(j)}"), "<f4", dims,
-                                                      sels[j % 3], filter_ops=ops) for j in range(200)])
-
-    res = asyncio.run(main())
-    assert b.stats["batches"] == 1 and b.stats["requests"] == 200
-    for j, r in enumerate(res):
-        if key(j) >= 150:
-            assert r is None
-        else:
-            t = truth[f"c-b_{key(j)}_0"]
-            np.testing.assert_array_equal(r, t if sels[j % 3] is None else t[sels[j % 3]])
-    assert all(n.pinned == 0 for n in cs.cache._lru.values())
