@@ -1091,6 +1091,7 @@ def main():
     ap.add_argument("--kernel-timing", type=int, default=0)
     ap.add_argument("--copy-ceiling", type=int, default=1, help="measure the HIP streaming-copy ceiling (2 GiB)")
     ap.add_argument("--e2e", type=int, default=1, help="also measure the PCIe-inclusive rate (N=1)")
+    ap.add_argument("--e2e-sub", type=int, default=8, help="PCIe-inclusive rate: pipelined sub-batches")
     ap.add_argument("--cfg3", type=int, default=1, help="also measure configs[2] decode+select (N=1)")
     ap.add_argument("--lz4", type=int, default=1, help="also measure Blosc-lz4 1 MiB chunks (N=1)")
     ap.add_argument("--bshuf", type=int, default=1, help="also measure bitshuffle+LZ4 1 MiB f32 chunks (N=1)")
@@ -1213,7 +1214,7 @@ def main():
                                           "oracle_port": round(vo, 3)}
         del r3
     if world == 1 and args.e2e:
-        out["e2e_pcie"] = run_e2e(r1, args, dev)
+        out["e2e_pcie"] = run_e2e(r1, args, dev, nsub=args.e2e_sub)
     if world == 1 and args.zstd:
         try:
             zu = args.unique
