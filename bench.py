@@ -287,27 +287,50 @@ def run_cfg3(args, dev):
         out["traffic_ratio"] = round(tr["bytes_per_step"] / (comp + plan.slab_nbytes), 3)
         out["traffic_source"] = tr["source"]
     if args.cpu_seconds > 0:
-        # the reference's per-chunk path on the box's cores: _uncompress (oracle c-blosc +
-        # libz, one chunk per thread) + chunkReadSelection / slab assignment (numpy)
+        # the reference's per-chunk path on the box's cores: _uncompress -- c-blosc's
+        # blosc_decompress, here the image's libblosc 1.21.0 (storUtil.py:195-208), one chunk
+        # per thread -- + chunkReadSelection / slab assignment (numpy, chunkUtil.py:882-929,
+        # chunk_crawl.py:395-418); the oracle port of the same decode is kept beside it
+        import ctypes
+        from concurrent.futures import ThreadPoolExecutor
         ns = min(512, len(ids))
-        samp = [enc[k % nuniq] for k in range(ns)]
+        samp = [np.ascontiguousarray(enc[k % nuniq]) for k in range(ns)]
         pieces = [plan.pieces[plan.by_rank[0][k]] for k in range(ns)]
         outb = [np.empty(csz * 2, np.uint8) for _ in range(ns)]
         cpu_slab = np.zeros(plan.slab_shape, np.int16)
+        lb = ctypes.CDLL(LIBBLOSC)
+        lb.blosc_decompress_ctx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        lb.blosc_decompress_ctx.restype = ctypes.c_int
+        lb.blosc_get_version_string.restype = ctypes.c_char_p
+
+        def one(k):
+            r = lb.blosc_decompress_ctx(samp[k].ctypes.data, outb[k].ctypes.data, csz * 2, 1)
+            assert r == csz * 2, r
+            p = pieces[k]
+            cpu_slab[p.data_slices] = outb[k].view(np.int16).reshape(CFG3_LAYOUT)[p.chunk_slices]
         done, t1 = 0, time.perf_counter()
-        while time.perf_counter() - t1 < min(args.cpu_seconds, 4.0):
+        with ThreadPoolExecutor(threads) as ex:
+            while time.perf_counter() - t1 < min(args.cpu_seconds, 4.0):
+                list(ex.map(one, range(ns)))
+                done += 1
+        cel = (time.perf_counter() - t1) / done
+        sel_bytes = int(sum(p.nbytes for p in pieces))
+        assert np.array_equal(cpu_slab[pieces[1].data_slices], host[pieces[1].data_slices])
+        pdone, t2 = 0, time.perf_counter()
+        while time.perf_counter() - t2 < min(args.cpu_seconds / 2, 2.0):
             _, stt = orc.uncompress_batch(samp, [csz * 2] * ns, "zlib", 1, 2, nthreads=threads, out=outb)
             assert (stt == csz * 2).all()
             for b, p in zip(outb, pieces):
                 cpu_slab[p.data_slices] = b.view(np.int16).reshape(CFG3_LAYOUT)[p.chunk_slices]
-            done += 1
-        cel = (time.perf_counter() - t1) / done
-        sel_bytes = int(sum(p.nbytes for p in pieces))
-        assert np.array_equal(cpu_slab[pieces[1].data_slices], host[pieces[1].data_slices])
+            pdone += 1
+        pel = (time.perf_counter() - t2) / pdone
         out["cpu_baseline"] = {"value": round(sel_bytes / cel / 1e9, 4), "unit": "GB/s selected", "cores": threads,
-                               "kind": "port", "cpu_model": cpu_model(),
-                               "sample": f"{done} x {ns} of the {len(ids)} chunks: oracle decode ({threads} threads) "
-                                         "+ numpy selection into the slab"}
+                               "kind": "reference", "cpu_model": cpu_model(),
+                               "sample": f"{done} x {ns} of the {len(ids)} chunks: libblosc "
+                                         f"{lb.blosc_get_version_string().decode()} blosc_decompress_ctx "
+                                         f"({threads} threads, one chunk each) + numpy selection into the slab",
+                               "port_value": round(sel_bytes / pel / 1e9, 4),
+                               "port_sample": f"{pdone} x {ns} chunks: oracle decode + numpy selection"}
     del gathered, slab, st
     torch.cuda.empty_cache()
     return out
@@ -701,14 +724,20 @@ def run_cfg5(args, dev, rank=0):
             "sample": f"{done} x 1 MiB bitshuffle+LZ4 encodes (oracle transposition + greedy LZ4)"}
     if args.cpu_seconds > 0 and rank == 0:
         threads = box_threads()
+        # the reference's encoder: libblosc's blosc_compress_ctx(4, shuffle, typesize 1, zlib)
+        v, n_enc, _, ver = cpu_encode_libblosc(samp, args.cpu_seconds / 3, threads, clevel=4, cname=b"zlib")
         t1 = time.perf_counter()
         done = 0
-        while time.perf_counter() - t1 < args.cpu_seconds / 2:
+        while time.perf_counter() - t1 < args.cpu_seconds / 6:
             orc.encode_batch(samp, op="blosc", typesize=1, clevel=4, shuffle=1, nthreads=threads)
             done += len(samp)
         cel = time.perf_counter() - t1
-        out["cpu_baseline"] = {"value": round(done * cbytes / cel / 1e9, 3), "unit": "GB/s", "cores": threads,
-                               "kind": "port", "sample": f"{done} x 1 MiB F1 encodes (oracle c-blosc + libz L4)"}
+        out["cpu_baseline"] = {"value": round(v, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
+                               "sample": f"{n_enc} x 1 MiB F1 encodes by libblosc {ver} blosc_compress_ctx "
+                                         f"(clevel 4, shuffle, typesize 1, zlib: the reference's _compress), "
+                                         f"{threads} threads",
+                               "port_value": round(done * cbytes / cel / 1e9, 3),
+                               "port_sample": f"{done} x 1 MiB F1 encodes (oracle c-blosc + libz L4)"}
     del slab, chunks, frames
     torch.cuda.empty_cache()
     return out
@@ -987,6 +1016,40 @@ def cpu_baseline_libblosc(blobs, seconds, threads):
             done += len(srcs)
     el = time.perf_counter() - t0
     return done * CHUNK_BYTES / el / 1e9, done, lb.blosc_get_version_string().decode()
+
+
+def cpu_encode_libblosc(raws, seconds, threads, clevel=4, cname=b"zlib"):
+    """The reference's own writer on the box's host cores: storUtil._compress
+    (storUtil.py:238-281) is numcodecs' Blosc(cname, clevel, shuffle).encode(bytes), i.e.
+    c-blosc's blosc_compress with typesize 1 and the automatic block size -- here the
+    image's libblosc 1.21.0 blosc_compress_ctx, one internal thread per call, `threads`
+    chunks at a time, bounded to about `seconds` of wall time.  Returns (GB/s of input,
+    chunks encoded, compressed bytes of one pass, library version string)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    lb = ctypes.CDLL(LIBBLOSC)
+    lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
+                                      ctypes.c_size_t, ctypes.c_int]
+    lb.blosc_compress_ctx.restype = ctypes.c_int
+    lb.blosc_get_version_string.restype = ctypes.c_char_p
+    srcs = [np.ascontiguousarray(r).reshape(-1).view(np.uint8) for r in raws]
+    outs = [np.empty(x.size + 16, np.uint8) for x in srcs]
+
+    def one(k):
+        return lb.blosc_compress_ctx(clevel, 1, 1, srcs[k].size, srcs[k].ctypes.data, outs[k].ctypes.data,
+                                     outs[k].size, cname, 0, 1)
+    done, csum = 0, 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < seconds:
+            rs = list(ex.map(one, range(len(srcs))))
+            assert min(rs) > 0, rs
+            csum = sum(rs)
+            done += len(srcs)
+    el = time.perf_counter() - t0
+    nbytes = sum(x.size for x in srcs) * done // max(1, len(srcs))
+    return nbytes / el / 1e9, done, csum, lb.blosc_get_version_string().decode()
 
 
 def cpu_baseline_bshuf(blobs, seconds, threads):

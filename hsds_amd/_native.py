@@ -8,8 +8,12 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# HSDS_AMD_LIB: development override (A/B timing of two builds); the default is the in-tree build
-LIB_PATH = os.environ.get("HSDS_AMD_LIB") or os.path.join(_HERE, "libhsds_amd.so")
+# The product always loads the in-tree build.  A/B timing of experiment builds (tools/*.sh)
+# swaps it with HSDS_AMD_LIB, honoured only together with the development flag
+# HSDS_AMD_DEV=1, which nothing in the product or its tests sets.
+LIB_PATH = os.path.join(_HERE, "libhsds_amd.so")
+if os.environ.get("HSDS_AMD_DEV") == "1" and os.environ.get("HSDS_AMD_LIB"):
+    LIB_PATH = os.environ["HSDS_AMD_LIB"]
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hsds_amd.h")
 
 OK = 0

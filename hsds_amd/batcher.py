@@ -141,9 +141,17 @@ class ChunkBatcher:
         # batch waits for the device once
         with store.lock:
             vals, finish = store.get_chunks_deferred(order, dtype, chunk_dims, **kw)
-            items = [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs]
-            plan = _gather_launch(items, dtype, chunk_dims)
-            torch.cuda.current_stream(store.cache.arena.buf.device).synchronize()
+            try:
+                items = [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs]
+                plan = _gather_launch(items, dtype, chunk_dims)
+                torch.cuda.current_stream(store.cache.arena.buf.device).synchronize()
+            except BaseException:
+                # the batch failed between its reads and finish(): its slot pins must not
+                # outlive it (pinned slots are never evicted)
+                abort = getattr(finish, "abort", None)
+                if abort is not None:
+                    abort()
+                raise
             vals = finish()
         return _gather_finish(plan, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
 

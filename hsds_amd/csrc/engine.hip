@@ -32,6 +32,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -436,8 +437,8 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(HZ
                       item_perm(it)};
       // (only wavefront 0 reports the decoded length of an inexact item)
       if (w != 0) job.out_len = nullptr;
-      st = hz2::inflate_stream<hz2::Stats, NW>(sh[w], job, tune, ring, (hz2::Stats*)nullptr, prof,
-                                               hz2::Pipe{&ctl, &sh[(w + NW - 1u) % NW], w});
+      st = hz2::inflate_stream_pipe<hz2::Stats, NW>(sh[w], job, tune, ring, (hz2::Stats*)nullptr, prof,
+                                                    hz2::Pipe{&ctl, &sh[(w + NW - 1u) % NW], w});
     }
     if (w == 0 && lane == 0 && st != HSDS_OK) atomicMin(&status[it.chunk], st);
     __syncthreads();
@@ -1622,7 +1623,8 @@ const char* hsds_strerror(int s) {
 int hsds_engine_create(int device, hsds_engine** out) {
   if (!out) return HSDS_ERR_ARG;
   if (hipSetDevice(device) != hipSuccess) return HSDS_ERR_DEVICE;
-  hsds_engine* e = new hsds_engine();
+  hsds_engine* e = new (std::nothrow) hsds_engine();
+  if (!e) return HSDS_ERR_DEVICE;
   e->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete e; return HSDS_ERR_DEVICE; }
@@ -1685,6 +1687,7 @@ int hsds_engine_create(int device, hsds_engine** out) {
                             // (round 2, register reader, K = 16: 512 best at 108.7)
   e->tune.max_rounds = 4;
   e->tune.over16 = 1;
+  e->tune.spin_max = 0;     // window pipeline waits: hz2::SPIN_MAX polls (~1 s), then one-wavefront re-decode
   // development override (A/B experiments): "W,rounds,over16"
   if (const char* ev = getenv("HSDS_INFLATE_TUNE")) {
     unsigned w, ov; int rd;
@@ -1900,8 +1903,16 @@ int hsds_partition_ids(const char* prefix, int rank, const int64_t* idx, int64_t
   int nt = (int)((n + 4095) / 4096);
   if (nt > 8) nt = 8;
   if (nt <= 1) { work(0, n); return HSDS_OK; }
+  // (nothing may throw across the C ABI: a range whose thread cannot be created -- thread
+  // limit, std::system_error -- or a failed allocation is done by the calling thread)
   std::vector<std::thread> th;
-  for (int t = 0; t < nt; t++) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+  int t = 0;
+  try {
+    th.reserve(nt);
+    for (; t < nt; t++) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+  } catch (...) {
+  }
+  for (; t < nt; t++) work(n * t / nt, n * (t + 1) / nt);
   for (auto& x : th) x.join();
   return HSDS_OK;
 }
@@ -2134,7 +2145,15 @@ int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* l
   int64_t parts = (int64_t)(total >> 21);
   parts = parts < 1 ? 1 : parts > 16 ? 16 : parts;
   if (parts > n) parts = n;
-  std::vector<int64_t> cut(parts + 1);
+  // (nothing may throw across the C ABI: an allocation failure is HSDS_ERR_DEVICE, and a
+  // helper thread that cannot be created -- thread limit, std::system_error -- only leaves
+  // its pieces to the threads that run, the calling one always among them)
+  std::vector<int64_t> cut;
+  try {
+    cut.resize(parts + 1);
+  } catch (...) {
+    return HSDS_ERR_DEVICE;
+  }
   for (int64_t p = 0; p <= parts; p++) cut[p] = n * p / parts;
   std::atomic<int64_t> next{0};
   std::atomic<int> rc{HSDS_OK};
@@ -2153,8 +2172,11 @@ int hsds_stage_upload(hsds_engine* e, const void* const* srcs, const uint64_t* l
   };
   const int nt = threads < 1 ? 0 : (threads > 64 ? 63 : threads - 1);
   std::vector<std::thread> pool;
-  pool.reserve(nt);
-  for (int t = 0; t < nt && t + 1 < parts; t++) pool.emplace_back(worker);
+  try {
+    pool.reserve(nt);
+    for (int t = 0; t < nt && t + 1 < parts; t++) pool.emplace_back(worker);
+  } catch (...) {
+  }
   worker();
   for (auto& t : pool) t.join();
   return rc.load();

@@ -108,7 +108,7 @@ constexpr uint32_t RS = HZ2_RS;           // ring words per lane (a multiple of 
 constexpr uint32_t OS = HZ2_OS;
 static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
 #ifndef HZ2_TICKN
-#define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 4)
+#define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 5)
 #endif
 constexpr uint32_t TICKN = HZ2_TICKN;     // tokens between ring refills
 static_assert(RS % 4 == 0 && RS >= 8, "RS: whole quads");
@@ -176,7 +176,12 @@ struct Tune {
   uint32_t W;          // warm-up bits before a segment
   int max_rounds;      // repair rounds per window
   uint32_t over16;     // segment over-provisioning against the previous block size, in 16ths
+  uint32_t spin_max;   // window pipeline: polls (s_sleep 2 each) before a wait gives up (0: SPIN_MAX)
 };
+
+// a wait of the window pipeline gave up (internal: the stream is then decoded again by one
+// wavefront, inflate_stream_pipe; never reported as a chunk status)
+constexpr int ST_HANG = -8;
 
 // Output address map: stream byte x -> dst offset.  n == 1: x + x0.  Otherwise the HDF5 /
 // Blosc byte unshuffle of a span of N elements of n bytes (`body` = N * n; tail bytes stay),
@@ -680,6 +685,7 @@ struct Stats {
   uint64_t steps_a, steps_e, extra_windows;
   uint64_t fill_max, fill_sum, span_sum;   // resolve: per-batch max lane source-map fill, total fill, spans
   uint64_t src_in, src_far[4];             // resolve: sources inside the batch; before it within 256/1536/4096/more
+  uint64_t hangs;                          // window pipeline: waits that gave up (one-wavefront re-decode)
 };
 
 }  // namespace hz2
@@ -772,6 +778,7 @@ struct Ctl {                     // in LDS, shared by the workgroup's wavefronts
   int32_t err;                   // the first error (0: none)
   uint32_t item;                 // the work item both wavefronts decode
   uint32_t bar;                  // CPU emulation: barrier generation counter
+  int32_t redo;                  // inflate_stream_pipe: status of the one-wavefront re-decode
   WinState next;
   uint64_t adler[NW_MAX][2];     // per wavefront: sum b, sum pos * b
 };
@@ -883,6 +890,10 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       LANE_LOOP { if (lane == 0) memcpy(sh.wnext, &nx, sizeof(nx)); }
     }
   };
+  // every wait is bounded; one that gives up is ST_HANG (not corrupt data: the caller
+  // decodes the stream again with one wavefront)
+  const uint32_t spin_max = tune.spin_max ? tune.spin_max : SPIN_MAX;
+  (void)spin_max;
   // wait until every output byte before this window is final (the other wavefront's M)
   auto wait_output = [&]() -> int {
     if (NW > 1) {
@@ -891,7 +902,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         if (ctl_ld(&c->mdone) == k) return ST_OK;
         const int32_t e = (int32_t)ctl_ld((const uint32_t*)&c->err);
         if (e) return e;
-        if (spin > SPIN_MAX) return ST_DATA;
+        if (spin > spin_max) return ST_HANG;
         HZ2_PAUSE();
       }
     }
@@ -913,7 +924,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         if (ctl_ld(&c->end_at) <= k) break;          // the stream ended before window k
         const int32_t e = (int32_t)ctl_ld((const uint32_t*)&c->err);
         if (e) { fail = e; break; }
-        if (spin > SPIN_MAX) { fail = ST_DATA; break; }
+        if (spin > spin_max) { fail = ST_HANG; break; }
         HZ2_PAUSE();
       }
       if (!got) break;
@@ -1799,6 +1810,34 @@ HZ_UNROLL
   if (job.exact && out != dst_len) return ST_SIZE;
   if (job.out_len) *job.out_len = out;
   return ST_OK;
+}
+
+// The window pipeline (NW > 1) with its timeout fallback.  A wait that gives up (ST_HANG:
+// a neighbouring window that never finished) is no evidence of corrupt data, so the stream
+// is decoded again by wavefront 0 alone (NW = 1, no waits), and every wavefront returns that
+// decode's status.  All NW wavefronts of the workgroup call this together: the fallback path
+// has a workgroup barrier.  (ST_HANG is uniform: inflate_stream<NW> returns Ctl::err, the
+// first failure of any wavefront, to all of them.)
+template <class StatsT, int NW>
+#if HZ_GPU
+__device__ __forceinline__
+#else
+static
+#endif
+int inflate_stream_pipe(Shared& sh, const Job job, const Tune tune, uint8_t* ring_base, StatsT* stats, HzProf* prof,
+                        Pipe pipe) {
+  int st = inflate_stream<StatsT, NW>(sh, job, tune, ring_base, stats, prof, pipe);
+  if (st == ST_HANG) {
+    if (stats) stats->hangs++;
+    if (pipe.w == 0u) {
+      const int r = inflate_stream<StatsT, 1>(sh, job, tune, ring_base, stats, prof);
+      // (not in Ctl::err: the other wavefronts may still be reading that one)
+      LANE_LOOP { if (lane == 0) ctl_st((uint32_t*)&pipe.ctl->redo, (uint32_t)r); }
+    }
+    HZ2_WGBAR();
+    st = (int32_t)ctl_ld((const uint32_t*)&pipe.ctl->redo);
+  }
+  return st;
 }
 
 }  // namespace hz2

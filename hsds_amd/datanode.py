@@ -492,10 +492,12 @@ class ChunkReader:
                 if data is None:
                     errors[ri] = HTTPNotFound(r.chunk_id)
                     continue
+                # the staging copy is the only copy of the object (a view is copied now); an
+                # ndarray is taken as its bytes, a flat uint8 view, so len() is its byte count
+                data = _as_blob(data)
                 if r.length and r.length > 0 and len(data) != r.length:
                     data = bytes(r.length)      # storUtil.py:480-485 (bytearray(length), data not copied)
-                # the staging copy is the only copy of the object (a view is copied now)
-                blobs.append(data if isinstance(data, (bytes, np.ndarray)) else bytes(data))
+                blobs.append(data)
                 jobs.append((ri, "plain", len(blobs) - 1, None))
                 continue
             # hyper chunk (datanode_lib.py:851-906)
@@ -595,13 +597,31 @@ class ChunkReader:
             # short contiguous reads near the end of the file are zero-extended (:833-844)
             for ri, kind, bi, _ in jobs:
                 if kind == "plain" and len(blobs[bi]) < chunk_size:
-                    blobs[bi] = blobs[bi] + bytes(chunk_size - len(blobs[bi]))
+                    pad = bytes(chunk_size - len(blobs[bi]))
+                    b = blobs[bi]
+                    blobs[bi] = np.concatenate([b, np.frombuffer(pad, np.uint8)]) if isinstance(b, np.ndarray) \
+                        else b + pad
         results = [None] * len(reads)
         for ri, e in errors.items():
             results[ri] = e
         need = [ri for ri in range(len(reads)) if ri not in errors]
         slots = {}
         pinned = []
+        released = [False]
+
+        def unpin_all(drop=False):
+            # the batch's slot pins, released exactly once: by finish(), or by abort() when
+            # the caller gives up on the batch, or here when the batch fails before returning.
+            # A batch given up also drops its reserved slots: their bytes were never decoded
+            if not released[0]:
+                released[0] = True
+                for cid in pinned:
+                    self.cache.unpin(cid)
+                    if drop and cid in self.cache and not self.cache.isDirty(cid):
+                        del self.cache[cid]
+
+        def abort():
+            unpin_all(drop=True)
 
         def reserve_slots():
             # destination slots (base tensor, byte offset): cache arena, else a batch tensor
@@ -642,6 +662,52 @@ class ChunkReader:
         # every chunk is placed whatever its status (a failed chunk's slot is dropped in
         # finish(), after the one stream synchronisation)
         dec = [j for j in jobs if j[1] in ("plain", "h5")]
+        st_host = None
+        try:
+            st_host = self._launch(reads, dtype, chunk_dims, hyper_dims, comp, shuffle, isz, blobs, jobs, dec,
+                                   chunk_size, h5_size, slots, reserve_slots)
+        except BaseException:
+            abort()
+            raise
+        for ri in need:
+            base, off = slots[ri]
+            if results[ri] is None:
+                results[ri] = device_view(base[off:off + chunk_size], chunk_dims, dtype)
+
+        def finish():
+            """after the stream has drained: decode failures become 500s (and leave the
+            cache), the batch's slots are unpinned"""
+            if st_host is not None:
+                st = st_host.numpy()
+                for k, (ri, _, _, _) in enumerate(dec):
+                    if st[k] != nat.OK:
+                        results[ri] = HTTPInternalServerError()
+            unpin_all()
+            for ri in need:
+                if isinstance(results[ri], HTTPInternalServerError) and self.cache is not None \
+                        and reads[ri].chunk_id in self.cache:
+                    del self.cache[reads[ri].chunk_id]     # failed reads are not cached
+            if self.cache is not None and self.cache.memUsed > self.cache.memTarget:
+                self.cache._reduce()
+            return results
+
+        finish.abort = abort
+        if defer:
+            return results, finish
+        try:
+            torch.cuda.current_stream(self.device).synchronize()
+        except BaseException:
+            abort()
+            raise
+        return finish()
+
+    def _launch(self, reads, dtype, chunk_dims, hyper_dims, comp, shuffle, isz, blobs, jobs, dec, chunk_size,
+                h5_size, slots, reserve_slots):
+        """read()'s device half: the decode batch, the slot reservation and the placement
+        copies, queued on the current stream.  Returns the page-locked status buffer (None
+        when nothing is decoded)."""
+        import torch
+        from .engine import COPY_DESC_DTYPE
         st_host = None
         if dec:
             sizes = [chunk_size if kind == "plain" else h5_size for _, kind, _, _ in dec]
@@ -684,33 +750,16 @@ class ChunkReader:
                 self.eng.copy(dbuf, base, recs[np.asarray(rows)])
         else:
             reserve_slots()
-        for ri in need:
-            base, off = slots[ri]
-            if results[ri] is None:
-                results[ri] = device_view(base[off:off + chunk_size], chunk_dims, dtype)
+        return st_host
 
-        def finish():
-            """after the stream has drained: decode failures become 500s (and leave the
-            cache), the batch's slots are unpinned"""
-            if st_host is not None:
-                st = st_host.numpy()
-                for k, (ri, _, _, _) in enumerate(dec):
-                    if st[k] != nat.OK:
-                        results[ri] = HTTPInternalServerError()
-            for cid in pinned:
-                self.cache.unpin(cid)
-            for ri in need:
-                if isinstance(results[ri], HTTPInternalServerError) and self.cache is not None \
-                        and reads[ri].chunk_id in self.cache:
-                    del self.cache[reads[ri].chunk_id]     # failed reads are not cached
-            if self.cache is not None and self.cache.memUsed > self.cache.memTarget:
-                self.cache._reduce()
-            return results
 
-        if defer:
-            return results, finish
-        torch.cuda.current_stream(self.device).synchronize()
-        return finish()
+def _as_blob(data):
+    """a fetched object as bytes, or an ndarray as a flat uint8 view of its bytes"""
+    if isinstance(data, bytes):
+        return data
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+    return bytes(data)
 
 
 # host threads copying a large batch into page-locked staging (the GPU box's CPU share is
@@ -846,7 +895,11 @@ class ChunkStore:
                                                     fill_value=fill_value, layout_class=layout_class,
                                                     hyper_dims=hyper_dims, chunk_init=chunk_init)
             import torch
-            torch.cuda.current_stream(self.cache.arena.buf.device).synchronize()
+            try:
+                torch.cuda.current_stream(self.cache.arena.buf.device).synchronize()
+            except BaseException:
+                finish.abort()
+                raise
             return finish()
 
     def get_chunks_deferred(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
@@ -885,22 +938,40 @@ class ChunkStore:
                         v = None                               # 404: no chunk
                     out[r.chunk_id] = v
         except BaseException:
+            if rfin is not None:
+                rfin.abort()
             for key in hits:
                 self.cache.unpin(key)
             raise
+        released = [False]
+
+        def release():
+            # every pin of this call, released exactly once (finish() or abort())
+            if not released[0]:
+                released[0] = True
+                for key in init:
+                    self.cache.unpin(key)
+                for key in hits:
+                    self.cache.unpin(key)
 
         def finish():
-            if rfin is not None:
-                res = rfin()
-                for r, v in zip(todo, res):
-                    if isinstance(v, HTTPInternalServerError):
-                        out[r.chunk_id] = v
-            for key in init:
-                self.cache.unpin(key)
-            for key in hits:
-                self.cache.unpin(key)
+            try:
+                if rfin is not None:
+                    res = rfin()
+                    for r, v in zip(todo, res):
+                        if isinstance(v, HTTPInternalServerError):
+                            out[r.chunk_id] = v
+            finally:
+                release()
             return [out[r.chunk_id] for r in reads]
 
+        def abort():
+            """give up on the batch (the caller failed before finish()): drop its pins"""
+            if rfin is not None:
+                rfin.abort()
+            release()
+
+        finish.abort = abort
         return [out[r.chunk_id] for r in reads], finish
 
     def _fill_new(self, keys, dtype, chunk_dims, fill_value):

@@ -14,6 +14,11 @@
 // nwaves == 2 or 4: the window pipeline of inflate2w_kernel -- one thread per emulated
 // wavefront, sharing a hz2::Ctl and the previous window's wavefront's LDS tables; all must
 // return the same status
+// Tune::spin_max of the emulated pipeline (0: hz2::SPIN_MAX); tests set it tiny to force the
+// pipeline's wait timeouts and so its one-wavefront fallback
+static uint32_t g_spin_max = 0;
+extern "C" void emu_set_spin_max(uint32_t v) { g_spin_max = v; }
+
 template <int NW>
 static int run_pipe(hz2::Shared* sh0, const hz2::Job& job, const hz2::Tune& tune, uint8_t* ring0, hz2::Stats& st) {
   hz2::Shared* sh[NW];
@@ -31,11 +36,11 @@ static int run_pipe(hz2::Shared* sh0, const hz2::Job& job, const hz2::Tune& tune
   std::thread t[NW];
   for (int w = 1; w < NW; w++)
     t[w] = std::thread([&, w]() {
-      rs[w] = hz2::inflate_stream<hz2::Stats, NW>(*sh[w], job, tune, ring[w], &sts[w], nullptr,
-                                                  hz2::Pipe{&ctl, sh[(w + NW - 1) % NW], (uint32_t)w});
+      rs[w] = hz2::inflate_stream_pipe<hz2::Stats, NW>(*sh[w], job, tune, ring[w], &sts[w], nullptr,
+                                                       hz2::Pipe{&ctl, sh[(w + NW - 1) % NW], (uint32_t)w});
     });
-  rs[0] = hz2::inflate_stream<hz2::Stats, NW>(*sh[0], job, tune, ring[0], &sts[0], nullptr,
-                                              hz2::Pipe{&ctl, sh[NW - 1], 0u});
+  rs[0] = hz2::inflate_stream_pipe<hz2::Stats, NW>(*sh[0], job, tune, ring[0], &sts[0], nullptr,
+                                                   hz2::Pipe{&ctl, sh[NW - 1], 0u});
   int r = rs[0];
   for (int w = 1; w < NW; w++) {
     t[w].join();
@@ -71,7 +76,7 @@ extern "C" int emu_inflate2_nw(const uint8_t* src, uint32_t src_len, uint8_t* ds
   const uint32_t n = perm_n < 1 ? 1 : perm_n;
   uint8_t* stage = n > 1 ? (uint8_t*)malloc(dst_len + 16) : nullptr;
   hz2::Job job = {src, src_len, n > 1 ? stage + (dst_off & 15u) : dst + dst_off, dst_len, 1u, nullptr, hz2::perm_make(1, 1, 0)};
-  hz2::Tune tune = {W, max_rounds, over16};
+  hz2::Tune tune = {W, max_rounds, over16, g_spin_max};
   int r = run_stream(sh, job, tune, ring, st, nwaves);
   if (n > 1) {
     if (r == 0) {
@@ -83,8 +88,8 @@ extern "C" int emu_inflate2_nw(const uint8_t* src, uint32_t src_len, uint8_t* ds
   }
   if (stats_out) {
     const uint64_t v[] = {st.windows, st.blocks, st.stored, st.tokens, st.matches, st.lanes_valid, st.repairs,
-                          st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows, st.fill_max, st.fill_sum, st.span_sum, st.src_in, st.src_far[0], st.src_far[1], st.src_far[2], st.src_far[3]};
-    for (int i = 0; i < 22; i++) stats_out[i] = v[i];
+                          st.repair_lanes, st.cuts, st.batches, st.hops, st.steps_a, st.steps_e, st.extra_windows, st.fill_max, st.fill_sum, st.span_sum, st.src_in, st.src_far[0], st.src_far[1], st.src_far[2], st.src_far[3], st.hangs};
+    for (int i = 0; i < 23; i++) stats_out[i] = v[i];
   }
   free(ring);
   free(sh);

@@ -115,3 +115,50 @@ def test_hits_stay_pinned_while_misses_reserve(oracle_lib):
         np.testing.assert_array_equal(r, truth[f"c-b_{i}_0"])
     assert all(n.pinned == 0 for n in cs.cache._lru.values())
 
+
+
+def test_failed_batch_releases_every_pin(oracle_lib, monkeypatch):
+    """a batch that fails between get_chunks_deferred and finish() (here: the
+    selection gather launch, then the reader's placement copy) must not leave slots pinned
+    -- pinned slots are never evicted.  The requests get the exception; afterwards every
+    node has pinned == 0 and the store still serves reads."""
+    import torch
+    import hsds_amd.batcher as hb
+    from hsds_amd.batcher import ChunkBatcher
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    dev = torch.device("cuda", 0)
+    dims = (64, 96)
+    truth, objs = _objs(oracle_lib, 24, dims, 13)
+    chunk_bytes = dims[0] * dims[1] * 4
+    cs = ChunkStore(lambda key, off, ln: objs.get(key), mem_target=32 * chunk_bytes, device=dev)
+    ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
+    cs.get_chunks([ChunkRead(f"c-b_{i}_0", f"k{i}") for i in range(8)], "<f4", dims, filter_ops=ops)   # hits
+    b = ChunkBatcher(cs, window_ms=50)
+
+    def boom(*a, **k):
+        raise RuntimeError("injected gather failure")
+
+    async def main():
+        return await asyncio.gather(*[b.get_chunk(ChunkRead(f"c-b_{i}_0", f"k{i}"), "<f4", dims, filter_ops=ops)
+                                      for i in range(16)], return_exceptions=True)
+
+    monkeypatch.setattr(hb, "_gather_launch", boom)
+    res = asyncio.run(main())
+    assert all(isinstance(r, RuntimeError) for r in res)
+    assert all(n.pinned == 0 for n in cs.cache._lru.values())
+    monkeypatch.undo()
+    # the reader's own device half failing after its slots are reserved
+    real_copy = cs.reader.eng.copy
+
+    def copy_boom(*a, **k):
+        raise RuntimeError("injected placement failure")
+
+    cs.reader.eng.copy = copy_boom
+    with pytest.raises(RuntimeError):
+        cs.get_chunks([ChunkRead(f"c-b_{i}_0", f"k{i}") for i in range(4, 20)], "<f4", dims, filter_ops=ops)
+    assert all(n.pinned == 0 for n in cs.cache._lru.values())
+    cs.reader.eng.copy = real_copy
+    vals = cs.get_chunks([ChunkRead(f"c-b_{i}_0", f"k{i}") for i in range(24)], "<f4", dims, filter_ops=ops)
+    for i, v in enumerate(vals):
+        np.testing.assert_array_equal(v.cpu().numpy(), truth[f"c-b_{i}_0"])
+    assert all(n.pinned == 0 for n in cs.cache._lru.values())

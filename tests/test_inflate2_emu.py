@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EMU = os.path.join(ROOT, "tests", "emu", "libinflate2_emu.so")
 SRC = os.path.join(ROOT, "tests", "emu", "inflate2_emu.cpp")
 STATS = ("windows blocks stored tokens matches lanes_valid repairs repair_lanes cuts batches hops "
-         "steps_a steps_e extra_windows fill_max fill_sum span_sum src_in far256 far1536 far4096 farmore").split()
+         "steps_a steps_e extra_windows fill_max fill_sum span_sum src_in far256 far1536 far4096 farmore hangs").split()
 
 
 @pytest.fixture(scope="module")
@@ -316,3 +316,40 @@ def test_two_wavefronts_corruptions_fail_like_libz(emu, nw):
     c = zlib.compress(data, 4)
     assert run(emu, c, len(data) - 1, nwaves=nw)[0] not in (0, -100)
     assert run(emu, c, len(data) + 1, nwaves=nw)[0] not in (0, -100)
+
+
+@pytest.mark.parametrize("nw", [2, 4])
+def test_pipeline_timeout_redecodes_with_one_wavefront(emu, nw):
+    """A window-pipeline wait that gives up (Tune::spin_max; inflate2.h inflate_stream /
+    inflate_stream_pipe) is not reported as corrupt data: wavefront 0 decodes the stream
+    again alone, so valid streams still come out bit-exact and corrupt ones keep libz's
+    verdict.  spin_max = 1 makes nearly every wait give up."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+    emu.emu_set_spin_max.argtypes = [ctypes.c_uint32]
+    emu.emu_set_spin_max(1)
+    try:
+        hangs = 0
+        for name, data in corpus().items():
+            c = zlib.compress(data, 4)
+            r, out, st = run(emu, c, len(data), nwaves=nw)
+            assert r == 0 and out == data, (name, r)
+            hangs += st["hangs"]
+        rng = np.random.default_rng(5)
+        base = corpus()["smooth_f32"][:60000]
+        good = zlib.compress(base, 4)
+        for t in range(24):
+            b = bytearray(good)
+            i = int(rng.integers(0, len(b)))
+            b[i] ^= 1 << int(rng.integers(0, 8))
+            ref = orc.uncompress(bytes(b), "zlib", 0, 1, len(base))
+            r, out, _ = run(emu, bytes(b), len(base), nwaves=nw)
+            r1, _, _ = run(emu, bytes(b), len(base), nwaves=1)
+            if isinstance(ref, int):
+                assert r < 0 and r != -100 and r == r1, (t, ref, r, r1)
+            else:
+                assert r == 0 and out == ref, (t, r)
+        assert hangs > 0, "the forced timeouts never fired"
+    finally:
+        emu.emu_set_spin_max(0)

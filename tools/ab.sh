@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for lib in "$@"; do
-  HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --e2e 0 --cfg3 0 --cfg5 0 --lz4 0 --zstd 0 --bshuf 0 --cfg1 0 --cfg5w 0 --cfg4 0 --cfg4-full 0 \
+  HSDS_AMD_DEV=1 HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --e2e 0 --cfg3 0 --cfg5 0 --lz4 0 --zstd 0 --bshuf 0 --cfg1 0 --cfg5w 0 --cfg4 0 --cfg4-full 0 \
     > gpurun_out/ab_$(basename $lib).log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -5 gpurun_out/ab_$(basename $lib).log; exit $rc; }
   python - "$lib" gpurun_out/ab_$(basename $lib).log <<'PY'

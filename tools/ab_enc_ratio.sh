@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for spec in "$@"; do
   IFS=: read -r lib chain far <<< "$spec"
   envs=()
-  [ "$lib" != "cur" ] && envs+=(HSDS_AMD_LIB="$lib")
+  [ "$lib" != "cur" ] && envs+=(HSDS_AMD_DEV=1 HSDS_AMD_LIB="$lib")
   [ "$chain" != "0" ] && envs+=(HSDS_DEFLATE_CHAIN="$chain")
   [ "$far" = "1" ] && envs+=(HSDS_DEFLATE_FAR=1)
   tag=$(echo "$spec" | tr '/:' '__')

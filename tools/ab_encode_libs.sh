@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for lib in "$@"; do
-  HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --headline 0 --steps 3 --warmup 1 --cpu-seconds 0 \
+  HSDS_AMD_DEV=1 HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --headline 0 --steps 3 --warmup 1 --cpu-seconds 0 \
     --cfg3 0 --cfg1 0 --cfg5 1 --cfg4-full 0 > gpurun_out/abe_$(basename $lib).log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -5 gpurun_out/abe_$(basename $lib).log; exit $rc; }
   python - $lib gpurun_out/abe_$(basename $lib).log <<'PY'

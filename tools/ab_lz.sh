@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for lib in "$@"; do
-  HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --e2e 0 --f2 0 --cfg3 0 --cfg5 0 --zstd 0 --cfg1 0 --cfg5w 0 --cfg4 0 --cfg4-full 0 \
+  HSDS_AMD_DEV=1 HSDS_AMD_LIB=$(realpath $lib) timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --e2e 0 --f2 0 --cfg3 0 --cfg5 0 --zstd 0 --cfg1 0 --cfg5w 0 --cfg4 0 --cfg4-full 0 \
     > gpurun_out/ablz_$(basename $lib).log 2>&1 || { echo "$lib failed"; tail -3 gpurun_out/ablz_$(basename $lib).log; exit 1; }
   python - "$lib" gpurun_out/ablz_$(basename $lib).log <<'PY'
 import json, sys

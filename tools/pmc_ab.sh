@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY"
 for lib in "$@"; do
   b=$(basename $lib .so)
-  HSDS_AMD_LIB=$R/$lib timeout -k 10 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/$b -o $b -- \
+  HSDS_AMD_DEV=1 HSDS_AMD_LIB=$R/$lib timeout -k 10 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/$b -o $b -- \
     python3 $R/tools/pmc_run.py F1 2048 > $OUT/$b.log 2>&1
   rc=$?; echo "$b rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/$b.log; exit $rc; }
   python3 - $OUT/$b <<'PY'

@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 for lib in "$@"; do
   b=$(basename $lib .so)
   for c in FETCH_SIZE WRITE_SIZE; do
-    HZ_NOCHECK=1 HSDS_AMD_LIB=$R/$lib timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/$b.$c -o x -- \
+    HZ_NOCHECK=1 HSDS_AMD_DEV=1 HSDS_AMD_LIB=$R/$lib timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/$b.$c -o x -- \
       python3 $R/tools/pmc_run.py F1 2048 > $OUT/$b.$c.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$b $c rc=$rc"; tail -5 $OUT/$b.$c.log; exit $rc; }
   done

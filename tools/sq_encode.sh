@@ -14,7 +14,7 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM"; do
   i=$((i+1))
-  HZ_PROF_LIB=$LIB HSDS_AMD_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $OUT/p$i -o p$i -- python3 $R/tools/deflate_profile.py > $OUT/p$i.log 2>&1
+  HZ_PROF_LIB=$LIB HSDS_AMD_DEV=1 HSDS_AMD_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $OUT/p$i -o p$i -- python3 $R/tools/deflate_profile.py > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit $rc; }
 done
