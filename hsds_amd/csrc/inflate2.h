@@ -1672,8 +1672,16 @@ HZ_UNROLL
               LV(fb) |= far << i;
               // one load: the 64-bit address selected as an integer (a pointer select becomes
               // a branch), a harmless in-range byte of dst (F) for slots that take no byte
+#ifdef HZ2_EXP_NOLITLOAD                  // (traffic attribution builds: outputs wrong)
+              const uint64_t la = (uint64_t)(uintptr_t)lits;
+#else
               const uint64_t la = (uint64_t)(uintptr_t)lits + L0 + lcnt + hz2::lane_rank(bm, lane);
+#endif
+#ifdef HZ2_EXP_NOFAR
+              const uint64_t da = (uint64_t)(uintptr_t)dst + F;
+#else
               const uint64_t da = (uint64_t)(uintptr_t)dst + (far ? F + q - d : F);
+#endif
               LV(bv)[k] = *HZ_GLOBAL(hz_gcu8*, (uintptr_t)(isl ? la : da));
               if (stats && far) stats->src_far[d - q <= 256u ? 0 : d - q <= 1536u ? 1 : d - q <= 4096u ? 2 : 3]++;
             }
@@ -1728,9 +1736,15 @@ HZ_UNROLL
           for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
             const uint32_t x0 = xa + 4u * k;
             const bool inside = (int32_t)x0 >= 0 && x0 + 4u <= dst_len && x0 + 4u <= F + span && (k > 0u || !mis || head);
+#ifdef HZ2_EXP_NOMSTORE                   // (traffic attribution builds: outputs wrong)
+            if (inside || true) {
+              (void)inside;
+            } else {
+#else
             if (inside) {
               *(hz_gu32*)(dst + x0) = sh.sbuf[k];
             } else {
+#endif
               for (uint32_t b = 0; b < 4u; b++) {
                 const uint32_t x = x0 + b;
                 if (x >= F && x < F + span && x < dst_len) dst[x] = ((const uint8_t*)sh.sbuf)[4u * k + b];

@@ -353,3 +353,22 @@ def test_pipeline_timeout_redecodes_with_one_wavefront(emu, nw):
         assert hangs > 0, "the forced timeouts never fired"
     finally:
         emu.emu_set_spin_max(0)
+
+
+@pytest.mark.parametrize("nw", [1, 2])
+def test_long_literal_runs_before_matches(emu, nw):
+    """Literal runs of 1..3000 random bytes, each followed by a repeat of earlier bytes, at
+    several levels: runs that cross many lanes' segments before a match (the round-5
+    4-byte-record experiment's escape path; kept as a regression case for any record
+    format)."""
+    rng = np.random.default_rng(21)
+    parts = []
+    for n in (1, 100, 509, 510, 511, 512, 513, 1000, 1023, 1024, 2047, 3000, 5, 511, 600):
+        parts.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        parts.append(parts[-1][: max(1, min(n, 40))] * 3)          # a match (or several) after the run
+    data = b"".join(parts) * 3
+    for level in (1, 6, 9):
+        c = zlib.compress(data, level)
+        r, out, st = run(emu, c, len(data), nwaves=nw)
+        assert r == 0 and out == data, (level, r)
+        assert st["matches"] > 0

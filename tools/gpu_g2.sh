@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_pipe.py tests/test_gpu_codec.py > gpurun_out/g2_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/g2_tests.log; [ $rc -eq 0 ] || exit $rc
+tools/ab.sh abtmp/rec8.so abtmp/rec4.so abtmp/rec4g8.so abtmp/rec8.so abtmp/rec4.so
+bash tools/pmc_traffic_ab.sh abtmp/rec8.so abtmp/rec4.so abtmp/rec4g8.so
