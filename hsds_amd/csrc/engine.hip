@@ -1173,28 +1173,141 @@ __global__ void __launch_bounds__(64) zstd_lit_kernel(const uint32_t* __restrict
   }
 }
 
+// zstd sequence tables, one FSE_Compressed_Mode set per frame (zstd_enc.h frame_tables):
+// zstd_count_kernel adds every segment's sequence codes to its frame's counts (lane per
+// segment; the counts of the first ZT_SLOTS frames of the wave's segments gather in LDS),
+// zstd_table_kernel builds each frame's tables and descriptions (thread per frame), and
+// zstd_seg_kernel encodes every block of a frame with them, ZT_SLOTS frames' tables in LDS
+// at a time (round 4's predefined tables made the objects 1.24x libblosc-zstd's)
+constexpr uint32_t ZT_SLOTS = 4;
+constexpr uint32_t ZT_NCODE = sizeof(hze::SeqCounts) / 4u;
+static_assert(ZT_NCODE == 36u + 32u + 53u, "SeqCounts: ll, of, ml codes");
+// zstd_count_kernel: one workgroup per ZC_SEGS consecutive segments, one lane per parse
+// lane of a segment: lane l walks its own token slots forward (the slots are interleaved by
+// parse lane, so the 64 lanes' loads are one coalesced 256-byte row), counting the codes of
+// its matches; the literal run of a lane's first match continues from earlier lanes (its
+// literal ordinal minus the ordinal after the nearest earlier match: an add scan and a max
+// scan over the lanes).  Each lane keeps its own counters in LDS (two 16-bit counts per
+// dword, code-major: no atomic contention, distinct banks); they go to the frame's counts in
+// HBM whenever the frame changes.  (A lane per segment walking all 64 columns serially
+// took 34 ms on the cfg5 slab: every load touched 64 lines.)
+constexpr uint32_t ZT_NW = (ZT_NCODE + 1u) / 2u;
+constexpr uint32_t ZC_SEGS = 8;
+__global__ void __launch_bounds__(64) zstd_count_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                        const SegMeta* __restrict__ meta,
+                                                        const hd::SegParse* __restrict__ sp,
+                                                        const uint16_t* __restrict__ tok,
+                                                        hze::SeqCounts* __restrict__ counts, uint32_t seg_cap) {
+  __shared__ uint32_t c[ZT_NW][64];
+  __shared__ hze::CodeTabs ct;
+  const uint32_t l = threadIdx.x;
+  for (uint32_t k = l; k < ZT_NW * 64u; k += 64u) (&c[0][0])[k] = 0;
+  hze::code_tabs_fill(ct, l, 64u);
+  uint32_t total = segoffs[nchunks];
+  if (total > seg_cap) total = seg_cap;
+  const uint32_t sa = blockIdx.x * ZC_SEGS;
+  if (sa >= total) return;
+  const uint32_t sb = sa + ZC_SEGS < total ? sa + ZC_SEGS : total;
+  __syncthreads();
+  auto add = [&](uint32_t code) { atomicAdd(&c[code >> 1][l], (code & 1u) ? 0x10000u : 1u); };
+  auto flush = [&](uint32_t item) {
+    __syncthreads();
+    if (l < ZT_NW) {
+      uint32_t a = 0, b = 0;
+      for (uint32_t k = 0; k < 64u; k++) {
+        const uint32_t v = c[l][k];
+        a += v & 0xffffu;
+        b += v >> 16;
+        c[l][k] = 0;
+      }
+      uint32_t* const dst = (uint32_t*)&counts[item];
+      if (a) atomicAdd(dst + 2u * l, a);
+      if (b && 2u * l + 1u < ZT_NCODE) atomicAdd(dst + 2u * l + 1u, b);
+    }
+    __syncthreads();
+  };
+  uint32_t cur = meta[sa].item;
+  for (uint32_t s = sa; s < sb; s++) {
+    const uint32_t item = meta[s].item;
+    if (item != cur) { flush(cur); cur = item; }
+    hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok + (size_t)s * hd::SEG_TOK);
+    uint32_t run = 0, lits = 0, lead = 0, hm = 0, want_dist = 0, ml = 0;
+    hze::slots_fwd(gw, sp[s].nslot[l], l, [&](uint32_t v) {
+      if (want_dist) {                               // (len | 0x8000, dist - 1): a match
+        const hze::Seq q = hze::make_seq_t(ct, run, ml, v + 1u);
+        if (hm) add(q.llc);                          // (a lane's first run: after the scans)
+        else lead = run;
+        add(36u + q.ofc);
+        add(68u + q.mlc);
+        hm = 1;
+        run = 0;
+        want_dist = 0;
+      } else if (v & 0x8000u) {
+        ml = (v & 0x7fffu) + 3u;
+        want_dist = 1;
+      } else {
+        run++;
+        lits++;
+      }
+    });
+    // literal ordinals: L = before this lane, q = after its last match (0: none before)
+    const uint32_t L = hz::wave_incl_scan_dpp(lits) - lits;
+    const uint32_t q = hm ? L + lits - run : 0u;
+    const uint32_t qprev = hz::wave_excl_max(q, (int)l);
+    if (hm) add(hze::make_seq_t(ct, L + lead - qprev, 3u, 1u).llc);
+  }
+  flush(cur);
+}
+
+__global__ void zstd_table_kernel(const uint32_t* __restrict__ offs, int64_t nchunks,
+                                  const hze::SeqCounts* __restrict__ counts, hze::Tabs* __restrict__ tabs,
+                                  uint32_t item_cap) {
+  const uint32_t total = offs[nchunks] < item_cap ? offs[nchunks] : item_cap;
+  const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= total) return;
+  hze::build_all(tabs[item]);      // (the predefined tables of a code type with < 2 distinct codes)
+  hze::frame_tables(tabs[item], counts[item]);
+}
+
 __global__ void __launch_bounds__(64) zstd_seg_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
                                                       const SegMeta* __restrict__ meta,
                                                       const EncItem* __restrict__ slots,
                                                       const hd::SegParse* __restrict__ sp,
                                                       const uint16_t* __restrict__ tok, uint8_t* __restrict__ zscr,
                                                       uint32_t* __restrict__ zsz, const uint8_t* __restrict__ lsec,
-                                                      const uint32_t* __restrict__ lsz, uint32_t seg_cap, int level) {
-  __shared__ hze::Tabs T;
-  if (threadIdx.x == 0) hze::build_all(T);
-  __syncthreads();
+                                                      const uint32_t* __restrict__ lsz, uint32_t seg_cap, int level,
+                                                      const hze::Tabs* __restrict__ tabs) {
+  __shared__ hze::Tabs T[ZT_SLOTS];
+  __shared__ hze::CodeTabs ct;
+  hze::code_tabs_fill(ct, threadIdx.x, 64u);
   uint32_t total = segoffs[nchunks];
   if (total > seg_cap) total = seg_cap;
-  const uint32_t s = blockIdx.x * 64u + threadIdx.x;
-  if (s >= total) return;
-  const SegMeta m = meta[s];
-  const EncItem it = slots[m.item];
-  const uint32_t g0 = segoffs[it.chunk] + it.seg0;
-  const uint32_t seg = s - g0;
-  hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
-  const uint32_t last = seg + 1 == hd::nsegments(it.len) ? 1u : 0u;
-  zsz[s] = hze::encode_segment(T, tok + (size_t)s * hd::SEG_TOK, sp + s, job, seg * (uint32_t)hd::SEG, m.seglen, last,
-                               zscr + (size_t)s * hze::ZCAP, hze::ZCAP, lsec + (size_t)s * hze::LCAP, lsz[s]);
+  const uint32_t s0 = blockIdx.x * 64u;
+  if (s0 >= total) return;
+  const uint32_t s = s0 + threadIdx.x;
+  const uint32_t base = meta[s0].item;
+  const uint32_t nframes = meta[(s0 + 64u < total ? s0 + 64u : total) - 1u].item - base + 1u;
+  // the wave's segments span nframes frames: their tables go to LDS ZT_SLOTS at a time
+  for (uint32_t f0 = 0; f0 < nframes; f0 += ZT_SLOTS) {
+    __syncthreads();
+    const uint32_t nf = nframes - f0 < ZT_SLOTS ? nframes - f0 : ZT_SLOTS;
+    constexpr uint32_t TW = sizeof(hze::Tabs) / 4u;
+    static_assert(sizeof(hze::Tabs) % 4u == 0u, "Tabs: whole dwords");
+    for (uint32_t k = threadIdx.x; k < nf * TW; k += 64u)
+      ((uint32_t*)&T[0])[k] = ((const uint32_t*)&tabs[base + f0])[k];
+    __syncthreads();
+    if (s >= total) continue;
+    const SegMeta m = meta[s];
+    if (m.item < base + f0 || m.item >= base + f0 + nf) continue;
+    const EncItem it = slots[m.item];
+    const uint32_t g0 = segoffs[it.chunk] + it.seg0;
+    const uint32_t seg = s - g0;
+    hd::EncJob job = {(const uint8_t*)it.src, it.len, level, it.ts, it.neb, it.off};
+    const uint32_t last = seg + 1 == hd::nsegments(it.len) ? 1u : 0u;
+    zsz[s] = hze::encode_segment(T[m.item - base - f0], ct, tok + (size_t)s * hd::SEG_TOK, sp + s, job,
+                                 seg * (uint32_t)hd::SEG, m.seglen, last, zscr + (size_t)s * hze::ZCAP, hze::ZCAP,
+                                 lsec + (size_t)s * hze::LCAP, lsz[s]);
+  }
 }
 
 __global__ void zstd_size_kernel(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ segoffs,
@@ -2292,18 +2405,30 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
                      clevel, 0u, item_cap, far,
                      e->enc_chain);
   if (cname == HSDS_CNAME_ZSTD) {
-    if (grow((void**)&e->ezs, &e->ezs_bytes, (size_t)seg_cap * (hze::ZCAP + hze::LCAP + 8) + 256)) return HSDS_ERR_DEVICE;
+    const size_t sz_zseg = al((size_t)seg_cap * (hze::ZCAP + hze::LCAP + 8));
+    const size_t sz_cnt = al((size_t)item_cap * sizeof(hze::SeqCounts));
+    if (grow((void**)&e->ezs, &e->ezs_bytes, sz_zseg + sz_cnt + (size_t)item_cap * sizeof(hze::Tabs) + 256))
+      return HSDS_ERR_DEVICE;
     uint8_t* zscr = e->ezs;
     uint8_t* lsec = zscr + (size_t)seg_cap * hze::ZCAP;
     uint32_t* zsz = (uint32_t*)(lsec + (size_t)seg_cap * hze::LCAP);
     uint32_t* lsz = zsz + seg_cap;
+    hze::SeqCounts* zcnt = (hze::SeqCounts*)(e->ezs + sz_zseg);
+    hze::Tabs* ztab = (hze::Tabs*)(e->ezs + sz_zseg + sz_cnt);
+    // the frames' sequence tables (FSE_Compressed_Mode, one set per frame)
+    if (hipMemsetAsync(zcnt, 0, sz_cnt, st) != hipSuccess) return HSDS_ERR_DEVICE;
+    hipLaunchKernelGGL(zstd_count_kernel, dim3((seg_cap + ZC_SEGS - 1) / ZC_SEGS), dim3(64), 0, st, segoffs, nchunks,
+                       meta, sp, tok,
+                       zcnt, seg_cap);
+    hipLaunchKernelGGL(zstd_table_kernel, dim3((item_cap + 63) / 64), dim3(64), 0, st, offs, nchunks,
+                       (const hze::SeqCounts*)zcnt, ztab, item_cap);
     if (hze::huff_lit_level(clevel))
       hipLaunchKernelGGL(zstd_lit_kernel, dim3(grid_for(e->zlit_blocks_per_cu, seg_cap)), dim3(64), 0, st, segoffs,
                          nchunks, sp, tok, lsec, lsz, seg_cap);
     else if (hipMemsetAsync(lsz, 0, (size_t)seg_cap * 4, st) != hipSuccess)
       return HSDS_ERR_DEVICE;
     hipLaunchKernelGGL(zstd_seg_kernel, dim3((seg_cap + 63) / 64), dim3(64), 0, st, segoffs, nchunks, meta, slots, sp,
-                       tok, zscr, zsz, lsec, lsz, seg_cap, clevel);
+                       tok, zscr, zsz, lsec, lsz, seg_cap, clevel, (const hze::Tabs*)ztab);
     hipLaunchKernelGGL(zstd_size_kernel, dim3((item_cap + 255) / 256), dim3(256), 0, st, offs, segoffs, nchunks, slots,
                        zsz, lzsize, seg_cap, item_cap);
     hipLaunchKernelGGL(layout_kernel, dim3(nb), dim3(tpb), 0, st, d_chunks, nchunks, (uint8_t*)d_dst, slots, counts,

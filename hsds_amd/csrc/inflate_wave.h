@@ -436,6 +436,28 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
   }
   return x - v;
 }
+// inclusive prefix sum over the 64 lanes by DPP (no LDS round trip): shifts of 1, 2, 4, 8
+// lanes inside each row of 16, then each row's last lane broadcast to the rows after it
+// (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3)
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+// exclusive prefix maximum over the lanes (lane 0: 0)
+__device__ __forceinline__ uint32_t wave_excl_max(uint32_t v, int lane) {
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x = y > x ? y : x;
+  }
+  const uint32_t e = __shfl_up(x, 1, 64);
+  return lane ? e : 0u;
+}
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;

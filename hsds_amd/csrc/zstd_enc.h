@@ -11,9 +11,13 @@
 //            per 8 KiB parse segment (the deflate encoder's P phase gives the matches);
 //   block    Compressed_Block: a Compressed_Literals_Block (the segment's own Huffman code,
 //            limited to 11 bits, its weights FSE-compressed; 4 streams) -- or the literal
-//            bytes raw when that is not smaller -- and a sequences section in
-//            Predefined_Mode for literal lengths, offsets and match lengths (offsets as
-//            Offset_Value = offset + 3: no repeat codes); a block whose content would not be
+//            bytes raw when that is not smaller -- and a sequences section whose literal
+//            length, offset and match length codes are FSE-coded with the FRAME's own
+//            tables (FSE_Compressed_Mode: frame_tables from the code counts of all its
+//            segments, count_segment; each block repeats the descriptions, so no block
+//            depends on an earlier one being compressed); a code type with fewer than two
+//            distinct codes in the frame uses the predefined table.  Offsets are sent as
+//            Offset_Value = offset + 3 (no repeat codes).  A block whose content would not be
 //            smaller than the segment is a Raw_Block.
 // lit_section: one wavefront per segment builds the literals section (token walk per parse
 // lane, the deflate encoder's cooperative Huffman build, weights + 4 streams).
@@ -41,9 +45,22 @@ struct CTab {
   int32_t dfs[MAXSYM];        // deltaFindState
   uint32_t log;
 };
+// the three sequence tables a block is encoded with, and how its sequences section
+// describes them: Symbol_Compression_Modes byte `mode` (0: all Predefined_Mode) followed by
+// `dsize` bytes of FSE_Compressed_Mode descriptions (LL, then OF, then ML)
+constexpr uint32_t DESC_MAX = 192;
 struct Tabs {
   CTab ll, of, ml;
+  uint32_t mode, dsize;
+  uint8_t desc[DESC_MAX];
 };
+// code counts of a frame's sequences (the input of its FSE_Compressed_Mode tables)
+struct SeqCounts {
+  uint32_t ll[36], of[32], ml[53];
+};
+// table logs of the compressed-mode tables: every block carries its descriptions, so they
+// stay short (RFC 8878 maxima: 9 / 8 / 9)
+constexpr uint32_t LL_LOG = 6, OF_LOG = 5, ML_LOG = 6;
 
 HZ_HD uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
@@ -102,6 +119,8 @@ HZ_HD void build_all(Tabs& T) {
   build(T.ll, 0);
   build(T.of, 1);
   build(T.ml, 2);
+  T.mode = 0;
+  T.dsize = 0;
 }
 
 // literal length -> code (RFC 8878 3.1.1.3.2.1.1)
@@ -209,6 +228,28 @@ HZ_HD Seq make_seq(uint32_t ll, uint32_t ml, uint32_t off) {
   return q;
 }
 
+// literal length / match length codes by table below 64 / 131 (ll_code and ml_code search
+// the baselines: lane-divergent loops that the whole wave runs), shared by a workgroup in LDS
+struct CodeTabs {
+  uint8_t ll[64];
+  uint8_t ml[128];           // match length 3 + i
+};
+HZ_HD void code_tabs_fill(CodeTabs& t, uint32_t i0, uint32_t step) {
+  for (uint32_t v = i0; v < 64u; v += step) t.ll[v] = (uint8_t)ll_code(v);
+  for (uint32_t v = i0; v < 128u; v += step) t.ml[v] = (uint8_t)ml_code(v + 3u);
+}
+HZ_HD Seq make_seq_t(const CodeTabs& t, uint32_t ll, uint32_t ml, uint32_t off) {
+  Seq q;
+  q.llc = ll < 64u ? t.ll[ll] : hb32(ll) + 19u;
+  q.llv = ll - zs::ll_base(q.llc);
+  q.mlc = ml - 3u < 128u ? t.ml[ml - 3u] : hb32(ml - 3u) + 36u;
+  q.mlv = ml - zs::ml_base(q.mlc);
+  const uint32_t ov = off + 3u;                    // Offset_Value: no repeat codes
+  q.ofc = hb32(ov);
+  q.ofv = ov - (1u << q.ofc);
+  return q;
+}
+
 // the 3-byte block header
 HZ_HD void block_header(uint8_t* out, uint32_t last, uint32_t type, uint32_t size) {
   const uint32_t h = last | (type << 1) | (size << 3);
@@ -281,6 +322,58 @@ HZ_HD uint32_t write_ncount(uint8_t* out, const int16_t* norm, uint32_t n, uint3
   out[o++] = (uint8_t)(bs >> 8);
   o -= 2u - (uint32_t)((bc + 7) / 8);
   return o;
+}
+
+// normalized counts norm[0..n) at `log` for counts cnt[0..n) (total > 0): every present
+// symbol gets at least one state, the rest in proportion, and the sum is exactly 2^log
+// (any such distribution is a valid FSE_Compressed_Mode table; n <= 2^log)
+HZ_HD void normalize(const uint32_t* cnt, uint32_t n, uint32_t log, int16_t* norm) {
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < n; k++) total += cnt[k];
+  const int32_t size = 1 << log;
+  int32_t sum = 0;
+  uint32_t big = 0;
+  for (uint32_t k = 0; k < n; k++) {
+    int32_t v = 0;
+    if (cnt[k]) {
+      v = (int32_t)(((uint64_t)cnt[k] * (uint32_t)size + total / 2u) / total);
+      v = v < 1 ? 1 : v;
+      if (cnt[k] > cnt[big]) big = k;
+    }
+    norm[k] = (int16_t)v;
+    sum += v;
+  }
+  while (sum > size) {                 // rounding overshoot: take from the largest
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < n; k++) if (norm[k] > norm[m]) m = k;
+    norm[m]--;
+    sum--;
+  }
+  norm[big] = (int16_t)(norm[big] + (size - sum));
+}
+
+// one code type's table: FSE_Compressed_Mode from the counts when at least two codes occur
+// (the description is appended to T.desc), else the predefined one.  which: 0 LL, 1 OF, 2 ML
+HZ_HD void frame_table(Tabs& T, CTab& t, const uint32_t* cnt, uint32_t n, uint32_t which, uint32_t log) {
+  uint32_t maxs = 0, distinct = 0;
+  for (uint32_t k = 0; k < n; k++) if (cnt[k]) { maxs = k; distinct++; }
+  if (distinct < 2u) { build(t, which); return; }
+  int16_t norm[MAXSYM];
+  normalize(cnt, maxs + 1u, log, norm);
+  build_norm(t, norm, maxs + 1u, log);
+  uint8_t d[80];
+  const uint32_t k = write_ncount(d, norm, maxs + 1u, log);
+  for (uint32_t i = 0; i < k && T.dsize < DESC_MAX; i++) T.desc[T.dsize++] = d[i];
+  T.mode |= 2u << (which == 0 ? 6u : which == 1 ? 4u : 2u);
+}
+
+// the tables of one frame (every block of it is encoded with them)
+HZ_HD void frame_tables(Tabs& T, const SeqCounts& c) {
+  T.mode = 0;
+  T.dsize = 0;
+  frame_table(T, T.ll, c.ll, 36u, 0u, LL_LOG);
+  frame_table(T, T.of, c.of, 32u, 1u, OF_LOG);
+  frame_table(T, T.ml, c.ml, 53u, 2u, ML_LOG);
 }
 
 // Huffman_Tree_Description of the code lengths len[0..256) into sh.tree (header byte
@@ -486,10 +579,49 @@ HZ_UNROLL
   }
 }
 
+// The sequences of a segment, last to first: emit(literal run, match length, offset).  The
+// backward walk knows a match's literal run once it reaches the match before it (or the
+// segment start), so each sequence is emitted one match late.
+template <class F>
+HZ_HD void walk_sequences(hz_gcu32* gw, const hd::SegParse* sp, F&& emit) {
+  uint32_t have = 0, pml = 0, poff = 0, run = 0;
+  for (int32_t l = hd::WAVE - 1; l >= 0; l--) {
+    // backward: slot k is held until slot k - 1 shows whether (k - 1, k) is a match
+    uint32_t pend = 0, hold = 0;
+    slots_bwd(gw, sp->nslot[l], (uint32_t)l, [&](uint32_t u) {
+      if (!hold) { pend = u; hold = 1; return; }
+      if (u & 0x8000u) {                           // (u, pend): a match
+        if (have) emit(run, pml, poff);
+        have = 1;
+        pml = (u & 0x7fffu) + 3u;
+        poff = pend + 1u;
+        run = 0;
+        hold = 0;
+      } else {
+        run++;                                     // pend: a literal (trailing ones belong to no sequence)
+        pend = u;
+      }
+    });
+    if (hold) run++;
+  }
+  if (have) emit(run, pml, poff);
+}
+
+// adds a segment's sequence codes to c (the frame's counts)
+HZ_HD void count_segment(const CodeTabs& ct, const uint16_t* tok, const hd::SegParse* sp, SeqCounts& c) {
+  hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
+  walk_sequences(gw, sp, [&](uint32_t ll, uint32_t ml, uint32_t off) {
+    const Seq q = make_seq_t(ct, ll, ml, off);
+    c.ll[q.llc]++;
+    c.of[q.ofc]++;
+    c.ml[q.mlc]++;
+  });
+}
+
 // Writes segment `seg` of a stream as one zstd block (header included) at out (cap bytes
 // of scratch, >= ZCAP).  tok / sp: the segment's parse tokens and counts; job / s0: the
 // stream input (a raw block copies the segment from it).  Returns the block size.
-HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegParse* sp, const hd::EncJob& job,
+HZ_HD uint32_t encode_segment(const Tabs& T, const CodeTabs& ct, const uint16_t* tok, const hd::SegParse* sp, const hd::EncJob& job,
                               uint32_t s0, uint32_t seglen, uint32_t last, uint8_t* out, uint32_t cap,
                               const uint8_t* lsec = nullptr, uint32_t lsize = 0) {
   hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
@@ -545,15 +677,14 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
     put8(out, p, cap, (nseq - 0x7f00u) >> 8, over);
   }
   if (nseq) {
-    put8(out, p, cap, 0u, over);                     // Predefined_Mode x 3
+    put8(out, p, cap, T.mode, over);                 // Symbol_Compression_Modes
+    for (uint32_t i = 0; i < T.dsize; i++) put8(out, p, cap, T.desc[i], over);
     BitD w;
     bd_init(w, out, p, cap, over);
     uint32_t sll = 0, sof = 0, sml = 0;
-    // backward walk: a match's literal run is known once the walk reaches the match
-    // before it (or the segment start), so each sequence is encoded one match late
-    uint32_t have = 0, pml = 0, poff = 0, run = 0, first = 1;
+    uint32_t first = 1;
     auto emit = [&](uint32_t ll, uint32_t ml, uint32_t off) {
-      const Seq q = make_seq(ll, ml, off);
+      const Seq q = make_seq_t(ct, ll, ml, off);
       if (first) {
         sml = fse_init(T.ml, q.mlc);
         sof = fse_init(T.of, q.ofc);
@@ -568,26 +699,7 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const uint16_t* tok, const hd::SegP
       bw_add(w, q.mlv, zs::ml_bits(q.mlc));
       bw_add(w, q.ofv, q.ofc);
     };
-    for (int32_t l = hd::WAVE - 1; l >= 0 && !w.over; l--) {
-      // backward: slot k is held until slot k - 1 shows whether (k - 1, k) is a match
-      uint32_t pend = 0, hold = 0;
-      slots_bwd(gw, sp->nslot[l], (uint32_t)l, [&](uint32_t u) {
-        if (!hold) { pend = u; hold = 1; return; }
-        if (u & 0x8000u) {                           // (u, pend): a match
-          if (have) emit(run, pml, poff);
-          have = 1;
-          pml = (u & 0x7fffu) + 3u;
-          poff = pend + 1u;
-          run = 0;
-          hold = 0;
-        } else {
-          run++;                                     // pend: a literal (trailing ones belong to no sequence)
-          pend = u;
-        }
-      });
-      if (hold) run++;
-    }
-    if (have) emit(run, pml, poff);
+    walk_sequences(gw, sp, emit);
     bw_add(w, sml, T.ml.log);
     bw_add(w, sof, T.of.log);
     bw_add(w, sll, T.ll.log);

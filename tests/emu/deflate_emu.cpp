@@ -119,7 +119,12 @@ extern "C" int64_t emu_blosclz_block(const uint8_t* src, uint32_t n, uint8_t* ds
 
 // zstd frame of one Blosc block (the zstd writer): parse, then one zstd block per 8 KiB
 // segment (zstd_enc.h), behind the frame header.  Returns the frame size or -1 past cap.
+// tables: 1 = the frame's FSE_Compressed_Mode sequence tables (the engine's), 0 = predefined
+extern "C" int64_t emu_zstd_frame_t(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level, int tables);
 extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level) {
+  return emu_zstd_frame_t(src, n, dst, cap, level, 1);
+}
+extern "C" int64_t emu_zstd_frame_t(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level, int tables) {
   const uint32_t nseg = hd::nsegments(n);
   std::vector<hd::SegParse> sp(nseg);
   std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
@@ -130,6 +135,14 @@ extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, 
   free(ps);
   hze::Tabs T;
   hze::build_all(T);
+  hze::CodeTabs ct;
+  hze::code_tabs_fill(ct, 0u, 1u);
+  if (tables) {
+    hze::SeqCounts c;
+    memset(&c, 0, sizeof(c));
+    for (uint32_t s = 0; s < nseg; s++) hze::count_segment(ct, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], c);
+    hze::frame_tables(T, c);
+  }
   std::vector<uint8_t> blk(hze::ZCAP), lsec(hze::LCAP);
   hze::LitShared* ls = (hze::LitShared*)calloc(1, sizeof(hze::LitShared));
   uint8_t hdr[16];
@@ -144,7 +157,7 @@ extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, 
     const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
     const uint32_t lsz = !hze::huff_lit_level(level) ? 0u
                          : hze::lit_section(*ls, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], lsec.data());
-    const uint32_t k = hze::encode_segment(T, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], job, s0, seglen,
+    const uint32_t k = hze::encode_segment(T, ct, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], job, s0, seglen,
                                            s + 1 == nseg ? 1u : 0u, blk.data(), hze::ZCAP, lsec.data(), lsz);
     put(blk.data(), k);
   }
