@@ -672,8 +672,8 @@ def run_cfg5(args, dev, rank=0):
     out["zstd_encode"] = {"value": round(slab_bytes / elz / 1e9, 2), "unit": "GB/s slab (scatter + encode)",
                           "ms_per_step": round(elz * 1e3, 3), "compressed_bytes": compz,
                           "encode_ms": round(eng.last_deflate_ms(), 3), "size_vs_libblosc_zstd": zr,
-                          "format": "Blosc-zstd frames (HCR blocksize, never split): raw literals + predefined "
-                                    "sequence tables, one zstd block per 8 KiB"}
+                          "format": "Blosc-zstd frames (HCR blocksize, never split): raw literals + each frame's "
+                                    "own FSE_Compressed_Mode sequence tables, one zstd block per 8 KiB"}
     # the same scatter + encode for a bitshuffle dataset (storUtil._shuffle codec 2:
     # bitshuffle+LZ4 objects, f32, 2048-element blocks, no outer compressor)
     from hsds_amd import _native as nat
