@@ -19,7 +19,11 @@ direct reads) wait for it instead of evicting slots the batch is gathering from.
 stored objects go up in one asynchronous copy from page-locked staging, the selections
 come back in one asynchronous copy into page-locked memory together with the decode
 statuses, and the batch waits for the device once; responses are views of that host
-buffer.
+buffer -- except responses smaller than 1/COPY_OUT_FRACTION of it, which are copied out, so
+that one small response kept by a slow client does not hold (page-locked, and never
+returned to the OS by torch's caching host allocator) a whole batch's buffer.
+stats["host_bytes"] counts the page-locked bytes the batches used, stats["copied_out"] the
+responses copied out.
 """
 import asyncio
 import json
@@ -28,6 +32,9 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 __all__ = ["ChunkBatcher"]
+
+# a response smaller than 1/COPY_OUT_FRACTION of its batch's page-locked buffer is copied out
+COPY_OUT_FRACTION = 8
 
 
 def _freeze(x):
@@ -66,7 +73,7 @@ class ChunkBatcher:
         self.max_batch = max_batch
         self.executor = executor or ThreadPoolExecutor(max_workers=1, thread_name_prefix="hsds-amd-batch")
         self._groups = {}        # group key -> {"reqs": [...], "timer": handle}
-        self.stats = {"batches": 0, "requests": 0, "reads": 0}
+        self.stats = {"batches": 0, "requests": 0, "reads": 0, "host_bytes": 0, "copied_out": 0}
 
     async def get_selection(self, read, dtype, chunk_dims, slices=None, filter_ops=None, fill_value=None,
                             layout_class=None, hyper_dims=None, chunk_init=False):
@@ -153,7 +160,12 @@ class ChunkBatcher:
                     abort()
                 raise
             vals = finish()
-        return _gather_finish(plan, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
+        if plan is not None:
+            self.stats["host_bytes"] += plan["host"].numel()
+        out = _gather_finish(plan, [(vals[index[r.chunk_id]], sl) for r, sl, _ in reqs], dtype, chunk_dims)
+        if plan is not None:
+            self.stats["copied_out"] += plan["copied"]
+        return out
 
 
 def _sel_shape(slices, chunk_dims):
@@ -235,11 +247,16 @@ def _gather_finish(plan, items, dtype, chunk_dims):
             out[k] = np.ascontiguousarray(a if slices is None else a[slices])
     if plan is not None:
         host = plan["host"].numpy()
+        small = host.size // COPY_OUT_FRACTION
+        plan["copied"] = 0
         for k, shape, o in zip(plan["dev_items"], plan["shapes"], plan["offs"]):
             if isinstance(items[k][0], BaseException):
                 continue                                       # the read failed after all
             n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
-            out[k] = host[o:o + n].view(dtype).reshape(shape)
+            v = host[o:o + n].view(dtype).reshape(shape)
+            # a small response is copied out: kept alone, a view would hold the whole buffer
+            out[k] = v.copy() if n < small else v
+            plan["copied"] += 1 if n < small else 0
     return out
 
 

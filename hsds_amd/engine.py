@@ -87,15 +87,23 @@ class HostBuffer:
             pass
 
 
-def to_device_bytes(arr, device):
-    """numpy structured / uint8 array -> uint8 tensor on `device`, queued on the current
-    stream: the bytes go through page-locked staging with an asynchronous copy (a pageable
-    copy makes torch synchronise the stream, i.e. wait for every kernel queued before it).
-    The staging block stays reserved by torch's pinned-memory cache until the copy ran."""
+def to_device_bytes(arr, device, stream=None):
+    """numpy structured / uint8 array -> uint8 tensor on `device`, queued on `stream` (the
+    current stream by default), the stream the kernel that reads it is launched on: the
+    bytes go through page-locked staging with an asynchronous copy (a pageable copy makes
+    torch synchronise the stream, i.e. wait for every kernel queued before it).  The
+    staging block stays reserved by torch's pinned-memory cache until the copy ran, and
+    the device tensor is recorded on `stream`, so its memory is not reused while a kernel
+    on that stream may still read it."""
     raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
     h = torch.empty(max(raw.size, 1), dtype=torch.uint8, pin_memory=True)
     h.numpy()[:raw.size] = raw
-    return h[:raw.size].to(device, non_blocking=True)
+    if stream is None:
+        return h[:raw.size].to(device, non_blocking=True)
+    with torch.cuda.stream(stream):
+        t = h[:raw.size].to(device, non_blocking=True)
+    t.record_stream(stream)
+    return t
 
 
 class ChunkEngine:
@@ -117,7 +125,7 @@ class ChunkEngine:
         per-chunk HSDS_* status codes land in `status` (int32 device tensor)."""
         if isinstance(chunk_descs, np.ndarray):
             n = chunk_descs.size
-            chunk_descs = to_device_bytes(chunk_descs, self.device)
+            chunk_descs = to_device_bytes(chunk_descs, self.device, stream)
         else:
             n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
         comp = {None: 0, "": 0, "scaleoffset": 0, "gzip": 1, "deflate": 1, "zlib": 1}.get(compressor, 2)
@@ -143,7 +151,7 @@ class ChunkEngine:
             raise NotImplementedError(f"Blosc codec {compressor!r} has no encoder in the hsds_amd engine")
         if isinstance(chunk_descs, np.ndarray):
             n = chunk_descs.size
-            chunk_descs = to_device_bytes(chunk_descs, self.device)
+            chunk_descs = to_device_bytes(chunk_descs, self.device, stream)
         else:
             n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
         rc = nat.lib().hsds_encode_batch_codec(self.eng.h, _ptr(src), _ptr(chunk_descs), n, _ptr(dst),
@@ -166,7 +174,7 @@ class ChunkEngine:
             n = chunk_descs.size
             if src_bytes is None:
                 src_bytes = int(chunk_descs["src_len"].sum()) if n else 0
-            chunk_descs = to_device_bytes(chunk_descs, self.device)
+            chunk_descs = to_device_bytes(chunk_descs, self.device, stream)
         else:
             n = chunk_descs.numel() // CHUNK_DESC_DTYPE.itemsize
         rc = nat.lib().hsds_encode_bitshuffle_batch(self.eng.h, _ptr(src), src.numel() * src.element_size(),
@@ -187,7 +195,7 @@ class ChunkEngine:
             if flags is None:
                 copy_descs = split_large_copy_descs(copy_descs)
             n = copy_descs.size
-            copy_descs = to_device_bytes(copy_descs, self.device)
+            copy_descs = to_device_bytes(copy_descs, self.device, stream)
         else:
             n = copy_descs.numel() // COPY_DESC_DTYPE.itemsize
         if flags is None:
@@ -203,7 +211,7 @@ class ChunkEngine:
     def compare(self, data, chunk, copy_descs, kind, differs, stream=None):
         if isinstance(copy_descs, np.ndarray):
             n = copy_descs.size
-            copy_descs = to_device_bytes(copy_descs, self.device)
+            copy_descs = to_device_bytes(copy_descs, self.device, stream)
         else:
             n = copy_descs.numel() // COPY_DESC_DTYPE.itemsize
         rc = nat.lib().hsds_compare_batch(self.eng.h, _ptr(data), _ptr(chunk), _ptr(copy_descs), n, int(kind),

@@ -162,3 +162,34 @@ def test_failed_batch_releases_every_pin(oracle_lib, monkeypatch):
     for i, v in enumerate(vals):
         np.testing.assert_array_equal(v.cpu().numpy(), truth[f"c-b_{i}_0"])
     assert all(n.pinned == 0 for n in cs.cache._lru.values())
+
+
+def test_small_responses_do_not_pin_the_batch_buffer(oracle_lib):
+    """responses are views of one page-locked buffer per batch; one smaller than
+    1/COPY_OUT_FRACTION of it is copied out, so keeping it does not keep the whole buffer.
+    A full-chunk response among 64 is a view (zero copy); the small selections own their
+    bytes."""
+    import torch
+    from hsds_amd.batcher import ChunkBatcher, COPY_OUT_FRACTION
+    from hsds_amd.datanode import ChunkRead, ChunkStore
+    dev = torch.device("cuda", 0)
+    dims = (64, 96)
+    truth, objs = _objs(oracle_lib, 8, dims, 14)
+    cs = ChunkStore(lambda key, off, ln: objs.get(key), mem_target=1 << 26, device=dev)
+    ops = {"compressor": "zlib", "shuffle": 1, "level": 4, "dtype": np.dtype("<f4")}
+    b = ChunkBatcher(cs, window_ms=50)
+    sels = [None] + [(slice(j, j + 1, 1), slice(0, 96, 1)) for j in range(63)]
+
+    async def main():
+        return await asyncio.gather(*[b.get_selection(ChunkRead(f"c-b_{j % 8}_0", f"k{j % 8}"), "<f4", dims,
+                                                      sels[j], filter_ops=ops) for j in range(64)])
+
+    res = asyncio.run(main())
+    assert b.stats["batches"] == 1 and b.stats["host_bytes"] > 0
+    full = res[0]
+    assert full.base is not None                              # the whole chunk: a view
+    for j in range(1, 64):
+        np.testing.assert_array_equal(res[j], truth[f"c-b_{j % 8}_0"][sels[j]])
+        assert res[j].nbytes * COPY_OUT_FRACTION < b.stats["host_bytes"]
+        assert res[j].base is None or res[j].base.nbytes == res[j].nbytes     # owns its bytes
+    assert b.stats["copied_out"] == 63
