@@ -101,12 +101,21 @@ static_assert(RGRP == 2 || RGRP == 4 || RGRP == 8, "RGRP: 2, 4 or 8 records");
 #define HZ2_RS 12
 #endif
 constexpr uint32_t RS = HZ2_RS;           // ring words per lane (a multiple of 4)
+#ifndef HZ2_MIRROR
+#define HZ2_MIRROR 1                      // a copy of ring slot 0 after slot RS - 1 (no wrap select)
+#endif
 // phase E literal staging: bytes per lane, stored whole (16: one 16-byte store per 16 literals)
 #ifndef HZ2_OS
 #define HZ2_OS 16
 #endif
 constexpr uint32_t OS = HZ2_OS;
 static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
+// wave priority by stream progress (s_setprio at every window start): HZ2_PRIO levels, the
+// highest for a stream's first 1/HZ2_PRIO; 0 = off (A/B round 5, 4096 chunks: F1 26.0 ->
+// 25.5 ms, F2 38.2 -> 35.9 ms; waves busy F1 0.897 -> 0.961, F2 0.83 -> 0.87)
+#ifndef HZ2_PRIO
+#define HZ2_PRIO 4
+#endif
 #ifndef HZ2_TICKN
 #define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 5)
 #endif
@@ -147,8 +156,13 @@ struct alignas(16) Shared {
       uint8_t lens[320 + 32];
     };
     struct {                      // phases A .. E
+#if HZ2_MIRROR
       uint32_t bring[RS + 1][WAVE];   // each lane's bit ring: stream word j in slot j % RS (word-major:
                                       // lanes hit distinct banks); slot RS mirrors slot 0
+#else
+      uint32_t bring[RS][WAVE];       // each lane's bit ring: stream word j in slot j % RS (word-major:
+                                      // lanes hit distinct banks)
+#endif
       union {
         uint32_t hbits[256];          // dynamic block header: 8192 stream bits from the header's quad
         uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
@@ -504,14 +518,20 @@ HZ_HD void br_put(Shared& sh, int lane, uint32_t k, uint32_t a0, uint32_t a1, ui
   sh.bring[k + 1u][lane] = a1;
   sh.bring[k + 2u][lane] = a2;
   sh.bring[k + 3u][lane] = a3;
+#if HZ2_MIRROR
   if (k == 0u) sh.bring[RS][lane] = a0;
+#endif
 }
 
 // ring words c+3 and c+4 (slot (c+3) % RS and the next; the mirror covers the wrap)
 HZ_HD void br_next(const Shared& sh, int lane, BR& r) {
   const uint32_t k = r.slot;
   r.n0 = sh.bring[k][lane];
+#if HZ2_MIRROR
   r.n1 = sh.bring[k + 1u][lane];
+#else
+  r.n1 = sh.bring[k + 1u == RS ? 0u : k + 1u][lane];
+#endif
 }
 
 HZ_HD uint32_t slot4(uint32_t k) { return k + 4u == RS ? 0u : k + 4u; }
@@ -934,6 +954,19 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
     }
     if (cur.kind == WK_END) break;
     const int wst = [&]() -> int {
+#if HZ_GPU && HZ2_PRIO
+      // VALU issue on a SIMD goes to the higher priority, then the OLDER wave: with one
+      // stream per wave the youngest waves finish last.  A wave's priority falls with its
+      // stream's progress, so the waves that lag get the issue slots
+      {
+        const uint32_t q = cur.out < dst_len ? (uint32_t)(((uint64_t)cur.out * HZ2_PRIO) / dst_len) : HZ2_PRIO - 1u;
+        const uint32_t pr = HZ2_UNI(HZ2_PRIO - 1u - q);
+        if (pr >= 3u) __builtin_amdgcn_s_setprio(3);
+        else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
+        else if (pr == 1u) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+#endif
       uint32_t pos = cur.pos, out = cur.out;
       uint32_t block_start = cur.block_start, bfinal = cur.bfinal, est = cur.est;
       int first_window = 0;
