@@ -110,6 +110,10 @@ constexpr uint32_t RS = HZ2_RS;           // ring words per lane (a multiple of 
 #endif
 constexpr uint32_t OS = HZ2_OS;
 static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
+// span stores: 16 bytes per lane where the span's dwords allow (1: on)
+#ifndef HZ2_ST16
+#define HZ2_ST16 1
+#endif
 // wave priority by stream progress (s_setprio at every window start): HZ2_PRIO levels, the
 // highest for a stream's first 1/HZ2_PRIO; 0 = off (A/B round 5, 4096 chunks: F1 26.0 ->
 // 25.5 ms, F2 38.2 -> 35.9 ms; waves busy F1 0.897 -> 0.961, F2 0.83 -> 0.87)
@@ -174,7 +178,7 @@ struct alignas(16) Shared {
     };
     struct {                      // phase M
       uint16_t smap[SPAN + 2];    // batch byte -> distance to its source (0: literal); [SPAN] stays 0
-      uint32_t sbuf[SPAN / 4 + 2];   // the batch's aligned dwords, assembled in LDS
+      alignas(16) uint32_t sbuf[SPAN / 4 + 4];   // the batch's aligned dwords, assembled in LDS
     };
   };
   uint32_t wnext[8];              // NW == 1: the next window's start (WinState), kept in LDS across E and M
@@ -1764,24 +1768,60 @@ HZ_UNROLL
         HZ_T(13);
         HZ2_MARK("M_STORE");
         // 4. store: whole dwords inside the span (dword 0 also when its head was loaded) and
-        // the stream; the span's edge bytes one by one
-        LANE_LOOP {
-          for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) {
+        // the stream; the span's edge bytes one by one.  HZ2_ST16: lane t takes dwords
+        // 4t .. 4t+3 with one 16-byte store when all four lie inside (a 1 KiB span is one
+        // store instruction); those lanes are a contiguous range [a, b] (only lane 0 can fail
+        // at the head, and a prefix of lanes fits the span), and the few dwords outside it
+        // -- [0, 4a) and [4b + 4, ndw) -- go dword by dword, one per lane
+        {
+          auto store_dword = [&](int lane, uint32_t k) {
+            (void)lane;
             const uint32_t x0 = xa + 4u * k;
             const bool inside = (int32_t)x0 >= 0 && x0 + 4u <= dst_len && x0 + 4u <= F + span && (k > 0u || !mis || head);
 #ifdef HZ2_EXP_NOMSTORE                   // (traffic attribution builds: outputs wrong)
-            if (inside || true) {
-              (void)inside;
-            } else {
+            (void)inside;
 #else
             if (inside) {
               *(hz_gu32*)(dst + x0) = sh.sbuf[k];
             } else {
-#endif
               for (uint32_t b = 0; b < 4u; b++) {
                 const uint32_t x = x0 + b;
                 if (x >= F && x < F + span && x < dst_len) dst[x] = ((const uint8_t*)sh.sbuf)[4u * k + b];
               }
+            }
+#endif
+          };
+#if HZ2_ST16
+          LANE_VAR(uint32_t, st4);
+          LANE_LOOP {
+            const uint32_t k0 = 4u * (uint32_t)lane, x0 = xa + 16u * (uint32_t)lane;
+            LV(st4) = (k0 + 4u <= ndw && (int32_t)x0 >= 0 && x0 + 16u <= dst_len && x0 + 16u <= F + span &&
+                       (lane > 0 || !mis || head)) ? 1u : 0u;
+          }
+          const uint64_t m4 = WAVE_BALLOT(LV(st4) != 0u);
+          if (m4) {
+            const uint32_t a = (uint32_t)__builtin_ctzll(m4), b = 63u - (uint32_t)__builtin_clzll(m4);
+            LANE_LOOP {
+#ifndef HZ2_EXP_NOMSTORE
+              if (LV(st4)) {
+                const uint32_t k0 = 4u * (uint32_t)lane;
+#if HZ_GPU
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(1))) u32x4 gu32x4;
+                *(gu32x4*)(dst + (uint32_t)(xa + 4u * k0)) = *(const u32x4*)&sh.sbuf[k0];   // (xa may wrap: 32-bit sum)
+#else
+                memcpy(dst + (uint32_t)(xa + 4u * k0), &sh.sbuf[k0], 16);
+#endif
+              }
+#endif
+              const uint32_t lo = 4u * a, hi = 4u * b + 4u, nun = lo + (ndw - hi);
+              for (uint32_t t = (uint32_t)lane; t < nun; t += 64u) store_dword(lane, t < lo ? t : hi + (t - lo));
+            }
+          } else
+#endif
+          {
+            LANE_LOOP {
+              for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) store_dword(lane, k);
             }
           }
         }
