@@ -818,7 +818,7 @@ def run_cfg4(args, dev, rank, world):
     return out
 
 
-TRAFFIC_ROUND = "r4"
+TRAFFIC_ROUND = "r5"
 
 
 def run_cfg4_full(args, dev, rank, world):

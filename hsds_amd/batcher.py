@@ -19,9 +19,11 @@ direct reads) wait for it instead of evicting slots the batch is gathering from.
 stored objects go up in one asynchronous copy from page-locked staging, the selections
 come back in one asynchronous copy into page-locked memory together with the decode
 statuses, and the batch waits for the device once; responses are views of that host
-buffer -- except responses smaller than 1/COPY_OUT_FRACTION of it, which are copied out, so
-that one small response kept by a slow client does not hold (page-locked, and never
-returned to the OS by torch's caching host allocator) a whole batch's buffer.
+buffer -- except small responses (at most COPY_OUT_MAX bytes and under 1/COPY_OUT_FRACTION of
+the buffer), which are copied out, so that one small selection kept by a slow client does not
+hold (page-locked, and never returned to the OS by torch's caching host allocator) a whole
+batch's buffer; whole chunks stay zero-copy views (copying 256 x 1 MiB responses took 3x the
+batch's own time).
 stats["host_bytes"] counts the page-locked bytes the batches used, stats["copied_out"] the
 responses copied out.
 """
@@ -33,8 +35,10 @@ import numpy as np
 
 __all__ = ["ChunkBatcher"]
 
-# a response smaller than 1/COPY_OUT_FRACTION of its batch's page-locked buffer is copied out
+# a response of at most COPY_OUT_MAX bytes and under 1/COPY_OUT_FRACTION of its batch's
+# page-locked buffer is copied out
 COPY_OUT_FRACTION = 8
+COPY_OUT_MAX = 16 << 10
 
 
 def _freeze(x):
@@ -247,7 +251,7 @@ def _gather_finish(plan, items, dtype, chunk_dims):
             out[k] = np.ascontiguousarray(a if slices is None else a[slices])
     if plan is not None:
         host = plan["host"].numpy()
-        small = host.size // COPY_OUT_FRACTION
+        small = min(host.size // COPY_OUT_FRACTION, COPY_OUT_MAX + 1)
         plan["copied"] = 0
         for k, shape, o in zip(plan["dev_items"], plan["shapes"], plan["offs"]):
             if isinstance(items[k][0], BaseException):

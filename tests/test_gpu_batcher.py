@@ -165,10 +165,10 @@ def test_failed_batch_releases_every_pin(oracle_lib, monkeypatch):
 
 
 def test_small_responses_do_not_pin_the_batch_buffer(oracle_lib):
-    """responses are views of one page-locked buffer per batch; one smaller than
-    1/COPY_OUT_FRACTION of it is copied out, so keeping it does not keep the whole buffer.
-    A full-chunk response among 64 is a view (zero copy); the small selections own their
-    bytes."""
+    """responses are views of one page-locked buffer per batch; a small one (at
+    most COPY_OUT_MAX bytes, under 1/COPY_OUT_FRACTION of it) is copied out, so keeping it
+    does not keep the whole buffer.  A full-chunk response among 64 is a view (zero copy);
+    the small selections own their bytes."""
     import torch
     from hsds_amd.batcher import ChunkBatcher, COPY_OUT_FRACTION
     from hsds_amd.datanode import ChunkRead, ChunkStore
