@@ -256,7 +256,24 @@ struct ParseShared {
     uint32_t freq[NSYM];
   };
 };
-static_assert(NSYM + 1 <= 5 * WAVE && NSYM + 1 <= HSIZE, "head entries saved per lane (counts + dummy)");
+// The parse's symbol counts, with one dummy entry per lane (a literal counts its absent
+// distance there): the LDS applies same-address atomics one after the other, and with one
+// dummy shared by all lanes every count instruction serialised on it (2/3 of the parse's
+// LDS cycles were bank conflicts, profiles/r5_sq_encode.txt; per-lane dummies: deflate
+// 125.5 -> 121.1 ms on the cfg5 slab).  HD_NREP > 1 spreads the counts over replicas, lane l
+// adding to replica l % HD_NREP (odd multiples of 4 dwords apart: different banks); measured
+// 122.1 ms at 4 and 6 replicas, so one set stays.  (An XOR bank swizzle of the ring and the
+// prev[] links -- the lanes start 128 bytes apart, one bank -- measured 130 ms: its address
+// arithmetic costs more than the conflicts.)
+#ifndef HD_NREP
+#define HD_NREP 1
+#endif
+constexpr uint32_t NREP = HD_NREP;
+constexpr uint32_t CSTR0 = (((uint32_t)NSYM + ((uint32_t)WAVE + NREP - 1u) / NREP) + 3u) & ~3u;
+constexpr uint32_t CSTR = (CSTR0 / 4u) % 2u ? CSTR0 : CSTR0 + 4u;   // entries per replica
+constexpr uint32_t CENT = NREP * CSTR;                               // head entries the counts take
+constexpr uint32_t NSAVE = (CENT + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;   // head entries saved per lane
+static_assert(CENT <= (uint32_t)HSIZE, "count replicas fit the head table");
 
 // bytes [p, p + 4) from the two words a, b they span: {b, a} >> 8 (p & 3) (v_alignbyte)
 HZ_HD uint32_t funnel(uint32_t a, uint32_t b, uint32_t p) {
@@ -464,8 +481,11 @@ HZ_HD uint32_t parse_range(ParseShared& sh, const EncJob& job, const Tune& tune,
     const uint32_t t0 = m ? (0x8000u | (best - 3u)) : lit;
     const uint32_t t1 = bd - 1u;
     // counts (sh.freq aliases sh.head; the dummy entry NSYM is restored with the heads)
-    lds_add(&sh.head[m ? 257u + len_code(best) : lit], 1u);
-    lds_add(&sh.head[m ? (uint32_t)NLL + dist_code(bd) : (uint32_t)NSYM], 1u);
+    {
+      const uint32_t rb = ((uint32_t)lane % NREP) * CSTR;
+      lds_add(&sh.head[rb + (m ? 257u + len_code(best) : lit)], 1u);
+      lds_add(&sh.head[rb + (m ? (uint32_t)NLL + dist_code(bd) : (uint32_t)NSYM + (uint32_t)lane / NREP)], 1u);
+    }
     pos += m ? best : 1u;
     // a pending slot pairs with t0; a match without one stores (t0, t1)
     if (npend || m)
@@ -572,20 +592,20 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
         }
       }
     }
-    // the symbol counts take head entries [0, NSYM) for the parse
-    LANE_VAR(uint32_t, hk0);
-    LANE_VAR(uint32_t, hk1);
-    LANE_VAR(uint32_t, hk2);
-    LANE_VAR(uint32_t, hk3);
-    LANE_VAR(uint32_t, hk4);
+    // the symbol counts (NREP replicas) take head entries [0, CENT) for the parse
+#if HZ_GPU
+    uint32_t hk[NSAVE];                  // (per lane: LV(hk)[u])
+#else
+    uint32_t hk[64][NSAVE];
+#endif
     HD_LDS_SYNC();
     LANE_LOOP {
-      LV(hk0) = sh.head[lane];
-      LV(hk1) = sh.head[lane + WAVE];
-      LV(hk2) = sh.head[lane + 2 * WAVE];
-      LV(hk3) = sh.head[lane + 3 * WAVE];
-      LV(hk4) = sh.head[lane + 4 * WAVE];
-      for (int k = lane; k < NSYM; k += WAVE) sh.freq[k] = 0;
+HZ_UNROLL
+      for (uint32_t u = 0; u < NSAVE; u++) {
+        const uint32_t k = (uint32_t)lane + u * (uint32_t)WAVE;
+        LV(hk)[u] = k < CENT ? sh.head[k] : 0u;
+      }
+      for (uint32_t k = (uint32_t)lane; k < CENT; k += WAVE) sh.head[k] = 0;
     }
     HD_LDS_SYNC();
 
@@ -604,12 +624,20 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     }
     HD_LDS_SYNC();
     LANE_LOOP {
-      for (int s = lane; s < NSYM; s += WAVE) out->freq[s] = sh.freq[s];
-      sh.head[lane] = LV(hk0);
-      sh.head[lane + WAVE] = LV(hk1);
-      sh.head[lane + 2 * WAVE] = LV(hk2);
-      sh.head[lane + 3 * WAVE] = LV(hk3);
-      sh.head[lane + 4 * WAVE] = LV(hk4);
+      for (int s = lane; s < NSYM; s += WAVE) {
+        uint32_t c = 0;
+HZ_UNROLL
+        for (uint32_t r = 0; r < NREP; r++) c += sh.head[r * CSTR + (uint32_t)s];
+        out->freq[s] = c;
+      }
+    }
+    HD_LDS_SYNC();
+    LANE_LOOP {
+HZ_UNROLL
+      for (uint32_t u = 0; u < NSAVE; u++) {
+        const uint32_t k = (uint32_t)lane + u * (uint32_t)WAVE;
+        if (k < CENT) sh.head[k] = LV(hk)[u];
+      }
       // the segment's chain links join the far ring once the segment is parsed (written
       // earlier, they would overwrite links FARW back that this parse still follows)
       if (gfar)
