@@ -123,6 +123,17 @@ static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
 #ifndef HZ2_TICKN
 #define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 5)
 #endif
+// one decode pass (HZ2_FUSE = 1): phases A, A' and R emit every token they count -- literal
+// bytes and match records -- into the lane's own fixed region of the scratch (lane s:
+// records [s MCAP_LANE, ...), literals [s LCAP_LANE, ...), numbered from the lane's first
+// recorded start), so phase E's second decode is gone.  A lane's valid range is a suffix
+// of what it emitted (from the record its predecessor met); phase M maps a window record
+// or literal rank to its lane's region with a wave-uniform cursor over the lanes' ranges.
+// The recorded starts live in registers (the LDS holds the staging instead).  0: phase E
+// decodes every valid range again into the window-ordered ring (rounds 2-5)
+#ifndef HZ2_FUSE
+#define HZ2_FUSE 1
+#endif
 constexpr uint32_t TICKN = HZ2_TICKN;     // tokens between ring refills
 static_assert(RS % 4 == 0 && RS >= 8, "RS: whole quads");
 // ring words a lane needs at a tick: TICKN tokens move the window at most
@@ -179,6 +190,13 @@ struct alignas(16) Shared {
     struct {                      // phase M
       uint16_t smap[SPAN + 2];    // batch byte -> distance to its source (0: literal); [SPAN] stays 0
       alignas(16) uint32_t sbuf[SPAN / 4 + 4];   // the batch's aligned dwords, assembled in LDS
+#if HZ2_FUSE
+      // lane s's share of the window (written after the prefix sums): its first window
+      // record mb[s] and literal rank lb[s], the region index minus the window index of its
+      // records (rdl) and literals (ldl), the window position minus the region position of
+      // its records (odl), and the end of its literal ranks (le)
+      uint32_t mb[WAVE], rdl[WAVE], odl[WAVE], lb[WAVE], le[WAVE], ldl[WAVE];
+#endif
     };
   };
   uint32_t wnext[8];              // NW == 1: the next window's start (WinState), kept in LDS across E and M
@@ -691,6 +709,26 @@ HZ_HD Tok rtok(const Shared* sh, const BR& r) {
 
 // a[u] for a register array and a runtime u < MPL (no dynamic register indexing)
 HZ_HD uint32_t sel4(const uint32_t* a, uint32_t u) { return u == 0u ? a[0] : u == 1u ? a[1] : u == 2u ? a[2] : a[3]; }
+// a[j] of a lane's K recorded starts (registers) for a runtime j < K: masks OR-ed (a select
+// chain is folded back into an indexed load, which puts the array in scratch)
+HZ_HD uint32_t selk(const uint32_t* a, uint32_t j) {
+  uint32_t v = 0;
+HZ_UNROLL
+  for (uint32_t i = 0; i < (uint32_t)K; i++) v |= a[i] & (0u - (uint32_t)(j == i));
+  return v;
+}
+HZ_HD void setk(uint32_t* a, uint32_t j, uint32_t v, bool on) {
+HZ_UNROLL
+  for (uint32_t i = 0; i < (uint32_t)K; i++) a[i] = (on && j == i) ? v : a[i];
+}
+// a lane's MPL match records (absolute position, len << 16 | dist - 1): one reaches before
+// the stream's first byte
+HZ_HD bool rec_bad(const uint32_t* o, const uint32_t* w) {
+  bool bad = false;
+HZ_UNROLL
+  for (uint32_t u = 0; u < MPL; u++) bad |= o[u] != 0xffffffffu && (w[u] & 0xffffu) + 1u > o[u];
+  return bad;
+}
 
 HZ_HD uint32_t tok_len(uint32_t t) { return (t & T_MATCH) ? ((t >> 16) & 0x1ffu) : 1u; }
 
@@ -1166,6 +1204,58 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       LANE_VAR(uint32_t, cl);      // literals since the first record
       LANE_VAR(uint32_t, ek);      // END_*
       LANE_VAR(uint32_t, ea);      // position after the EOB token
+#if HZ2_FUSE
+      LANE_ARR(uint32_t, rcv, K);  // the lane's recorded starts
+      LANE_ARR(uint32_t, nxr, K);  // its successor's (phase A')
+      // lane s's successor's recorded starts into its registers (every lane active)
+      auto fetch_succ = [&]() {
+#if HZ_GPU
+        const int sl = ((HZ_LANE_ID() + 1) & 63) << 2;
+HZ_UNROLL
+        for (uint32_t j = 0; j < (uint32_t)K; j++) nxr[j] = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)rcv[j]);
+#else
+        for (int s = 0; s < 63; s++)
+          for (uint32_t j = 0; j < (uint32_t)K; j++) nxr[s][j] = rcv[s + 1][j];
+#endif
+      };
+      // a counted token into the lane's region: the literal byte and the match record
+      // (position = output bytes since the first record) are staged unconditionally -- the one
+      // that does not apply sits in the slot the next literal / match overwrites -- and a
+      // completed group of OS literals / RGRP records is stored whole
+      auto emit = [&](int lane, const Tok& t, bool cnt, uint32_t o, uint32_t m, uint32_t l) {
+        sh.ostage[lane][l & (OS - 1u)] = (uint8_t)t.v;
+        sh.rstage[lane][m & (RGRP - 1u)] = (uint64_t)o | ((uint64_t)((t.len << 16) | (t.v - 1u)) << 32);
+        if (cnt && t.kind == TK_LIT && ((l + 1u) & (OS - 1u)) == 0u) {
+          hz_gu8* const p = lits + (uint32_t)lane * LCAP_LANE + (l + 1u - OS);
+#if HZ_GPU
+          if constexpr (OS == 16u) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(1))) u32x4 gu32x4;
+            *(gu32x4*)p = *(const u32x4*)&sh.ostage[lane][0];
+          } else if constexpr (OS == 8u) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            typedef __attribute__((address_space(1))) u32x2 gu32x2;
+            *(gu32x2*)p = *(const u32x2*)&sh.ostage[lane][0];
+          } else {
+            *(hz_gu32*)p = *(const uint32_t*)&sh.ostage[lane][0];
+          }
+#else
+          memcpy(p, &sh.ostage[lane][0], OS);
+#endif
+        }
+        if (cnt && t.kind == TK_MATCH && (m & (RGRP - 1u)) == RGRP - 1u) {
+          hz_gu64* const p = ring64 + (uint32_t)lane * MCAP_LANE + (m & ~(RGRP - 1u));
+#if HZ_GPU
+          typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+          typedef __attribute__((address_space(1))) u64x2 gu64x2;
+HZ_UNROLL
+          for (uint32_t k = 0; k < RGRP; k += 2u) *(gu64x2*)(p + k) = *(const u64x2*)&sh.rstage[lane][k];
+#else
+          for (uint32_t k = 0; k < RGRP; k++) p[k] = sh.rstage[lane][k];
+#endif
+        }
+      };
+#endif
       LANE_LOOP {
         const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
         const uint32_t p0 = (lane > 0 && ss - ws > W) ? ss - W : ws;
@@ -1173,6 +1263,10 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
         br_init(sh, lane, S, r, p0);
         uint32_t steps = 0;
         uint32_t nr = 0, o = 0, m = 0, l = 0, e = END_NONE, after = 0;
+#if HZ2_FUSE
+HZ_UNROLL
+        for (uint32_t j = 0; j < (uint32_t)K; j++) LV(rcv)[j] = 0u;
+#endif
         // one loop for the warm-up (tokens before ss are decoded and dropped: whatever they
         // are, even invalid codes, which advance by their table length) and the segment.
         // Branch-free body: the only exit is at the top (a token that ends the lane sets e
@@ -1183,6 +1277,18 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           if (tp >= se || e != END_NONE) break;
           br_next(sh, lane, r);
           const bool inseg = tp >= ss;
+#if HZ2_FUSE
+          {
+            // the first K starts in the segment (registers; the select chain only runs while
+            // some lane still records)
+            const bool rk = inseg && nr < (uint32_t)K;
+#if HZ_GPU
+            if (WAVE_BALLOT(rk))
+#endif
+              setk(LV(rcv), nr, rec_pack(tp - ss, o, m, l), rk);
+            nr += rk ? 1u : 0u;
+          }
+#else
           {
             // a record past the K-th (or in the warm-up) goes to the lane's endp word,
             // which phase A' overwrites
@@ -1191,12 +1297,16 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             *rp = rec_pack(tp - ss, o, m, l);
             nr += rk ? 1u : 0u;
           }
+#endif
           const Tok t = rtok(&sh, r);
           const bool ismatch = t.kind == TK_MATCH, islit = t.kind == TK_LIT;
           const bool stop = inseg && (t.kind >= TK_EOB || (ismatch && m >= MCAP_LANE) || (islit && l >= LCAP_LANE));
           e = stop ? (t.kind == TK_EOB ? END_EOB : t.kind == TK_ERR ? END_ERR : END_CUT) : e;
           after = stop ? tp + t.n : after;
           const bool cnt = inseg && !stop;
+#if HZ2_FUSE
+          emit(lane, t, cnt, o, m, l);
+#endif
           o += cnt ? t.len : 0u;
           m += (cnt && ismatch) ? 1u : 0u;
           l += (cnt && islit) ? 1u : 0u;
@@ -1213,6 +1323,33 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       HZ_T(4);
       // -------- phase A': continuation until lane+1's recorded path is met --------
       // (a lane that ended leaves its successor at SYNC_NONE)
+      // (in the loop below: the successor's recorded starts at or past `rel` -- k, the first
+      // of them -- are passed: none left ends the search; one at `rel` is the sync)
+#if HZ2_FUSE
+      // registers: every start compared at once (a runtime index would put them in scratch)
+#define HZ2_SYNC_TEST(lane_)                                                                     \
+      {                                                                                          \
+        uint32_t nlt = 0, hit = SYNC_FAIL;                                                       \
+        HZ_UNROLL for (uint32_t i = 0; i < (uint32_t)K; i++) {                                   \
+          const uint32_t q = hz2::rec_rel(LV(nxr)[i]);                                           \
+          nlt += (i < nrn && q < rel) ? 1u : 0u;                                                 \
+          hit = (i < nrn && q == rel) ? i : hit;                                                 \
+        }                                                                                        \
+        k = nlt;                                                                                 \
+        if (k >= nrn) break;                                                                     \
+        if (hit != SYNC_FAIL) { res = hit; break; }                                              \
+      }
+#define HZ2_EMIT(lane_, t_, c_, o_, m_, l_) emit((lane_), (t_), (c_), (o_), (m_), (l_))
+      fetch_succ();
+#else
+#define HZ2_SYNC_TEST(lane_)                                                                     \
+      {                                                                                          \
+        while (k < nrn && hz2::rec_rel(sh.rec[k][(lane_) + 1]) < rel) k++;                      \
+        if (k >= nrn) break;                                                                     \
+        if (hz2::rec_rel(sh.rec[k][(lane_) + 1]) == rel) { res = k; break; }                    \
+      }
+#define HZ2_EMIT(lane_, t_, c_, o_, m_, l_) do { } while (0)
+#endif
 #define HZ2_CONTINUE(lane_)                                                                      \
       do {                                                                                       \
         BR r = LV(rd);                                                                           \
@@ -1228,9 +1365,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           for (;;) {                                                                             \
             const uint32_t tp = hz2::br_pos(r);                                                  \
             const uint32_t rel = tp - base;                                                      \
-            while (k < nrn && hz2::rec_rel(sh.rec[k][(lane_) + 1]) < rel) k++;                   \
-            if (k >= nrn) break;                                                                 \
-            if (hz2::rec_rel(sh.rec[k][(lane_) + 1]) == rel) { res = k; break; }                 \
+            HZ2_SYNC_TEST(lane_);                                                                \
             hz2::br_next(sh, lane, r);                                                           \
             const hz2::Tok t = hz2::rtok(&sh, r);                                                \
             if (t.kind >= hz2::TK_EOB) {                                                         \
@@ -1239,6 +1374,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
             if ((t.kind == hz2::TK_MATCH && m >= MCAP_LANE) || (t.kind == hz2::TK_LIT && l >= LCAP_LANE)) { \
               e = END_CUT; res = SYNC_NONE; break;                                               \
             }                                                                                    \
+            HZ2_EMIT(lane, t, true, o, m, l);                                                    \
             o += t.len;                                                                          \
             m += t.kind == hz2::TK_MATCH ? 1u : 0u;                                              \
             l += t.kind == hz2::TK_LIT ? 1u : 0u;                                                \
@@ -1272,10 +1408,16 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
               const uint32_t tp = br_pos(r);
               if (!(tp < se || nr == 0)) break;
               br_next(sh, lane, r);
+#if HZ2_FUSE
+              setk(LV(rcv), nr, rec_pack(tp - ss, o, m, l), nr < (uint32_t)K);
+              nr += nr < (uint32_t)K ? 1u : 0u;
+#else
               if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m, l); nr++; }
+#endif
               const Tok t = rtok(&sh, r);
               if (t.kind >= TK_EOB) { e = t.kind == TK_EOB ? END_EOB : END_ERR; after = tp + t.n; break; }
               if ((t.kind == TK_MATCH && m >= MCAP_LANE) || (t.kind == TK_LIT && l >= LCAP_LANE)) { e = END_CUT; break; }
+              HZ2_EMIT(lane, t, true, o, m, l);
               o += t.len;
               m += t.kind == TK_MATCH ? 1u : 0u;
               l += t.kind == TK_LIT ? 1u : 0u;
@@ -1288,12 +1430,17 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
           }
         }
         HZ2_LSYNC();
+#if HZ2_FUSE
+        fetch_succ();     // (a successor redone in an earlier round has new starts)
+#endif
         LANE_LOOP {
           if ((redo_m >> lane) & 1ull) HZ2_CONTINUE(lane);
         }
         HZ2_LSYNC();
       }
 #undef HZ2_CONTINUE
+#undef HZ2_SYNC_TEST
+#undef HZ2_EMIT
 
       HZ_T(6);
       // -------- validity, window end, prefix sums --------
@@ -1307,11 +1454,19 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       LANE_VAR(uint32_t, wmat);
       LANE_VAR(uint32_t, wlit);
       LANE_VAR(uint32_t, sbit);    // exact start bit of the lane's range
+#if HZ2_FUSE
+      LANE_VAR(uint32_t, srec);    // the record the lane's range starts at
+#endif
       LANE_LOOP {
         uint32_t wo = 0, wm = 0, wl = 0, sb = 0;
         if ((uint32_t)lane < V) {
           const uint32_t k = sh.syncw[lane];
+#if HZ2_FUSE
+          const uint32_t rc = selk(LV(rcv), k);
+          LV(srec) = rc;
+#else
           const uint32_t rc = sh.rec[k][lane];
+#endif
           wo = LV(co) - rec_out(rc);
           wm = LV(cm) - rec_mat(rc);
           wl = LV(cl) - rec_lit(rc);
@@ -1365,6 +1520,29 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       if (stats) stats->matches += mtotal;
       if (out + wtotal > dst_len) return ST_SIZE;
       if (npos > limit_bits) return ST_TRUNC;
+#if HZ2_FUSE
+      // the valid lanes' last, partial groups (the staging dies below: the maps overlay it)
+      LANE_LOOP {
+        if ((uint32_t)lane < V) {
+          const uint32_t m = LV(cm), l = LV(cl);
+          hz_gu64* const rp = ring64 + (uint32_t)lane * MCAP_LANE;
+          hz_gu8* const lp = lits + (uint32_t)lane * LCAP_LANE;
+          for (uint32_t k = m & ~(RGRP - 1u); k < m; k++) rp[k] = sh.rstage[lane][k & (RGRP - 1u)];
+          for (uint32_t k = l & ~(OS - 1u); k < l; k++) lp[k] = sh.ostage[lane][k & (OS - 1u)];
+        }
+      }
+      HZ2_LSYNC();
+      LANE_LOOP {
+        const uint32_t rc = (uint32_t)lane < V ? LV(srec) : 0u;
+        sh.mb[lane] = LV(mbase);
+        sh.rdl[lane] = (uint32_t)lane * MCAP_LANE + rec_mat(rc) - LV(mbase);
+        sh.odl[lane] = out + LV(obase) - rec_out(rc);
+        sh.lb[lane] = LV(lbase);
+        sh.le[lane] = LV(lbase) + LV(wlit);
+        sh.ldl[lane] = (uint32_t)lane * LCAP_LANE + rec_lit(rc) - LV(lbase);
+      }
+      HZ2_LSYNC();
+#endif
 
       {  // the next window's start: the other wavefront may begin its sync phases now
         WinState nx;
@@ -1392,6 +1570,7 @@ int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_bas
       }
 
       HZ_T(7);
+#if !HZ2_FUSE
       // -------- phase E: exact decode of every valid range --------
       // Nothing goes to dst here: literal bytes go to the window's literal stream (lane i's
       // literals at lbase[i]..., staged 16 bytes at a time in LDS and stored whole), matches
@@ -1489,6 +1668,7 @@ HZ_UNROLL
         if (stats) stats->steps_e += steps;
       }
       if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
+#endif
       HZ2_GSYNC();
 
       {
@@ -1517,6 +1697,58 @@ HZ_UNROLL
       LANE_LOOP { LV(ra1) = 0; LV(ra2) = 0; }
       LANE_ARR(uint32_t, ro, MPL);
       LANE_ARR(uint32_t, rw, MPL);
+#if HZ2_FUSE
+      // window records jb + lane + 64 u from their lanes' regions (positions made absolute):
+      // rcur, the last lane whose first record is at or before jb, only grows; the lanes
+      // whose records the MPL x 64 touch are walked from it (a batch spans a few)
+      uint32_t rcur = 0;
+      auto load_recs = [&](uint32_t jb, auto& xo, auto& xw) {
+        // the lanes' shares into registers (one LDS round trip), walked by v_readlane
+        LANE_VAR(uint32_t, vmb);
+        LANE_VAR(uint32_t, vrd);
+        LANE_VAR(uint32_t, vod);
+        LANE_LOOP { LV(vmb) = sh.mb[lane]; LV(vrd) = sh.rdl[lane]; LV(vod) = sh.odl[lane]; }
+        while (rcur < 63u && LV_AT(vmb, rcur + 1u) <= jb) rcur++;
+        LANE_ARR(uint32_t, dr, MPL);
+        LANE_ARR(uint32_t, dd, MPL);
+        {
+          const uint32_t r0 = LV_AT(vrd, rcur), o0 = LV_AT(vod, rcur);
+          LANE_LOOP {
+HZ_UNROLL
+            for (uint32_t u = 0; u < MPL; u++) { LV(dr)[u] = r0; LV(dd)[u] = o0; }
+          }
+        }
+        const uint32_t jl = jb + 64u * MPL;
+        for (uint32_t s = rcur; s < 63u;) {
+          const uint32_t b = LV_AT(vmb, s + 1u);
+          if (b >= jl || b >= mtotal) break;
+          s++;
+          const uint32_t r1 = LV_AT(vrd, s), o1 = LV_AT(vod, s);
+          LANE_LOOP {
+HZ_UNROLL
+            for (uint32_t u = 0; u < MPL; u++) {
+              const bool in = jb + (uint32_t)lane + 64u * u >= b;
+              LV(dr)[u] = in ? r1 : LV(dr)[u];
+              LV(dd)[u] = in ? o1 : LV(dd)[u];
+            }
+          }
+        }
+        LANE_LOOP {
+HZ_UNROLL
+          for (uint32_t u = 0; u < MPL; u++) {
+            // (unconditional loads: a record past the window reads slot 0)
+            const uint32_t j = jb + (uint32_t)lane + 64u * u;
+            const bool ok = j < mtotal;
+            const uint64_t v = ring64[ok ? j + LV(dr)[u] : 0u];
+            LV(xo)[u] = ok ? (uint32_t)v + LV(dd)[u] : 0xffffffffu;
+            LV(xw)[u] = ok ? (uint32_t)(v >> 32) : 0u;
+          }
+        }
+      };
+      load_recs(0u, ro, rw);
+      // literal ranks -> regions: the cursor lane lcur holds ranks up to lend (exclusive)
+      uint32_t lcur = 0, lend = HZ2_UNI(sh.le[0]), lcd = HZ2_UNI(sh.ldl[0]);
+#else
       LANE_LOOP {
 HZ_UNROLL
         for (uint32_t u = 0; u < MPL; u++) {
@@ -1525,6 +1757,7 @@ HZ_UNROLL
           LV(rw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
         }
       }
+#endif
       LANE_LOOP { if (lane == 0) sh.smap[SPAN] = 0; }
       const uint32_t wend = out + wtotal;
       uint32_t F = out, L0 = 0;      // frontier and its rank in the literal stream
@@ -1541,6 +1774,10 @@ HZ_UNROLL
         HZ_T(14);
         HZ2_MARK("M_BATCH");
         if (stats) stats->batches++;
+#if HZ2_FUSE
+        // (phase E's check, on the records' absolute positions: a distance past the stream start)
+        if (WAVE_BALLOT(hz2::rec_bad(LV(ro), LV(rw)))) return ST_DATA;
+#endif
         uint32_t nb = 0, open_ = 1;
 HZ_UNROLL
         for (uint32_t u = 0; u < MPL; u++) {
@@ -1563,8 +1800,15 @@ HZ_UNROLL
         const uint32_t xa = F - mis;                           // stream position of dword 0
         const uint32_t ndw = (span + mis + 3u) >> 2;
         const bool head = mis && (int32_t)xa >= 0 && xa + 4u <= dst_len;   // dword 0 loaded (whole-stored)
-        uint32_t hv = 0;
-        if (head) hv = hcar_ok ? hcar : *(hz_gu32*)(dst + xa);   // the previous span's last dword
+        // (the previous span's last dword; loaded only for a window's first span, and waited
+        // for inside that branch: a load left pending at the merge makes the compiler wait
+        // for it -- a memory latency -- on every span)
+        uint32_t hl = hcar;
+        if (head && !hcar_ok) {
+          hl = *(hz_gu32*)(dst + xa);
+          HZ2_VMWAIT();
+        }
+        const uint32_t hv = head ? hl : 0u;
         HZ_T(8);
         // the whole map is cleared (three 16-byte stores per lane): slots past the span read 0
         static_assert(SPAN % 256u == 0u, "smap clear: whole 8-byte stores per lane");
@@ -1625,6 +1869,9 @@ HZ_UNROLL
         // prefetch the next batch's records
         LANE_ARR(uint32_t, no, MPL);
         LANE_ARR(uint32_t, nw, MPL);
+#if HZ2_FUSE
+        load_recs(b0 + nb, no, nw);
+#else
         LANE_LOOP {
 HZ_UNROLL
           for (uint32_t u = 0; u < MPL; u++) {
@@ -1633,6 +1880,7 @@ HZ_UNROLL
             LV(nw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
           }
         }
+#endif
         HZ_T(11);
         HZ2_MARK("M_JUMP");
         // 2. pointer jumping over the span's match bytes (branch-free per slot: a slot's
@@ -1692,6 +1940,12 @@ HZ_UNROLL
         LANE_LOOP { LV(lb) = 0; LV(fb) = 0; if (lane == 0) sh.sbuf[0] = hv; }
         HZ2_LSYNC();
         uint32_t lcnt = 0;                      // literals of the span so far (wave-uniform)
+#if HZ2_FUSE
+        LANE_VAR(uint32_t, vlb);                // the lanes' literal shares (registers, v_readlane)
+        LANE_VAR(uint32_t, vle);
+        LANE_VAR(uint32_t, vld);
+        LANE_LOOP { LV(vlb) = sh.lb[lane]; LV(vle) = sh.le[lane]; LV(vld) = sh.ldl[lane]; }
+#endif
         // two halves of GH slots: GH loaded bytes in flight per lane (all 24 spill)
         constexpr uint32_t GH = RGP / 2u;
 HZ_UNROLL
@@ -1701,6 +1955,19 @@ HZ_UNROLL
           for (uint32_t k = 0; k < GH; k++) {
             const uint32_t i = h + k;
             const uint64_t bm = WAVE_BALLOT(((LV(vm) >> i) & 1u) && LV(dq)[i] == 0u);
+#if HZ2_FUSE
+            // the slot's literal ranks [R0, R1): region deltas by the cursor
+            const uint32_t R0 = L0 + lcnt, R1 = R0 + (uint32_t)hz::popc64(bm);
+            LANE_VAR(uint32_t, ldx);
+            LANE_LOOP { LV(ldx) = lcd; }
+            while (R1 > lend && lcur < 63u) {
+              lcur++;
+              const uint32_t b = LV_AT(vlb, lcur);
+              lend = LV_AT(vle, lcur);
+              lcd = LV_AT(vld, lcur);
+              LANE_LOOP { LV(ldx) = R0 + hz2::lane_rank(bm, lane) >= b ? lcd : LV(ldx); }
+            }
+#endif
             LANE_LOOP {
               const uint32_t q = (uint32_t)lane + 64u * i, d = LV(dq)[i];
               const uint32_t isl = (LV(vm) >> i) & (d == 0u ? 1u : 0u);
@@ -1711,6 +1978,8 @@ HZ_UNROLL
               // a branch), a harmless in-range byte of dst (F) for slots that take no byte
 #ifdef HZ2_EXP_NOLITLOAD                  // (traffic attribution builds: outputs wrong)
               const uint64_t la = (uint64_t)(uintptr_t)lits;
+#elif HZ2_FUSE
+              const uint64_t la = (uint64_t)(uintptr_t)lits + (uint32_t)(R0 + hz2::lane_rank(bm, lane) + LV(ldx));
 #else
               const uint64_t la = (uint64_t)(uintptr_t)lits + L0 + lcnt + hz2::lane_rank(bm, lane);
 #endif

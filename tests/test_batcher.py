@@ -50,7 +50,7 @@ def test_64_concurrent_requests_one_batch():
     res = asyncio.run(main())
     assert len(store.calls) == 1                           # one decode launch for all 64
     assert len(store.calls[0]) == 48                       # each chunk id read once
-    assert b.stats == {"batches": 1, "requests": 64, "reads": 48}
+    assert {k: b.stats[k] for k in ("batches", "requests", "reads")} == {"batches": 1, "requests": 64, "reads": 48}
     for i, r in enumerate(res):
         np.testing.assert_array_equal(r, chunks[f"c-{i % 48}"][sel])
 
