@@ -60,6 +60,17 @@ using hz::T_ERR;
 using hz::T_MATCH;
 using hz::ADLER_MOD;
 
+// one decode pass (HZ2_FUSE = 1): phases A, A' and R emit every token they count -- literal
+// bytes and match records -- into the lane's own fixed region of the scratch (lane s:
+// records [s MCAP_LANE, ...), literals [s LCAP_LANE, ...), numbered from the lane's first
+// recorded start), so phase E's second decode is gone.  A lane's valid range is a suffix
+// of what it emitted (from the record its predecessor met); phase M maps a window record
+// or literal rank to its lane's region with a wave-uniform cursor over the lanes' ranges.
+// The recorded starts live in registers (the LDS holds the staging instead).  0: phase E
+// decodes every valid range again into the window-ordered ring (rounds 2-5)
+#ifndef HZ2_FUSE
+#define HZ2_FUSE 1
+#endif
 #ifndef HZ2_K
 #define HZ2_K 8
 #endif
@@ -122,17 +133,6 @@ static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
 #endif
 #ifndef HZ2_TICKN
 #define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 5)
-#endif
-// one decode pass (HZ2_FUSE = 1): phases A, A' and R emit every token they count -- literal
-// bytes and match records -- into the lane's own fixed region of the scratch (lane s:
-// records [s MCAP_LANE, ...), literals [s LCAP_LANE, ...), numbered from the lane's first
-// recorded start), so phase E's second decode is gone.  A lane's valid range is a suffix
-// of what it emitted (from the record its predecessor met); phase M maps a window record
-// or literal rank to its lane's region with a wave-uniform cursor over the lanes' ranges.
-// The recorded starts live in registers (the LDS holds the staging instead).  0: phase E
-// decodes every valid range again into the window-ordered ring (rounds 2-5)
-#ifndef HZ2_FUSE
-#define HZ2_FUSE 1
 #endif
 constexpr uint32_t TICKN = HZ2_TICKN;     // tokens between ring refills
 static_assert(RS % 4 == 0 && RS >= 8, "RS: whole quads");
