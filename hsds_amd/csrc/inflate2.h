@@ -66,10 +66,14 @@ using hz::ADLER_MOD;
 // recorded start), so phase E's second decode is gone.  A lane's valid range is a suffix
 // of what it emitted (from the record its predecessor met); phase M maps a window record
 // or literal rank to its lane's region with a wave-uniform cursor over the lanes' ranges.
-// The recorded starts live in registers (the LDS holds the staging instead).  0: phase E
-// decodes every valid range again into the window-ordered ring (rounds 2-5)
+// The recorded starts live in registers (the LDS holds the staging instead).  The two-pass
+// form (phase E decodes every valid range again into the window-ordered ring, rounds 2-5)
+// stays for the window pipeline (inflate_stream below)
 #ifndef HZ2_FUSE
-#define HZ2_FUSE 1
+#define HZ2_FUSE 1                        // one pass for one wavefront per stream
+#endif
+#ifndef HZ2_FUSE_PIPE
+#define HZ2_FUSE_PIPE 0                   // one pass in the window pipeline (NW > 1) as well
 #endif
 #ifndef HZ2_K
 #define HZ2_K 8
@@ -190,13 +194,11 @@ struct alignas(16) Shared {
     struct {                      // phase M
       uint16_t smap[SPAN + 2];    // batch byte -> distance to its source (0: literal); [SPAN] stays 0
       alignas(16) uint32_t sbuf[SPAN / 4 + 4];   // the batch's aligned dwords, assembled in LDS
-#if HZ2_FUSE
-      // lane s's share of the window (written after the prefix sums): its first window
-      // record mb[s] and literal rank lb[s], the region index minus the window index of its
-      // records (rdl) and literals (ldl), the window position minus the region position of
-      // its records (odl), and the end of its literal ranks (le)
+      // one-pass decoder: lane s's share of the window (written after the prefix sums): its
+      // first window record mb[s] and literal rank lb[s], the region index minus the window
+      // index of its records (rdl) and literals (ldl), the window position minus the region
+      // position of its records (odl), and the end of its literal ranks (le)
       uint32_t mb[WAVE], rdl[WAVE], odl[WAVE], lb[WAVE], le[WAVE], ldl[WAVE];
-#endif
     };
   };
   uint32_t wnext[8];              // NW == 1: the next window's start (WinState), kept in LDS across E and M
@@ -889,6 +891,23 @@ inline void emu_wgbar(Ctl* c, int n) {
 // waiting for the other's M before their own M, so one window's header, sync phases and
 // emit run beside the other's resolve (pipe.ctl in LDS; a continuation window copies the
 // block's tables from the other wavefront's LDS).
+// The stream decoder, compiled in its two forms (inflate2_stream.inc):
+#define HZ2_ONEPASS 1
+#define HZ2_STREAM_FN inflate_stream_1p
+#include "inflate2_stream.inc"
+#undef HZ2_STREAM_FN
+#undef HZ2_ONEPASS
+#define HZ2_ONEPASS 0
+#define HZ2_STREAM_FN inflate_stream_2p
+#include "inflate2_stream.inc"
+#undef HZ2_STREAM_FN
+#undef HZ2_ONEPASS
+
+// one pass for one wavefront per stream (the batch path: phase E's second decode is work
+// the wave would do itself); two passes for the window pipeline, whose critical path is the
+// chain of the windows' sync phases -- there phase E runs beside the other wavefront's M, and
+// emitting inside phase A would lengthen the chain (one F2 chunk on four wavefronts: 16.9 ms
+// one-pass, 14.7 two-pass)
 template <class StatsT, int NW>
 #if HZ_GPU
 __device__ __forceinline__
@@ -897,1275 +916,10 @@ static
 #endif
 int inflate_stream(Shared& sh, const Job job, const Tune tune, uint8_t* ring_base, StatsT* stats, HzProf* prof = nullptr,
                    Pipe pipe = Pipe{nullptr, nullptr, 0u}) {
-  (void)prof;
-  const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 15u);
-  const Src S = {HZ_GLOBAL(hz_gcu8*, job.src - a), a, a + job.src_len, ((a + job.src_len - 1u) >> 2) & ~3u};
-  const uint32_t limit_bits = S.hi * 8u;
-  const uint32_t dst_len = job.dst_len;
-  hz_gu8* const dst = HZ_GLOBAL(hz_gu8*, job.dst);
-  hz_gu32* const ring = HZ_GLOBAL(hz_gu32*, ring_base);
-#if HZ_GPU
-  typedef __attribute__((address_space(1))) uint64_t hz_gu64;
-#else
-  typedef uint64_t hz_gu64;
-#endif
-  hz_gu64* const ring64 = HZ_GLOBAL(hz_gu64*, ring_base);
-  hz_gu8* const lits = HZ_GLOBAL(hz_gu8*, ring_base + RING_BYTES);
-  if (job.perm.n > 1u) return ST_SIZE;      // no output map: shuffled streams are staged
-
-  LANE_VAR(uint32_t, s1);     // adler32 partial sums of the bytes this lane wrote: sum b, sum pos*b
-  LANE_VAR(uint32_t, s2);
-  LANE_LOOP { LV(s1) = 0; LV(s2) = 0; }
-
-  // ---- zlib header (RFC 1950) ----
-  if (job.src_len < 2) return ST_TRUNC;
-  {
-    GRd r;
-    g_init(S, r, S.lo * 8u);
-    const uint64_t two = g_peek(r);
-    const uint32_t cmf = (uint32_t)(two & 0xffu), flg = (uint32_t)((two >> 8) & 0xffu);
-    if ((cmf & 0x0f) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0) return ST_DATA;
-    if (flg & 0x20) return ST_DATA;   // preset dictionary: Z_NEED_DICT
-  }
-  (void)pipe;
-  WinState cur;                        // the current window's start
-  cur.pos = S.lo * 8u + 16u;
-  cur.out = 0;
-  cur.kind = WK_NEWBLOCK;
-  cur.block_start = 0;
-  cur.bfinal = 0;
-  cur.est = 0;
-  cur.prev_block_bits = 0;
-  static_assert(NW >= 1 && NW <= NW_MAX, "wavefronts per stream");
-  uint32_t k = NW > 1 ? pipe.w : 0u;   // window index
-  static_assert(sizeof(WinState) <= sizeof(sh.wnext), "WinState in Shared::wnext");
-
-  // the next window's start to whoever decodes it
-  auto publish = [&](const WinState& nx) {
-    if (NW > 1) {
-      Ctl* c = pipe.ctl;
-      c->next = nx;
-      if (nx.kind == WK_END) ctl_st(&c->end_at, k + 1u);
-      ctl_st(&c->synced, k + 1u);
-    } else {
-      // (in LDS: no register holds it across phases E and M)
-      LANE_LOOP { if (lane == 0) memcpy(sh.wnext, &nx, sizeof(nx)); }
-    }
-  };
-  // every wait is bounded; one that gives up is ST_HANG (not corrupt data: the caller
-  // decodes the stream again with one wavefront)
-  const uint32_t spin_max = tune.spin_max ? tune.spin_max : SPIN_MAX;
-  (void)spin_max;
-  // wait until every output byte before this window is final (the other wavefront's M)
-  auto wait_output = [&]() -> int {
-    if (NW > 1) {
-      Ctl* c = pipe.ctl;
-      for (uint32_t spin = 0;; spin++) {
-        if (ctl_ld(&c->mdone) == k) return ST_OK;
-        const int32_t e = (int32_t)ctl_ld((const uint32_t*)&c->err);
-        if (e) return e;
-        if (spin > spin_max) return ST_HANG;
-        HZ2_PAUSE();
-      }
-    }
-    return ST_OK;
-  };
-  auto output_done = [&]() {
-    if (NW > 1) ctl_st(&pipe.ctl->mdone, k + 1u);
-  };
-
-  int fail = ST_OK;
-  for (;; k += NW) {
-    if (NW > 1) {
-      // window k's start: published by the other wavefront's sync phases of window k - 1
-      Ctl* c = pipe.ctl;
-      int got = 0;
-      for (uint32_t spin = 0;; spin++) {
-        if (k == 0u) { got = 1; break; }             // window 0 starts at the stream's first block
-        if (ctl_ld(&c->synced) == k) { cur = c->next; got = 1; break; }
-        if (ctl_ld(&c->end_at) <= k) break;          // the stream ended before window k
-        const int32_t e = (int32_t)ctl_ld((const uint32_t*)&c->err);
-        if (e) { fail = e; break; }
-        if (spin > spin_max) { fail = ST_HANG; break; }
-        HZ2_PAUSE();
-      }
-      if (!got) break;
-    } else if (k > 0) {
-      HZ2_LSYNC();
-      memcpy(&cur, sh.wnext, sizeof(cur));
-    }
-    if (cur.kind == WK_END) break;
-    const int wst = [&]() -> int {
-#if HZ_GPU && HZ2_PRIO
-      // VALU issue on a SIMD goes to the higher priority, then the OLDER wave: with one
-      // stream per wave the youngest waves finish last.  A wave's priority falls with its
-      // stream's progress, so the waves that lag get the issue slots
-      {
-        const uint32_t q = cur.out < dst_len ? (uint32_t)(((uint64_t)cur.out * HZ2_PRIO) / dst_len) : HZ2_PRIO - 1u;
-        const uint32_t pr = HZ2_UNI(HZ2_PRIO - 1u - q);
-        if (pr >= 3u) __builtin_amdgcn_s_setprio(3);
-        else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
-        else if (pr == 1u) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-#endif
-      uint32_t pos = cur.pos, out = cur.out;
-      uint32_t block_start = cur.block_start, bfinal = cur.bfinal, est = cur.est;
-      int first_window = 0;
-      if (cur.kind == WK_NEWBLOCK) {
-      HZ_T(1);
-      if (pos + 3u > limit_bits) return ST_TRUNC;
-      uint32_t h3;
-      {
-        GRd r;
-        g_init(S, r, pos);
-        h3 = (uint32_t)(g_peek(r) & 7u);
-      }
-      block_start = pos;
-      pos += 3;
-      bfinal = h3 & 1u;
-      const uint32_t btype = h3 >> 1;
-      if (stats) stats->blocks++;
-      if (btype == 3) return ST_DATA;
-        if (btype == 0) {
-        // ---- stored block: copied through the output map ----
-        pos = (pos + 7u) & ~7u;
-        if (pos + 32u > limit_bits) return ST_TRUNC;
-        GRd r;
-        g_init(S, r, pos);
-        const uint32_t ln = (uint32_t)(g_peek(r) & 0xffffffffu);
-        const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
-        if ((len ^ 0xffffu) != nlen) return ST_DATA;
-        pos += 32u;
-        if (pos + len * 8u > limit_bits) return ST_TRUNC;
-        if (out + len > dst_len) return ST_SIZE;
-        {
-          WinState nx = cur;
-          nx.pos = pos + len * 8u;
-          nx.out = out + len;
-          nx.kind = bfinal ? WK_END : WK_NEWBLOCK;
-          publish(nx);
-          const int wr = wait_output();
-          if (wr != ST_OK) return wr;
-        }
-        const uint32_t sb = pos >> 3;
-        LANE_LOOP {
-          uint32_t a1 = LV(s1), a2 = LV(s2);
-          for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
-            const uint32_t b = S.base[sb + i];
-            dst[out + i] = (uint8_t)b;
-            a1 += b;
-            a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
-          }
-          LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
-        }
-        if (stats) stats->stored++;
-        HZ2_GSYNC();
-        output_done();
-        return ST_OK;
-        }
-      // ---- Huffman code lengths ----
-      uint32_t nlen = 288, ndist = 32;
-      if (btype == 1) {
-        LANE_LOOP {
-          for (int q = lane; q < 320; q += 64) sh.lens[q] = q >= 288 ? 5 : q < 144 ? 8 : q < 256 ? 9 : q < 280 ? 7 : 8;
-        }
-        HZ2_LSYNC();
-      } else {
-        // dynamic header (RFC 1951 3.2.7): the wave loads the 8192 stream bits from the header's
-        // quad into LDS at once (a header is at most 14 + 19 x 3 + 320 x 14 bits), then lane 0
-        // decodes it serially from LDS -- no global load latency per refill
-        const uint32_t hq = (pos >> 5) & ~3u;
-        LANE_LOOP {
-          uint32_t a0, a1, a2, a3;
-          g_quad(S, hq + 4u * (uint32_t)lane, a0, a1, a2, a3);
-          sh.hbits[4 * lane] = a0; sh.hbits[4 * lane + 1] = a1; sh.hbits[4 * lane + 2] = a2; sh.hbits[4 * lane + 3] = a3;
-        }
-        HZ2_LSYNC();
-        LANE_LOOP {
-          if (lane == 0) {
-            int st = ST_OK;
-            HR r = {sh.hbits, pos - hq * 32u, hq * 32u};
-            const uint32_t hlit = (r.peek() & 31u) + 257u, hdist = ((r.peek() >> 5) & 31u) + 1u;
-            const uint32_t hclen = ((r.peek() >> 10) & 15u) + 4u;
-            r.drop(14);
-            if (hlit > 286 || hdist > 30) st = ST_DATA;
-            uint16_t* cl = sh.sorted_cl;
-            for (int i = 0; i < 19; i++) cl[i] = 0;
-            for (uint32_t i = 0; i < hclen; i++) {
-              cl[hz::cl_order(i)] = (uint16_t)(r.peek() & 7u);
-              r.drop(3);
-            }
-            uint16_t* cnt = sh.cnt_cl;
-            for (int l = 0; l < 16; l++) cnt[l] = 0;
-            for (int i = 0; i < 19; i++) cnt[cl[i]]++;
-            cnt[0] = 0;
-            int left = 1, maxl = 0;
-            for (int l = 1; l <= 7; l++) {
-              left <<= 1; left -= cnt[l];
-              if (cnt[l]) maxl = l;
-              if (left < 0) st = ST_DATA;
-            }
-            if (left > 0 || maxl == 0) st = ST_DATA;   // code-length code must be complete
-            uint16_t* clut = sh.lut_d;                   // 7-bit LUT (sym | len << 8), rebuilt below
-            if (st == ST_OK) {
-              uint16_t* next = sh.tb_next;                 // next code per length (LDS: no scratch)
-              uint32_t code = 0;
-              for (int l = 1; l <= 7; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; next[l] = (uint16_t)code; }
-              for (int i = 0; i < 19; i++) {
-                const uint32_t l = cl[i];
-                if (!l) continue;
-                const uint32_t rc = hz::rev_bits(next[l]++, (int)l);
-                for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint16_t)(i | (l << 8));
-              }
-            }
-            const uint32_t total = hlit + hdist;
-            uint32_t n = 0, prevl = 0;
-            HRR rr;
-            rr.init(sh.hbits, r.p, r.base);
-            while (st == ST_OK && n < total) {
-              if (rr.pos() > limit_bits + 64u) { st = ST_TRUNC; break; }
-              const uint32_t bits = rr.peek();
-              const uint32_t e = clut[bits & 127u];
-              const uint32_t sym = e & 0xffu, l = e >> 8;
-              if (sym < 16) { rr.drop(l); sh.lens[n++] = (uint8_t)sym; prevl = sym; continue; }
-              // a repeat: its extra bits follow the code in the same peek (7 + 7 bits)
-              const uint32_t x = bits >> l;
-              uint32_t rep, val = 0;
-              if (sym == 16) {
-                if (n == 0) { st = ST_DATA; break; }
-                val = prevl; rep = 3 + (x & 3u); rr.drop(l + 2u);
-              } else if (sym == 17) { rep = 3 + (x & 7u); rr.drop(l + 3u); }
-              else { rep = 11 + (x & 127u); rr.drop(l + 7u); }
-              if (n + rep > total) { st = ST_DATA; break; }
-              for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
-              prevl = val;
-            }
-            r.p = rr.p;
-            if (st == ST_OK && r.pos() > limit_bits) st = ST_TRUNC;
-            if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;   // missing end-of-block code
-            if (st == ST_OK) {
-              for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
-              for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
-              for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
-            }
-            sh.u_status = st;
-            sh.u_pos = r.pos();
-            sh.u_nlen = hlit;
-            sh.u_ndist = hdist;
-          }
-        }
-        HZ2_LSYNC();
-        const int hst = sh.u_status;
-        if (hst != ST_OK) return hst;
-        pos = sh.u_pos;
-        nlen = sh.u_nlen;
-        ndist = sh.u_ndist;
-      }
-      HZ_T(2);
-      {
-        int bst = ST_OK;
-        hz::TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB, 1};
-        HZ_BUILD_TABLE(sh, tll, bst);
-        if (bst != ST_OK) return bst;
-        hz::TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB, 1};
-        HZ_BUILD_TABLE(sh, td, bst);
-        if (bst != ST_OK) return bst;
-      }
-      HZ2_LSYNC();
-
-      est = cur.prev_block_bits ? cur.prev_block_bits : 200000u;
-      {
-        const uint32_t rem = limit_bits > pos ? limit_bits - pos : 0u;
-        if (est > rem + 64u) est = rem + 64u;
-      }
-      est += (uint32_t)(((uint64_t)est * tune.over16) >> 4);
-        first_window = 1;
-      } else if (NW > 1) {
-        // a continuation window: the block's tables are the previous window's wavefront's
-        const Shared& o = *pipe.other;
-        LANE_LOOP {
-          for (uint32_t i = (uint32_t)lane; i < (uint32_t)((1 << LL_ROOT) + LL_SUB); i += 64u) sh.lut_ll[i] = o.lut_ll[i];
-          for (uint32_t i = (uint32_t)lane; i < (uint32_t)((1 << D_ROOT) + D_SUB); i += 64u) sh.lut_d[i] = o.lut_d[i];
-        }
-        HZ2_LSYNC();
-      }
-      if (stats) { stats->windows++; if (!first_window) stats->extra_windows++; }
-      const uint32_t ws = pos;
-      uint32_t L = (est + 63u) >> 6;
-      L = L < LMIN ? LMIN : L > LMAX ? LMAX : L;
-      const uint32_t W = tune.W;
-
-      HZ_T(3);
-      // -------- phase A: warm-up + own segment, first K token starts recorded --------
-      LANE_VAR(BR, rd);
-      LANE_VAR(uint32_t, co);      // output bytes since the first record
-      LANE_VAR(uint32_t, cm);      // matches since the first record
-      LANE_VAR(uint32_t, cl);      // literals since the first record
-      LANE_VAR(uint32_t, ek);      // END_*
-      LANE_VAR(uint32_t, ea);      // position after the EOB token
-#if HZ2_FUSE
-      LANE_ARR(uint32_t, rcv, K);  // the lane's recorded starts
-      LANE_ARR(uint32_t, nxr, K);  // its successor's (phase A')
-      // lane s's successor's recorded starts into its registers (every lane active)
-      auto fetch_succ = [&]() {
-#if HZ_GPU
-        const int sl = ((HZ_LANE_ID() + 1) & 63) << 2;
-HZ_UNROLL
-        for (uint32_t j = 0; j < (uint32_t)K; j++) nxr[j] = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)rcv[j]);
-#else
-        for (int s = 0; s < 63; s++)
-          for (uint32_t j = 0; j < (uint32_t)K; j++) nxr[s][j] = rcv[s + 1][j];
-#endif
-      };
-      // a counted token into the lane's region: the literal byte and the match record
-      // (position = output bytes since the first record) are staged unconditionally -- the one
-      // that does not apply sits in the slot the next literal / match overwrites -- and a
-      // completed group of OS literals / RGRP records is stored whole
-      auto emit = [&](int lane, const Tok& t, bool cnt, uint32_t o, uint32_t m, uint32_t l) {
-        sh.ostage[lane][l & (OS - 1u)] = (uint8_t)t.v;
-        sh.rstage[lane][m & (RGRP - 1u)] = (uint64_t)o | ((uint64_t)((t.len << 16) | (t.v - 1u)) << 32);
-        if (cnt && t.kind == TK_LIT && ((l + 1u) & (OS - 1u)) == 0u) {
-          hz_gu8* const p = lits + (uint32_t)lane * LCAP_LANE + (l + 1u - OS);
-#if HZ_GPU
-          if constexpr (OS == 16u) {
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            typedef __attribute__((address_space(1))) u32x4 gu32x4;
-            *(gu32x4*)p = *(const u32x4*)&sh.ostage[lane][0];
-          } else if constexpr (OS == 8u) {
-            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            typedef __attribute__((address_space(1))) u32x2 gu32x2;
-            *(gu32x2*)p = *(const u32x2*)&sh.ostage[lane][0];
-          } else {
-            *(hz_gu32*)p = *(const uint32_t*)&sh.ostage[lane][0];
-          }
-#else
-          memcpy(p, &sh.ostage[lane][0], OS);
-#endif
-        }
-        if (cnt && t.kind == TK_MATCH && (m & (RGRP - 1u)) == RGRP - 1u) {
-          hz_gu64* const p = ring64 + (uint32_t)lane * MCAP_LANE + (m & ~(RGRP - 1u));
-#if HZ_GPU
-          typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-          typedef __attribute__((address_space(1))) u64x2 gu64x2;
-HZ_UNROLL
-          for (uint32_t k = 0; k < RGRP; k += 2u) *(gu64x2*)(p + k) = *(const u64x2*)&sh.rstage[lane][k];
-#else
-          for (uint32_t k = 0; k < RGRP; k++) p[k] = sh.rstage[lane][k];
-#endif
-        }
-      };
-#endif
-      LANE_LOOP {
-        const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
-        const uint32_t p0 = (lane > 0 && ss - ws > W) ? ss - W : ws;
-        BR r;
-        br_init(sh, lane, S, r, p0);
-        uint32_t steps = 0;
-        uint32_t nr = 0, o = 0, m = 0, l = 0, e = END_NONE, after = 0;
-#if HZ2_FUSE
-HZ_UNROLL
-        for (uint32_t j = 0; j < (uint32_t)K; j++) LV(rcv)[j] = 0u;
-#endif
-        // one loop for the warm-up (tokens before ss are decoded and dropped: whatever they
-        // are, even invalid codes, which advance by their table length) and the segment.
-        // Branch-free body: the only exit is at the top (a token that ends the lane sets e
-        // and does not advance, so the next test fails)
-        for (;;) {
-          HZ2_MARK("A_TOP");
-          const uint32_t tp = br_pos(r);
-          if (tp >= se || e != END_NONE) break;
-          br_next(sh, lane, r);
-          const bool inseg = tp >= ss;
-#if HZ2_FUSE
-          {
-            // the first K starts in the segment (registers; the select chain only runs while
-            // some lane still records)
-            const bool rk = inseg && nr < (uint32_t)K;
-#if HZ_GPU
-            if (WAVE_BALLOT(rk))
-#endif
-              setk(LV(rcv), nr, rec_pack(tp - ss, o, m, l), rk);
-            nr += rk ? 1u : 0u;
-          }
-#else
-          {
-            // a record past the K-th (or in the warm-up) goes to the lane's endp word,
-            // which phase A' overwrites
-            const bool rk = inseg && nr < (uint32_t)K;
-            uint32_t* rp = rk ? &sh.rec[nr < (uint32_t)K ? nr : 0u][lane] : &sh.endp[lane];
-            *rp = rec_pack(tp - ss, o, m, l);
-            nr += rk ? 1u : 0u;
-          }
-#endif
-          const Tok t = rtok(&sh, r);
-          const bool ismatch = t.kind == TK_MATCH, islit = t.kind == TK_LIT;
-          const bool stop = inseg && (t.kind >= TK_EOB || (ismatch && m >= MCAP_LANE) || (islit && l >= LCAP_LANE));
-          e = stop ? (t.kind == TK_EOB ? END_EOB : t.kind == TK_ERR ? END_ERR : END_CUT) : e;
-          after = stop ? tp + t.n : after;
-          const bool cnt = inseg && !stop;
-#if HZ2_FUSE
-          emit(lane, t, cnt, o, m, l);
-#endif
-          o += cnt ? t.len : 0u;
-          m += (cnt && ismatch) ? 1u : 0u;
-          l += (cnt && islit) ? 1u : 0u;
-          br_adv(r, stop ? 0u : t.n);
-          HZ2_RTICK(steps);
-        }
-        sh.nrec[lane] = nr;
-        sh.syncw[lane] = lane == 0 ? 0u : SYNC_NONE;
-        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;
-        if (stats) stats->steps_a += steps;
-      }
-      HZ2_LSYNC();
-
-      HZ_T(4);
-      // -------- phase A': continuation until lane+1's recorded path is met --------
-      // (a lane that ended leaves its successor at SYNC_NONE)
-      // (in the loop below: the successor's recorded starts at or past `rel` -- k, the first
-      // of them -- are passed: none left ends the search; one at `rel` is the sync)
-#if HZ2_FUSE
-      // registers: every start compared at once (a runtime index would put them in scratch)
-#define HZ2_SYNC_TEST(lane_)                                                                     \
-      {                                                                                          \
-        uint32_t nlt = 0, hit = SYNC_FAIL;                                                       \
-        HZ_UNROLL for (uint32_t i = 0; i < (uint32_t)K; i++) {                                   \
-          const uint32_t q = hz2::rec_rel(LV(nxr)[i]);                                           \
-          nlt += (i < nrn && q < rel) ? 1u : 0u;                                                 \
-          hit = (i < nrn && q == rel) ? i : hit;                                                 \
-        }                                                                                        \
-        k = nlt;                                                                                 \
-        if (k >= nrn) break;                                                                     \
-        if (hit != SYNC_FAIL) { res = hit; break; }                                              \
-      }
-#define HZ2_EMIT(lane_, t_, c_, o_, m_, l_) emit((lane_), (t_), (c_), (o_), (m_), (l_))
-      fetch_succ();
-#else
-#define HZ2_SYNC_TEST(lane_)                                                                     \
-      {                                                                                          \
-        while (k < nrn && hz2::rec_rel(sh.rec[k][(lane_) + 1]) < rel) k++;                      \
-        if (k >= nrn) break;                                                                     \
-        if (hz2::rec_rel(sh.rec[k][(lane_) + 1]) == rel) { res = k; break; }                    \
-      }
-#define HZ2_EMIT(lane_, t_, c_, o_, m_, l_) do { } while (0)
-#endif
-#define HZ2_CONTINUE(lane_)                                                                      \
-      do {                                                                                       \
-        BR r = LV(rd);                                                                           \
-        uint32_t o = LV(co), m = LV(cm), l = LV(cl), e = LV(ek), after = LV(ea);                 \
-        uint32_t res = SYNC_NONE;                                                                \
-        if (e == END_NONE && (lane_) < 63) {                                                     \
-          /* A ticked at most TICKN - 1 tokens ago: refill now, so the tick counter can restart */ \
-          hz2::br_tick(sh, lane, S, r);                                                          \
-          const uint32_t base = ws + (uint32_t)((lane_) + 1) * L;                                \
-          const uint32_t nrn = sh.nrec[(lane_) + 1];                                             \
-          uint32_t k = 0, ct = 0;                                                                \
-          res = SYNC_FAIL;                                                                       \
-          for (;;) {                                                                             \
-            const uint32_t tp = hz2::br_pos(r);                                                  \
-            const uint32_t rel = tp - base;                                                      \
-            HZ2_SYNC_TEST(lane_);                                                                \
-            hz2::br_next(sh, lane, r);                                                           \
-            const hz2::Tok t = hz2::rtok(&sh, r);                                                \
-            if (t.kind >= hz2::TK_EOB) {                                                         \
-              e = t.kind == hz2::TK_EOB ? END_EOB : END_ERR; after = tp + t.n; res = SYNC_NONE; break; \
-            }                                                                                    \
-            if ((t.kind == hz2::TK_MATCH && m >= MCAP_LANE) || (t.kind == hz2::TK_LIT && l >= LCAP_LANE)) { \
-              e = END_CUT; res = SYNC_NONE; break;                                               \
-            }                                                                                    \
-            HZ2_EMIT(lane, t, true, o, m, l);                                                    \
-            o += t.len;                                                                          \
-            m += t.kind == hz2::TK_MATCH ? 1u : 0u;                                              \
-            l += t.kind == hz2::TK_LIT ? 1u : 0u;                                                \
-            hz2::br_adv(r, t.n);                                                                 \
-            HZ2_RTICK(ct);                                                                       \
-          }                                                                                      \
-        }                                                                                        \
-        if ((lane_) < 63) sh.syncw[(lane_) + 1] = res;                                           \
-        sh.endp[lane_] = hz2::br_pos(r);                                                         \
-        LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;              \
-      } while (0)
-      LANE_LOOP { HZ2_CONTINUE(lane); }
-      HZ2_LSYNC();
-
-      HZ_T(5);
-      // -------- repair rounds --------
-      // a lane whose predecessor exists but never met its path re-runs A + A' from the
-      // predecessor's exit (a token boundary), recording its new path; its successor's sync
-      // is recomputed.  Adjacent lanes are never redone in the same round.
-      for (int round = 0; round < tune.max_rounds; round++) {
-        const uint64_t redo_m = WAVE_BALLOT(lane > 0 && sh.syncw[lane] == SYNC_FAIL && sh.syncw[lane - 1] < (uint32_t)K);
-        if (!redo_m) break;
-        if (stats) { stats->repairs++; stats->repair_lanes += hz::popc64(redo_m); }
-        LANE_LOOP {
-          if ((redo_m >> lane) & 1ull) {
-            const uint32_t ss = ws + (uint32_t)lane * L, se = ss + L;
-            BR r;
-            br_init(sh, lane, S, r, sh.endp[lane - 1]);
-            uint32_t nr = 0, o = 0, m = 0, l = 0, e = END_NONE, after = 0, ct = 0;
-            for (;;) {
-              const uint32_t tp = br_pos(r);
-              if (!(tp < se || nr == 0)) break;
-              br_next(sh, lane, r);
-#if HZ2_FUSE
-              setk(LV(rcv), nr, rec_pack(tp - ss, o, m, l), nr < (uint32_t)K);
-              nr += nr < (uint32_t)K ? 1u : 0u;
-#else
-              if (nr < (uint32_t)K) { sh.rec[nr][lane] = rec_pack(tp - ss, o, m, l); nr++; }
-#endif
-              const Tok t = rtok(&sh, r);
-              if (t.kind >= TK_EOB) { e = t.kind == TK_EOB ? END_EOB : END_ERR; after = tp + t.n; break; }
-              if ((t.kind == TK_MATCH && m >= MCAP_LANE) || (t.kind == TK_LIT && l >= LCAP_LANE)) { e = END_CUT; break; }
-              HZ2_EMIT(lane, t, true, o, m, l);
-              o += t.len;
-              m += t.kind == TK_MATCH ? 1u : 0u;
-              l += t.kind == TK_LIT ? 1u : 0u;
-              br_adv(r, t.n);
-              HZ2_RTICK(ct);
-            }
-            sh.nrec[lane] = nr;
-            sh.syncw[lane] = 0;                       // its path starts at record 0
-            LV(rd) = r; LV(co) = o; LV(cm) = m; LV(cl) = l; LV(ek) = e; LV(ea) = after;
-          }
-        }
-        HZ2_LSYNC();
-#if HZ2_FUSE
-        fetch_succ();     // (a successor redone in an earlier round has new starts)
-#endif
-        LANE_LOOP {
-          if ((redo_m >> lane) & 1ull) HZ2_CONTINUE(lane);
-        }
-        HZ2_LSYNC();
-      }
-#undef HZ2_CONTINUE
-#undef HZ2_SYNC_TEST
-#undef HZ2_EMIT
-
-      HZ_T(6);
-      // -------- validity, window end, prefix sums --------
-      // lane i is valid when every lane before it is and lane i-1 met its path
-      uint32_t V = 1;
-      {
-        const uint64_t okm = WAVE_BALLOT(lane == 0 || sh.syncw[lane] < (uint32_t)K);
-        while (V < 64u && ((okm >> V) & 1ull)) V++;
-      }
-      LANE_VAR(uint32_t, wout);
-      LANE_VAR(uint32_t, wmat);
-      LANE_VAR(uint32_t, wlit);
-      LANE_VAR(uint32_t, sbit);    // exact start bit of the lane's range
-#if HZ2_FUSE
-      LANE_VAR(uint32_t, srec);    // the record the lane's range starts at
-#endif
-      LANE_LOOP {
-        uint32_t wo = 0, wm = 0, wl = 0, sb = 0;
-        if ((uint32_t)lane < V) {
-          const uint32_t k = sh.syncw[lane];
-#if HZ2_FUSE
-          const uint32_t rc = selk(LV(rcv), k);
-          LV(srec) = rc;
-#else
-          const uint32_t rc = sh.rec[k][lane];
-#endif
-          wo = LV(co) - rec_out(rc);
-          wm = LV(cm) - rec_mat(rc);
-          wl = LV(cl) - rec_lit(rc);
-          sb = ws + (uint32_t)lane * L + rec_rel(rc);
-        }
-        LV(wout) = wo; LV(wmat) = wm; LV(wlit) = wl; LV(sbit) = sb;
-      }
-      // the first valid lane that ended (EOB / ERR / CUT) closes the window
-      int end_lane = -1;
-      {
-        const uint64_t em = WAVE_BALLOT((uint32_t)lane < V && LV(ek) != END_NONE);
-        if (em) end_lane = (int)__builtin_ctzll(em);
-      }
-      if (end_lane >= 0) V = (uint32_t)end_lane + 1u;
-      if (stats) stats->lanes_valid += V;
-      uint32_t end_kind = END_NONE, npos = 0;
-      LANE_LOOP {
-        if ((uint32_t)lane >= V) { LV(wout) = 0; LV(wmat) = 0; LV(wlit) = 0; }
-        if (lane == (end_lane >= 0 ? end_lane : (int)V - 1)) {
-          sh.u_status = (int32_t)LV(ek);
-          sh.u_pos = LV(ek) == END_EOB ? LV(ea) : sh.endp[lane];
-          sh.u_nlen = sh.endp[lane];
-        }
-      }
-      HZ2_LSYNC();
-      end_kind = (uint32_t)sh.u_status;
-      npos = sh.u_pos;
-      if (end_kind == END_ERR) {
-        // the first invalid code on the true path: a stream that ran out of input is
-        // truncated, anything else is corrupt
-        return sh.u_nlen + 64u > limit_bits ? ST_TRUNC : ST_DATA;
-      }
-      LANE_VAR(uint32_t, obase);
-      LANE_VAR(uint32_t, mbase);
-      LANE_VAR(uint32_t, lbase);
-      uint32_t wtotal = 0, mtotal = 0, ltotal = 0;
-#if HZ_GPU
-      obase = wave_excl_scan32(wout);
-      mbase = wave_excl_scan32(wmat);
-      lbase = wave_excl_scan32(wlit);
-      wtotal = hz::wave_sum(wout);
-      mtotal = hz::wave_sum(wmat);
-      ltotal = hz::wave_sum(wlit);
-#else
-      for (int lane = 0; lane < 64; lane++) {
-        obase[lane] = wtotal; mbase[lane] = mtotal; lbase[lane] = ltotal;
-        wtotal += wout[lane]; mtotal += wmat[lane]; ltotal += wlit[lane];
-      }
-#endif
-      (void)ltotal;
-      if (stats) stats->matches += mtotal;
-      if (out + wtotal > dst_len) return ST_SIZE;
-      if (npos > limit_bits) return ST_TRUNC;
-#if HZ2_FUSE
-      // the valid lanes' last, partial groups (the staging dies below: the maps overlay it)
-      LANE_LOOP {
-        if ((uint32_t)lane < V) {
-          const uint32_t m = LV(cm), l = LV(cl);
-          hz_gu64* const rp = ring64 + (uint32_t)lane * MCAP_LANE;
-          hz_gu8* const lp = lits + (uint32_t)lane * LCAP_LANE;
-          for (uint32_t k = m & ~(RGRP - 1u); k < m; k++) rp[k] = sh.rstage[lane][k & (RGRP - 1u)];
-          for (uint32_t k = l & ~(OS - 1u); k < l; k++) lp[k] = sh.ostage[lane][k & (OS - 1u)];
-        }
-      }
-      HZ2_LSYNC();
-      LANE_LOOP {
-        const uint32_t rc = (uint32_t)lane < V ? LV(srec) : 0u;
-        sh.mb[lane] = LV(mbase);
-        sh.rdl[lane] = (uint32_t)lane * MCAP_LANE + rec_mat(rc) - LV(mbase);
-        sh.odl[lane] = out + LV(obase) - rec_out(rc);
-        sh.lb[lane] = LV(lbase);
-        sh.le[lane] = LV(lbase) + LV(wlit);
-        sh.ldl[lane] = (uint32_t)lane * LCAP_LANE + rec_lit(rc) - LV(lbase);
-      }
-      HZ2_LSYNC();
-#endif
-
-      {  // the next window's start: the other wavefront may begin its sync phases now
-        WinState nx;
-        nx.pos = npos;
-        nx.out = out + wtotal;
-        nx.prev_block_bits = cur.prev_block_bits;
-        nx.block_start = block_start;
-        nx.bfinal = bfinal;
-        nx.est = 0;
-        if (end_kind == END_EOB) {
-          nx.kind = bfinal ? WK_END : WK_NEWBLOCK;
-          nx.prev_block_bits = npos - block_start;
-        } else {
-          nx.kind = WK_CONT;
-          // the block goes on: the rest is estimated from what is left of the estimate
-          const uint32_t used = npos - ws;
-          uint32_t e2 = est > used ? est - used : 0u;
-          const uint32_t floor_est = ((npos - block_start) >> 3) + 64u * LMIN;
-          e2 = e2 < floor_est ? floor_est : e2;
-          const uint32_t rem = limit_bits > npos ? limit_bits - npos : 0u;
-          if (e2 > rem + 64u) e2 = rem + 64u;
-          nx.est = e2;
-        }
-        publish(nx);
-      }
-
-      HZ_T(7);
-#if !HZ2_FUSE
-      // -------- phase E: exact decode of every valid range --------
-      // Nothing goes to dst here: literal bytes go to the window's literal stream (lane i's
-      // literals at lbase[i]..., staged 16 bytes at a time in LDS and stored whole), matches
-      // to the match ring as (position, length, distance) records (staged per lane, stored as
-      // aligned groups).  Phase M then writes every output byte of the window exactly once.
-      LANE_VAR(int, lerr);
-      LANE_LOOP {
-        int err = 0;
-        uint32_t steps = 0;
-        if ((uint32_t)lane < V) {
-          BR r;
-          br_init(sh, lane, S, r, LV(sbit));
-          const uint32_t stop = sh.endp[lane];
-          uint32_t o = out + LV(obase), mi = LV(mbase);
-          const uint32_t l0 = LV(lbase);
-          uint32_t lk = l0;
-          const uint32_t m0 = mi;                          // the lane's first record
-          // branch-free body but for the two flushes: a token's literal byte and its match
-          // record are both staged unconditionally -- the one that does not apply sits in the
-          // slot the next literal / match overwrites (lk / mi do not move for it)
-          while (br_pos(r) < stop && !err) {
-            HZ2_MARK("E_TOP");
-            br_next(sh, lane, r);
-            const Tok tk = rtok(&sh, r);
-            br_adv(r, tk.n);
-            HZ2_RTICK(steps);
-            const bool islit = tk.kind == TK_LIT, ismatch = tk.kind == TK_MATCH;
-            // (E decodes ranges A verified: an EOB / invalid code or a distance past the
-            // output start here is a bug, reported as corrupt data)
-            err |= (!islit && (!ismatch || tk.v > o)) ? 1 : 0;
-            sh.ostage[lane][lk & (OS - 1u)] = (uint8_t)tk.v;
-#if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
-            sh.rstage[lane][mi & (RGRP - 1u)] = (uint64_t)o | ((uint64_t)((tk.len << 16) | (tk.v - 1u)) << 32);
-#endif
-            lk += islit ? 1u : 0u;
-#ifndef HZ2_EXP_NOSTORE
-            if (islit && !(lk & (OS - 1u))) {            // OS bytes of the literal stream complete
-              const uint32_t g = lk - OS;
-              if (g >= l0) {
-#if HZ_GPU
-                if constexpr (OS == 16u) {
-                  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                  typedef __attribute__((address_space(1))) u32x4 gu32x4;
-                  *(gu32x4*)(lits + g) = *(const u32x4*)&sh.ostage[lane][0];
-                } else if constexpr (OS == 8u) {
-                  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                  typedef __attribute__((address_space(1))) u32x2 gu32x2;
-                  *(gu32x2*)(lits + g) = *(const u32x2*)&sh.ostage[lane][0];
-                } else {
-                  *(hz_gu32*)(lits + g) = *(const uint32_t*)&sh.ostage[lane][0];
-                }
-#else
-                memcpy(lits + g, &sh.ostage[lane][0], OS);
-#endif
-              } else {                                   // the group starts in the previous lane's literals
-                for (uint32_t k = l0; k < lk; k++) lits[k] = sh.ostage[lane][k & (OS - 1u)];
-              }
-            }
-#endif
-#if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
-            if (ismatch && (mi & (RGRP - 1u)) == RGRP - 1u) {
-              const uint32_t g = mi & ~(RGRP - 1u);
-              if (g >= m0) {                             // a whole group of this lane: stored at once
-#if HZ_GPU
-                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-                typedef __attribute__((address_space(1))) u64x2 gu64x2;
-HZ_UNROLL
-                for (uint32_t k = 0; k < RGRP; k += 2u)
-                  *(gu64x2*)(ring64 + g + k) = *(const u64x2*)&sh.rstage[lane][k];
-#else
-                for (uint32_t k = 0; k < RGRP; k++) ring64[g + k] = sh.rstage[lane][k];
-#endif
-              } else {                                   // the group starts in the previous lane's records
-                for (uint32_t k = m0; k <= mi; k++) ring64[k] = sh.rstage[lane][k & (RGRP - 1u)];
-              }
-            }
-#endif
-            mi += ismatch ? 1u : 0u;
-            o += islit ? 1u : ismatch ? tk.len : 0u;
-          }
-#if !defined(HZ2_EXP_NOSTORE) && !defined(HZ2_EXP_NORING)
-          {                                            // the lane's last, partial group
-            const uint32_t g = mi & ~(RGRP - 1u);
-            for (uint32_t k = g > m0 ? g : m0; k < mi; k++) ring64[k] = sh.rstage[lane][k & (RGRP - 1u)];
-          }
-#endif
-#ifndef HZ2_EXP_NOSTORE
-          {                                            // the lane's last, partial 16 literal bytes
-            const uint32_t g = lk & ~(OS - 1u);
-            for (uint32_t k = g > l0 ? g : l0; k < lk; k++) lits[k] = sh.ostage[lane][k & (OS - 1u)];
-          }
-#endif
-        }
-        LV(lerr) = err;
-        if (stats) stats->steps_e += steps;
-      }
-      if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
-#endif
-      HZ2_GSYNC();
-
-      {
-        const int wr = wait_output();    // every byte before `out` final (the other wavefront's M)
-        if (wr != ST_OK) return wr;
-      }
-      HZ_T(8);
-      // -------- phase M: write the window's output, one span at a time --------
-      // The window's output [out, out + wtotal) is cut into consecutive spans [F, F + span):
-      // span = the frontier F up to the end of the last of the next <= 256 matches that fit
-      // SPAN bytes (a span of literals only when no match fits).  Per span:
-      //   1. smap[x - F] = distance from match byte x to an equal earlier byte (the periodic
-      //      extension of an overlapping copy), literal bytes 0;
-      //   2. pointer jumping: while a byte's source is a match byte of the span, add that
-      //      byte's distance (rounds over all bytes, one LDS round trip each) -- after it every
-      //      match byte's source is either before F (final in dst) or a literal of the span;
-      //   3. every lane gathers its byte slots q = lane + 64 i at once: literals from the
-      //      literal stream (rank among the span's literals by ballot), sources before F from
-      //      dst; in-span sources (literals) then from LDS;
-      //   4. the span's aligned dwords are stored from LDS, whole where they lie inside the
-      //      span (and the stream), byte by byte at its edges.
-      // Every output byte is written once, coalesced; E stored nothing to dst.
-      // match bytes' adler sums: a1 < 2^32 and a2 < 2^64 for any window (< 2^24 bytes)
-      LANE_VAR(uint32_t, ra1);
-      LANE_VAR(uint64_t, ra2);
-      LANE_LOOP { LV(ra1) = 0; LV(ra2) = 0; }
-      LANE_ARR(uint32_t, ro, MPL);
-      LANE_ARR(uint32_t, rw, MPL);
-#if HZ2_FUSE
-      // window records jb + lane + 64 u from their lanes' regions (positions made absolute):
-      // rcur, the last lane whose first record is at or before jb, only grows; the lanes
-      // whose records the MPL x 64 touch are walked from it (a batch spans a few)
-      uint32_t rcur = 0;
-      auto load_recs = [&](uint32_t jb, auto& xo, auto& xw) {
-        // the lanes' shares into registers (one LDS round trip), walked by v_readlane
-        LANE_VAR(uint32_t, vmb);
-        LANE_VAR(uint32_t, vrd);
-        LANE_VAR(uint32_t, vod);
-        LANE_LOOP { LV(vmb) = sh.mb[lane]; LV(vrd) = sh.rdl[lane]; LV(vod) = sh.odl[lane]; }
-        while (rcur < 63u && LV_AT(vmb, rcur + 1u) <= jb) rcur++;
-        LANE_ARR(uint32_t, dr, MPL);
-        LANE_ARR(uint32_t, dd, MPL);
-        {
-          const uint32_t r0 = LV_AT(vrd, rcur), o0 = LV_AT(vod, rcur);
-          LANE_LOOP {
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) { LV(dr)[u] = r0; LV(dd)[u] = o0; }
-          }
-        }
-        const uint32_t jl = jb + 64u * MPL;
-        for (uint32_t s = rcur; s < 63u;) {
-          const uint32_t b = LV_AT(vmb, s + 1u);
-          if (b >= jl || b >= mtotal) break;
-          s++;
-          const uint32_t r1 = LV_AT(vrd, s), o1 = LV_AT(vod, s);
-          LANE_LOOP {
-HZ_UNROLL
-            for (uint32_t u = 0; u < MPL; u++) {
-              const bool in = jb + (uint32_t)lane + 64u * u >= b;
-              LV(dr)[u] = in ? r1 : LV(dr)[u];
-              LV(dd)[u] = in ? o1 : LV(dd)[u];
-            }
-          }
-        }
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            // (unconditional loads: a record past the window reads slot 0)
-            const uint32_t j = jb + (uint32_t)lane + 64u * u;
-            const bool ok = j < mtotal;
-            const uint64_t v = ring64[ok ? j + LV(dr)[u] : 0u];
-            LV(xo)[u] = ok ? (uint32_t)v + LV(dd)[u] : 0xffffffffu;
-            LV(xw)[u] = ok ? (uint32_t)(v >> 32) : 0u;
-          }
-        }
-      };
-      load_recs(0u, ro, rw);
-      // literal ranks -> regions: the cursor lane lcur holds ranks up to lend (exclusive)
-      uint32_t lcur = 0, lend = HZ2_UNI(sh.le[0]), lcd = HZ2_UNI(sh.ldl[0]);
-#else
-      LANE_LOOP {
-HZ_UNROLL
-        for (uint32_t u = 0; u < MPL; u++) {
-          const uint32_t j = (uint32_t)lane + 64u * u;
-          LV(ro)[u] = j < mtotal ? ring[2u * j] : 0xffffffffu;
-          LV(rw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
-        }
-      }
-#endif
-      LANE_LOOP { if (lane == 0) sh.smap[SPAN] = 0; }
-      const uint32_t wend = out + wtotal;
-      uint32_t F = out, L0 = 0;      // frontier and its rank in the literal stream
-      // the dword that holds the frontier: the last one the previous span assembled (its
-      // bytes before F are final: that span's own or its head), so only a window's first
-      // span loads it
-      uint32_t hcar = 0;
-      bool hcar_ok = false;
-#ifdef HZ2_EXP_NOM
-      for (uint32_t b0 = 0; F < 0u;) {
-#else
-      for (uint32_t b0 = 0; F < wend;) {
-#endif
-        HZ_T(14);
-        HZ2_MARK("M_BATCH");
-        if (stats) stats->batches++;
-#if HZ2_FUSE
-        // (phase E's check, on the records' absolute positions: a distance past the stream start)
-        if (WAVE_BALLOT(hz2::rec_bad(LV(ro), LV(rw)))) return ST_DATA;
-#endif
-        uint32_t nb = 0, open_ = 1;
-HZ_UNROLL
-        for (uint32_t u = 0; u < MPL; u++) {
-          const uint64_t fit = WAVE_BALLOT(LV(ro)[u] != 0xffffffffu && LV(ro)[u] + (LV(rw)[u] >> 16) - F <= SPAN);
-          const uint32_t k = ~fit ? (uint32_t)__builtin_ctzll(~fit) : 64u;   // leading fitting matches
-          nb += open_ ? k : 0u;
-          open_ = open_ && k == 64u;
-        }
-        uint32_t span;
-        if (nb) {
-          const uint32_t last_o = LVA_AT(ro, (nb - 1u) >> 6, (nb - 1u) & 63u);
-          const uint32_t last_w = LVA_AT(rw, (nb - 1u) >> 6, (nb - 1u) & 63u);
-          span = last_o + (last_w >> 16) - F;
-        } else {
-          const uint32_t nxt = b0 < mtotal ? LVA_AT(ro, 0u, 0u) : wend;
-          span = nxt - F < SPAN ? nxt - F : SPAN;
-        }
-        // the span's first dword holds bytes before F (final): loaded now, merged below
-        const uint32_t mis = (uint32_t)((uintptr_t)(job.dst + F) & 3u);
-        const uint32_t xa = F - mis;                           // stream position of dword 0
-        const uint32_t ndw = (span + mis + 3u) >> 2;
-        const bool head = mis && (int32_t)xa >= 0 && xa + 4u <= dst_len;   // dword 0 loaded (whole-stored)
-        // (the previous span's last dword; loaded only for a window's first span, and waited
-        // for inside that branch: a load left pending at the merge makes the compiler wait
-        // for it -- a memory latency -- on every span)
-        uint32_t hl = hcar;
-        if (head && !hcar_ok) {
-          hl = *(hz_gu32*)(dst + xa);
-          HZ2_VMWAIT();
-        }
-        const uint32_t hv = head ? hl : 0u;
-        HZ_T(8);
-        // the whole map is cleared (three 16-byte stores per lane): slots past the span read 0
-        static_assert(SPAN % 256u == 0u, "smap clear: whole 8-byte stores per lane");
-        LANE_LOOP {
-#if HZ_GPU
-          if constexpr (SPAN % 512u == 0u) {
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            u32x4* const zp = (u32x4*)&sh.smap[(SPAN / 64u) * (uint32_t)lane];
-            const u32x4 z = {0u, 0u, 0u, 0u};
-HZ_UNROLL
-            for (uint32_t k = 0; k < SPAN / 512u; k++) zp[k] = z;
-          } else {
-            uint64_t* const zp = (uint64_t*)&sh.smap[(SPAN / 64u) * (uint32_t)lane];
-HZ_UNROLL
-            for (uint32_t k = 0; k < SPAN / 256u; k++) zp[k] = 0ull;
-          }
-#else
-          memset(&sh.smap[(SPAN / 64u) * (uint32_t)lane], 0, SPAN / 32u);
-#endif
-        }
-        HZ2_LSYNC();
-        if (stats) {
-          uint64_t mx = 0, sm = 0;
-          for (int l = 0; l < 64; l++) {
-            uint64_t f = 0;
-            for (uint32_t u = 0; u < MPL; u++)
-              if ((uint32_t)l + 64u * u < nb) f += LVA_AT(rw, u, l) >> 16;
-            mx = f > mx ? f : mx;
-            sm += f;
-          }
-          stats->fill_max += mx; stats->fill_sum += sm; stats->span_sum += span;
-        }
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            if ((uint32_t)lane + 64u * u < nb) {
-              const uint32_t o0 = LV(ro)[u] - F, ln = LV(rw)[u] >> 16, d = (LV(rw)[u] & 0xffffu) + 1u;
-              // byte t copies o - d + (t mod d): distance d + d * floor(t / d).  Four bytes
-              // per iteration (bytes past the match go to the junk entry SPAN + 1): the wave
-              // runs as many iterations as its longest match needs
-              uint32_t dist = d, jj = 0;
-              for (uint32_t t0 = 0; t0 < ln; t0 += 4u) {
-HZ_UNROLL
-                for (uint32_t k = 0; k < 4u; k++) {
-                  const uint32_t t = t0 + k;
-                  sh.smap[t < ln ? o0 + t : SPAN + 1u] = (uint16_t)dist;
-                  jj++;
-                  const bool w = jj == d;
-                  jj = w ? 0u : jj;
-                  dist += w ? d : 0u;
-                }
-              }
-            }
-          }
-        }
-        HZ2_LSYNC();
-        HZ_T(15);
-        // prefetch the next batch's records
-        LANE_ARR(uint32_t, no, MPL);
-        LANE_ARR(uint32_t, nw, MPL);
-#if HZ2_FUSE
-        load_recs(b0 + nb, no, nw);
-#else
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) {
-            const uint32_t j = b0 + nb + (uint32_t)lane + 64u * u;
-            LV(no)[u] = j < mtotal ? ring[2u * j] : 0xffffffffu;
-            LV(nw)[u] = j < mtotal ? ring[2u * j + 1u] : 0u;
-          }
-        }
-#endif
-        HZ_T(11);
-        HZ2_MARK("M_JUMP");
-        // 2. pointer jumping over the span's match bytes (branch-free per slot: a slot's
-        // source index is min(q - d, SPAN), and smap[SPAN] stays 0, so literal slots (d = 0
-        // reads smap[q] = 0), sources before F (q - d wraps) and slots past the span (d = 0)
-        // never move; every slot's entry is written back each round)
-        LANE_ARR(uint32_t, dq, RGP);
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t i = 0; i < RGP; i++) LV(dq)[i] = sh.smap[(uint32_t)lane + 64u * i];
-        }
-        if (nb) {
-          for (;;) {
-            LANE_VAR(uint32_t, chg);
-            LANE_LOOP {
-              uint32_t d2[RGP];
-HZ_UNROLL
-              for (uint32_t i = 0; i < RGP; i++) {
-                const uint32_t y = (uint32_t)lane + 64u * i - LV(dq)[i];
-                d2[i] = sh.smap[y < SPAN ? y : SPAN];
-              }
-              uint32_t c = 0;
-HZ_UNROLL
-              for (uint32_t i = 0; i < RGP; i++) {
-                c |= d2[i];
-                LV(dq)[i] += d2[i];
-              }
-              LV(chg) = c;
-              if (stats) for (uint32_t i = 0; i < RGP; i++) stats->hops += d2[i] != 0u;
-            }
-            if (stats) stats->tokens++;                // (emulator statistic: pointer-jumping rounds)
-            if (!WAVE_BALLOT(LV(chg) != 0u)) break;
-            HZ2_LSYNC();
-            LANE_LOOP {
-HZ_UNROLL
-              for (uint32_t i = 0; i < RGP; i++) sh.smap[(uint32_t)lane + 64u * i] = (uint16_t)LV(dq)[i];
-            }
-            HZ2_LSYNC();
-          }
-        }
-        HZ_T(12);
-        HZ2_MARK("M_GATHER");
-        // 3. gather, branch-free per slot: two byte loads each (a literal's from the literal
-        // stream -- its rank among the span's literals by ballot -- and a source before F from
-        // dst; the other load reads a harmless in-range byte) and a select; LDS byte writes of
-        // slots that take no byte go to a junk byte past the span buffer
-        constexpr uint32_t JUNK = (SPAN / 4u + 2u) * 4u - 1u;
-        LANE_VAR(uint32_t, vm);                 // slots inside the span
-        LANE_LOOP {
-          const uint32_t nv = span > (uint32_t)lane ? ((span - 1u - (uint32_t)lane) >> 6) + 1u : 0u;
-          LV(vm) = nv >= 32u ? ~0u : (1u << nv) - 1u;
-        }
-        // per-slot flags live as VGPR bit masks (bit i: slot i), not as per-slot predicates:
-        // the compiler would keep 24 of those in SGPR pairs across the batch and spill them
-        LANE_VAR(uint32_t, lb);                 // literal slots
-        LANE_VAR(uint32_t, fb);                 // match bytes whose source lies before F
-        LANE_LOOP { LV(lb) = 0; LV(fb) = 0; if (lane == 0) sh.sbuf[0] = hv; }
-        HZ2_LSYNC();
-        uint32_t lcnt = 0;                      // literals of the span so far (wave-uniform)
-#if HZ2_FUSE
-        LANE_VAR(uint32_t, vlb);                // the lanes' literal shares (registers, v_readlane)
-        LANE_VAR(uint32_t, vle);
-        LANE_VAR(uint32_t, vld);
-        LANE_LOOP { LV(vlb) = sh.lb[lane]; LV(vle) = sh.le[lane]; LV(vld) = sh.ldl[lane]; }
-#endif
-        // two halves of GH slots: GH loaded bytes in flight per lane (all 24 spill)
-        constexpr uint32_t GH = RGP / 2u;
-HZ_UNROLL
-        for (uint32_t h = 0; h < RGP; h += GH) {
-          LANE_ARR(uint32_t, bv, GH);
-HZ_UNROLL
-          for (uint32_t k = 0; k < GH; k++) {
-            const uint32_t i = h + k;
-            const uint64_t bm = WAVE_BALLOT(((LV(vm) >> i) & 1u) && LV(dq)[i] == 0u);
-#if HZ2_FUSE
-            // the slot's literal ranks [R0, R1): region deltas by the cursor
-            const uint32_t R0 = L0 + lcnt, R1 = R0 + (uint32_t)hz::popc64(bm);
-            LANE_VAR(uint32_t, ldx);
-            LANE_LOOP { LV(ldx) = lcd; }
-            while (R1 > lend && lcur < 63u) {
-              lcur++;
-              const uint32_t b = LV_AT(vlb, lcur);
-              lend = LV_AT(vle, lcur);
-              lcd = LV_AT(vld, lcur);
-              LANE_LOOP { LV(ldx) = R0 + hz2::lane_rank(bm, lane) >= b ? lcd : LV(ldx); }
-            }
-#endif
-            LANE_LOOP {
-              const uint32_t q = (uint32_t)lane + 64u * i, d = LV(dq)[i];
-              const uint32_t isl = (LV(vm) >> i) & (d == 0u ? 1u : 0u);
-              const uint32_t far = d > q ? 1u : 0u;      // (never for a slot past the span: d = 0)
-              LV(lb) |= isl << i;
-              LV(fb) |= far << i;
-              // one load: the 64-bit address selected as an integer (a pointer select becomes
-              // a branch), a harmless in-range byte of dst (F) for slots that take no byte
-#ifdef HZ2_EXP_NOLITLOAD                  // (traffic attribution builds: outputs wrong)
-              const uint64_t la = (uint64_t)(uintptr_t)lits;
-#elif HZ2_FUSE
-              const uint64_t la = (uint64_t)(uintptr_t)lits + (uint32_t)(R0 + hz2::lane_rank(bm, lane) + LV(ldx));
-#else
-              const uint64_t la = (uint64_t)(uintptr_t)lits + L0 + lcnt + hz2::lane_rank(bm, lane);
-#endif
-#ifdef HZ2_EXP_NOFAR
-              const uint64_t da = (uint64_t)(uintptr_t)dst + F;
-#else
-              const uint64_t da = (uint64_t)(uintptr_t)dst + (far ? F + q - d : F);
-#endif
-              LV(bv)[k] = *HZ_GLOBAL(hz_gcu8*, (uintptr_t)(isl ? la : da));
-              if (stats && far) stats->src_far[d - q <= 256u ? 0 : d - q <= 1536u ? 1 : d - q <= 4096u ? 2 : 3]++;
-            }
-            lcnt += (uint32_t)hz::popc64(bm);
-          }
-          LANE_LOOP {
-            uint32_t a1 = 0, b2 = 0;       // adler: sum b, batch-relative sum (x - F) b
-            uint8_t* const sb = (uint8_t*)sh.sbuf;
-            const uint32_t tb = LV(lb) | LV(fb);
-HZ_UNROLL
-            for (uint32_t k = 0; k < GH; k++) {
-              const uint32_t i = h + k;
-              const uint32_t q = (uint32_t)lane + 64u * i, v = LV(bv)[k];
-              const uint32_t tk = (tb >> i) & 1u;       // a literal or a byte from before F
-              sb[tk ? q + mis : JUNK] = (uint8_t)v;
-              a1 += tk * v;
-              b2 += tk * (q * v);
-            }
-            LV(ra1) += a1;
-            LV(ra2) += (uint64_t)F * a1 + b2;
-          }
-        }
-        HZ2_LSYNC();
-        // in-span sources: literals of the span, now in LDS
-        LANE_LOOP {
-          uint32_t a1 = 0, b2 = 0;
-          uint8_t* const sb = (uint8_t*)sh.sbuf;
-          const uint32_t ib = LV(vm) & ~(LV(lb) | LV(fb));
-          uint32_t v[RGP];
-HZ_UNROLL
-          for (uint32_t i = 0; i < RGP; i++) {
-            const uint32_t q = (uint32_t)lane + 64u * i;
-            v[i] = sb[((ib >> i) & 1u) ? q - LV(dq)[i] + mis : JUNK];
-          }
-HZ_UNROLL
-          for (uint32_t i = 0; i < RGP; i++) {
-            const uint32_t q = (uint32_t)lane + 64u * i, inb = (ib >> i) & 1u;
-            sb[inb ? q + mis : JUNK] = (uint8_t)v[i];
-            a1 += inb * v[i];
-            b2 += inb * (q * v[i]);
-            if (stats && inb) stats->src_in++;
-          }
-          LV(ra1) += a1;
-          LV(ra2) += (uint64_t)F * a1 + b2;
-        }
-        HZ2_LSYNC();
-        HZ_T(13);
-        HZ2_MARK("M_STORE");
-        // 4. store: whole dwords inside the span (dword 0 also when its head was loaded) and
-        // the stream; the span's edge bytes one by one.  HZ2_ST16: lane t takes dwords
-        // 4t .. 4t+3 with one 16-byte store when all four lie inside (a 1 KiB span is one
-        // store instruction); those lanes are a contiguous range [a, b] (only lane 0 can fail
-        // at the head, and a prefix of lanes fits the span), and the few dwords outside it
-        // -- [0, 4a) and [4b + 4, ndw) -- go dword by dword, one per lane
-        {
-          auto store_dword = [&](int lane, uint32_t k) {
-            (void)lane;
-            const uint32_t x0 = xa + 4u * k;
-            const bool inside = (int32_t)x0 >= 0 && x0 + 4u <= dst_len && x0 + 4u <= F + span && (k > 0u || !mis || head);
-#ifdef HZ2_EXP_NOMSTORE                   // (traffic attribution builds: outputs wrong)
-            (void)inside;
-#else
-            if (inside) {
-              *(hz_gu32*)(dst + x0) = sh.sbuf[k];
-            } else {
-              for (uint32_t b = 0; b < 4u; b++) {
-                const uint32_t x = x0 + b;
-                if (x >= F && x < F + span && x < dst_len) dst[x] = ((const uint8_t*)sh.sbuf)[4u * k + b];
-              }
-            }
-#endif
-          };
-#if HZ2_ST16
-          LANE_VAR(uint32_t, st4);
-          LANE_LOOP {
-            const uint32_t k0 = 4u * (uint32_t)lane, x0 = xa + 16u * (uint32_t)lane;
-            LV(st4) = (k0 + 4u <= ndw && (int32_t)x0 >= 0 && x0 + 16u <= dst_len && x0 + 16u <= F + span &&
-                       (lane > 0 || !mis || head)) ? 1u : 0u;
-          }
-          const uint64_t m4 = WAVE_BALLOT(LV(st4) != 0u);
-          if (m4) {
-            const uint32_t a = (uint32_t)__builtin_ctzll(m4), b = 63u - (uint32_t)__builtin_clzll(m4);
-            LANE_LOOP {
-#ifndef HZ2_EXP_NOMSTORE
-              if (LV(st4)) {
-                const uint32_t k0 = 4u * (uint32_t)lane;
-#if HZ_GPU
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                typedef __attribute__((address_space(1))) u32x4 gu32x4;
-                *(gu32x4*)(dst + (uint32_t)(xa + 4u * k0)) = *(const u32x4*)&sh.sbuf[k0];   // (xa may wrap: 32-bit sum)
-#else
-                memcpy(dst + (uint32_t)(xa + 4u * k0), &sh.sbuf[k0], 16);
-#endif
-              }
-#endif
-              const uint32_t lo = 4u * a, hi = 4u * b + 4u, nun = lo + (ndw - hi);
-              for (uint32_t t = (uint32_t)lane; t < nun; t += 64u) store_dword(lane, t < lo ? t : hi + (t - lo));
-            }
-          } else
-#endif
-          {
-            LANE_LOOP {
-              for (uint32_t k = (uint32_t)lane; k < ndw; k += 64u) store_dword(lane, k);
-            }
-          }
-        }
-        hcar = sh.sbuf[ndw - 1u];
-        hcar_ok = true;
-        HZ2_GSYNC();      // this wave reads the stored dwords back as far sources
-        LANE_LOOP {
-HZ_UNROLL
-          for (uint32_t u = 0; u < MPL; u++) { LV(ro)[u] = LV(no)[u]; LV(rw)[u] = LV(nw)[u]; }
-        }
-        HZ2_MARK("M_END");
-        b0 += nb;
-        F += span;
-        L0 += lcnt;
-      }
-      LANE_LOOP {
-        LV(s1) = (LV(s1) + LV(ra1) % ADLER_MOD) % ADLER_MOD;
-        LV(s2) = (uint32_t)((LV(s2) + LV(ra2) % ADLER_MOD) % ADLER_MOD);
-      }
-
-      HZ_T(10);
-      output_done();
-      return ST_OK;
-    }();
-    if (wst != ST_OK) {
-      fail = wst;
-      if (NW > 1) atomic_min_err(pipe.ctl, wst);
-      break;
-    }
-  }
-  if (NW > 1) {
-    // all wavefronts: every window done (or failed); the adler sums of all
-    if (fail != ST_OK) atomic_min_err(pipe.ctl, fail);
-    HZ2_WGBAR();
-    const int32_t e = (int32_t)ctl_ld((const uint32_t*)&pipe.ctl->err);
-    if (e) return e;
-    cur = pipe.ctl->next;                 // the END state: trailer position and total output
-  } else if (fail != ST_OK) {
-    return fail;
-  }
-  uint32_t pos = cur.pos;
-  const uint32_t out = cur.out;
-  // ---- trailer: adler32 (big-endian) after byte alignment ----
-  HZ_T(9);
-  pos = (pos + 7u) & ~7u;
-  if (pos + 32u > limit_bits) return ST_TRUNC;
-  uint32_t t32;
-  {
-    GRd r;
-    g_init(S, r, pos);
-    t32 = (uint32_t)(g_peek(r) & 0xffffffffu);
-  }
-  const uint32_t want = (t32 >> 24) | ((t32 >> 8) & 0xff00u) | ((t32 << 8) & 0xff0000u) | (t32 << 24);
-  uint64_t S1 = 0, S2 = 0;
-#if HZ_GPU
-  S1 = hz::wave_sum64((uint64_t)s1);
-  S2 = hz::wave_sum64((uint64_t)s2);
-#else
-  for (int lane = 0; lane < 64; lane++) { S1 += s1[lane]; S2 += s2[lane]; }
-#endif
-  if (NW > 1) {
-    // the wavefronts' partial sums, added up through LDS
-    Ctl* c = pipe.ctl;
-    c->adler[pipe.w][0] = S1;
-    c->adler[pipe.w][1] = S2;
-    HZ2_WGBAR();
-    S1 = 0; S2 = 0;
-    for (int i = 0; i < NW; i++) { S1 += c->adler[i][0]; S2 += c->adler[i][1]; }
-  }
-  const uint32_t A = (uint32_t)((1u + S1) % ADLER_MOD);
-  const uint32_t B = (uint32_t)(((uint64_t)(out % ADLER_MOD) * A + ADLER_MOD - (S2 % ADLER_MOD)) % ADLER_MOD);
-  if (((B << 16) | A) != want) return ST_DATA;
-  if (job.exact && out != dst_len) return ST_SIZE;
-  if (job.out_len) *job.out_len = out;
-  return ST_OK;
+  if constexpr ((NW == 1 && HZ2_FUSE) || (NW > 1 && HZ2_FUSE_PIPE))
+    return inflate_stream_1p<StatsT, NW>(sh, job, tune, ring_base, stats, prof, pipe);
+  else
+    return inflate_stream_2p<StatsT, NW>(sh, job, tune, ring_base, stats, prof, pipe);
 }
 
 // The window pipeline (NW > 1) with its timeout fallback.  A wait that gives up (ST_HANG:

@@ -19,7 +19,7 @@ STATS = ("windows blocks stored tokens matches lanes_valid repairs repair_lanes 
 
 @pytest.fixture(scope="module")
 def emu():
-    hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("inflate2.h", "inflate_wave.h")]
+    hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("inflate2.h", "inflate2_stream.inc", "inflate_wave.h")]
     if not os.path.exists(EMU) or os.path.getmtime(EMU) < max(os.path.getmtime(p) for p in [SRC] + hdrs):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", EMU, SRC])
     L = ctypes.CDLL(EMU)
