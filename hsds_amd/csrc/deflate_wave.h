@@ -56,9 +56,12 @@ constexpr uint32_t FARW = 32768;            // zlib window: with a far ring, mat
 #ifndef HD_HBITS
 #define HD_HBITS 11
 #endif
+#ifndef HD_SKEW
+#define HD_SKEW 1                           // skewed lane ranges (lane_start)
+#endif
 constexpr int HBITS = HD_HBITS;
 constexpr int HSIZE = 1 << HBITS;
-constexpr int LANE_MAX = SEG / WAVE;        // input bytes per lane (a full segment)
+constexpr int LANE_MAX = SEG / WAVE + 4;    // input bytes per lane (a full segment; lane_start's skew)
 constexpr int TSLOTS = LANE_MAX;            // 16-bit token slots per lane
 constexpr int SEG_TOK = TSLOTS * WAVE;      // token slots per segment in HBM
 constexpr int STAGE_WORDS = SEG / 4 + 24;   // a block is never emitted above its stored size
@@ -236,6 +239,21 @@ HZ_HD uint32_t load_stream_word(const EncJob& job, uint32_t p, uint32_t hi) {
     v = (w0 >> s) | (w1 << (32u - s));
   }
   return v;
+}
+
+// Lane l's range of a segment of seglen bytes: [lane_start(l), lane_start(l + 1)), R =
+// ceil(seglen / 64) bytes each with the start skewed by 4 floor(l / 2) bytes.  Unskewed, the
+// lanes start 128 bytes apart, so their input-ring words (and their 16-bit predecessor links)
+// sit in one LDS bank -- and stay near it as the lanes advance at similar rates; skewed, the
+// first ring words of the 64 lanes fall in 64 banks.  A range grows by at most 4 bytes.
+HZ_HD uint32_t lane_start(uint32_t l, uint32_t seglen) {
+  const uint32_t R = (seglen + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;
+#if HD_SKEW
+  const uint32_t a = l * R + 4u * (l >> 1);
+#else
+  const uint32_t a = l * R;
+#endif
+  return a < seglen ? a : seglen;
 }
 
 // token slot s of lane `lane` inside one segment's SEG_TOK slots: pairs of a lane
@@ -612,9 +630,7 @@ HZ_UNROLL
     // ---- lane-parallel greedy parse, tokens to HBM ----
     HZ_T(3);
     LANE_LOOP {
-      const uint32_t R = (seglen + WAVE - 1) / WAVE;
-      const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
-      const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+      const uint32_t a0 = lane_start((uint32_t)lane, seglen), a1 = lane_start((uint32_t)lane + 1u, seglen);
       uint32_t pos = s0 + a0;
       const uint32_t end = s0 + a1;
       const uint32_t ns = tune.stored ? 0u

@@ -254,11 +254,9 @@ HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const
   for (uint32_t sg = 0; sg < nseg; sg++) {
     const uint32_t s0 = sg * (uint32_t)hd::SEG;
     const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
-    const uint32_t R = (seglen + hd::WAVE - 1) / hd::WAVE;
     hz_gcu8* const gtok = HZ_GLOBAL(hz_gcu8*, tok + (size_t)sg * hd::SEG_TOK);
     LANE_LOOP {
-      const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
-      const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+      const uint32_t a0 = hd::lane_start((uint32_t)lane, seglen), a1 = hd::lane_start((uint32_t)lane + 1u, seglen);
       uint32_t has = 0, h = 0, ml0 = 0, rs = 0, lit0 = s0 + a0;
       lane_matches(gtok, sp[sg].nslot[lane], lane, s0 + a0, n, [&](uint32_t pos, uint32_t ml, uint32_t) {
         if (!has) { has = 1; h = pos - lit0; ml0 = ml; } else { rs += seq_size(pos - lit0, ml); }
@@ -305,7 +303,7 @@ HZ_HD uint32_t lz4_block_wave(const hd::SegParse* sp, const uint16_t* tok, const
     if (write) {
       LANE_LOOP {
         if (LV(sr)) {
-          const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
+          const uint32_t a0 = hd::lane_start((uint32_t)lane, seglen);
           Out o = {HZ_GLOBAL(hz_gu8*, out + base + LV(osz)), 0u, 1};
           InRd in;
           in_init(in, job);
@@ -379,11 +377,9 @@ HZ_HD uint32_t blosclz_block_wave(const hd::SegParse* sp, const uint16_t* tok, c
   for (uint32_t sg = 0; sg < nseg; sg++) {
     const uint32_t s0 = sg * (uint32_t)hd::SEG;
     const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
-    const uint32_t R = (seglen + hd::WAVE - 1) / hd::WAVE;
     hz_gcu8* const gtok = HZ_GLOBAL(hz_gcu8*, tok + (size_t)sg * hd::SEG_TOK);
     LANE_LOOP {
-      const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
-      const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+      const uint32_t a0 = hd::lane_start((uint32_t)lane, seglen), a1 = hd::lane_start((uint32_t)lane + 1u, seglen);
       uint32_t lit0 = s0 + a0, sz = 0;
       lane_tokens(gtok, sp[sg].nslot[lane], lane, s0 + a0, [&](uint32_t pos, uint32_t len, uint32_t dist) {
         sz += blz_lit_size(pos - lit0) + blz_match_size(len, dist);
@@ -407,8 +403,7 @@ HZ_HD uint32_t blosclz_block_wave(const hd::SegParse* sp, const uint16_t* tok, c
 #endif
     if (write) {
       LANE_LOOP {
-        const uint32_t a0 = (uint32_t)lane * R < seglen ? (uint32_t)lane * R : seglen;
-        const uint32_t a1 = a0 + R < seglen ? a0 + R : seglen;
+        const uint32_t a0 = hd::lane_start((uint32_t)lane, seglen), a1 = hd::lane_start((uint32_t)lane + 1u, seglen);
         Out o = {HZ_GLOBAL(hz_gu8*, out + base + LV(osz)), 0u, 1};
         InRd in;
         in_init(in, job);
