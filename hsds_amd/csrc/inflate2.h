@@ -129,11 +129,16 @@ static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
 #ifndef HZ2_ST16
 #define HZ2_ST16 1
 #endif
-// wave priority by stream progress (s_setprio at every window start): HZ2_PRIO levels, the
-// highest for a stream's first 1/HZ2_PRIO; 0 = off (A/B round 5, 4096 chunks: F1 26.0 ->
-// 25.5 ms, F2 38.2 -> 35.9 ms; waves busy F1 0.897 -> 0.961, F2 0.83 -> 0.87)
+// wave priority by the stream's remaining work (s_setprio at every window start): HZ2_PRIO
+// levels, one per HZ2_PRIO_ABS KiB of input left (the highest from 3 x 40 KiB up); 0 = off.
+// A/B round 5, 4096 chunks: by output fraction (HZ2_PRIO_ABS 0) F1 26.0 -> 25.5 ms, F2 38.2 ->
+// 35.9 ms, waves busy F1 0.897 -> 0.961, F2 0.83 -> 0.87; by remaining input, 40 KiB per level,
+// F1 180.4 -> 183.0 GB/s, F2 115.1 -> 120.0 (16 / 24 / 32 / 64 / 128 KiB measured worse)
 #ifndef HZ2_PRIO
 #define HZ2_PRIO 4
+#endif
+#ifndef HZ2_PRIO_ABS
+#define HZ2_PRIO_ABS 40
 #endif
 #ifndef HZ2_TICKN
 #define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 5)
