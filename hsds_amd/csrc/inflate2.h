@@ -78,7 +78,11 @@ using hz::ADLER_MOD;
 #ifndef HZ2_K
 #define HZ2_K 8
 #endif
-constexpr int K = HZ2_K;                  // recorded token starts per lane
+constexpr int K = HZ2_K;                  // recorded token starts per lane (two-pass form, LDS)
+#ifndef HZ2_K1
+#define HZ2_K1 8
+#endif
+constexpr int K1 = HZ2_K1;                // recorded token starts per lane (one-pass form, registers)
 constexpr uint32_t LMIN = 64;
 constexpr uint32_t LMAX = 1u << 16;       // segment bits (lane output stays well inside u32)
 constexpr uint32_t MCAP_LANE = 256;       // matches per lane per window (ring bound)
@@ -92,6 +96,10 @@ constexpr uint32_t SCRATCH_BYTES = RING_BYTES + LIT_BYTES;   // per resident wav
 #endif
 constexpr uint32_t SPAN = HZ2_SPAN;       // resolve batch: output bytes covered by the source map
 constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
+#ifndef HZ2_FILLCAP
+#define HZ2_FILLCAP 16
+#endif
+constexpr uint32_t FILL_CAP = HZ2_FILLCAP;   // resolve: source-map bytes a lane fills per match (258: all)
 static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 static_assert(SPL <= 24, "resolve slots per lane");
@@ -156,7 +164,7 @@ constexpr uint32_t END_NONE = 0, END_EOB = 1, END_ERR = 2, END_CUT = 3;
 // record: bits 0-9 token start relative to the segment, 10-21 output bytes, 22-26 matches,
 // 27-31 literals (cumulative from the lane's first record: the first record lies within 48
 // bits of the segment start, and K - 1 <= 15 tokens of <= 48 bits / <= 258 bytes follow)
-static_assert(K >= 1 && K <= 16, "record fields hold K <= 16 tokens");
+static_assert(K >= 1 && K <= 16 && K1 >= 1 && K1 <= 16, "record fields hold K <= 16 tokens");
 HZ_HD uint32_t rec_pack(uint32_t rel, uint32_t o, uint32_t m, uint32_t l) { return rel | (o << 10) | (m << 22) | (l << 27); }
 HZ_HD uint32_t rec_rel(uint32_t r) { return r & 0x3ffu; }
 HZ_HD uint32_t rec_out(uint32_t r) { return (r >> 10) & 0xfffu; }
@@ -718,15 +726,24 @@ HZ_HD Tok rtok(const Shared* sh, const BR& r) {
 HZ_HD uint32_t sel4(const uint32_t* a, uint32_t u) { return u == 0u ? a[0] : u == 1u ? a[1] : u == 2u ? a[2] : a[3]; }
 // a[j] of a lane's K recorded starts (registers) for a runtime j < K: masks OR-ed (a select
 // chain is folded back into an indexed load, which puts the array in scratch)
+template <int N>
 HZ_HD uint32_t selk(const uint32_t* a, uint32_t j) {
   uint32_t v = 0;
 HZ_UNROLL
-  for (uint32_t i = 0; i < (uint32_t)K; i++) v |= a[i] & (0u - (uint32_t)(j == i));
+  for (uint32_t i = 0; i < (uint32_t)N; i++) v |= a[i] & (0u - (uint32_t)(j == i));
   return v;
 }
+template <int N>
 HZ_HD void setk(uint32_t* a, uint32_t j, uint32_t v, bool on) {
 HZ_UNROLL
-  for (uint32_t i = 0; i < (uint32_t)K; i++) a[i] = (on && j == i) ? v : a[i];
+  for (uint32_t i = 0; i < (uint32_t)N; i++) a[i] = (on && j == i) ? v : a[i];
+}
+// a lane's batch records: one of the span's (index < nb) longer than FILL_CAP
+HZ_HD bool has_long(const uint32_t* w, uint32_t lane, uint32_t nb) {
+  bool r = false;
+HZ_UNROLL
+  for (uint32_t u = 0; u < MPL; u++) r |= lane + 64u * u < nb && (w[u] >> 16) > FILL_CAP;
+  return r;
 }
 // a lane's MPL match records (absolute position, len << 16 | dist - 1): one reaches before
 // the stream's first byte

@@ -60,7 +60,11 @@ def run(fmt, n, unique, tune=None):
 if __name__ == "__main__":
     n1 = int(os.environ.get("HZ_PROF_N1", "1024"))
     run("F1", n1, 256)
-    run("F2", int(os.environ.get("HZ_PROF_N2", "256")), 128)
+    if os.environ.get("HZ_PROF_F2W1", "0") == "1":
+        # one wavefront per stream (the batch path's one-pass decoder), so the phases are stamped
+        run("F2", int(os.environ.get("HZ_PROF_N2", "1024")), 128, tune={"waves_per_stream": 1})
+    else:
+        run("F2", int(os.environ.get("HZ_PROF_N2", "256")), 128)
     if os.environ.get("HZ_PROF_ZSTD", "0") == "1":
         run("ZSTD", int(os.environ.get("HZ_PROF_NZS", "512")), 128)
     if os.environ.get("HZ_PROF_LZ", "1") == "1":
