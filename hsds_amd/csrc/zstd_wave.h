@@ -24,6 +24,9 @@
 #define LZ_LANE0_ZW
 #endif
 
+#ifndef ZW_PRIO_KB
+#define ZW_PRIO_KB 32                 // wave priority: one level per 32 KiB of the split's input left (0: off)
+#endif
 namespace zw {
 
 constexpr int NSEQ = 128;
@@ -884,6 +887,18 @@ inline int frame(Shared& ls, const uint8_t* src, uint32_t n, uint8_t* dstp, uint
     // the frame walk is uniform: re-assert it at each block (a lane loop's exit value can
     // otherwise make the compiler treat the loop-carried state as divergent)
     q = uni(q); op = uni(op);
+#if HZ_GPU && ZW_PRIO_KB
+    {
+      // wave priority by the split's remaining input (inflate2.h HZ2_PRIO_ABS): the waves with
+      // the most work left get the SIMD's issue slots (A/B round 5, bench zstd leg: off 52.4,
+      // 16 KiB 51.8, 32 KiB 54.0, 64 KiB 53.8 GB/s)
+      const uint32_t lv = (n > q ? (n - q) >> 10 : 0u) / (uint32_t)ZW_PRIO_KB;
+      if (lv >= 3u) __builtin_amdgcn_s_setprio(3);
+      else if (lv == 2u) __builtin_amdgcn_s_setprio(2);
+      else if (lv == 1u) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     if (q + 3 > n) return zs::E_TRUNC;
     const uint32_t bh = ub8(in, q) | (ub8(in, q + 1) << 8) | (ub8(in, q + 2) << 16);
     q += 3;
