@@ -25,6 +25,9 @@
 #pragma once
 #include "inflate_wave.h"
 
+#ifndef LZ_PRIO_KB
+#define LZ_PRIO_KB 16                 // wave priority: one level per 16 KiB of the group's largest input left (0: off)
+#endif
 namespace lz {
 
 #ifndef LZ_GK
@@ -243,6 +246,24 @@ inline void lz_group(SH& ls, Stage* stage, HzProf* prof = nullptr) {
   WAVE_SYNC();
   for (;;) {
     if (!WAVE_BALLOT(LV(active))) break;
+#if HZ_GPU && LZ_PRIO_KB
+    {
+      // wave priority by the group's largest remaining input (inflate2.h HZ2_PRIO_ABS): the
+      // waves with the most work left get the SIMD's issue slots (A/B round 5, bench lz4 leg:
+      // off 148.1, 16 KiB 158.7, 32 KiB 156.5 GB/s)
+      uint32_t rem = 0;
+HZ_UNROLL
+      for (int l = 0; l < GROUP; l++) {
+        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)(LV(active) ? LV(rd).hi - (LV(ps).ip + LV(rd).lo) : 0u), l);
+        rem = r > rem ? r : rem;
+      }
+      const uint32_t lv = (rem >> 10) / (uint32_t)LZ_PRIO_KB;
+      if (lv >= 3u) __builtin_amdgcn_s_setprio(3);
+      else if (lv == 2u) __builtin_amdgcn_s_setprio(2);
+      else if (lv == 1u) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     HZ_T(1);
     // ---- stage: SW dwords of every active split's input from its parse position ----
     if constexpr (STAGE) {
