@@ -19,6 +19,9 @@
 #pragma once
 #include "lz_wave.h"
 
+#ifndef BS_PRIO_KB
+#define BS_PRIO_KB 64                 // wave priority: one level per 64 KiB of the chunk's input left (0: off)
+#endif
 namespace bs {
 
 // bshuf_default_block_size: an 8 KiB target, a multiple of 8, at least 128 elements
@@ -146,6 +149,17 @@ inline int chunk(Shared& sh, const uint8_t* srcp, uint32_t n, uint8_t* dstp, uin
   const uint32_t nel = chunk_bytes / es;
   uint32_t p = 12, e = 0;
   while (e + 8u <= nel) {
+#if HZ_GPU && BS_PRIO_KB
+    {
+      // wave priority by the chunk's remaining input (inflate2.h HZ2_PRIO_ABS; A/B round 5,
+      // bench bshuf leg: off 274.6, 64 KiB 285.2, 128 KiB 282.9, 192 KiB 280.0 GB/s)
+      const uint32_t lv = ((n - p) >> 10) / (uint32_t)BS_PRIO_KB;
+      if (lv >= 3u) __builtin_amdgcn_s_setprio(3);
+      else if (lv == 2u) __builtin_amdgcn_s_setprio(2);
+      else if (lv == 1u) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     // ---- lane 0 walks the next GROUP block headers ----
     WAVE_SYNC();
     LANE_LOOP {

@@ -247,7 +247,7 @@ inline void lz_group(SH& ls, Stage* stage, HzProf* prof = nullptr) {
   for (;;) {
     if (!WAVE_BALLOT(LV(active))) break;
 #if HZ_GPU && LZ_PRIO_KB
-    {
+    if constexpr (STAGE) {          // (lz_kernel; the bitshuffle decoder sets its own per chunk)
       // wave priority by the group's largest remaining input (inflate2.h HZ2_PRIO_ABS): the
       // waves with the most work left get the SIMD's issue slots (A/B round 5, bench lz4 leg:
       // off 148.1, 16 KiB 158.7, 32 KiB 156.5 GB/s)
