@@ -698,6 +698,13 @@ struct HuffShared {
   uint32_t next_code[17];
 };
 
+#ifndef HD_HUFF_X2
+#define HD_HUFF_X2 0   // timing experiments only: bit 1/2/4 runs the sort / parents / counts twice
+#endif
+#ifndef HD_HUFF_REG
+#define HD_HUFF_REG 1  // GPU: phases 1 and 3 by the whole wave (huff_parents_wave, huff_counts_wave)
+#endif
+
 // Serial part of the Huffman build (lane 0): keys[0..n) are sorted ascending by
 // (frequency, symbol).  Minimum-redundancy lengths in place (Moffat & Katajainen
 // 1995) and Kraft-exact limiting to maxbits give the code count per length
@@ -803,6 +810,159 @@ HZ_HD void huff_counts_serial(HuffShared& sh, int n, int maxbits) {
   }
 }
 
+#if HZ_GPU && HD_HUFF_REG
+// Phases 1 and 3 on the GPU with the whole wave in lock step (round 5).  Lane 0 alone spent
+// 45 % (phase 1) and 17 % (phase 3) of huff_kernel's time in dependent LDS round trips.
+//
+// Phase 1, the same two queues (leaves ascending, internal nodes in creation order) and the
+// same tie rule as huff_parents_serial, but each queue's current 64-entry chunk sits in a
+// register across the lanes, read by v_readlane and written by a lane select at wave-uniform
+// indices: wl = the leaf weights of chunk leaf >> 6, iw = the internal weights being written
+// (chunk next >> 6), ir = those of chunk root >> 6 once next has left it, pw = the parents of
+// chunk root >> 6.  A chunk goes to LDS only when its cursor leaves it: internal weights into
+// work[] (read back into ir), parents over them (their weights are dead by then), so work[]
+// ends as huff_parents_serial leaves it for every node but the root.
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); }
+__device__ __forceinline__ uint32_t wrl(uint32_t v, int i, uint32_t old) {
+  return HZ_LANE_ID() == i ? v : old;
+}
+__device__ __forceinline__ void huff_parents_wave(HuffShared& sh, int n_) {
+  const int lane = HZ_LANE_ID();
+  const int n = __builtin_amdgcn_readfirstlane(n_);
+  uint32_t* A = sh.work;
+  auto leaf_chunk = [&](int c) -> uint32_t {
+    const int i = 64 * c + lane;
+    return i < n ? sh.keys[i] >> 9 : 0u;
+  };
+  uint32_t wl = leaf_chunk(0), iw = 0, ir = 0, pw = 0;
+  iw = wrl(rdl(wl, 0) + rdl(wl, 1), 0, iw);
+  int root = 0, leaf = 2;
+  auto take_leaf = [&]() -> uint32_t {
+    const uint32_t w = rdl(wl, leaf & 63);
+    leaf++;
+    if ((leaf & 63) == 0) wl = leaf_chunk(leaf >> 6);
+    return w;
+  };
+  for (int next = 1; next < n - 1; next++) {
+    if ((next & 63) == 0) {               // next leaves its chunk: keep it for root, store it
+      if ((root >> 6) == (next >> 6) - 1) ir = iw;
+      A[next - 64 + lane] = iw;
+      iw = 0;
+    }
+    auto take_root = [&]() -> uint32_t {
+      const uint32_t w = rdl((root >> 6) == (next >> 6) ? iw : ir, root & 63);
+      pw = wrl((uint32_t)next, root & 63, pw);
+      root++;
+      if ((root & 63) == 0) {             // root leaves its chunk: its parents are final
+        A[root - 64 + lane] = pw;
+        if ((root >> 6) < (next >> 6)) ir = root + lane < NLL ? A[root + lane] : 0u;
+      }
+      return w;
+    };
+    const uint32_t iv1 = rdl((root >> 6) == (next >> 6) ? iw : ir, root & 63);
+    const uint32_t lv1 = leaf < n ? rdl(wl, leaf & 63) : 0u;
+    uint32_t w = (leaf >= n || iv1 < lv1) ? take_root() : take_leaf();
+    const uint32_t iv2 = rdl((root >> 6) == (next >> 6) ? iw : ir, root & 63);
+    const uint32_t lv2 = leaf < n ? rdl(wl, leaf & 63) : 0u;
+    w += (leaf >= n || (root < next && iv2 < lv2)) ? take_root() : take_leaf();
+    iw = wrl(w, next & 63, iw);
+  }
+  if (64 * (root >> 6) + lane < root) A[64 * (root >> 6) + lane] = pw;
+}
+
+// Phase 3 from a histogram: H[d] internal nodes at depth d (d >= 16 pooled) give
+// bl_count[d] = 2 H[d - 1] - H[d] leaves (the serial walk's avbl - used), the pooled
+// 2 H[15] + H[>= 16] at 16; then the fold onto maxbits, the Kraft fix-up and next_code as
+// huff_counts_serial, with bl_count[l] in lane l.
+__device__ __forceinline__ void huff_counts_wave(HuffShared& sh, int n_, int maxbits) {
+  const int lane = HZ_LANE_ID();
+  const int n = __builtin_amdgcn_readfirstlane(n_);
+  const uint32_t* A = sh.work;
+  uint32_t hv = 0;                        // H[lane] for lane <= 16
+  uint32_t d[5];
+  HZ_UNROLL for (int k = 0; k < 5; k++) {
+    const int i = 64 * k + lane;
+    d[k] = i < n - 1 ? (A[i] > 16u ? 16u : A[i]) : 99u;
+  }
+  HZ_UNROLL for (int k = 0; k < 5; k++) {
+    if (64 * k >= n - 1) break;
+    for (int t = 0; t <= 16; t++) {
+      const uint32_t c = (uint32_t)__builtin_popcountll(__ballot(d[k] == (uint32_t)t));
+      if (lane == t) hv += c;
+    }
+  }
+  const uint32_t hprev = (uint32_t)__shfl_up((int)hv, 1, 64);
+  uint32_t b = lane == 0 ? 0u : lane < 16 ? 2u * hprev - hv : lane == 16 ? 2u * hprev + hv : 0u;
+  // fold the lengths above maxbits onto maxbits
+  uint32_t over = lane > maxbits ? b : 0u;
+  over = hz::wave_sum(over);
+  if (lane > maxbits) b = 0;
+  if (lane == maxbits) b += over;
+  uint32_t kr = (lane >= 1 && lane <= maxbits) ? b << (maxbits - lane) : 0u;
+  uint32_t total = __builtin_amdgcn_readfirstlane(hz::wave_sum(kr));
+  while (total != (1u << maxbits)) {
+    const uint64_t m = __ballot(lane >= 1 && lane < maxbits && b != 0u);
+    const int l = m ? 63 - __builtin_clzll(m) : 0;
+    if (lane == maxbits) b -= 1u;
+    if (l && lane == l) b -= 1u;
+    if (l && lane == l + 1) b += 2u;
+    total--;
+  }
+  uint32_t code = 0, nc = 0;
+  for (int l = 1; l <= 15; l++) {
+    code = (code + (l > 1 ? rdl(b, l - 1) : 0u)) << 1;
+    nc = wrl(code, l, nc);
+  }
+  if (lane <= 16) { sh.bl_count[lane] = b; sh.next_code[lane] = nc; }
+}
+
+// The code lengths and canonical codes with bl_count / next_code in registers: a symbol of
+// rank r (from the most frequent) gets length 1 + #{l < 15 : bl_count[1] + .. + bl_count[l] <= r},
+// the serial walk's result; codes by ballots per length as before, the running next_code[L]
+// in lane L instead of one LDS read-modify-write per length.
+__device__ __forceinline__ void huff_lens_wave(HuffShared& sh, int n_, uint8_t* lens) {
+  const int lane = HZ_LANE_ID();
+  const int n = __builtin_amdgcn_readfirstlane(n_);
+  const uint32_t cum = hz::wave_incl_scan_dpp(lane <= 16 ? sh.bl_count[lane] : 0u);
+  uint32_t cs[15];
+  HZ_UNROLL for (int l = 1; l < 15; l++) cs[l] = rdl(cum, l);
+  for (int i = lane; i < n; i += 64) {
+    const uint32_t r = (uint32_t)(n - 1 - i);
+    uint32_t len = 1;
+    HZ_UNROLL for (int l = 1; l < 15; l++) len += cs[l] <= r ? 1u : 0u;
+    lens[sh.keys[i] & 511u] = (uint8_t)len;
+  }
+}
+__device__ __forceinline__ void huff_codes_wave(HuffShared& sh, int nsym, int maxbits, const uint8_t* lens,
+                                                uint16_t* codes) {
+  const int lane = HZ_LANE_ID();
+  uint32_t ncv = lane <= 15 ? sh.next_code[lane] : 0u;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int c = 0; c < nsym; c += 64) {
+    const uint32_t ln = c + lane < nsym ? (uint32_t)lens[c + lane] : 0u;
+    uint32_t code = 0;
+    for (int L = 1; L <= maxbits; L++) {
+      const uint64_t m = __ballot(ln == (uint32_t)L);
+      if (!m) continue;
+      if (ln == (uint32_t)L) code = rev16(rdl(ncv, L) + hz::popc64(m & below), (uint32_t)L);
+      if (lane == L) ncv += hz::popc64(m);
+    }
+    if (c + lane < nsym) codes[c + lane] = (uint16_t)code;
+  }
+}
+#endif
+
+#if HZ_GPU && HD_HUFF_REG
+#define HD_HUFF_PARENTS(sh, NN) hd::huff_parents_wave(sh, NN)
+#define HD_HUFF_COUNTS(sh, NN, MB) hd::huff_counts_wave(sh, NN, MB)
+#define HD_HUFF_LENS(sh, LENS) hd::huff_lens_wave(sh, (int)(sh).cnt, LENS)
+#define HD_HUFF_CODES(sh, N, MB, LENS, CODES) hd::huff_codes_wave(sh, N, MB, LENS, CODES)
+#else
+#define HD_HUFF_PARENTS(sh, NN) LANE_LOOP { if (lane == 0) hd::huff_parents_serial(sh, NN); }
+#define HD_HUFF_COUNTS(sh, NN, MB) LANE_LOOP { if (lane == 0) hd::huff_counts_serial(sh, NN, MB); }
+#define HD_HUFF_LENS(sh, LENS) HD_HUFF_LENS_SERIAL(sh, LENS)
+#define HD_HUFF_CODES(sh, N, MB, LENS, CODES) HD_HUFF_CODES_SERIAL(sh, N, MB, LENS, CODES)
+#endif
 // cooperative Huffman build for FREQ[0..N) limited to MAXBITS (NP: power of two >= N)
 #define HD_BUILD_HUFF(sh, FREQ, N, NP, MAXBITS, LENS, CODES)                                    \
   do {                                                                                          \
@@ -827,6 +987,7 @@ HZ_HD void huff_counts_serial(HuffShared& sh, int n, int maxbits) {
         (sh).keys[_s] = (_s < (N) && (FREQ)[_s]) ? (((FREQ)[_s] << 9) | (uint32_t)_s) : hd::KEY_NONE; \
     }                                                                                           \
     WAVE_SYNC();                                                                                \
+    for (int _x2 = 0; _x2 < ((HD_HUFF_X2 & 1) ? 2 : 1); _x2++)                                 \
     for (int _k = 2; _k <= (NP); _k <<= 1) {                                                    \
       for (int _j = _k >> 1; _j > 0; _j >>= 1) {                                                \
         LANE_LOOP {                                                                             \
@@ -840,12 +1001,27 @@ HZ_HD void huff_counts_serial(HuffShared& sh, int n, int maxbits) {
         WAVE_SYNC();                                                                            \
       }                                                                                         \
     }                                                                                           \
-    LANE_LOOP { if (lane == 0) hd::huff_parents_serial(sh, (int)(sh).cnt); }                  \
+    for (int _x2 = 0; _x2 < ((HD_HUFF_X2 & 2) ? 2 : 1); _x2++) {                               \
+      HD_HUFF_PARENTS(sh, (int)(sh).cnt);                                                       \
+      WAVE_SYNC();                                                                              \
+    }                                                                                           \
     WAVE_SYNC();                                                                                \
     HD_HUFF_DEPTHS(sh, (int)(sh).cnt);                                                          \
-    LANE_LOOP { if (lane == 0) hd::huff_counts_serial(sh, (int)(sh).cnt, (MAXBITS)); }         \
+    for (int _x2 = 0; _x2 < ((HD_HUFF_X2 & 4) ? 2 : 1); _x2++) {                               \
+      HD_HUFF_COUNTS(sh, (int)(sh).cnt, (MAXBITS));                                             \
+      WAVE_SYNC();                                                                              \
+    }                                                                                           \
     WAVE_SYNC();                                                                                \
     /* lengths: the most frequent symbols (end of keys) get the shortest codes */              \
+    HD_HUFF_LENS(sh, LENS);                                                                     \
+    WAVE_SYNC();                                                                                \
+    /* canonical codes: rank within a length by ballots, 64 symbols at a time */               \
+    HD_HUFF_CODES(sh, N, MAXBITS, LENS, CODES);                                                 \
+  } while (0)
+
+// the serial forms (CPU emulation, HD_HUFF_REG=0) of huff_lens_wave / huff_codes_wave
+#define HD_HUFF_LENS_SERIAL(sh, LENS)                                                           \
+  do {                                                                                          \
     LANE_LOOP {                                                                                 \
       const int _n = (int)(sh).cnt;                                                             \
       for (int _i = lane; _i < _n; _i += 64) {                                                  \
@@ -855,8 +1031,9 @@ HZ_HD void huff_counts_serial(HuffShared& sh, int n, int maxbits) {
         (LENS)[(sh).keys[_i] & 511u] = (uint8_t)_l;                                             \
       }                                                                                         \
     }                                                                                           \
-    WAVE_SYNC();                                                                                \
-    /* canonical codes: rank within a length by ballots, 64 symbols at a time */               \
+  } while (0)
+#define HD_HUFF_CODES_SERIAL(sh, N, MAXBITS, LENS, CODES)                                       \
+  do {                                                                                          \
     for (int _c = 0; _c < (N); _c += 64) {                                                      \
       LANE_VAR(uint32_t, _ln);                                                                  \
       LANE_LOOP {                                                                               \
