@@ -1231,30 +1231,11 @@ __global__ void __launch_bounds__(64) zstd_count_kernel(const uint32_t* __restri
     const uint32_t item = meta[s].item;
     if (item != cur) { flush(cur); cur = item; }
     hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok + (size_t)s * hd::SEG_TOK);
-    uint32_t run = 0, lits = 0, lead = 0, hm = 0, want_dist = 0, ml = 0;
-    hze::slots_fwd(gw, sp[s].nslot[l], l, [&](uint32_t v) {
-      if (want_dist) {                               // (len | 0x8000, dist - 1): a match
-        const hze::Seq q = hze::make_seq_t(ct, run, ml, v + 1u);
-        if (hm) add(q.llc);                          // (a lane's first run: after the scans)
-        else lead = run;
-        add(36u + q.ofc);
-        add(68u + q.mlc);
-        hm = 1;
-        run = 0;
-        want_dist = 0;
-      } else if (v & 0x8000u) {
-        ml = (v & 0x7fffu) + 3u;
-        want_dist = 1;
-      } else {
-        run++;
-        lits++;
-      }
-    });
+    const hze::LaneCount r = hze::lane_count(ct, gw, sp[s].nslot[l], l, add);
     // literal ordinals: L = before this lane, q = after its last match (0: none before)
-    const uint32_t L = hz::wave_incl_scan_dpp(lits) - lits;
-    const uint32_t q = hm ? L + lits - run : 0u;
-    const uint32_t qprev = hz::wave_excl_max(q, (int)l);
-    if (hm) add(hze::make_seq_t(ct, L + lead - qprev, 3u, 1u).llc);
+    const uint32_t L = hz::wave_incl_scan_dpp(r.lits) - r.lits;
+    const uint32_t qprev = hz::wave_excl_max(hze::lane_q(L, r), (int)l);
+    if (r.hm) add(hze::make_seq_t(ct, hze::first_run(L, r, qprev), 3u, 1u).llc);
   }
   flush(cur);
 }

@@ -322,6 +322,11 @@ struct Src {
 
 HZ_HD uint32_t gword(const Src& s, uint32_t k) { return hz::load_word(s.base, k, s.lo, s.hi); }
 
+// the compressed stream is read once (A's warm-up overlaps aside): HZ2_NTBITS = 1 loads it
+// non-temporally, so it does not push the match records and recent output out of L2
+#ifndef HZ2_NTBITS
+#define HZ2_NTBITS 0
+#endif
 // quad qa (clamped to the stream's last quad: an aligned 16-byte block holding a stream
 // byte never crosses a page, so the load is always safe)
 HZ_HD void g_quad(const Src& s, uint32_t qa, uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3) {
@@ -329,7 +334,11 @@ HZ_HD void g_quad(const Src& s, uint32_t qa, uint32_t& a0, uint32_t& a1, uint32_
 #if HZ_GPU
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+#if HZ2_NTBITS
+  const u32x4 v = __builtin_nontemporal_load((gu32x4*)(s.base + b0));
+#else
   const u32x4 v = *(gu32x4*)(s.base + b0);
+#endif
   a0 = v.x; a1 = v.y; a2 = v.z; a3 = v.w;
 #else
   uint8_t t[16] = {0};

@@ -1,29 +1,19 @@
-// inflate_wave.h -- one-wavefront-per-stream zlib (RFC 1950/1951) decoder.
+// inflate_wave.h -- shared pieces of the zlib (RFC 1950/1951) decoder in inflate2.h.
 //
-// Replaces, for the HSDS data-node hot path, the zlib inflate that the reference
-// reaches through storUtil._uncompress (hsds/util/storUtil.py:209-220, CPython
-// zlib.decompress) and through c-blosc's zlib_wrap_decompress for every Blosc split
-// (storUtil.py:195-208).  Output must be bit-identical to libz; errors map to the
-// same "500" outcome (corrupt data, truncated stream, adler32 mismatch).
-//
-// Algorithm (see DESIGN.md "Inflate"):
-//   The 64 lanes of a wavefront cooperate on ONE deflate stream.  Inside a Huffman
-//   block the bitstream window [win_start, win_start + 64*L) is cut into 64 segments
-//   of L bits.  Phase A: lane i speculatively decodes tokens starting W bits before
-//   its segment (lane 0 starts exactly at the known token boundary), marking every
-//   token start in an LDS bitmap and storing tokens in LDS.  Phase B: lane i is
-//   "synced" when the exit position of lane i-1 (first token start at or after the
-//   end of segment i-1) is one of lane i's marked token starts; from there on its
-//   decode is the true decode (Huffman self-synchronisation).  The longest synced
-//   prefix of lanes is accepted.  Phase C: output offsets by a wave prefix sum,
-//   literals written, LZ77 matches resolved in rounds against a frontier F (all
-//   output below F is final), adler32 accumulated per lane as position-weighted
-//   sums and combined once per stream.
-//
-// The file is SINGLE SOURCE for two drivers:
-//   * HIP (gfx950):  every lane is a real SIMT lane, LANE_LOOP is one iteration.
-//   * CPU emulation (tests/emu): LANE_LOOP iterates lanes 0..63 in order, so the
-//     same orchestration (including every cross-lane step) is unit-tested on CPU.
+// The decoder itself (inflate2.h, inflate2_stream.inc) replaces, for the HSDS data-node hot
+// path, the zlib inflate that the reference reaches through storUtil._uncompress
+// (hsds/util/storUtil.py:209-220, CPython zlib.decompress) and through c-blosc's
+// zlib_wrap_decompress for every Blosc split (storUtil.py:195-208).  This header holds what
+// it shares with the other wave kernels:
+//   * the single-source SIMT conventions (LANE_LOOP, LANE_VAR, WAVE_BALLOT, wave scans):
+//     HIP (gfx950) runs every lane as a real SIMT lane and LANE_LOOP is one iteration; the
+//     CPU emulation (tests/emu) iterates lanes 0..63 in order, so every cross-lane step is
+//     unit-tested on CPU;
+//   * status codes, the 16-bit decode-table entry formats (ent_sym / ent_sub / ent_rich);
+//   * the cooperative canonical-Huffman table build (HZ_BUILD_TABLE, zlib inflate_table's
+//     acceptance rules) and the global-memory word loader.
+// (The round-1 decoder that lived here -- LDS-staged windows, token slots -- was retired in
+// round 6; inflate2.h replaced it in round 2.)
 #pragma once
 #include <stdint.h>
 
@@ -101,40 +91,11 @@ constexpr int D_ROOT = 8;
 // second-level entries (codes longer than the root).  Sized at or above zlib's exact
 // worst cases (ENOUGH: 286 symbols / root 10 -> 308 extra entries; 30 symbols /
 // root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
-// Window sizes (LMAX, SCAP, SLOTS) are set so that sizeof(Shared) = 20480 B: eight
-// wavefronts per CU (A/B on MI355X: 7 -> 8 waves/CU gave F1 +7 %, F2 +14 %; smaller
-// windows at 9-10 waves/CU lost more to per-window overhead than they gained).
 #ifndef HZ_LL_SUB
 #define HZ_LL_SUB 320
 #endif
 constexpr int LL_SUB = HZ_LL_SUB;
 constexpr int D_SUB = 384;
-#ifndef HZ_SLOTS
-#define HZ_SLOTS 50
-#endif
-constexpr int SLOTS = HZ_SLOTS;           // 16-bit token slots per lane per window (a match takes two)
-#ifndef HZ_LMAX
-#define HZ_LMAX 288
-#endif
-constexpr int LMAX = HZ_LMAX;           // max segment length (bits)
-constexpr int LMIN = 64;
-constexpr uint32_t ADAPT_FILL16 = 11; // adaptive L aims at this many 16ths of SLOTS token slots per segment
-#ifndef HZ_SCAP
-#define HZ_SCAP 4608
-#endif
-constexpr int SCAP = HZ_SCAP;           // window output bytes resolved in LDS
-#ifndef HZ_CMAX
-#define HZ_CMAX 256
-#endif
-constexpr int CMAX = HZ_CMAX;
-#ifndef HZ_SCAP_FILL8
-#define HZ_SCAP_FILL8 7                 // adaptive L aims at this many 8ths of SCAP output bytes per window
-#endif           // max continuation bits into the next segment
-constexpr int OVR = 64;             // bitmap bits past the last token start
-constexpr int BM_WORDS = (LMAX + CMAX + OVR) / 32 + 1;
-// staged input dwords: window (64 L) + warm-up (<= L) + alignment + overrun/peek
-constexpr int WMAX = 1024;
-constexpr int IN_WORDS = (WAVE * LMAX + WMAX + CMAX + 256) / 32 + 8;
 constexpr uint32_t ADLER_MOD = 65521;
 
 // status codes (include/hsds_amd.h)
@@ -180,61 +141,6 @@ HZ_HD uint16_t ent_rich(int kind, uint32_t len, uint32_t sym) {
 constexpr uint32_t T_MATCH = 0x80000000u;
 constexpr uint32_t T_EOB = 0x100u;        // == its stored slot value S_EOB
 constexpr uint32_t T_ERR = 0x101u;        // == S_ERR
-// stored token slots (16 bit): literal byte, S_EOB, S_ERR, or a match as two slots
-// 0x8000 | (len - 3) followed by (dist - 1).  A lane's token k sits at slot
-// k + popcount(match mask of tokens < k).
-constexpr uint32_t S_EOB = 0x100u, S_ERR = 0x101u, S_MATCH = 0x8000u;
-
-
-struct Shared {
-  uint16_t lut_ll[(1 << LL_ROOT) + LL_SUB];
-  uint16_t lut_d[(1 << D_ROOT) + D_SUB];
-  uint16_t tb_first[16];
-  uint16_t tb_offs[17];
-  uint16_t tb_next[16];
-  // token slots, lane-interleaved in pairs: slot s of lane l is half (s & 1) of dword
-  // (s >> 1) * 64 + l, so lanes reading any slots hit distinct banks
-  union {
-    uint16_t tok[SLOTS * WAVE];
-    uint32_t tokw[SLOTS / 2 * WAVE];
-  };
-  // The window's decode state (input staging, token-start bitmaps, per-lane exit /
-  // sync / repair flags) is dead once phase C starts building the byte reference
-  // map, and is rebuilt by the next window's staging / phase A: the two share LDS.
-  union {
-    struct {
-      union {
-        uint32_t bitmap[WAVE][BM_WORDS];
-        struct {                         // Huffman table build scratch (dead while windows run)
-          uint16_t sorted_ll[288];
-          uint16_t sorted_d[32];
-          uint16_t cnt_ll[16];
-          uint16_t cnt_d[16];
-          uint16_t cnt_cl[16];
-          uint16_t sorted_cl[20];
-          uint8_t lens[320 + 32];
-        };
-      };
-      uint32_t in32[IN_WORDS + 4];
-      uint32_t exitpos[WAVE];
-      uint32_t syncpos[WAVE];
-      uint32_t flag[WAVE];
-      uint32_t flag2[WAVE];
-    };
-    uint16_t ref[SCAP];
-  };
-  uint32_t contpos[WAVE];
-  uint32_t obase[WAVE + 1];
-  uint16_t tcur_l[WAVE];
-  uint16_t tend_l[WAVE];
-  // uniform scalars published by lane 0
-  int32_t u_status;
-  uint32_t u_pos;
-  uint32_t u_nlen, u_ndist;
-  uint32_t u_stage_base;
-  uint32_t u_stored_len;
-};
-
 HZ_HD uint32_t bmask(uint32_t n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1u); }
 
 HZ_HD uint32_t popc32(uint32_t x) {
@@ -278,138 +184,6 @@ HZ_HD uint32_t rev_bits(uint32_t v, int n) {
   return r;
 }
 
-// ---- LDS bit access ---------------------------------------------------------
-// Bit positions are relative to the 4-byte aligned base of the stream, so every
-// staged dword load is aligned.  peek64 returns >= 64 valid bits at `pos`.
-HZ_HD uint64_t peek64(const Shared* sh, uint32_t pos) {
-  uint32_t w = pos - sh->u_stage_base;
-  uint32_t i = w >> 5, s = w & 31u;
-  uint64_t lo = (uint64_t)sh->in32[i] | ((uint64_t)sh->in32[i + 1] << 32);
-  uint64_t hi = sh->in32[i + 2];
-  return s ? ((lo >> s) | (hi << (64 - s))) : lo;
-}
-
-HZ_HD uint32_t lookup_ll(const Shared* sh, uint64_t bits) {
-  uint32_t e = sh->lut_ll[bits & ((1u << LL_ROOT) - 1)];
-  if (!(e & 15u)) e = sh->lut_ll[(1u << LL_ROOT) + ((e >> 4) & 511u) + ((uint32_t)(bits >> LL_ROOT) & bmask(e >> 13))];
-  return e;
-}
-HZ_HD uint32_t lookup_d(const Shared* sh, uint64_t bits) {
-  uint32_t e = sh->lut_d[bits & ((1u << D_ROOT) - 1)];
-  if (!(e & 15u)) e = sh->lut_d[(1u << D_ROOT) + ((e >> 4) & 511u) + ((uint32_t)(bits >> D_ROOT) & bmask(e >> 13))];
-  return e;
-}
-
-// ---- register bit reader over the staged window ------------------------------
-// bb holds `avail` (>= 32 after fill) bits starting at bit position `pos`; the next
-// staged dword is prefetched into `nxt` so a refill never waits on LDS.
-struct BitRd {
-  uint64_t bb;
-  uint32_t avail;
-  uint32_t widx;
-  uint32_t nxt;
-  uint32_t pos;
-};
-
-HZ_HD void br_init(const Shared* sh, BitRd& r, uint32_t p, uint32_t stage_base) {
-  const uint32_t w = p - stage_base, i = w >> 5, s = w & 31u;
-  const uint64_t lo = (uint64_t)sh->in32[i] | ((uint64_t)sh->in32[i + 1] << 32);
-  r.bb = lo >> s;
-  r.avail = 64u - s;
-  r.widx = i + 2u;
-  r.nxt = sh->in32[i + 2];
-  r.pos = p;
-}
-
-HZ_HD void br_fill(const Shared* sh, BitRd& r) {
-  // branch-free: always read the next staged word, keep it only when used
-  const uint32_t need = r.avail < 32u;
-  const uint64_t add = (uint64_t)r.nxt << (r.avail & 31u);
-  r.bb |= need ? add : 0ull;
-  r.avail += need ? 32u : 0u;
-  r.widx += need;
-  const uint32_t nn = sh->in32[r.widx];
-  r.nxt = need ? nn : r.nxt;
-}
-
-HZ_HD void br_drop(BitRd& r, uint32_t n) { r.bb >>= n; r.avail -= n; r.pos += n; }
-
-// decode one token at r.pos and advance past it.  Invalid codes advance by their
-// table length (any deterministic advance keeps speculative decoders consistent;
-// a real error stops the stream at the ERR token's start).
-HZ_HD uint32_t next_token(const Shared* sh, BitRd& r) {
-  br_fill(sh, r);
-  const uint32_t e = lookup_ll(sh, r.bb);
-  const uint32_t nb = e & 15u, p = e >> 4;
-  // RFC 1951 3.2.5 length codes: symbol 257+s, s < 8 -> 3+s, s == 28 -> 258,
-  // otherwise ((4 | s&3) << x) + 3 with x = (s-4)/4 extra bits
-  const uint32_t s = p - 257u;
-  const int islen = s < 29u;
-  const uint32_t xb = (islen && s >= 8u && s < 28u) ? (s - 4u) >> 2 : 0u;
-  const uint32_t base = s < 8u ? s + 3u : s == 28u ? 258u : ((4u | (s & 3u)) << xb) + 3u;
-  const uint32_t len = base + ((uint32_t)(r.bb >> nb) & bmask(xb));
-  br_drop(r, nb + xb);
-  uint32_t tok = p <= 256u ? p : T_ERR;     // literal byte or T_EOB (= 256)
-  if (islen) {
-    br_fill(sh, r);
-    const uint32_t ed = lookup_d(sh, r.bb);
-    const uint32_t nd = ed & 15u, d = ed >> 4;
-    // distance codes: d < 4 -> d+1, otherwise ((2 | d&1) << x) + 1 with x = d/2-1
-    const int ok = d < 30u;
-    const uint32_t xd = (ok && d >= 2u) ? (d - 2u) >> 1 : 0u;
-    const uint32_t dist = (d < 4u ? d + 1u : ((2u | (d & 1u)) << xd) + 1u) + ((uint32_t)(r.bb >> nd) & bmask(xd));
-    br_drop(r, ok ? nd + xd : nd);
-    tok = ok ? (T_MATCH | (len << 16) | (dist - 1u)) : T_ERR;
-  }
-  return tok;
-}
-
-HZ_HD uint32_t tok_idx(uint32_t s, int lane) { return ((s >> 1) * (uint32_t)WAVE + (uint32_t)lane) * 2u + (s & 1u); }
-HZ_HD uint32_t tok_at(const Shared* sh, uint32_t s, int lane) { return sh->tok[tok_idx(s, lane)]; }
-// store decoder token tokv at slot ns of `lane`; returns the slots used (1 or 2)
-HZ_HD uint32_t put_tok(Shared* sh, int lane, uint32_t ns, uint32_t tokv) {
-  const uint32_t m = tokv & T_MATCH;
-  const uint32_t i0 = tok_idx(ns, lane);
-  sh->tok[i0] = (uint16_t)(m ? (S_MATCH | (((tokv >> 16) & 0x1ffu) - 3u)) : tokv);
-  if (m) sh->tok[i0 + ((ns & 1u) ? 2u * (uint32_t)WAVE - 1u : 1u)] = (uint16_t)(tokv & 0x7fffu);
-  return m ? 2u : 1u;
-}
-// token at slot t of lane j: v = the slot, d = distance of a match (the next slot + 1);
-// two independent dword reads instead of two dependent 16-bit ones
-HZ_HD void tok_pair(const Shared* sh, uint32_t t, int j, uint32_t& v, uint32_t& d) {
-  const uint32_t q = t >> 1;
-  const uint32_t q1 = q + 1u < (uint32_t)(SLOTS / 2) ? q + 1u : q;
-  const uint32_t w0 = sh->tokw[q * (uint32_t)WAVE + (uint32_t)j];
-  const uint32_t w1 = sh->tokw[q1 * (uint32_t)WAVE + (uint32_t)j];
-  v = (t & 1u) ? (w0 >> 16) : (w0 & 0xffffu);
-  d = ((t & 1u) ? (w1 & 0xffffu) : (w0 >> 16)) + 1u;
-}
-// slot of token k of a lane whose match mask is mb
-HZ_HD uint32_t tok_slot(uint64_t mb, uint32_t k) { return k + popc64(k >= 64u ? mb : mb & ((1ull << k) - 1ull)); }
-
-HZ_HD void mark_bit(Shared* sh, int lane, uint32_t rel) {
-  if (rel < (uint32_t)(BM_WORDS * 32)) sh->bitmap[lane][rel >> 5] |= 1u << (rel & 31u);
-}
-
-// relative bit position of the k-th (0-based) mark of a lane
-HZ_HD uint32_t nth_mark(const Shared* sh, int lane, uint32_t k) {
-  uint32_t c = 0;
-  for (uint32_t w = 0; w < (uint32_t)BM_WORDS; w++) {
-    uint32_t m = sh->bitmap[lane][w];
-    const uint32_t pc = popc32(m);
-    if (c + pc > k) {
-      for (;;) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m);
-        if (c == k) return w * 32u + b;
-        c++;
-        m &= m - 1u;
-      }
-    }
-    c += pc;
-  }
-  return 0xffffffffu;
-}
-
 // ---- global memory helpers -------------------------------------------------
 // aligned dword k of the stream's aligned base; bytes outside [lo, hi) are zero.
 HZ_HD uint32_t load_word(hz_gcu8* base, uint32_t k, uint32_t lo, uint32_t hi) {
@@ -438,7 +212,11 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
 }
 // inclusive prefix sum over the 64 lanes by DPP (no LDS round trip): shifts of 1, 2, 4, 8
 // lanes inside each row of 16, then each row's last lane broadcast to the rows after it
-// (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3)
+// (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).  row_bcast exists on
+// GFX9 (CDNA) only: the engine is built for gfx950 alone, and any other target stops here
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "wave_incl_scan_dpp: row_bcast DPP controls are GFX9 / CDNA only (build with --offload-arch=gfx950)"
+#endif
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
@@ -671,773 +449,3 @@ struct TableArgs {
     }                                                                                   \
     status_out = (sh).u_status;                                                         \
   } while (0)
-
-namespace hz {
-
-// Work description for one zlib stream.
-struct StreamJob {
-  const uint8_t* src;   // stream bytes (any alignment)
-  uint32_t src_len;
-  uint8_t* dst;         // output
-  uint32_t dst_len;     // expected size (exact) or capacity (exact == 0)
-  uint32_t exact;       // 1: output must be exactly dst_len bytes
-  uint32_t* out_len;    // optional: decoded length
-};
-
-// Tunables (runtime so that tests can sweep them)
-struct Tune {
-  uint32_t L0;     // initial segment bits
-  uint32_t W;      // warm-up bits
-  uint32_t adapt;  // 0: fixed L; 1: adapt L to the token density; n > 1: same, aiming at n/16 of SLOTS slots
-  uint32_t C;      // continuation budget (bits)
-  int max_rounds;  // repair rounds per window
-};
-
-// Statistics (emulator / diagnostics only)
-struct Stats {
-  uint64_t windows, lanes_valid, tokens, matches, match_bytes, lit_bytes, rounds, blocks, stored;
-  uint64_t steps_max, steps_sum, repairs, hops, maxhops;
-};
-
-}  // namespace hz
-
-// ===========================================================================
-// The stream decoder.  `sh` is the wave's LDS block.  Returns a status code
-// (uniform).  Written in SIMT style: code outside LANE_LOOP is uniform across the
-// wave and runs redundantly on every lane; LANE_LOOP bodies never break/continue
-// at their top level and never return.
-// ===========================================================================
-#define HZ_STAGE(sh, base_al, lo, hi, first_word, nwords)                          \
-  do {                                                                              \
-    WAVE_SYNC();                                                                    \
-    LANE_LOOP {                                                                     \
-      for (uint32_t _k = (uint32_t)lane; _k < (uint32_t)(nwords) + 4u; _k += 64)    \
-        (sh).in32[_k] = _k < (uint32_t)(nwords)                                     \
-                            ? hz::load_word((base_al), (first_word) + _k, (lo), (hi)) : 0u; \
-    }                                                                               \
-    (sh).u_stage_base = (first_word) * 32u;                                          \
-    WAVE_SYNC();                                                                    \
-  } while (0)
-
-namespace hz {
-
-template <class StatsT>
-#if HZ_GPU
-__device__
-#else
-static
-#endif
-int inflate_stream(Shared& sh, const StreamJob job, const Tune tune, StatsT* stats, HzProf* prof = nullptr) {
-  (void)prof;
-  // aligned base so that every staged dword load is aligned
-  const uint32_t a = (uint32_t)(((uintptr_t)job.src) & 3u);
-  hz_gcu8* base = HZ_GLOBAL(hz_gcu8*, job.src - a);
-  const uint32_t lo = a, hi = a + job.src_len;   // valid byte range of the stream
-  const uint32_t limit_bits = hi * 8u;
-  const uint32_t dst_len = job.dst_len;
-  hz_gu8* const dst = HZ_GLOBAL(hz_gu8*, job.dst);
-
-  LANE_VAR(uint32_t, s1);   // adler32 partial sums: S1 = sum b, S2 = sum pos*b (mod 65521)
-  LANE_VAR(uint32_t, s2);
-  LANE_LOOP { LV(s1) = 0; LV(s2) = 0; }
-
-  // ---- zlib header (RFC 1950) ----
-  if (job.src_len < 2) return ST_TRUNC;
-  HZ_STAGE(sh, base, lo, hi, 0u, 2u);
-  {
-    uint32_t hdr16 = (uint32_t)(peek64(&sh, lo * 8u) & 0xffffu);
-    uint32_t cmf = hdr16 & 0xff, flg = hdr16 >> 8;
-    if ((cmf & 0x0f) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0) return ST_DATA;
-    if (flg & 0x20) return ST_DATA;  // preset dictionary: Z_NEED_DICT
-  }
-  uint32_t pos = lo * 8u + 16u;
-  uint32_t out = 0;
-  uint32_t L = tune.L0 < (uint32_t)LMIN ? (uint32_t)LMIN : tune.L0 > (uint32_t)LMAX ? (uint32_t)LMAX : tune.L0;
-
-  for (;;) {  // ---- deflate blocks ----
-    HZ_T(1);
-    HZ_STAGE(sh, base, lo, hi, pos >> 5, 128u);
-    if (pos + 3u > limit_bits) return ST_TRUNC;
-    const uint32_t h3 = (uint32_t)(peek64(&sh, pos) & 7u);
-    pos += 3;
-    const uint32_t bfinal = h3 & 1u, btype = h3 >> 1;
-    if (stats) stats->blocks++;
-    if (btype == 3) return ST_DATA;
-    if (btype == 0) {
-      // ---- stored block ----
-      pos = (pos + 7u) & ~7u;
-      if (pos + 32u > limit_bits) return ST_TRUNC;
-      const uint32_t ln = (uint32_t)(peek64(&sh, pos) & 0xffffffffu);
-      const uint32_t len = ln & 0xffffu, nlen = ln >> 16;
-      if ((len ^ 0xffffu) != nlen) return ST_DATA;
-      pos += 32u;
-      if (pos + len * 8u > limit_bits) return ST_TRUNC;
-      if (out + len > dst_len) return ST_SIZE;
-      const uint32_t sb = pos >> 3;  // byte index relative to the aligned base
-      LANE_LOOP {
-        uint32_t a1 = LV(s1), a2 = LV(s2);
-        for (uint32_t i = (uint32_t)lane; i < len; i += 64) {
-          const uint32_t b = base[sb + i];
-          dst[out + i] = (uint8_t)b;
-          a1 += b;
-          a2 = (uint32_t)((a2 + (uint64_t)((out + i) % ADLER_MOD) * b) % ADLER_MOD);
-        }
-        LV(s1) = a1 % ADLER_MOD; LV(s2) = a2;
-      }
-      out += len;
-      pos += len * 8u;
-      if (stats) stats->stored++;
-      WAVE_SYNC_GLOBAL();
-      if (bfinal) break;
-      continue;
-    }
-    // ---- Huffman code lengths ----
-    HZ_T(2);
-    uint32_t nlen = 288, ndist = 32;
-    if (btype == 1) {
-      LANE_LOOP {
-        for (int s = lane; s < 320; s += 64)
-          sh.lens[s] = s >= 288 ? 5 : s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-      }
-      WAVE_SYNC();
-    } else {
-      // dynamic header (RFC 1951 3.2.7): lane 0 decodes it serially from the staged
-      // input with a register bit reader and a 7-bit code-length lookup table
-      LANE_LOOP {
-        if (lane == 0) {
-          int st = ST_OK;
-          BitRd r;
-          br_init(&sh, r, pos, sh.u_stage_base);
-          br_fill(&sh, r);
-          const uint32_t hlit = (uint32_t)(r.bb & 31u) + 257u, hdist = (uint32_t)((r.bb >> 5) & 31u) + 1u;
-          const uint32_t hclen = (uint32_t)((r.bb >> 10) & 15u) + 4u;
-          br_drop(r, 14);
-          if (hlit > 286 || hdist > 30) st = ST_DATA;
-          uint16_t* cl = sh.sorted_cl;               // code-length code lengths (19)
-          for (int i = 0; i < 19; i++) cl[i] = 0;
-          for (uint32_t i = 0; i < hclen; i++) {
-            br_fill(&sh, r);
-            cl[cl_order(i)] = (uint16_t)(r.bb & 7u);
-            br_drop(r, 3);
-          }
-          uint16_t* cnt = sh.cnt_cl;
-          for (int l = 0; l < 16; l++) cnt[l] = 0;
-          for (int i = 0; i < 19; i++) cnt[cl[i]]++;
-          cnt[0] = 0;
-          int left = 1, maxl = 0;
-          for (int l = 1; l <= 7; l++) {
-            left <<= 1; left -= cnt[l];
-            if (cnt[l]) maxl = l;
-            if (left < 0) st = ST_DATA;
-          }
-          if (left > 0 || maxl == 0) st = ST_DATA;  // code-length code must be complete
-          // 7-bit LUT (sym | len << 8) in the distance table's space (rebuilt below)
-          uint16_t* clut = sh.lut_d;
-          if (st == ST_OK) {
-            uint32_t next[8];
-            uint32_t code = 0;
-            for (int l = 1; l <= 7; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; next[l] = code; }
-            for (int i = 0; i < 19; i++) {
-              const uint32_t l = cl[i];
-              if (!l) continue;
-              const uint32_t rc = rev_bits(next[l]++, (int)l);
-              for (uint32_t k = rc; k < 128u; k += 1u << l) clut[k] = (uint16_t)(i | (l << 8));
-            }
-          }
-          const uint32_t total = hlit + hdist;
-          uint32_t n = 0;
-          const uint32_t stage_end = sh.u_stage_base + 128u * 32u;
-          while (st == ST_OK && n < total) {
-            if (r.pos + 64u > stage_end) { st = ST_DATA; break; }   // header longer than any valid one
-            br_fill(&sh, r);
-            const uint32_t e = clut[r.bb & 127u];
-            const uint32_t sym = e & 0xffu, l = e >> 8;
-            br_drop(r, l);
-            if (sym < 16) { sh.lens[n++] = (uint8_t)sym; continue; }
-            uint32_t rep, val = 0;
-            if (sym == 16) {
-              if (n == 0) { st = ST_DATA; break; }
-              val = sh.lens[n - 1]; rep = 3 + (uint32_t)(r.bb & 3u); br_drop(r, 2);
-            } else if (sym == 17) { rep = 3 + (uint32_t)(r.bb & 7u); br_drop(r, 3); }
-            else { rep = 11 + (uint32_t)(r.bb & 127u); br_drop(r, 7); }
-            if (n + rep > total) { st = ST_DATA; break; }
-            for (uint32_t k = 0; k < rep; k++) sh.lens[n++] = (uint8_t)val;
-          }
-          if (st == ST_OK && r.pos > limit_bits) st = ST_TRUNC;
-          if (st == ST_OK && sh.lens[256] == 0) st = ST_DATA;  // missing end-of-block code
-          if (st == ST_OK) {
-            for (int i = (int)hdist - 1; i >= 0; i--) sh.lens[288 + i] = sh.lens[hlit + i];
-            for (uint32_t i = hlit; i < 288; i++) sh.lens[i] = 0;
-            for (uint32_t i = 288 + hdist; i < 320; i++) sh.lens[i] = 0;
-          }
-#if !HZ_GPU && defined(HZ_DEBUG)
-          { unsigned long long hsh = 0; for (uint32_t i = 0; i < 320; i++) hsh = hsh * 31 + sh.lens[i];
-            printf("HDR pos=%u end=%u hlit=%u hdist=%u st=%d hash=%llu\n", pos, r.pos, hlit, hdist, st, hsh); }
-#endif
-          sh.u_status = st;
-          sh.u_pos = r.pos;
-          sh.u_nlen = hlit;
-          sh.u_ndist = hdist;
-        }
-      }
-      WAVE_SYNC();
-      const int hst = sh.u_status;
-      if (hst != ST_OK) return hst;
-      pos = sh.u_pos;
-      nlen = sh.u_nlen;
-      ndist = sh.u_ndist;
-    }
-    {
-      int bst = ST_OK;
-      TableArgs tll = {sh.lens, (int)nlen, sh.cnt_ll, sh.sorted_ll, sh.lut_ll, LL_ROOT, 1, LL_SUB};
-      HZ_T(3);
-      HZ_BUILD_TABLE(sh, tll, bst);
-      if (bst != ST_OK) return bst;
-      TableArgs td = {sh.lens + 288, (int)ndist, sh.cnt_d, sh.sorted_d, sh.lut_d, D_ROOT, 2, D_SUB};
-      HZ_BUILD_TABLE(sh, td, bst);
-      if (bst != ST_OK) return bst;
-    }
-
-    // ---- windows over the Huffman block ----
-    for (;;) {
-      if (stats) stats->windows++;
-      HZ_T(4);
-      const uint32_t win_start = pos;
-      // a continuation never runs past its successor's segment: phase B counts a
-      // lane's valid tokens from the point where its predecessor met its marks
-      const uint32_t W = tune.W, C = tune.C < L ? tune.C : L;
-      {
-        const uint32_t first_bit = win_start >= W ? win_start - W : 0u;
-        const uint32_t words = (64u * L + W + C + 256u) / 32u + 3u;
-        HZ_STAGE(sh, base, lo, hi, first_bit >> 5, words);
-      }
-
-      HZ_T(5);
-      // -------- Phase A: speculative decode of 64 segments --------
-      // lane i decodes from (segment start - W); tokens whose start lies inside its
-      // own segment [ss, ss+L) are stored and their start bits marked.
-      const uint32_t stage_base = ((win_start >= W ? win_start - W : 0u) >> 5) * 32u;
-      LANE_VAR(uint32_t, seg_start);
-      LANE_VAR(uint32_t, ntok);      // tokens stored
-      LANE_VAR(uint32_t, nslot);     // slots they use
-      LANE_VAR(uint64_t, mbits);     // bit k: token k is a match (two slots)
-      LANE_VAR(int, storing);
-      LANE_VAR(uint32_t, nsteps);
-      LANE_LOOP {
-        const uint32_t ss = win_start + (uint32_t)lane * L;
-        const uint32_t se = ss + L;
-        const uint32_t p0 = (lane > 0 && ss - win_start > W) ? ss - W : win_start;
-        int st = p0 >= ss;
-        uint32_t nt = 0, ns = 0, steps = 0;
-        uint64_t mb = 0;
-        for (int w = 0; w < BM_WORDS; w++) sh.bitmap[lane][w] = 0;
-        uint32_t mw_idx = 0, mw = 0;  // bitmap word cached in a register (monotonic positions)
-        BitRd r;
-        br_init(&sh, r, p0, stage_base);
-        while (r.pos < se) {
-          if (!st && r.pos >= ss) st = 1;
-          if (st && ns + 2u > (uint32_t)SLOTS) break;
-          const uint32_t tp = r.pos;
-          const uint32_t tokv = next_token(&sh, r);
-          steps++;
-          if (st) {
-            const uint32_t rel = tp - ss, wi = rel >> 5;
-            if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
-            mw |= 1u << (rel & 31u);
-            const uint32_t w = put_tok(&sh, lane, ns, tokv);
-            mb |= (uint64_t)(w - 1u) << nt;
-            ns += w;
-            nt++;
-          }
-        }
-        if (st) {
-          sh.bitmap[lane][mw_idx] |= mw;
-          mark_bit(&sh, lane, r.pos - ss);   // exit boundary (start of the next token)
-        }
-        LV(seg_start) = ss;
-        LV(ntok) = nt;
-        LV(nslot) = ns;
-        LV(mbits) = mb;
-        LV(storing) = st;
-        LV(nsteps) = steps;
-        sh.exitpos[lane] = r.pos;
-        sh.syncpos[lane] = 0xffffffffu;
-      }
-      WAVE_SYNC();
-
-      HZ_T(6);
-      // -------- Phase A': continuation --------
-      // lane i keeps decoding from its exit until it reaches a token start that
-      // lane i+1 marked (then both decodes coincide from there on), for at most C
-      // bits into segment i+1.  Tokens decoded here belong to lane i.
-      LANE_LOOP {
-        const uint32_t ss = LV(seg_start);
-        uint32_t nt = LV(ntok), ns = LV(nslot), steps = 0;
-        uint64_t mb = LV(mbits);
-        uint32_t pend = sh.exitpos[lane];
-        if (lane < 63 && LV(storing)) {
-          const uint32_t ssn = ss + L;
-          BitRd r;
-          br_init(&sh, r, pend, stage_base);
-          uint32_t nw_idx = 0xffffffffu, nw = 0;     // cached word of lane+1's bitmap
-          uint32_t mw_idx = (r.pos - ss) >> 5, mw = 0;
-          for (;;) {
-            const uint32_t reln = r.pos - ssn;
-            if (r.pos >= ssn && reln < (uint32_t)(BM_WORDS * 32)) {
-              if ((reln >> 5) != nw_idx) { nw_idx = reln >> 5; nw = sh.bitmap[lane + 1][nw_idx]; }
-              if ((nw >> (reln & 31u)) & 1u) { sh.syncpos[lane + 1] = r.pos; break; }
-            }
-            if (r.pos >= ssn + C || ns + 2u > (uint32_t)SLOTS) break;
-            const uint32_t rel = r.pos - ss, wi = rel >> 5;
-            const uint32_t tokv = next_token(&sh, r);
-            steps++;
-            if (wi != mw_idx) { sh.bitmap[lane][mw_idx] |= mw; mw = 0; mw_idx = wi; }
-            mw |= 1u << (rel & 31u);
-            const uint32_t w = put_tok(&sh, lane, ns, tokv);
-            mb |= (uint64_t)(w - 1u) << nt;
-            ns += w;
-            nt++;
-          }
-          if (mw_idx < (uint32_t)BM_WORDS) sh.bitmap[lane][mw_idx] |= mw;
-          pend = r.pos;
-          mark_bit(&sh, lane, pend - ss);     // final boundary of this lane's decode
-        }
-        LV(ntok) = nt;
-        LV(nslot) = ns;
-        LV(mbits) = mb;
-        LV(nsteps) += steps;
-        sh.contpos[lane] = pend;
-      }
-      WAVE_SYNC();
-      HZ_T(7);
-      // -------- repair rounds --------
-      // A lane whose predecessor's continuation never met one of its marks is
-      // "failed": its speculative path had not merged with the true path.  It
-      // re-decodes its segment from the predecessor's final position (a true token
-      // boundary once the predecessor is valid) and continues into its successor.
-      LANE_VAR(int, failed);
-      LANE_LOOP {
-        LV(failed) = lane > 0 && sh.syncpos[lane] == 0xffffffffu;
-        sh.flag[lane] = (uint32_t)LV(failed);
-      }
-      WAVE_SYNC();
-#if !HZ_GPU
-      uint32_t rsteps[64] = {0};
-#endif
-      for (int round = 0; round < tune.max_rounds; round++) {
-        const uint64_t fm = WAVE_BALLOT(LV(failed));
-        if (!fm) break;
-        if (stats) stats->repairs++;
-        LANE_LOOP {
-          const int redo = LV(failed) && !sh.flag[lane - 1 < 0 ? 0 : lane - 1] &&
-                           sh.contpos[lane - 1 < 0 ? 0 : lane - 1] >= LV(seg_start);
-          const int next_failed = lane < 63 ? (int)sh.flag[lane + 1] : 1;
-          uint32_t steps = 0;
-          if (redo) {
-            // re-decode from the predecessor's true exit; as soon as the true path
-            // lands on a token start of this lane's own speculative path, the rest
-            // of that path (tokens, continuation, successor sync) is already right:
-            // splice it in instead of decoding it again
-            const uint32_t ss = LV(seg_start), se = ss + L;
-            const uint32_t old_nt = LV(ntok), old_ns = LV(nslot);
-            const uint64_t old_mb = LV(mbits);
-            const uint32_t start = sh.contpos[lane - 1];
-            const uint32_t old_sync_next = lane < 63 ? sh.syncpos[lane + 1] : 0xffffffffu;
-            if (lane < 63 && !next_failed) sh.syncpos[lane + 1] = 0xffffffffu;
-            uint32_t cw = (start - ss) >> 5;          // bitmap word being rewritten
-            uint32_t oldc = 0;                        // old marks below word cw
-            for (uint32_t w = 0; w < cw && w < (uint32_t)BM_WORDS; w++) {
-              oldc += popc32(sh.bitmap[lane][w]);
-              sh.bitmap[lane][w] = 0;
-            }
-            uint32_t ow = cw < (uint32_t)BM_WORDS ? sh.bitmap[lane][cw] : 0u;   // its old marks
-            uint32_t mw = 0;                          // its new marks
-            uint32_t nt = 0, ns = 0;
-            uint64_t mb = 0;
-            int merged = 0, nomerge = 0;
-            BitRd r;
-            br_init(&sh, r, start, stage_base);
-            uint32_t nw_idx = 0xffffffffu, nw = 0;
-            for (;;) {
-              const uint32_t rel = r.pos - ss, wi = rel >> 5;
-              if (wi != cw) {
-                oldc += popc32(ow);
-                if (cw < (uint32_t)BM_WORDS) sh.bitmap[lane][cw] = mw;
-                for (uint32_t w = cw + 1; w < wi && w < (uint32_t)BM_WORDS; w++) {
-                  oldc += popc32(sh.bitmap[lane][w]);
-                  sh.bitmap[lane][w] = 0;
-                }
-                cw = wi; mw = 0;
-                ow = wi < (uint32_t)BM_WORDS ? sh.bitmap[lane][wi] : 0u;
-              }
-              const uint32_t jcur = oldc + popc32(ow & bmask(rel & 31u));   // old tokens before here
-              const uint32_t scur = jcur <= old_nt ? tok_slot(old_mb, jcur) : old_ns;   // their slots
-              if (((ow >> (rel & 31u)) & 1u) && !nomerge && jcur <= old_nt) {
-                // ns <= scur: new tokens only ever overwrote old slots below scur
-                sh.bitmap[lane][cw] = mw | (ow & ~bmask(rel & 31u));
-                if (ns < scur) {
-                  for (uint32_t t = scur; t < old_ns; t++) sh.tok[tok_idx(ns + t - scur, lane)] = sh.tok[tok_idx(t, lane)];
-                }
-                mb |= (old_mb >> jcur) << nt;
-                ns += old_ns - scur;
-                nt += old_nt - jcur;
-                merged = 1;
-                break;
-              }
-              if (r.pos >= se) {                      // continuation into the successor
-                if (lane == 63 || next_failed) break;
-                const uint32_t reln = r.pos - se;
-                if (reln < (uint32_t)(BM_WORDS * 32)) {
-                  if ((reln >> 5) != nw_idx) { nw_idx = reln >> 5; nw = sh.bitmap[lane + 1][nw_idx]; }
-                  if ((nw >> (reln & 31u)) & 1u) { sh.syncpos[lane + 1] = r.pos; break; }
-                }
-                if (r.pos >= se + C) break;
-              }
-              if (ns + 2u > (uint32_t)SLOTS) break;
-              const uint32_t tokv = next_token(&sh, r);
-              steps++;
-              mw |= 1u << (rel & 31u);
-              const uint32_t w = (tokv & T_MATCH) ? 2u : 1u;
-              if (ns + w > scur) nomerge = 1;         // would overwrite a possibly needed old slot
-              put_tok(&sh, lane, ns, tokv);
-              mb |= (uint64_t)(w - 1u) << nt;
-              ns += w;
-              nt++;
-            }
-#if !HZ_GPU && defined(HZ_DEBUG)
-            if (!merged) printf("NOMERGE lane=%d L=%u start=%u end=%u old_nt=%u nt=%u nomerge=%d next_failed=%d oldc=%u se=%u\n", lane, L, start - ss, r.pos - ss, old_nt, nt, nomerge, next_failed, oldc, se - ss);
-#endif
-            if (merged) {
-              if (lane < 63) sh.syncpos[lane + 1] = old_sync_next;   // the old continuation stands
-            } else {
-              // final boundary mark; old marks at or after it are stale
-              const uint32_t rel = r.pos - ss;
-              if (cw < (uint32_t)BM_WORDS) sh.bitmap[lane][cw] = mw;
-              for (uint32_t w = cw + 1; w < (uint32_t)BM_WORDS; w++) sh.bitmap[lane][w] = 0;
-              mark_bit(&sh, lane, rel);
-              sh.contpos[lane] = r.pos;
-            }
-            sh.syncpos[lane] = start;                 // whole token list is valid
-            LV(ntok) = nt;
-            LV(nslot) = ns;
-            LV(mbits) = mb;
-            if (stats) { stats->matches++; stats->match_bytes += (uint64_t)merged; }
-          }
-          LV(nsteps) += steps;
-#if !HZ_GPU
-          rsteps[lane] = steps;
-#endif
-          sh.flag2[lane] = (uint32_t)redo;
-        }
-        WAVE_SYNC();
-#if !HZ_GPU
-        if (stats) { uint32_t mx = 0; for (int l = 0; l < 64; l++) mx = rsteps[l] > mx ? rsteps[l] : mx; stats->lit_bytes += mx; }
-#endif
-        LANE_LOOP {
-          if (sh.flag2[lane]) LV(failed) = 0;
-          else if (lane > 0 && sh.flag2[lane - 1] && sh.syncpos[lane] == 0xffffffffu) LV(failed) = 1;
-        }
-        WAVE_SYNC();
-        LANE_LOOP { sh.flag[lane] = (uint32_t)LV(failed); }
-        WAVE_SYNC();
-      }
-      if (stats) {
-#if !HZ_GPU
-        uint32_t mx = 0; uint64_t sm = 0;
-        for (int lane = 0; lane < 64; lane++) { mx = nsteps[lane] > mx ? nsteps[lane] : mx; sm += nsteps[lane]; }
-        stats->steps_max += mx; stats->steps_sum += sm;
-#endif
-      }
-
-      HZ_T(8);
-      // -------- Phase B: validity --------
-      LANE_VAR(uint32_t, tok_first);
-      LANE_VAR(uint32_t, tok_end);
-      LANE_VAR(int, endk);       // 0 none, 1 EOB, 2 ERR inside the valid range
-      LANE_LOOP {
-        uint32_t tf = 0;
-        int ok = lane == 0;
-        if (lane > 0 && sh.syncpos[lane] != 0xffffffffu && !LV(failed)) {
-          ok = 1;
-          const uint32_t sp = sh.syncpos[lane];
-          const uint32_t rel = sp >= LV(seg_start) ? sp - LV(seg_start) : 0u;
-          uint32_t c = 0;
-          for (uint32_t w = 0; w < (rel >> 5); w++) c += popc32(sh.bitmap[lane][w]);
-          c += popc32(sh.bitmap[lane][rel >> 5] & bmask(rel & 31u));
-          tf = c;
-        }
-        uint32_t te = LV(ntok);
-        int ek = 0;
-        if (ok) {
-          uint32_t sl = tok_slot(LV(mbits), tf);
-          for (uint32_t t = tf; t < te; t++) {
-            const uint32_t v = tok_at(&sh, sl, lane);
-            if (v == S_EOB || v == S_ERR) { ek = v == S_EOB ? 1 : 2; te = t; break; }
-            sl += (v & S_MATCH) ? 2u : 1u;
-          }
-        }
-        LV(tok_first) = ok ? tf : 0xffffffffu;
-        LV(tok_end) = te;
-        LV(endk) = ek;
-      }
-      const uint64_t smask = WAVE_BALLOT(LV(tok_first) != 0xffffffffu);
-      uint32_t V = 0;
-      while (V < 64u && ((smask >> V) & 1ull)) V++;
-      const uint64_t emask = WAVE_BALLOT(LV(endk) != 0) & (V >= 64 ? ~0ull : ((1ull << V) - 1ull));
-      int end_lane = -1;
-      for (uint32_t k = 0; k < V; k++) if ((emask >> k) & 1ull) { end_lane = (int)k; break; }
-      if (end_lane >= 0) V = (uint32_t)end_lane + 1u;
-      if (stats) stats->lanes_valid += V;
-
-      HZ_T(9);
-      // -------- Phase C: emit --------
-      LANE_VAR(uint32_t, tcur);
-      LANE_VAR(uint32_t, tend);
-      LANE_VAR(uint32_t, olen);
-      LANE_LOOP {
-        uint32_t tf = LV(tok_first), te = LV(tok_end), ol = 0;
-        if ((uint32_t)lane >= V) { tf = 0; te = 0; }
-        if (lane == end_lane) {
-          sh.u_status = LV(endk);
-          // bit position after the EOB token = the mark following token te
-          sh.u_pos = nth_mark(&sh, lane, te + 1u) + LV(seg_start);
-        }
-        const uint32_t sf = tok_slot(LV(mbits), tf);
-        uint32_t sl = sf;
-        for (uint32_t t = tf; t < te; t++) {
-          const uint32_t v = tok_at(&sh, sl, lane);
-          const uint32_t m = v & S_MATCH;
-          ol += m ? (v & 0xffu) + 3u : 1u;
-          sl += m ? 2u : 1u;
-        }
-        LV(tcur) = sf; LV(tend) = sl; LV(olen) = ol;
-      }
-      WAVE_SYNC();
-      if (end_lane >= 0 && sh.u_status == 2) {
-        return sh.u_pos + 64u > limit_bits ? ST_TRUNC : ST_DATA;
-      }
-      HZ_T(10);
-      // output offsets; the window keeps only what fits the LDS reference map
-      LANE_VAR(uint32_t, obase);
-#if HZ_GPU
-      obase = wave_excl_scan(olen, HZ_LANE_ID());
-#else
-      { uint32_t acc = 0; for (int lane = 0; lane < 64; lane++) { obase[lane] = acc; acc += olen[lane]; } }
-#endif
-      uint32_t npos;
-      {
-        const uint64_t over = WAVE_BALLOT((uint32_t)lane < V && LV(obase) + LV(olen) > (uint32_t)SCAP);
-        uint32_t k = 0;
-        while (k < V && !((over >> k) & 1ull)) k++;
-        if (k < V) {
-          if (k == 0) {
-            // lane 0 alone overflows: keep its first tokens that fit (>= 1 token)
-            LANE_LOOP {
-              if (lane == 0) {
-                uint32_t sl = LV(tcur), t = 0, acc = 0;     // lane 0's tokens start at token 0
-                while (sl < LV(tend)) {
-                  const uint32_t v = tok_at(&sh, sl, lane);
-                  const uint32_t m = v & S_MATCH;
-                  const uint32_t n = m ? (v & 0xffu) + 3u : 1u;
-                  if (acc + n > (uint32_t)SCAP) break;
-                  acc += n; sl += m ? 2u : 1u; t++;
-                }
-                LV(tend) = sl; LV(olen) = acc;
-                sh.u_pos = win_start + nth_mark(&sh, lane, t);
-              }
-            }
-            WAVE_SYNC();
-            npos = sh.u_pos;
-            V = 1;
-          } else {
-            V = k;
-            npos = sh.contpos[k - 1];
-          }
-          end_lane = -1;                 // an EOB beyond the cut is met again next window
-          LANE_LOOP { if ((uint32_t)lane >= V) { LV(tcur) = 0; LV(tend) = 0; LV(olen) = 0; } }
-        } else {
-          npos = end_lane >= 0 ? sh.u_pos : sh.contpos[V - 1];
-        }
-      }
-      uint32_t wtotal = 0, ntok_valid = 0;
-#if HZ_GPU
-      wtotal = wave_sum(olen);
-      ntok_valid = wave_sum(tend - tcur);
-#else
-      for (int lane = 0; lane < 64; lane++) { wtotal += olen[lane]; ntok_valid += tend[lane] - tcur[lane]; }
-#endif
-      if (stats) stats->tokens += ntok_valid;
-      if (out + wtotal > dst_len) return ST_SIZE;
-      if (npos > limit_bits) return ST_TRUNC;
-
-      // ---- byte-level source map in LDS ----
-      // ref[r] for window byte r: 0x4000|b literal, r' < 0x4000 internal reference,
-      // 0x8000|(x-1) the byte x positions before the window (final in dst).
-      const uint32_t wbeg = out;
-      // publish per-lane token ranges so that any lane can walk any lane's tokens
-      LANE_LOOP {
-        sh.obase[lane] = LV(obase);
-        sh.tcur_l[lane] = (uint16_t)LV(tcur);
-        sh.tend_l[lane] = (uint16_t)LV(tend);
-        if (lane == 63) sh.obase[64] = wtotal;
-      }
-      WAVE_SYNC();
-      LANE_VAR(int, lerr);
-      LANE_LOOP {
-        // lane w produces the references of output bytes [w*B, (w+1)*B): balanced
-        // whatever the token / output distribution across the owning lanes
-        int err = 0;
-        const uint32_t B = (wtotal + 63u) >> 6;
-        const uint32_t x0 = (uint32_t)lane * B;
-        const uint32_t x1 = x0 + B < wtotal ? x0 + B : wtotal;
-        if (x0 < x1) {
-          int lo_j = 0, hi_j = 63;                 // owner: largest j with obase[j] <= x0
-          while (lo_j < hi_j) {
-            const int mid = (lo_j + hi_j + 1) >> 1;
-            if (sh.obase[mid] <= x0) lo_j = mid; else hi_j = mid - 1;
-          }
-          int j = lo_j;
-          uint32_t t = sh.tcur_l[j], q = sh.obase[j];     // t: slot of lane j
-          uint32_t v, d;
-          tok_pair(&sh, t, j, v, d);
-          uint32_t m = v & S_MATCH;
-          uint32_t n = m ? (v & 0xffu) + 3u : 1u;
-          while (q + n <= x0) {                    // token of lane j containing x0
-            q += n; t += m ? 2u : 1u;
-            tok_pair(&sh, t, j, v, d);
-            m = v & S_MATCH;
-            n = m ? (v & 0xffu) + 3u : 1u;
-          }
-          d = m ? d : 1u;
-          uint32_t jj = m ? (x0 - q) % d : 0u;
-          int32_t base = (int32_t)q - (int32_t)d;
-          uint32_t tend_j = sh.tend_l[j];
-          if (m && d > wbeg + q) err = 1;
-          for (uint32_t x = x0; x < x1 && !err; x++) {
-            if (x == q + n) {                      // next token (possibly of the next lane)
-              q = x; t += m ? 2u : 1u;
-              while (t >= tend_j) { j++; t = sh.tcur_l[j]; tend_j = sh.tend_l[j]; }
-              tok_pair(&sh, t, j, v, d);
-              m = v & S_MATCH;
-              n = m ? (v & 0xffu) + 3u : 1u;
-              d = m ? d : 1u;
-              base = (int32_t)q - (int32_t)d;
-              jj = 0;
-              if (m && d > wbeg + q) { err = 1; break; }
-            }
-            const int32_t srcq = base + (int32_t)jj;
-            const uint32_t rv = !m ? (0x4000u | v)
-                              : srcq >= 0 ? (uint32_t)srcq : (0x8000u | (uint32_t)(-srcq - 1));
-            sh.ref[x] = (uint16_t)rv;
-            jj++;
-            jj = jj == d ? 0u : jj;
-          }
-        }
-        LV(lerr) = err;
-      }
-      WAVE_SYNC();
-      if (WAVE_BALLOT(LV(lerr))) return ST_DATA;
-      if (stats) stats->rounds++;
-      HZ_T(11);
-      // chase: references strictly decrease, so every chain ends in a literal or an
-      // external byte; resolved values are written back (benign races: every stored
-      // value is a valid ancestor of the position)
-      LANE_LOOP {
-        for (uint32_t r = (uint32_t)lane; r < wtotal; r += 64) {
-          uint32_t v = sh.ref[r];
-          uint32_t hops = 0;
-          while (v < 0x4000u) { v = sh.ref[v]; hops++; }
-          sh.ref[r] = (uint16_t)v;
-          if (stats) { stats->hops += hops; if (hops > stats->maxhops) stats->maxhops = hops; }
-        }
-      }
-      WAVE_SYNC();
-      // external bytes: gather from dst, 8 independent loads in flight per lane
-      LANE_LOOP {
-        for (uint32_t r0 = (uint32_t)lane; r0 < wtotal; r0 += 64u * 8u) {
-          uint32_t v[8], b[8];
-HZ_UNROLL
-          for (int k = 0; k < 8; k++) {
-            const uint32_t r = r0 + 64u * (uint32_t)k;
-            v[k] = r < wtotal ? sh.ref[r] : 0x4000u;
-          }
-HZ_UNROLL
-          for (int k = 0; k < 8; k++) b[k] = (v[k] & 0x8000u) ? (uint32_t)dst[wbeg - (v[k] & 0x7fffu) - 1u] : v[k];
-HZ_UNROLL
-          for (int k = 0; k < 8; k++) {
-            const uint32_t r = r0 + 64u * (uint32_t)k;
-            if (r < wtotal && (v[k] & 0x8000u)) sh.ref[r] = (uint16_t)b[k];
-          }
-        }
-      }
-      WAVE_SYNC();
-      HZ_T(12);
-      // flush: 4-byte stores (byte stores at the unaligned head / tail) + adler sums
-      LANE_LOOP {
-        uint32_t b1 = 0, b2 = 0;                  // sum b, sum r*b over this lane's bytes
-        const uint32_t head = (uint32_t)((4u - (((uintptr_t)(dst + wbeg)) & 3u)) & 3u);
-        const uint32_t h = head < wtotal ? head : wtotal;
-        if ((uint32_t)lane < h) {
-          const uint32_t bv = sh.ref[lane] & 0xffu;
-          dst[wbeg + lane] = (uint8_t)bv;
-          b1 += bv; b2 += (uint32_t)lane * bv;
-        }
-        for (uint32_t r = h + 4u * (uint32_t)lane; r < wtotal; r += 256u) {
-          const uint32_t n = wtotal - r < 4u ? wtotal - r : 4u;
-          uint32_t w = 0;
-          for (uint32_t k = 0; k < n; k++) {
-            const uint32_t bv = sh.ref[r + k] & 0xffu;
-            w |= bv << (8u * k);
-            b1 += bv; b2 += (r + k) * bv;
-          }
-          if (n == 4u) *(hz_gu32*)(dst + wbeg + r) = w;
-          else for (uint32_t k = 0; k < n; k++) dst[wbeg + r + k] = (uint8_t)(w >> (8u * k));
-        }
-        LV(s1) = (LV(s1) + b1) % ADLER_MOD;
-        LV(s2) = (uint32_t)((LV(s2) + (uint64_t)(wbeg % ADLER_MOD) * b1 + b2) % ADLER_MOD);
-      }
-      WAVE_SYNC_GLOBAL();
-      if (stats) stats->lit_bytes += 0;
-      HZ_T(14);
-      out += wtotal;
-      pos = npos;
-      if (end_lane >= 0) break;        // EOB: the next block header follows
-      // next segment length: about half of SLOTS token slots per segment (room for the
-      // continuation) and an expected window output of about 3/4 of the LDS map
-      if (tune.adapt) {
-        const uint32_t used = npos - win_start;
-        const uint32_t bpt16 = ntok_valid ? (used * 16u) / ntok_valid : 16u * 8u;   // bits/token x16
-        const uint32_t fill16 = tune.adapt > 1u ? tune.adapt : ADAPT_FILL16;   // of SLOTS, /16
-        uint32_t target = (bpt16 * (uint32_t)SLOTS * fill16) / (16u * 16u);   // bpt16: bits per slot
-        if (wtotal && used) {
-          const uint64_t lim = ((uint64_t)SCAP * HZ_SCAP_FILL8 / 8u) * used / ((uint64_t)wtotal * 64u);
-          if (lim < target) target = (uint32_t)lim;
-        }
-        L = target < (uint32_t)LMIN ? (uint32_t)LMIN : target > (uint32_t)LMAX ? (uint32_t)LMAX : target;
-      }
-    }
-    if (bfinal) break;
-  }
-  // ---- trailer: adler32 (big-endian) after byte alignment ----
-  HZ_T(15);
-  pos = (pos + 7u) & ~7u;
-  if (pos + 32u > limit_bits) return ST_TRUNC;
-  HZ_STAGE(sh, base, lo, hi, pos >> 5, 4u);
-  const uint32_t t32 = (uint32_t)(peek64(&sh, pos) & 0xffffffffu);
-  const uint32_t want = (t32 >> 24) | ((t32 >> 8) & 0xff00u) | ((t32 << 8) & 0xff0000u) | (t32 << 24);
-  uint64_t S1 = 0, S2 = 0;
-#if HZ_GPU
-  S1 = wave_sum64((uint64_t)s1);
-  S2 = wave_sum64((uint64_t)s2);
-#else
-  for (int lane = 0; lane < 64; lane++) { S1 += s1[lane]; S2 += s2[lane]; }
-#endif
-  const uint32_t A = (uint32_t)((1u + S1) % ADLER_MOD);
-  const uint32_t B = (uint32_t)(((uint64_t)(out % ADLER_MOD) * A + ADLER_MOD - (S2 % ADLER_MOD)) % ADLER_MOD);
-  if (((B << 16) | A) != want) return ST_DATA;
-  if (job.exact && out != dst_len) return ST_SIZE;
-  if (job.out_len) *job.out_len = out;
-  return ST_OK;
-}
-
-}  // namespace hz

@@ -104,7 +104,18 @@ HZ_HD void build_norm(CTab& t, const int16_t* norm, uint32_t n, uint32_t log) {
       total += (uint32_t)c;
     }
   }
+  // codes outside the distribution (s >= n) are absent, as a zero count is
+  for (uint32_t s = n; s < MAXSYM; s++) {
+    t.dnb[s] = (int32_t)(((log + 1u) << 16) - size);
+    t.dfs[s] = 0;
+  }
   t.log = log;
+}
+
+// a code with no state in table t (normalized count 0): encoding it would corrupt the
+// sequences, so a block that needs one is written as a Raw_Block instead (encode_segment)
+HZ_HD bool absent(const CTab& t, uint32_t s) {
+  return s >= MAXSYM || t.dnb[s] == (int32_t)(((t.log + 1u) << 16) - (1u << t.log));
 }
 
 // which: 0 LL (36 codes, log 6), 1 OF (29, log 5), 2 ML (53, log 6): the predefined tables
@@ -363,7 +374,8 @@ HZ_HD void frame_table(Tabs& T, CTab& t, const uint32_t* cnt, uint32_t n, uint32
   build_norm(t, norm, maxs + 1u, log);
   uint8_t d[80];
   const uint32_t k = write_ncount(d, norm, maxs + 1u, log);
-  for (uint32_t i = 0; i < k && T.dsize < DESC_MAX; i++) T.desc[T.dsize++] = d[i];
+  if (T.dsize + k > DESC_MAX) { build(t, which); return; }   // (no room: the predefined table)
+  for (uint32_t i = 0; i < k; i++) T.desc[T.dsize++] = d[i];
   T.mode |= 2u << (which == 0 ? 6u : which == 1 ? 4u : 2u);
 }
 
@@ -607,6 +619,64 @@ HZ_HD void walk_sequences(hz_gcu32* gw, const hd::SegParse* sp, F&& emit) {
   if (have) emit(run, pml, poff);
 }
 
+// zstd_count_kernel's share of parse lane l in a segment's counts (the kernel's per-lane
+// algorithm; count_segment_lanes below runs it lane by lane on the CPU): the lane walks its
+// own token slots forward and adds (code index into SeqCounts: LL 0-35, OF 36-67, ML 68-120)
+// the offset and match-length codes of its matches and the literal-length codes of all but
+// its first match, whose literal run may begin in earlier lanes (first_run, after the scans)
+struct LaneCount {
+  uint32_t lits;     // literals in the lane's range
+  uint32_t run;      // literals after its last match
+  uint32_t lead;     // literals before its first match
+  uint32_t hm;       // it has a match
+};
+template <class Add>
+HZ_HD LaneCount lane_count(const CodeTabs& ct, hz_gcu32* gw, uint32_t ns, uint32_t l, Add&& add) {
+  LaneCount r = {0u, 0u, 0u, 0u};
+  uint32_t want_dist = 0, ml = 0;
+  slots_fwd(gw, ns, l, [&](uint32_t v) {
+    if (want_dist) {                               // (len | 0x8000, dist - 1): a match
+      const Seq q = make_seq_t(ct, r.run, ml, v + 1u);
+      if (r.hm) add(q.llc);
+      else r.lead = r.run;
+      add(36u + q.ofc);
+      add(68u + q.mlc);
+      r.hm = 1;
+      r.run = 0;
+      want_dist = 0;
+    } else if (v & 0x8000u) {
+      ml = (v & 0x7fffu) + 3u;
+      want_dist = 1;
+    } else {
+      r.run++;
+      r.lits++;
+    }
+  });
+  return r;
+}
+// literal ordinal after the lane's last match (0: no match); L = literals before the lane
+HZ_HD uint32_t lane_q(uint32_t L, const LaneCount& r) { return r.hm ? L + r.lits - r.run : 0u; }
+// the literal run of the lane's first match: qprev = max lane_q over the earlier lanes
+HZ_HD uint32_t first_run(uint32_t L, const LaneCount& r, uint32_t qprev) { return L + r.lead - qprev; }
+
+#if !HZ_GPU
+// zstd_count_kernel's algorithm for one segment on the CPU: lane_count for every parse lane,
+// the kernel's add scan (L) and exclusive max scan (qprev) done serially
+inline void count_segment_lanes(const CodeTabs& ct, const uint16_t* tok, const hd::SegParse* sp, SeqCounts& c) {
+  hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
+  uint32_t* const cw = (uint32_t*)&c;
+  LaneCount lc[hd::WAVE];
+  for (uint32_t l = 0; l < (uint32_t)hd::WAVE; l++) lc[l] = lane_count(ct, gw, sp->nslot[l], l, [&](uint32_t k) { cw[k]++; });
+  uint32_t L = 0, qmax = 0;
+  for (uint32_t l = 0; l < (uint32_t)hd::WAVE; l++) {
+    if (lc[l].hm) cw[make_seq_t(ct, first_run(L, lc[l], qmax), 3u, 1u).llc]++;
+    const uint32_t q = lane_q(L, lc[l]);
+    qmax = q > qmax ? q : qmax;
+    L += lc[l].lits;
+  }
+}
+#endif
+
 // adds a segment's sequence codes to c (the frame's counts)
 HZ_HD void count_segment(const CodeTabs& ct, const uint16_t* tok, const hd::SegParse* sp, SeqCounts& c) {
   hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
@@ -682,9 +752,10 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const CodeTabs& ct, const uint16_t*
     BitD w;
     bd_init(w, out, p, cap, over);
     uint32_t sll = 0, sof = 0, sml = 0;
-    uint32_t first = 1;
+    uint32_t first = 1, bad = 0;
     auto emit = [&](uint32_t ll, uint32_t ml, uint32_t off) {
       const Seq q = make_seq_t(ct, ll, ml, off);
+      bad |= (absent(T.ll, q.llc) || absent(T.of, q.ofc) || absent(T.ml, q.mlc)) ? 1u : 0u;
       if (first) {
         sml = fse_init(T.ml, q.mlc);
         sof = fse_init(T.of, q.ofc);
@@ -705,7 +776,7 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const CodeTabs& ct, const uint16_t*
     bw_add(w, sll, T.ll.log);
     bw_add(w, 1u, 1u);                               // end mark
     p = bd_finish(w);
-    over = w.over;
+    over = w.over || bad;
   }
   const uint32_t csize = p - 3u;
   if (over || csize >= seglen) {

@@ -677,12 +677,14 @@ class ChunkReader:
         def finish():
             """after the stream has drained: decode failures become 500s (and leave the
             cache), the batch's slots are unpinned"""
-            if st_host is not None:
-                st = st_host.numpy()
-                for k, (ri, _, _, _) in enumerate(dec):
-                    if st[k] != nat.OK:
-                        results[ri] = HTTPInternalServerError()
-            unpin_all()
+            try:
+                if st_host is not None:
+                    st = st_host.numpy()
+                    for k, (ri, _, _, _) in enumerate(dec):
+                        if st[k] != nat.OK:
+                            results[ri] = HTTPInternalServerError()
+            finally:
+                unpin_all()           # (pinned slots are never evicted: release them whatever happens)
             for ri in need:
                 if isinstance(results[ri], HTTPInternalServerError) and self.cache is not None \
                         and reads[ri].chunk_id in self.cache:
@@ -923,14 +925,15 @@ class ChunkStore:
             elif r.chunk_id not in seen:
                 seen.add(r.chunk_id)
                 todo.append(r)
-        rfin, init = None, []
+        rfin, init, init_pinned = None, [], False
         try:
             if todo:
                 res, rfin = self.reader.read(todo, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
                                              layout_class=layout_class, hyper_dims=hyper_dims, defer=True)
                 init = [r.chunk_id for r, v in zip(todo, res) if isinstance(v, HTTPNotFound) and chunk_init]
                 if init:
-                    self._fill_new(init, dtype, chunk_dims, fill_value)
+                    self._fill_new(init, dtype, chunk_dims, fill_value)   # (unpins its own keys when it fails)
+                    init_pinned = True
                 for r, v in zip(todo, res):
                     if isinstance(v, HTTPNotFound) and chunk_init:
                         v = self.cache[r.chunk_id]
@@ -940,7 +943,7 @@ class ChunkStore:
         except BaseException:
             if rfin is not None:
                 rfin.abort()
-            for key in hits:
+            for key in (init if init_pinned else []) + hits:
                 self.cache.unpin(key)
             raise
         released = [False]

@@ -168,3 +168,29 @@ extern "C" int64_t emu_zstd_frame_t(const uint8_t* src, uint32_t n, uint8_t* dst
 extern "C" int emu_parse_shared_bytes() { return (int)sizeof(hd::ParseShared); }
 extern "C" int emu_huff_shared_bytes() { return (int)sizeof(hd::HuffShared); }
 extern "C" int emu_emit_shared_bytes() { return (int)sizeof(hd::EmitShared); }
+
+// the sequence-code counts of a zstd frame's segments two ways: count_segment (the serial
+// backward sequence walk encode_segment uses) into c_walk, and zstd_count_kernel's per-lane
+// algorithm (count_segment_lanes) into c_lanes; 121 u32 each.  Returns the segment count.
+extern "C" int emu_zstd_counts(const uint8_t* src, uint32_t n, int level, uint32_t* c_walk, uint32_t* c_lanes) {
+  const uint32_t nseg = hd::nsegments(n);
+  std::vector<hd::SegParse> sp(nseg);
+  std::vector<uint16_t> tok((size_t)nseg * hd::SEG_TOK);
+  hd::ParseShared* ps = (hd::ParseShared*)calloc(1, sizeof(hd::ParseShared));
+  std::vector<uint16_t> fr(hd::FARW, 0);
+  hd::EncJob job = {src, n, level, 1u, 0u, 0u};
+  hd::parse_stream(*ps, job, hd::tune_for_level(level), sp.data(), tok.data(), nullptr, fr.data());
+  free(ps);
+  hze::CodeTabs ct;
+  hze::code_tabs_fill(ct, 0u, 1u);
+  hze::SeqCounts a, b;
+  memset(&a, 0, sizeof(a));
+  memset(&b, 0, sizeof(b));
+  for (uint32_t s = 0; s < nseg; s++) {
+    hze::count_segment(ct, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], a);
+    hze::count_segment_lanes(ct, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], b);
+  }
+  memcpy(c_walk, &a, sizeof(a));
+  memcpy(c_lanes, &b, sizeof(b));
+  return (int)nseg;
+}

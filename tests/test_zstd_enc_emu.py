@@ -144,3 +144,37 @@ def test_blosc_zstd_geometry_against_libblosc():
                 assert flags & 0x10 and flags >> 5 == 4, (nbytes, level, ts, flags)
                 n += 1
     assert n == 5 * 70 + 2 * 20
+
+
+def _long_literal_runs(r):
+    # random stretches (literals that run across many parse lanes) between short repeats
+    parts = []
+    for _ in range(12):
+        parts.append(r.integers(0, 256, int(r.integers(2000, 9000)), dtype=np.uint8))
+        parts.append(np.tile(np.frombuffer(b"0123456789", np.uint8), int(r.integers(1, 30))))
+    return np.concatenate(parts)
+
+
+@pytest.mark.parametrize("name", sorted(CASES) + ["long_literal_runs", "sparse_matches"])
+@pytest.mark.parametrize("level", [1, 5])
+def test_count_kernel_lane_algorithm_matches_sequence_walk(name, level):
+    """zstd_count_kernel builds each frame's FSE tables from a per-lane count (the
+    first match's literal run from an add scan and a max scan over the lanes), while
+    encode_segment emits codes from a serial backward walk.  The kernel's per-lane algorithm
+    (hze::lane_count + first_run, run lane by lane) must count exactly what the walk emits."""
+    L = ctypes.CDLL(LIB)
+    L.emu_zstd_counts.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    r = np.random.default_rng(11)
+    if name == "long_literal_runs":
+        a = _long_literal_runs(r)
+    elif name == "sparse_matches":
+        a = r.integers(0, 256, 200000, dtype=np.uint8)
+        for k in range(0, a.size - 64, 9000):
+            a[k + 32:k + 40] = a[k:k + 8]          # one 8-byte repeat per 9000 literals
+    else:
+        a = np.ascontiguousarray(CASES[name](r), np.uint8)
+    cw = np.zeros(121, np.uint32)
+    cl = np.zeros(121, np.uint32)
+    nseg = L.emu_zstd_counts(a.ctypes.data if a.size else 0, a.size, level, cw.ctypes.data, cl.ctypes.data)
+    assert nseg >= 1
+    assert np.array_equal(cw, cl), (name, np.nonzero(cw != cl))

@@ -58,6 +58,12 @@ def run(fmt, n, unique, tune=None):
 
 
 if __name__ == "__main__":
+    if os.environ.get("HZ_PROF_LONE", "0") == "1":
+        # one chunk alone on the GPU (latency): F1 and F2 with one and four wavefronts per stream
+        for fmt in ("F1", "F2"):
+            for w in (1, 4):
+                run(fmt, 1, 1, tune={"waves_per_stream": w})
+        sys.exit(0)
     n1 = int(os.environ.get("HZ_PROF_N1", "1024"))
     run("F1", n1, 256)
     if os.environ.get("HZ_PROF_F2W1", "0") == "1":
