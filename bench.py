@@ -413,6 +413,17 @@ CFG5_DIMS = (65536, 131072)
 CFG5_DSET = "d-7f6e5d4c-3b2a1908-f7e6-d5c4b3-a29180"
 
 
+def _partial(cid, sel):
+    """the selection covers chunk `cid` (a 512 x 512 chunk of CFG5_DIMS) only in part"""
+    from hsds_amd import selection as hsel
+    idx = hsel.getChunkIndex(cid)
+    for k, s in enumerate(sel):
+        lo, hi = idx[k] * CFG5_CHUNK[k], min((idx[k] + 1) * CFG5_CHUNK[k], CFG5_DIMS[k])
+        if s.start > lo or s.stop < hi:
+            return True
+    return False
+
+
 def run_cfg5_sharded(args, dev, rank, world):
     """configs[4] through the write path itself (crawl.ShardedWriter): f32 dataset
     65536 x 131072 in 512x512 chunks; the request covers 8192 x world rows (all 32 768 chunks
@@ -444,15 +455,30 @@ def run_cfg5_sharded(args, dev, rank, world):
             slab[r0:r0 + 512] = torch.round(torch.cumsum(z, dim=1), decimals=2).to(torch.float32)
             del z
     per_rank = 4096 * 1024 * 1024 * 5 // 4 + (1 << 30)
-    store = ChunkStore(lambda k, o, n: None, mem_target=per_rank, device=dev)
+    # the DN's object storage: S3 key -> stored F1 object (filled from the first variant's
+    # encode); a chunk the cache does not hold is read from here (get_chunk's fetch)
+    objects = {}
+    store = ChunkStore(lambda k, o, n: (objects[k][o:o + n] if n else objects[k][o:]) if k in objects else None,
+                       mem_target=per_rank, device=dev)
     out = {}
-    for name, (y0, x0) in (("full", (0, 0)), ("offset_100_100", (100, 100))):
+    variants = [v for v in (("full", (0, 0)), ("offset_100_100", (100, 100)))
+                if v[0] in args.cfg5w_variants.split(",")]
+    for name, (y0, x0) in variants:
         sel = (slice(y0, rows, 1), slice(x0, cols, 1))
         req = slab[y0:, x0:].contiguous() if rank == 0 else None
         stats = {}
+        # the chunks this request covers only in part: PUT_Chunk reads them (RMW).  Before every
+        # step they leave the cache, so each step decodes their stored objects as a DN does
+        # for a chunk it does not hold (chunk_dn.py:174-190, datanode_lib.get_chunk)
+        plan0 = crawl.SelectionPlan(CFG5_DSET, CFG5_DIMS, CFG5_CHUNK, sel, np.float32, world)
+        edge = [c for c in plan0.chunk_ids(rank) if _partial(c, sel)] if objects else []
 
         def step():
             t0 = time.perf_counter()
+            for cid in edge:
+                if cid in store.cache:
+                    store.cache.clearDirty(cid)
+                    del store.cache[cid]
             plan = crawl.SelectionPlan(CFG5_DSET, CFG5_DIMS, CFG5_CHUNK, sel, np.float32, world)
             t1 = time.perf_counter()
             w = crawl.ShardedWriter(plan, rank, store)
@@ -464,9 +490,20 @@ def run_cfg5_sharded(args, dev, rank, world):
             step()
         torch.cuda.synchronize()
         assert int((stats["status"][:len(stats["ids"])] != 0).sum()) == 0, "encode status errors"
+        if not objects and stats["ids"]:
+            # the stored objects of this rank's chunks (the s3sync of the first variant)
+            from hsds_amd.partition import getS3Key
+            hs = stats["sizes"].cpu().numpy()
+            hf = stats["frames"].cpu().numpy()
+            for k, cid in enumerate(stats["ids"]):
+                o = int(stats["descs"][k]["dst_off"])
+                objects[getS3Key(cid)] = hf[o:o + int(hs[k])].tobytes()
+            del hf
         ok = 1
         if rank == 0 and stats["ids"]:
-            # sampled objects decode (oracle) to the request's bytes of that chunk
+            # sampled objects (a fully covered chunk, and a partly covered one at the offset,
+            # whose uncovered part came from its stored object) decode (oracle) to the chunk
+            # the request and the previous contents make: here the slab's block
             from oracle import oracle as orc
             from hsds_amd import selection as hsel
             hs = stats["sizes"].cpu().numpy()
@@ -476,9 +513,8 @@ def run_cfg5_sharded(args, dev, rank, world):
                 o = int(stats["descs"][k]["dst_off"])
                 fr = stats["frames"][o:o + int(hs[k])].cpu().numpy().tobytes()
                 got = np.frombuffer(orc.uncompress(fr, "zlib", 1, 1, 1 << 20), np.float32).reshape(CFG5_CHUNK)
-                ys, xs = max(i * 512, y0), max(j * 512, x0)
-                want = slab[ys:(i + 1) * 512, xs:(j + 1) * 512].cpu().numpy()
-                ok &= int(np.array_equal(got[ys - i * 512:, xs - j * 512:], want))
+                want = slab[i * 512:(i + 1) * 512, j * 512:(j + 1) * 512].cpu().numpy()
+                ok &= int(np.array_equal(got, want))
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -501,12 +537,14 @@ def run_cfg5_sharded(args, dev, rank, world):
         out[name] = {"value": round(nbytes / el / 1e9, 2), "unit": "GB/s of request array (all ranks)",
                      "ms_per_step": round(el * 1e3, 3), "request_bytes": nbytes,
                      "chunks": int(len(stats["plan"].idx)), "chunks_this_rank": len(stats["ids"]),
+                     "rmw_chunks_from_storage_rank0": len(edge),
                      "plan_ms": round(float(np.mean(pms)), 2), "compressed_bytes_rank0": comp,
                      "sample_check": bool(ok)}
         del req
     out["workload"] = (f"configs[4]: f32 {CFG5_DIMS[0]}x{CFG5_DIMS[1]}, 512x512 chunks, request rows [0:{rows}] "
                        f"(and offset by (100,100)), md5-sharded over {world} rank(s): plan + root gather + RCCL "
-                       "scatter + PUT_Chunk RMW (compare + copy) + F1 zlib L4 encode")
+                       "scatter + PUT_Chunk RMW (compare + copy) + F1 zlib L4 encode; the offset request's "
+                       "partly covered chunks are read back from their stored F1 objects every step")
     del slab, store
     torch.cuda.empty_cache()
     return out
@@ -1179,6 +1217,9 @@ def main():
     ap.add_argument("--cfg5", type=int, default=1, help="also measure configs[4] scatter+encode (N=1)")
     ap.add_argument("--cfg5w", type=int, default=1, help="configs[4] through the sharded write path (all N)")
     ap.add_argument("--cfg5-steps", type=int, default=3)
+    ap.add_argument("--cfg5w-variants", default="full,offset_100_100",
+                    help="cfg5w requests: full (aligned), offset_100_100 (edge RMW); the offset one reads its "
+                         "edge chunks from the objects the first variant stored")
     ap.add_argument("--cfg4", type=int, default=1,
                     help="configs[3] sharded decode+select (+RCCL gather when N > 1)")
     ap.add_argument("--cfg4-steps", type=int, default=3)
@@ -1222,6 +1263,8 @@ def main():
             legs["cfg1"] = run_cfg1(args, dev)
         if world == 1 and args.cfg5:
             legs["cfg5"] = run_cfg5(args, dev, rank)
+        if args.cfg5w:
+            legs["cfg5_sharded_write"] = run_cfg5_sharded(args, dev, rank, world)
         if args.cfg4 == 1:
             legs["cfg4"] = run_cfg4(args, dev, rank, world)
         if args.cfg4_full:

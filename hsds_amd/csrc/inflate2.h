@@ -693,6 +693,16 @@ struct HRR {
   HZ2_HM uint32_t pos() const { return base + p; }
 };
 
+// lens[n .. n + rep) = val (a code-length run): bytes up to a dword boundary, then dwords
+HZ2_HM void fill_run(uint8_t* p, uint32_t n, uint32_t rep, uint32_t val) {
+  uint32_t i = n;
+  const uint32_t e = n + rep;
+  while (i < e && ((uintptr_t)(p + i) & 3u)) p[i++] = (uint8_t)val;
+  const uint32_t w = val * 0x01010101u;
+  for (; i + 4u <= e; i += 4u) *(uint32_t*)(p + i) = w;
+  while (i < e) p[i++] = (uint8_t)val;
+}
+
 enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_ERR = 3 };
 struct Tok {
   uint32_t n;      // bits
@@ -729,6 +739,16 @@ HZ_HD Tok rtok(const Shared* sh, const BR& r) {
   t.len = lit ? 1u : v + bfe32(lo, nb, x);
   t.v = lit ? v : dist;
   return t;
+}
+
+// c + the dot product of the four bytes of a and of b (v_dot4_u32_u8)
+HZ_HD uint32_t dot4(uint32_t a, uint32_t b, uint32_t c) {
+#if HZ_GPU
+  return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+  for (uint32_t i = 0; i < 32u; i += 8u) c += ((a >> i) & 255u) * ((b >> i) & 255u);
+  return c;
+#endif
 }
 
 // a[u] for a register array and a runtime u < MPL (no dynamic register indexing)

@@ -160,6 +160,15 @@ HZ_HD uint32_t cl_order(uint32_t i) {
   return (uint32_t)((i < 12 ? lo >> (5 * i) : hi >> (5 * (i - 12))) & 31u);
 }
 
+// position of code-length symbol s in that order (the inverse of cl_order), s < 19
+HZ_HD uint32_t cl_pos(uint32_t s) {
+  // 0:3 1:17 2:15 3:13 4:11 5:9 6:7 7:5 8:4 9:6 10:8 11:10 | 12:12 13:14 14:16 15:18 16:0 17:1 18:2
+  const uint64_t lo = 3ull | 17ull << 5 | 15ull << 10 | 13ull << 15 | 11ull << 20 | 9ull << 25 | 7ull << 30 |
+                      5ull << 35 | 4ull << 40 | 6ull << 45 | 8ull << 50 | 10ull << 55;
+  const uint64_t hi = 12ull | 14ull << 5 | 16ull << 10 | 18ull << 15 | 0ull << 20 | 1ull << 25 | 2ull << 30;
+  return (uint32_t)((s < 12 ? lo >> (5 * s) : hi >> (5 * (s - 12))) & 31u);
+}
+
 HZ_HD uint32_t popc64(uint64_t x) {
 #if HZ_GPU
   return (uint32_t)__popcll(x);

@@ -175,6 +175,10 @@ def _torch_dtype(dtype):
     return _TORCH_DT[dt]
 
 
+# get_chunks_deferred(views=False): the value of a chunk that is resident in the cache
+RESIDENT = object()
+
+
 def device_view(u8, shape, dtype):
     """Typed torch view of a uint8 device slice (falls back to the uint8 bytes for
     numpy dtypes torch has no equivalent of, e.g. compound types)."""
@@ -905,20 +909,22 @@ class ChunkStore:
             return finish()
 
     def get_chunks_deferred(self, reads, dtype, chunk_dims, filter_ops=None, fill_value=None, layout_class=None,
-                            hyper_dims=None, chunk_init=False):
+                            hyper_dims=None, chunk_init=False, views=True):
         """get_chunks without waiting for the device: (values, finish).  The values are
         device views (None for a 404, an exception for a malformed request) whose bytes
         are ready once the current stream has drained; finish(), called after that,
         returns the final list with decode failures as HTTPInternalServerError.  Call it
         under self.lock and keep the lock until the views are consumed (the batcher
         gathers its selections in between).  Cache hits stay pinned until finish(), so
-        the misses' slot reservations cannot evict them."""
+        the misses' slot reservations cannot evict them.  views=False: a cache hit's value
+        is RESIDENT instead of a device view (a caller that addresses the slots itself, as
+        the write paths do, skips building thousands of tensor views on the host)."""
         out = {}
         todo, seen, hits = [], set(), []
         for r in reads:
             if r.chunk_id in self.cache:
                 if r.chunk_id not in out:
-                    out[r.chunk_id] = self.cache[r.chunk_id]
+                    out[r.chunk_id] = self.cache[r.chunk_id] if views else RESIDENT
                     self.cache.pin(r.chunk_id)
                     hits.append(r.chunk_id)
                 self.reader.stats["cache_hits"] += 1
@@ -976,6 +982,23 @@ class ChunkStore:
 
         finish.abort = abort
         return [out[r.chunk_id] for r in reads], finish
+
+    def _resident(self, reads, dtype, chunk_dims, filter_ops, fill_value):
+        """PUT_Chunk's read (get_chunk with chunk_init, chunk_dn.py:174-190): every target
+        chunk resident in the cache -- a stored object decoded, else the fill value.  A read's
+        own error (get_chunk's 500) is raised.  The write paths address the slots by their
+        offsets, so cache hits build no device views (views=False)."""
+        import torch
+        vals, finish = self.get_chunks_deferred(reads, dtype, chunk_dims, filter_ops=filter_ops,
+                                                fill_value=fill_value, chunk_init=True, views=False)
+        try:
+            torch.cuda.current_stream(self.cache.arena.buf.device).synchronize()
+        except BaseException:
+            finish.abort()
+            raise
+        for v in finish():
+            if isinstance(v, Exception):
+                raise v
 
     def _fill_new(self, keys, dtype, chunk_dims, fill_value):
         """get_chunk's chunk_init for missing objects (datanode_lib.py:1132-1138): a cache
@@ -1039,11 +1062,7 @@ class ChunkStore:
                                                       fill_value, write_zero_chunks)))
             return [res[i] for i in range(len(writes))]
         reads = [w[0] for w in writes]
-        arrs = self.get_chunks(reads, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
-                               chunk_init=True)
-        for v in arrs:
-            if isinstance(v, Exception):
-                raise v                      # the read's own error (get_chunk's 500 surfaces from PUT_Chunk)
+        self._resident(reads, dtype, chunk_dims, filter_ops, fill_value)
         # pin the target slots while the update runs
         for r in reads:
             n = self.cache._lru.get(r.chunk_id)
@@ -1077,7 +1096,6 @@ class ChunkStore:
             if d or write_zero_chunks:
                 self.cache.setDirty(r.chunk_id)
             out.append(bool(d))
-        del arrs
         return out
 
     @_locked
@@ -1103,11 +1121,7 @@ class ChunkStore:
         chunk_dims = tuple(int(c) for c in chunk_dims)
         if len({r.chunk_id for r in reads}) != len(reads):
             raise ValueError("put_pieces takes each chunk once")
-        arrs = self.get_chunks(reads, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
-                               chunk_init=True)
-        for v in arrs:
-            if isinstance(v, Exception):
-                raise v                      # the read's own error (a 500 from get_chunk)
+        self._resident(reads, dtype, chunk_dims, filter_ops, fill_value)
         for r in reads:
             n = self.cache._lru.get(r.chunk_id)
             if n is None:
@@ -1130,7 +1144,6 @@ class ChunkStore:
             if d or write_zero_chunks:
                 self.cache.setDirty(r.chunk_id)
             out.append(bool(d))
-        del arrs
         return out
 
     @_locked

@@ -6,6 +6,7 @@ Restated from the reference (pinned by tests/golden/selection_cases.json):
 With `count` = number of GPUs, getObjPartition is the multi-GPU sharding rule
 (SURVEY.md section 8e): identical to HSDS's chunk -> DN rule when dn_count == count.
 """
+import functools
 import hashlib
 
 
@@ -26,8 +27,10 @@ def _hex32(obj_id):
     return uuid.replace("-", "")
 
 
+@functools.lru_cache(maxsize=1 << 18)
 def getS3Key(chunk_id):
-    """Storage key of an HSDS v2 chunk id: db/<8>-<8>/d/<4>-<6>-<6>[/p<N>]/<i>_<j>..."""
+    """Storage key of an HSDS v2 chunk id: db/<8>-<8>/d/<4>-<6>-<6>[/p<N>]/<i>_<j>...
+    (memoised: a DN computes the keys of the same chunks request after request)"""
     if not chunk_id.startswith("c"):
         raise ValueError(f"Unexpected id: {chunk_id}")
     h = _hex32(chunk_id)

@@ -374,3 +374,51 @@ def test_long_literal_runs_before_matches(emu, nw):
         r, out, st = run(emu, c, len(data), nwaves=nw)
         assert r == 0 and out == data, (level, r)
         assert st["matches"] > 0
+
+
+def _alphabet_cases():
+    """streams whose dynamic headers exercise every code-length symbol: sparse alphabets
+    (zero runs: symbols 17 and 18), skewed ones (repeats of the previous length: 16),
+    dense ones (two literal lengths per lookup of the header's two-symbol LUT), long and
+    short distance alphabets"""
+    rng = np.random.default_rng(2026)
+    out = []
+    for k in range(48):
+        nsym = int(rng.choice([2, 3, 5, 9, 17, 40, 90, 160, 256]))
+        alpha = rng.choice(256, nsym, replace=False).astype(np.uint8)
+        p = rng.dirichlet(np.full(nsym, float(rng.choice([0.05, 0.3, 1.0, 5.0]))))
+        data = alpha[rng.choice(nsym, int(rng.integers(300, 40000)), p=p)]
+        if k % 3 == 0:        # repeats at many distances
+            reps = [data[i:i + 40] for i in rng.integers(0, max(1, data.size - 40), 200)]
+            data = np.concatenate([data] + reps)
+        out.append(data.tobytes())
+    return out
+
+
+def test_dynamic_headers_all_code_length_symbols(emu):
+    for k, data in enumerate(_alphabet_cases()):
+        for level in (1, 6, 9):
+            c = zlib.compress(data, level)
+            r, out, _ = run(emu, c, len(data))
+            assert r == 0 and out == data, (k, level, r)
+
+
+def test_dynamic_header_corruptions_match_zlib(emu):
+    """bit flips inside the first dynamic header (HLIT / HDIST / HCLEN, the code-length code,
+    the code lengths): the emulator must accept exactly what zlib accepts, bit-exact"""
+    rng = np.random.default_rng(7)
+    data = _alphabet_cases()[5]
+    c = bytearray(zlib.compress(data, 6))
+    for t in range(160):
+        b = bytearray(c)
+        bit = int(rng.integers(19, min(len(b) * 8, 19 + 600)))    # after the zlib header and BFINAL/BTYPE
+        b[bit // 8] ^= 1 << (bit % 8)
+        try:
+            ref = zlib.decompress(bytes(b))
+        except zlib.error:
+            ref = None
+        r, out, _ = run(emu, bytes(b), len(data))
+        if ref is not None and len(ref) == len(data):
+            assert r == 0 and out == ref, (t, bit, r)
+        else:
+            assert r != 0, (t, bit)
