@@ -1775,10 +1775,10 @@ int hsds_engine_create(int device, hsds_engine** out) {
   }
   e->huff_blocks_per_cu = o2;
   e->emit_blocks_per_cu = o3;
-  // warm-up 512 bits, segments sized to 1 + 1/16 of the previous block, 4 repair rounds
-  e->tune.W = 768;          // GPU sweep (tools/ab_tune.sh), bit-ring decoder with K = 8 recorded starts:
-                            // 384 / 512 / 640 / 768 bits -> F1 116.2 / 119.5 / 120.9 / 121.6 GB/s
-                            // (round 2, register reader, K = 16: 512 best at 108.7)
+  // warm-up 1024 bits, segments sized to 1 + 1/16 of the previous block, 4 repair rounds
+  e->tune.W = 1024;         // GPU sweep (tools/ab_tune.sh) with the warm-up in a loop of its own (round 6,
+                            // profiles/r6_ab_warmup.txt): 640 / 768 / 1024 / 1280 bits -> F1 188.3 / 190.8 /
+                            // 190.7 / 189.2 GB/s, F2 141.9 / 145.8 / 146.7 / 148.4 (round 5: 768 best)
   e->tune.max_rounds = 4;
   e->tune.over16 = 1;
   e->tune.spin_max = 0;     // window pipeline waits: hz2::SPIN_MAX polls (~1 s), then one-wavefront re-decode

@@ -148,6 +148,10 @@ static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
 #ifndef HZ2_PRIO_ABS
 #define HZ2_PRIO_ABS 40
 #endif
+// phase A's warm-up decoded by a loop of its own (1) or inside the segment loop (0)
+#ifndef HZ2_WARM2
+#define HZ2_WARM2 1
+#endif
 #ifndef HZ2_TICKN
 #define HZ2_TICKN (HZ2_RS >= 16 ? 8 : 5)
 #endif

@@ -187,10 +187,15 @@ HZ_HD void atomicAdd_lds(uint16_t* p, int v) {
 #endif
 }
 
+// the low n bits of v reversed (n <= 32): v_bfrev_b32 and a shift on the GPU
 HZ_HD uint32_t rev_bits(uint32_t v, int n) {
+#if HZ_GPU
+  return n > 0 ? __builtin_bitreverse32(v) >> (32 - n) : 0u;
+#else
   uint32_t r = 0;
   for (int i = 0; i < n; i++) { r = (r << 1) | (v & 1u); v >>= 1; }
   return r;
+#endif
 }
 
 // ---- global memory helpers -------------------------------------------------
@@ -387,12 +392,15 @@ struct TableArgs {
     LANE_LOOP {                                                                         \
       for (int idx = lane; idx < (1 << (A).root); idx += 64) {                          \
         const uint32_t rc = hz::rev_bits((uint32_t)idx, (A).root);                      \
-        uint32_t el = 1, es = hz::SYM_BAD;                                            \
+        uint32_t el = 1, si = 0xffffu;     /* the code's length and its rank in sorted[] */ \
         _Pragma("unroll") for (int len = 1; len <= 15; len++) {                         \
           if (len > (A).root) break;                                                    \
           const uint32_t d = (rc >> ((A).root - len)) - _fc[len];                       \
-          if (d < _cn[len]) { el = (uint32_t)len; es = (A).sorted[_of[len] + d]; }      \
+          const bool hit = d < _cn[len];                                                \
+          el = hit ? (uint32_t)len : el;                                                \
+          si = hit ? _of[len] + d : si;                                                 \
         }                                                                               \
+        const uint32_t es = si != 0xffffu ? (uint32_t)(A).sorted[si] : hz::SYM_BAD;     \
         const uint32_t e = (A).rich ? hz::ent_rich((A).kind, el, es) : hz::ent_sym(el, es); \
         (A).lut[idx] = (uint16_t)e;                                                     \
       }                                                                                 \
