@@ -61,7 +61,7 @@ constexpr uint32_t FARW = 32768;            // zlib window: with a far ring, mat
 #endif
 constexpr int HBITS = HD_HBITS;
 constexpr int HSIZE = 1 << HBITS;
-constexpr int LANE_MAX = SEG / WAVE + 4;    // input bytes per lane (a full segment; lane_start's skew)
+constexpr int LANE_MAX = SEG / WAVE + (HD_SKEW == 2 ? 6 : 4);   // input bytes per lane (a full segment; lane_start's skew)
 constexpr int TSLOTS = LANE_MAX;            // 16-bit token slots per lane
 constexpr int SEG_TOK = TSLOTS * WAVE;      // token slots per segment in HBM
 constexpr int STAGE_WORDS = SEG / 4 + 24;   // a block is never emitted above its stored size
@@ -248,7 +248,12 @@ HZ_HD uint32_t load_stream_word(const EncJob& job, uint32_t p, uint32_t hi) {
 // first ring words of the 64 lanes fall in 64 banks.  A range grows by at most 4 bytes.
 HZ_HD uint32_t lane_start(uint32_t l, uint32_t seglen) {
   const uint32_t R = (seglen + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;
-#if HD_SKEW
+#if HD_SKEW == 2
+  // ds_read_b32 banks are (a / 4) mod 32 per 32-lane group: 4 l bytes put lane l's ring word
+  // in bank l, and 2 more bytes for lanes 16-31 of each group put its 16-bit link (bank
+  // (p / 2) mod 32 = 2 l + 1) apart from lane l - 16's
+  const uint32_t a = l * R + 4u * l + 2u * ((l >> 4) & 1u);
+#elif HD_SKEW
   const uint32_t a = l * R + 4u * (l >> 1);
 #else
   const uint32_t a = l * R;

@@ -99,7 +99,8 @@ constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
 #ifndef HZ2_FILLCAP
 #define HZ2_FILLCAP 16
 #endif
-constexpr uint32_t FILL_CAP = HZ2_FILLCAP;   // resolve: source-map bytes a lane fills per match (258: all)
+constexpr uint32_t FILL_CAP = HZ2_FILLCAP;
+   // resolve: source-map bytes a lane fills per match (258: all)
 static_assert(MPL == 4, "sel4 selects among four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 static_assert(SPL <= 24, "resolve slots per lane");
@@ -590,6 +591,27 @@ HZ_HD uint32_t slot4(uint32_t k) { return k + 4u == RS ? 0u : k + 4u; }
 // all loads issued before the first write.  Leaves wr in [c + RS, c + RS + 3]: every word a
 // token reads within the next TICKN tokens is in the ring (NEED <= RS).  TICKN tokens read at
 // most 48 TICKN bits, so two quads always restore the ring (and br_init needs two at most)
+#if HZ2_RS > 12
+// a larger ring (latency experiments: fewer ticks per token): as many quads as fit
+constexpr uint32_t NQF = RS / 4u;
+HZ_HD void br_fill(Shared& sh, int lane, const Src& S, BR& r) {
+  uint32_t a[4 * NQF];
+  bool f[NQF];
+HZ_UNROLL
+  for (uint32_t q = 0; q < NQF; q++) {
+    f[q] = r.wr + 4u * q + 1u <= r.c + RS;
+    if (f[q]) g_quad(S, r.wr + 4u * q, a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+  }
+HZ_UNROLL
+  for (uint32_t q = 0; q < NQF; q++) {
+    if (f[q]) {
+      br_put(sh, lane, r.wslot, a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+      r.wr += 4u;
+      r.wslot = slot4(r.wslot);
+    }
+  }
+}
+#else
 static_assert((48u * TICKN + 31u) / 32u <= 8u && RS - 8u + 3u <= 8u, "two quads per refill");
 HZ_HD void br_fill(Shared& sh, int lane, const Src& S, BR& r) {
   if (r.wr + 1u > r.c + RS) return;
@@ -603,6 +625,7 @@ HZ_HD void br_fill(Shared& sh, int lane, const Src& S, BR& r) {
   r.wr += two ? 8u : 4u;
   r.wslot = two ? slot4(k1) : k1;
 }
+#endif
 
 // position p: the window (words c .. c+2) from two quad loads and a full ring (from quad q)
 HZ_HD void br_init(Shared& sh, int lane, const Src& S, BR& r, uint32_t p) {
@@ -745,6 +768,15 @@ HZ_HD Tok rtok(const Shared* sh, const BR& r) {
   return t;
 }
 
+// a * b for a, b < 2^24 with a product < 2^32 (v_mul_u32_u24: full rate)
+HZ_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if HZ_GPU
+  return __umul24(a, b);
+#else
+  return a * b;
+#endif
+}
+
 // c + the dot product of the four bytes of a and of b (v_dot4_u32_u8)
 HZ_HD uint32_t dot4(uint32_t a, uint32_t b, uint32_t c) {
 #if HZ_GPU
@@ -865,7 +897,9 @@ void emu_wgbar(Ctl* c, int n);
 #define HZ2_TICK(it) do { ++(it); } while (0)
 #endif
 // ring reader tick (r: the lane's hz2::BR)
-#define HZ2_RTICK(it) do { if ((HZ2_UNI(++(it)) % hz2::TICKN) == 0u) hz2::br_tick(sh, lane, S, r); } while (0)
+// (the counter is wave-uniform -- the lanes of a loop tick together -- and kept so: a scalar
+// register, no per-token VALU increment and readfirstlane)
+#define HZ2_RTICK(it) do { (it) = HZ2_UNI(it) + 1u; if ((it) % hz2::TICKN == 0u) hz2::br_tick(sh, lane, S, r); } while (0)
 
 namespace hz2 {
 
