@@ -1240,6 +1240,61 @@ __global__ void __launch_bounds__(64) zstd_count_kernel(const uint32_t* __restri
   flush(cur);
 }
 
+// zstd_seq_kernel: the compact sequence array of every segment, one wave per segment, each
+// lane on its own parse lane (zstd_enc.h "the compact sequences"); the raw literals section
+// straight into the segment's block scratch (levels below 6).  Runs after zstd_count_kernel and
+// zstd_lit_kernel: the sequences overwrite the token slots they read.
+__global__ void __launch_bounds__(64) zstd_seq_kernel(const uint32_t* __restrict__ segoffs, int64_t nchunks,
+                                                      const hd::SegParse* __restrict__ sp, uint16_t* __restrict__ tok,
+                                                      uint8_t* __restrict__ zscr, const uint32_t* __restrict__ lsz,
+                                                      uint32_t seg_cap) {
+  __shared__ uint32_t sa[hze::SEQ_MAX];
+  __shared__ uint16_t sb[hze::SEQ_MAX];
+  __shared__ uint8_t lbuf[hd::SEG + 16];
+  uint32_t total = segoffs[nchunks];
+  if (total > seg_cap) total = seg_cap;
+  const uint32_t l = threadIdx.x;
+  for (uint32_t s = blockIdx.x; s < total; s += gridDim.x) {
+    uint16_t* const ts = tok + (size_t)s * hd::SEG_TOK;
+    hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, ts);
+    const uint32_t ns = sp[s].nslot[l];
+    const hze::LaneSeq r = hze::lane_seq_count(gw, ns, l);
+    const uint32_t Li = hz::wave_incl_scan_dpp(r.lits), Si = hz::wave_incl_scan_dpp(r.nm);
+    const uint32_t L = Li - r.lits, S = Si - r.nm;
+    const uint32_t qprev = hz::wave_excl_max(r.hm ? Li - r.run : 0u, (int)l);
+    const uint32_t nlit = (uint32_t)__builtin_amdgcn_readlane((int)Li, 63);
+    const uint32_t nseq = (uint32_t)__builtin_amdgcn_readlane((int)Si, 63);
+    hze::lane_seq_emit(gw, ns, l, L + r.lead - qprev,
+                       [&](uint32_t k, uint32_t v) { lbuf[L + k] = (uint8_t)v; },
+                       [&](uint32_t j, uint32_t run, uint32_t ml, uint32_t off) {
+                         sa[S + j] = run | (ml << 16);
+                         sb[S + j] = (uint16_t)(off - 1u);
+                       });
+    __syncthreads();            // every lane's slot reads are done: the sequences may overwrite them
+    uint32_t* const ga = hze::seq_a(ts);
+    uint16_t* const gb = hze::seq_b(ts);
+    for (uint32_t i = l; i < nseq; i += 64u) { ga[i] = sa[i]; gb[i] = sb[i]; }
+    if (lsz[s] == 0u) {
+      // dwords of the block scratch from byte 0: bytes 0-2 the block header (encode_segment
+      // writes it last), then the literals section header and the literal bytes
+      uint32_t* const out = (uint32_t*)(zscr + (size_t)s * hze::ZCAP);
+      uint8_t h[3] = {0, 0, 0};
+      const uint32_t p0 = 3u + hze::lit_header(nlit, h), end = p0 + nlit;
+      for (uint32_t k = l; 4u * k < end; k += 64u) {
+        uint32_t w = 0;
+HZ_UNROLL
+        for (uint32_t b = 0; b < 4u; b++) {
+          const uint32_t x = 4u * k + b;
+          const uint32_t v = x < 3u ? 0u : x < p0 ? h[x - 3u] : x < end ? lbuf[x - p0] : 0u;
+          w |= v << (8u * b);
+        }
+        out[k] = w;
+      }
+    }
+    __syncthreads();            // (the LDS of the next segment)
+  }
+}
+
 __global__ void zstd_table_kernel(const uint32_t* __restrict__ offs, int64_t nchunks,
                                   const hze::SeqCounts* __restrict__ counts, hze::Tabs* __restrict__ tabs,
                                   uint32_t item_cap) {
@@ -1287,7 +1342,7 @@ __global__ void __launch_bounds__(64) zstd_seg_kernel(const uint32_t* __restrict
     const uint32_t last = seg + 1 == hd::nsegments(it.len) ? 1u : 0u;
     zsz[s] = hze::encode_segment(T[m.item - base - f0], ct, tok + (size_t)s * hd::SEG_TOK, sp + s, job,
                                  seg * (uint32_t)hd::SEG, m.seglen, last, zscr + (size_t)s * hze::ZCAP, hze::ZCAP,
-                                 lsec + (size_t)s * hze::LCAP, lsz[s]);
+                                 lsec + (size_t)s * hze::LCAP, lsz[s], 1);
   }
 }
 
@@ -2408,6 +2463,8 @@ int hsds_encode_batch_codec(hsds_engine* e, const void* d_src, const hsds_chunk_
                          nchunks, sp, tok, lsec, lsz, seg_cap);
     else if (hipMemsetAsync(lsz, 0, (size_t)seg_cap * 4, st) != hipSuccess)
       return HSDS_ERR_DEVICE;
+    hipLaunchKernelGGL(zstd_seq_kernel, dim3(grid_for(6, seg_cap)), dim3(64), 0, st, segoffs, nchunks, sp, tok, zscr,
+                       (const uint32_t*)lsz, seg_cap);
     hipLaunchKernelGGL(zstd_seg_kernel, dim3((seg_cap + 63) / 64), dim3(64), 0, st, segoffs, nchunks, meta, slots, sp,
                        tok, zscr, zsz, lsec, lsz, seg_cap, clevel, (const hze::Tabs*)ztab);
     hipLaunchKernelGGL(zstd_size_kernel, dim3((item_cap + 255) / 256), dim3(256), 0, st, offs, segoffs, nchunks, slots,

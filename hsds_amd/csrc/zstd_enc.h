@@ -688,12 +688,129 @@ HZ_HD void count_segment(const CodeTabs& ct, const uint16_t* tok, const hd::SegP
   });
 }
 
+// ---- the compact sequences of a segment (zstd_seq_kernel, round 6) ------------------------
+// zstd_seg_kernel's lane per segment used to walk the 64 parse lanes' token slots itself --
+// twice (literals forward, sequences backward), each load of its lane touching its own cache
+// lines, 64 segments' slots per wave.  zstd_seq_kernel (one wave per segment, each lane on its
+// own parse lane: coalesced rows) turns the slots into a compact sequence array in the same
+// scratch -- a[i] = literal run | match length << 16, b[i] = offset - 1, in segment order --
+// and writes the raw literals section's bytes into the block scratch.
+constexpr uint32_t SEQ_MAX = (uint32_t)hd::SEG / 3u + 1u;     // a match covers >= 3 input bytes
+static_assert(SEQ_MAX * 6u <= (uint32_t)hd::SEG_TOK * 2u, "the compact sequences fit the segment's token slots");
+HZ_HD uint32_t* seq_a(uint16_t* tok) { return (uint32_t*)tok; }
+HZ_HD uint16_t* seq_b(uint16_t* tok) { return tok + 2u * SEQ_MAX; }
+HZ_HD const uint32_t* seq_a(const uint16_t* tok) { return (const uint32_t*)tok; }
+HZ_HD const uint16_t* seq_b(const uint16_t* tok) { return tok + 2u * SEQ_MAX; }
+// the raw literals section header (Literals_Section_Header, Raw_Literals_Block) for n bytes
+HZ_HD uint32_t lit_header(uint32_t n, uint8_t* h) {
+  if (n < 32u) { h[0] = (uint8_t)(n << 3); return 1; }
+  if (n < 4096u) { h[0] = (uint8_t)((1u << 2) | ((n & 15u) << 4)); h[1] = (uint8_t)(n >> 4); return 2; }
+  h[0] = (uint8_t)((3u << 2) | ((n & 15u) << 4)); h[1] = (uint8_t)((n >> 4) & 0xffu); h[2] = (uint8_t)(n >> 12);
+  return 3;
+}
+// parse lane l's part of the segment, pass 1: literals, the run after its last match, the run
+// before its first match, whether it has one, its matches
+struct LaneSeq {
+  uint32_t lits, run, lead, hm, nm;
+};
+HZ_HD LaneSeq lane_seq_count(hz_gcu32* gw, uint32_t ns, uint32_t l) {
+  LaneSeq r = {0u, 0u, 0u, 0u, 0u};
+  uint32_t want_dist = 0;
+  slots_fwd(gw, ns, l, [&](uint32_t v) {
+    if (want_dist) {
+      if (!r.hm) r.lead = r.run;
+      r.hm = 1; r.nm++; r.run = 0; want_dist = 0;
+    } else if (v & 0x8000u) {
+      want_dist = 1;
+    } else {
+      r.run++; r.lits++;
+    }
+  });
+  return r;
+}
+// pass 2: lit(k, byte) for the lane's k-th literal, seq(j, run, length, offset) for its j-th
+// match (the first one's run = first, from the scans over the lanes)
+template <class Lit, class Sq>
+HZ_HD void lane_seq_emit(hz_gcu32* gw, uint32_t ns, uint32_t l, uint32_t first, Lit&& lit, Sq&& sq) {
+  uint32_t want_dist = 0, ml = 0, run = 0, k = 0, j = 0;
+  slots_fwd(gw, ns, l, [&](uint32_t v) {
+    if (want_dist) {
+      sq(j, j ? run : first, ml, v + 1u);
+      j++; run = 0; want_dist = 0;
+    } else if (v & 0x8000u) {
+      ml = (v & 0x7fffu) + 3u;
+      want_dist = 1;
+    } else {
+      lit(k, v);
+      k++; run++;
+    }
+  });
+}
+#if !HZ_GPU
+// zstd_seq_kernel on the CPU: both passes lane by lane, the kernel's scans done serially; the
+// raw literals (header included) into out + 3 when `raw` (the block scratch)
+inline void extract_sequences(uint16_t* tok, const hd::SegParse* sp, uint8_t* out, int raw) {
+  hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
+  LaneSeq lc[hd::WAVE];
+  uint32_t L[hd::WAVE], S[hd::WAVE], Q[hd::WAVE];
+  uint32_t nlit = 0, nseq = 0, qmax = 0;
+  for (uint32_t l = 0; l < (uint32_t)hd::WAVE; l++) {
+    lc[l] = lane_seq_count(gw, sp->nslot[l], l);
+    L[l] = nlit; S[l] = nseq; Q[l] = qmax;
+    const uint32_t q = lc[l].hm ? nlit + lc[l].lits - lc[l].run : 0u;
+    qmax = q > qmax ? q : qmax;
+    nlit += lc[l].lits; nseq += lc[l].nm;
+  }
+  static thread_local uint32_t A[SEQ_MAX];
+  static thread_local uint16_t B[SEQ_MAX];
+  static thread_local uint8_t lbuf[hd::SEG + 16];
+  for (uint32_t l = 0; l < (uint32_t)hd::WAVE; l++)
+    lane_seq_emit(gw, sp->nslot[l], l, L[l] + lc[l].lead - Q[l],
+                  [&](uint32_t k, uint32_t v) { lbuf[L[l] + k] = (uint8_t)v; },
+                  [&](uint32_t j, uint32_t run, uint32_t ml, uint32_t off) {
+                    A[S[l] + j] = run | (ml << 16); B[S[l] + j] = (uint16_t)(off - 1u); });
+  memcpy(seq_a(tok), A, nseq * 4u);
+  memcpy(seq_b(tok), B, nseq * 2u);
+  if (raw) {
+    const uint32_t h = lit_header(nlit, out + 3);
+    memcpy(out + 3 + h, lbuf, nlit);
+  }
+}
+#endif
+
+// the compact sequences last to first (8 per batch: one memory latency per batch)
+template <class F>
+HZ_HD void seqs_bwd(const uint32_t* A, const uint16_t* B, uint32_t n, F&& emit) {
+  hz_gcu32* const ga = HZ_GLOBAL(hz_gcu32*, A);
+  const hz_gu16* const gb = HZ_GLOBAL(const hz_gu16*, B);
+  uint32_t i1 = n;
+  while (i1 > 0u) {
+    const uint32_t cnt = i1 < 8u ? i1 : 8u;
+    uint32_t av[8], bv[8];
+HZ_UNROLL
+    for (uint32_t i = 0; i < 8u; i++) {
+      const uint32_t k = i < cnt ? i1 - 1u - i : i1 - 1u;
+      av[i] = ga[k];
+      bv[i] = gb[k];
+    }
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t a = av[0], b = bv[0];
+HZ_UNROLL
+      for (uint32_t i = 0; i + 1 < 8u; i++) { av[i] = av[i + 1]; bv[i] = bv[i + 1]; }
+      emit(a & 0xffffu, a >> 16, b + 1u);
+    }
+    i1 -= cnt;
+  }
+}
+
 // Writes segment `seg` of a stream as one zstd block (header included) at out (cap bytes
 // of scratch, >= ZCAP).  tok / sp: the segment's parse tokens and counts; job / s0: the
 // stream input (a raw block copies the segment from it).  Returns the block size.
+// seqs: tok holds the compact sequences (zstd_seq_kernel), and out + 3 the raw literals section
+// unless lsize (the Huffman section in lsec)
 HZ_HD uint32_t encode_segment(const Tabs& T, const CodeTabs& ct, const uint16_t* tok, const hd::SegParse* sp, const hd::EncJob& job,
                               uint32_t s0, uint32_t seglen, uint32_t last, uint8_t* out, uint32_t cap,
-                              const uint8_t* lsec = nullptr, uint32_t lsize = 0) {
+                              const uint8_t* lsec = nullptr, uint32_t lsize = 0, int seqs = 0) {
   hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, tok);
   uint32_t nlit = 0, nseq = 0;
   for (uint32_t s = 0; s < 256u; s++) nlit += sp->freq[s];
@@ -716,7 +833,10 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const CodeTabs& ct, const uint16_t*
   // literal bytes, forward over the lanes' token ranges
   // (gathered in a register and stored a dword at a time: the lane's scratch block is
   // 4-byte aligned; bytes already written below p in the first word are kept)
-  if (!lsize && !over) {
+  if (!lsize && !over && seqs) {
+    if (p + nlit > cap) over = 1;           // (zstd_seq_kernel wrote them)
+    else p += nlit;
+  } else if (!lsize && !over) {
     if (p + nlit > cap) {
       over = 1;
     } else {
@@ -770,7 +890,8 @@ HZ_HD uint32_t encode_segment(const Tabs& T, const CodeTabs& ct, const uint16_t*
       bw_add(w, q.mlv, zs::ml_bits(q.mlc));
       bw_add(w, q.ofv, q.ofc);
     };
-    walk_sequences(gw, sp, emit);
+    if (seqs) seqs_bwd(seq_a(tok), seq_b(tok), nseq, emit);
+    else walk_sequences(gw, sp, emit);
     bw_add(w, sml, T.ml.log);
     bw_add(w, sof, T.of.log);
     bw_add(w, sll, T.ll.log);

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
+#include <algorithm>
 #include "../../hsds_amd/csrc/deflate_wave.h"
 #include "../../hsds_amd/csrc/lz4_enc.h"
 #include "../../hsds_amd/csrc/zstd_enc.h"
@@ -124,6 +125,8 @@ extern "C" int64_t emu_zstd_frame_t(const uint8_t* src, uint32_t n, uint8_t* dst
 extern "C" int64_t emu_zstd_frame(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level) {
   return emu_zstd_frame_t(src, n, dst, cap, level, 1);
 }
+static int g_zstd_seqs = 0;     // 1: the zstd_seq_kernel path (compact sequences, literals pre-written)
+extern "C" void emu_zstd_set_seqs(int on) { g_zstd_seqs = on; }
 extern "C" int64_t emu_zstd_frame_t(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap, int level, int tables) {
   const uint32_t nseg = hd::nsegments(n);
   std::vector<hd::SegParse> sp(nseg);
@@ -157,8 +160,13 @@ extern "C" int64_t emu_zstd_frame_t(const uint8_t* src, uint32_t n, uint8_t* dst
     const uint32_t seglen = n - s0 < (uint32_t)hd::SEG ? n - s0 : (uint32_t)hd::SEG;
     const uint32_t lsz = !hze::huff_lit_level(level) ? 0u
                          : hze::lit_section(*ls, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], lsec.data());
+    if (g_zstd_seqs) {
+      std::fill(blk.begin(), blk.end(), (uint8_t)0xA5);
+      hze::extract_sequences(tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], blk.data(), lsz == 0u);
+    }
     const uint32_t k = hze::encode_segment(T, ct, tok.data() + (size_t)s * hd::SEG_TOK, &sp[s], job, s0, seglen,
-                                           s + 1 == nseg ? 1u : 0u, blk.data(), hze::ZCAP, lsec.data(), lsz);
+                                           s + 1 == nseg ? 1u : 0u, blk.data(), hze::ZCAP, lsec.data(), lsz,
+                                           g_zstd_seqs);
     put(blk.data(), k);
   }
   free(ls);

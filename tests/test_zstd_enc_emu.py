@@ -178,3 +178,29 @@ def test_count_kernel_lane_algorithm_matches_sequence_walk(name, level):
     nseg = L.emu_zstd_counts(a.ctypes.data if a.size else 0, a.size, level, cw.ctypes.data, cl.ctypes.data)
     assert nseg >= 1
     assert np.array_equal(cw, cl), (name, np.nonzero(cw != cl))
+
+
+@pytest.mark.parametrize("name", sorted(CASES) + ["long_literal_runs"])
+@pytest.mark.parametrize("level", [1, 5, 9])
+def test_compact_sequence_path_writes_the_same_frames(emu, name, level):
+    """zstd_seq_kernel's path (round 6): the segment's sequences extracted once into a compact
+    array over its token slots and its raw literals written into the block scratch first, then
+    encode_segment in seq mode -- the frames must equal the slot-walking path's byte for byte"""
+    L = ctypes.CDLL(LIB)
+    L.emu_zstd_set_seqs.argtypes = [ctypes.c_int]
+    r = np.random.default_rng(3)
+    a = _long_literal_runs(r) if name == "long_literal_runs" else np.ascontiguousarray(CASES[name](r), np.uint8)
+    try:
+        L.emu_zstd_set_seqs(0)
+        f0 = frame(L_frame(L), a, level)
+        L.emu_zstd_set_seqs(1)
+        f1 = frame(L_frame(L), a, level)
+    finally:
+        L.emu_zstd_set_seqs(0)
+    assert f0 == f1, (name, level, len(f0), len(f1))
+
+
+def L_frame(L):
+    L.emu_zstd_frame.restype = ctypes.c_int64
+    L.emu_zstd_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+    return L
