@@ -872,7 +872,7 @@ def run_cfg4(args, dev, rank, world):
     return out
 
 
-TRAFFIC_ROUND = "r5"
+TRAFFIC_ROUND = "r6"
 
 
 def run_cfg4_full(args, dev, rank, world):

@@ -56,7 +56,7 @@ class CopyDesc(ctypes.Structure):
                 ("count", ctypes.c_int64 * MAX_RANK), ("rank", ctypes.c_int32), ("itemsize", ctypes.c_int32)]
 
 
-PLAN_PACK, PLAN_PLACE, PLAN_GATHER, PLAN_APPLY, PLAN_APPLY_BCAST = 0, 1, 2, 3, 4
+PLAN_PACK, PLAN_PLACE, PLAN_GATHER, PLAN_APPLY, PLAN_APPLY_BCAST, PLAN_DIRECT = 0, 1, 2, 3, 4, 5
 
 
 class PlanGeom(ctypes.Structure):

@@ -224,8 +224,9 @@ class SelectionPlan:
     # tables and per-piece grid index / packed offset / chunk offset travel over PCIe --
     def device_descs(self, mode, device, ranks=None, chunk_offsets=None, packed_base=0, slab_base=0):
         """COPY_DESC records as a uint8 device tensor for `mode` (nat.PLAN_*):
-        PACK / APPLY / APPLY_BCAST for ranks=[r] with chunk_offsets (one per owned piece),
-        PLACE / GATHER for `ranks` (default all) at their rank_base offsets."""
+        PACK / APPLY / APPLY_BCAST / DIRECT for ranks=[r] with chunk_offsets (one per owned
+        piece), PLACE / GATHER for `ranks` (default all) at their rank_base offsets.
+        DIRECT is direct_descs built on the device (chunk -> slab at slab_base)."""
         import torch
         from . import _native as nat
         from .engine import COPY_DESC_DTYPE, _ptr, _stream_handle
@@ -235,7 +236,7 @@ class SelectionPlan:
         out = torch.empty(max(n, 1) * COPY_DESC_DTYPE.itemsize, dtype=torch.uint8, device=device)
         if n == 0:
             return out[:0]
-        chunk_side = mode in (nat.PLAN_PACK, nat.PLAN_APPLY, nat.PLAN_APPLY_BCAST)
+        chunk_side = mode in (nat.PLAN_PACK, nat.PLAN_APPLY, nat.PLAN_APPLY_BCAST, nat.PLAN_DIRECT)
         if mode == nat.PLAN_APPLY_BCAST:
             poff = np.full(n, int(packed_base), np.int64)
         elif chunk_side:
@@ -470,11 +471,22 @@ class ShardedReader:
             "d_dst": d_dst,
             "d_status": torch.zeros(max(len(present), 1), dtype=torch.int32, device=self.device),
             "offs": offs,
-            "d_pack": self.plan.device_descs(nat.PLAN_PACK, self.device, ranks=[self.rank], chunk_offsets=offs),
             "npack": len(ids),
-            "d_place": self.plan.device_descs(nat.PLAN_PLACE, self.device) if self.rank == self.root else None,
             "itemsize": self.plan.itemsize,
+            **self._records(self.plan, offs),
         }
+
+    def _records(self, plan, offs):
+        """Copy records of a staged batch.  The root places its own pieces straight from its
+        decoded chunks into the slab (one copy, no packed buffer: DIRECT) and the peers'
+        packed pieces from the gathered buffer (PLACE); every other rank packs (PACK)."""
+        if self.rank != self.root:
+            return {"d_pack": plan.device_descs(nat.PLAN_PACK, self.device, ranks=[self.rank], chunk_offsets=offs),
+                    "d_direct": None, "d_place": None}
+        peers = [r for r in range(plan.world) if r != self.root and len(plan.by_rank[r])]
+        return {"d_pack": None,
+                "d_direct": plan.device_descs(nat.PLAN_DIRECT, self.device, ranks=[self.rank], chunk_offsets=offs),
+                "d_place": plan.device_descs(nat.PLAN_PLACE, self.device, ranks=peers) if peers else None}
 
     def replan(self, st, plan):
         """Take a freshly built plan of the same request (same chunks per rank) for a
@@ -483,52 +495,62 @@ class ShardedReader:
         if [len(b) for b in plan.by_rank] != [len(b) for b in self.plan.by_rank]:
             raise ValueError("replan needs the same request")
         self.plan = plan
-        st["d_pack"] = plan.device_descs(nat.PLAN_PACK, self.device, ranks=[self.rank], chunk_offsets=st["offs"])
-        st["d_place"] = plan.device_descs(nat.PLAN_PLACE, self.device) if self.rank == self.root else None
+        st.update(self._records(plan, st["offs"]))
         return st
 
-    def decode_and_pack(self, st, packed, stream=None):
+    def _decode(self, st, stream=None):
         if st["n"]:
             self.eng.decode(st["d_src"], st["d_desc"], st["d_dst"], st["d_status"], compressor=self.compressor,
                             shuffle=self.shuffle, itemsize=st["itemsize"], stream=stream)
+
+    def decode_and_pack(self, st, packed, stream=None):
+        """A non-root rank: decode, then pack its pieces for the gather."""
+        self._decode(st, stream)
         if st["npack"]:
             self.eng.copy(st["d_dst"], packed, st["d_pack"], stream=stream)
+
+    def decode_and_place(self, st, slab, stream=None):
+        """The root: decode, then copy its own pieces straight into the slab."""
+        self._decode(st, stream)
+        if st["npack"]:
+            self.eng.copy(st["d_dst"], slab, st["d_direct"], stream=stream)
 
     def read(self, st, slab=None, gathered=None, fill_value=None, check=True):
         """Whole read; returns the slab (uint8 tensor, C order) on the root."""
         torch = self.torch
         plan = self.plan
         if self.rank == self.root:
-            if gathered is None:
+            if slab is None:
+                slab = torch.empty(max(plan.slab_nbytes, 1), dtype=torch.uint8, device=self.device)
+                fill = np.zeros(1, plan.dtype)
+                if fill_value is not None:
+                    fill[...] = fill_value
+                if fill.view(np.uint8).any():
+                    pat = torch.from_numpy(np.full(plan.slab_nbytes // plan.itemsize, fill[0], plan.dtype)
+                                           .view(np.uint8).copy()).to(self.device)
+                    slab[:plan.slab_nbytes].copy_(pat)
+                else:
+                    slab.zero_()
+            if plan.world > 1 and gathered is None:
                 gathered = torch.empty(max(plan.gathered_nbytes, 1), dtype=torch.uint8, device=self.device)
+            # the root's own section of the gathered buffer stays unused: its pieces go
+            # straight from its decoded chunks into the slab
             b = int(plan.rank_base[self.root])
-            packed = gathered[b:b + max(plan.rank_bytes[self.root], 1)]
+            packed = None if plan.world == 1 else gathered[b:b + max(plan.rank_bytes[self.root], 1)]
+            self.decode_and_place(st, slab)
         else:
             packed = torch.empty(max(plan.rank_bytes[self.rank], 1), dtype=torch.uint8, device=self.device)
-        self.decode_and_pack(st, packed)
+            self.decode_and_pack(st, packed)
         if check and st["n"]:
             bad = st["d_status"][:st["n"]].ne(0).any()
             if bool(bad):
                 raise RuntimeError("chunk decode failed: " + str(torch.unique(st["d_status"][:st["n"]]).tolist()))
         if plan.world > 1:
-            got = exchange(packed, plan, self.rank, self.root, self.group, gathered)
-        else:
-            got = gathered
+            exchange(packed, plan, self.rank, self.root, self.group, gathered)
         if self.rank != self.root:
             return None
-        if slab is None:
-            slab = torch.empty(max(plan.slab_nbytes, 1), dtype=torch.uint8, device=self.device)
-            fill = np.zeros(1, plan.dtype)
-            if fill_value is not None:
-                fill[...] = fill_value
-            if fill.view(np.uint8).any():
-                pat = torch.from_numpy(np.full(plan.slab_nbytes // plan.itemsize, fill[0], plan.dtype)
-                                       .view(np.uint8).copy()).to(self.device)
-                slab[:plan.slab_nbytes].copy_(pat)
-            else:
-                slab.zero_()
-        if len(plan.idx):
-            self.eng.copy(got, slab, st["d_place"])
+        if st["d_place"] is not None:
+            self.eng.copy(gathered, slab, st["d_place"])
         return slab
 
 

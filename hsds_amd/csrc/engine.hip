@@ -2229,6 +2229,26 @@ __global__ void plan_descs_kernel(hsds_plan_geom g, const int64_t* __restrict__ 
   for (int d = HSDS_MAX_RANK - 1; d >= 0; d--) {
     if (d < R) { pst[d] = acc; acc *= cnt[d]; } else pst[d] = 0;
   }
+  if (g.mode == HSDS_PLAN_DIRECT) {
+    // chunk [chunk_sel] -> slab [data_sel]: no packed buffer in between
+    int64_t so = coff[k], dof = g.slab_base;
+#pragma unroll
+    for (int d = 0; d < HSDS_MAX_RANK; d++) {
+      if (d < R) {
+        so += cst[d] * g.chunk_stride[d];
+        dof += dst[d] * g.slab_stride[d];
+      }
+      r.src_stride[d] = d < R ? g.chunk_stride[d] * g.step[d] : 0;
+      r.dst_stride[d] = d < R ? g.slab_stride[d] : 0;
+      r.count[d] = cnt[d];
+    }
+    r.src_off = (uint64_t)so;
+    r.dst_off = (uint64_t)dof;
+    r.rank = R;
+    r.itemsize = g.itemsize;
+    out[k] = r;
+    return;
+  }
   const bool chunk_side = g.mode == HSDS_PLAN_PACK || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST;
   const bool to_region = g.mode == HSDS_PLAN_PLACE || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST;
   int64_t roff = chunk_side ? coff[k] : g.slab_base;
@@ -2338,9 +2358,10 @@ int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d
   if (n == 0) return HSDS_OK;
   const hsds_plan_geom g = *geom;
   if (g.rank < 1 || g.rank > HSDS_MAX_RANK || g.itemsize < 1 || g.mode < HSDS_PLAN_PACK ||
-      g.mode > HSDS_PLAN_APPLY_BCAST || !d_tabs || !d_piece || !d_poff || !d_out)
+      g.mode > HSDS_PLAN_DIRECT || !d_tabs || !d_piece || (!d_poff && g.mode != HSDS_PLAN_DIRECT) || !d_out)
     return HSDS_ERR_ARG;
-  const bool chunk_side = g.mode == HSDS_PLAN_PACK || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST;
+  const bool chunk_side = g.mode == HSDS_PLAN_PACK || g.mode == HSDS_PLAN_APPLY || g.mode == HSDS_PLAN_APPLY_BCAST ||
+                          g.mode == HSDS_PLAN_DIRECT;
   if (chunk_side && !d_coff) return HSDS_ERR_ARG;
   for (int d = 0; d < g.rank; d++)
     if (g.nk[d] < 1) return HSDS_ERR_ARG;

@@ -198,11 +198,13 @@ typedef struct {
 #define HSDS_PLAN_GATHER 2      /* slab [data_sel] -> packed piece (SN write gather)     */
 #define HSDS_PLAN_APPLY 3       /* packed piece -> chunk [chunk_sel] (PUT_Chunk)         */
 #define HSDS_PLAN_APPLY_BCAST 4 /* the one element at d_poff[k] -> chunk [chunk_sel]     */
+#define HSDS_PLAN_DIRECT 5      /* decoded chunk [chunk_sel] -> slab [data_sel] (PACK and
+                                   PLACE in one record: the root's own pieces; d_poff unused) */
 /* One copy record per piece, built on the device (chunk_crawl.py:118-150,395-418):
  * d_tabs holds, per dimension d in order, nk[d] chunk-relative starts, nk[d] counts and
  * nk[d] slab starts (int64); d_piece[k] is piece k's index in the product grid,
  * d_poff[k] its byte offset in the packed buffer and d_coff[k] (PACK / APPLY) the byte
- * offset of its chunk array.  Records go to d_out[0..n). */
+ * offset of its chunk array (PACK / APPLY / DIRECT).  Records go to d_out[0..n). */
 int hsds_plan_descs(hsds_engine* e, const hsds_plan_geom* geom, const int64_t* d_tabs, const int64_t* d_piece,
                     const int64_t* d_poff, const int64_t* d_coff, int64_t n, hsds_copy_desc* d_out,
                     void* stream);

@@ -1,7 +1,7 @@
 """Device-built hyperslab copy records (hsds_plan_descs) equal the host plan's records
 (crawl.SelectionPlan._descs, the restatement of chunk_crawl.py:118-150,395-418 pinned
-by the selection goldens) for every direction: read pack / place, write gather / apply /
-broadcast apply, over strided, offset and sparse (step > chunk) selections."""
+by the selection goldens) for every direction: read pack / place / direct, write gather /
+apply / broadcast apply, over strided, offset and sparse (step > chunk) selections."""
 import numpy as np
 import pytest
 
@@ -54,4 +54,7 @@ def test_device_records_equal_host(dev, case):
         assert np.array_equal(device(plan.device_descs(nat.PLAN_APPLY_BCAST, dev, ranks=[r], chunk_offsets=co,
                                                        packed_base=8)),
                               host(plan.apply_descs(r, co, packed_base=8, broadcast=True))), r
+        assert np.array_equal(device(plan.device_descs(nat.PLAN_DIRECT, dev, ranks=[r], chunk_offsets=co,
+                                                       slab_base=1024)),
+                              host(plan.direct_descs(r, co, slab_base=1024))), r
     assert COPY_DESC_DTYPE.itemsize == 216

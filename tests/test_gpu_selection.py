@@ -89,9 +89,10 @@ CASES = [
 
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_sharded_read_matches_numpy(case, dev, oracle_lib):
-    """Every rank of the plan runs in this process (on cuda:0) and packs into its slice
-    of the gathered buffer; the root placement then assembles the slab -- the same
-    kernels and descriptors the multi-GPU run uses around the RCCL exchange."""
+    """Every rank of the plan runs in this process (on cuda:0); the non-root ranks pack
+    into their slices of the gathered buffer, the root copies its own pieces straight
+    into the slab and then places the peers' -- the same kernels and descriptors the
+    multi-GPU run uses around the RCCL exchange."""
     import torch
     from hsds_amd import crawl, selection as sel
     dims, layout, dt, selection, world = CASES[case][:5]
@@ -116,18 +117,53 @@ def test_sharded_read_matches_numpy(case, dev, oracle_lib):
         rd = crawl.ShardedReader(plan, r, dev, root=0, compressor=comp, shuffle=1 if comp else 0)
         st = rd.upload(blobs, fill_value=fill)
         b = int(plan.rank_base[r])
-        rd.decode_and_pack(st, gathered[b:b + max(plan.rank_bytes[r], 1)])
-        if st["n"]:
-            assert int(st["d_status"][:st["n"]].abs().sum()) == 0
+        if r:
+            rd.decode_and_pack(st, gathered[b:b + max(plan.rank_bytes[r], 1)])
+            assert st["d_direct"] is None and st["d_place"] is None
         sts.append((rd, st))
+    # the root: its own pieces straight into the slab, then the peers' packed pieces
     rd0, st0 = sts[0]
     slab = torch.full((plan.slab_nbytes,), 0, dtype=torch.uint8, device=dev)
     slab.copy_(torch.from_numpy(np.full(plan.slab_shape, fill, dt).view(np.uint8).reshape(-1).copy()).to(dev))
-    rd0.eng.copy(gathered, slab, st0["d_place"])
+    rd0.decode_and_place(st0, slab)
+    assert st0["d_pack"] is None and (world > 1 or st0["d_place"] is None)
+    if st0["d_place"] is not None:
+        rd0.eng.copy(gathered, slab, st0["d_place"])
+    for _, st in sts:
+        if st["n"]:
+            assert int(st["d_status"][:st["n"]].abs().sum()) == 0
     got = slab.cpu().numpy().view(dt).reshape(plan.slab_shape)
     expect = full[selection].copy()
     if missing is not None:
         # the missing chunk's piece reads as the fill value
         p = plan.pieces[0]
         expect[p.data_slices] = fill
+    assert np.array_equal(got, expect)
+
+
+@pytest.mark.parametrize("case", [0, 2, 7])
+def test_single_rank_read(case, dev, oracle_lib):
+    """ShardedReader.read at world size 1: decode + one direct copy per piece into a
+    fill-valued slab (a missing chunk reads as the fill value)."""
+    from hsds_amd import crawl, selection as sel
+    dims, layout, dt, selection = CASES[case][:4]
+    comp = CASES[case][5] if len(CASES[case]) > 5 else "zlib"
+    rng = np.random.default_rng(100 + case)
+    full = (np.cumsum(rng.normal(size=dims), axis=-1) * 100).astype(dt)
+    plan = crawl.SelectionPlan("d-0a1b2c3d-4e5f6a7b-8c9d-0e1f2a-3b4c5d", dims, layout, selection, dt, 1)
+    missing = plan.pieces[-1].chunk_id
+    blobs = {}
+    for cid in plan.chunk_ids(0):
+        if cid == missing:
+            continue
+        idx = sel.getChunkIndex(cid)
+        c = np.zeros(layout, dt)
+        reg = tuple(slice(i * L, min((i + 1) * L, n)) for i, L, n in zip(idx, layout, dims))
+        c[tuple(slice(0, s.stop - s.start) for s in reg)] = full[reg]
+        blobs[cid] = oracle_lib.blosc_encode(c.tobytes(), typesize=1, clevel=4, shuffle=1) if comp else c.tobytes()
+    rd = crawl.ShardedReader(plan, 0, dev, compressor=comp, shuffle=1 if comp else 0)
+    st = rd.upload(blobs, fill_value=3)
+    got = rd.read(st, fill_value=3).cpu().numpy()[:plan.slab_nbytes].view(dt).reshape(plan.slab_shape)
+    expect = full[selection].copy()
+    expect[plan.pieces[-1].data_slices] = 3
     assert np.array_equal(got, expect)

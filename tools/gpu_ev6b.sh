@@ -5,6 +5,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_encode.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_enc_tests.log 2>&1
+rc=$?; echo "encode tests rc=$rc"; tail -2 gpurun_out/gpu_enc_tests.log; [ $rc -eq 0 ] || exit $rc
+bash tools/ab_enc5.sh abtmp/attr_base.so abtmp/zseq.so abtmp/attr_base.so abtmp/zseq.so || exit 1
 bash tools/ab.sh abtmp/r5.so abtmp/attr_base.so abtmp/r5.so abtmp/attr_base.so || exit 1
 RND=r6 bash tools/pmc_traffic.sh > gpurun_out/traffic.log 2>&1; rc=$?; tail -4 gpurun_out/traffic.log; [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_sq_bench.sh sq_r6 > gpurun_out/sq_r6.log 2>&1 || { tail gpurun_out/sq_r6.log; exit 1; }
