@@ -110,14 +110,23 @@ constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = 
 // no s_waitcnt vmcnt(0) -- loads in flight (the next span's records) stay in flight, and
 // two wavefronts of one workgroup can decode two windows of a stream independently
 // (inflate2w_kernel); their hand-offs are workgroup-scope release / acquire on Ctl.
-// phase E: match records are staged per lane and stored as whole aligned 32-byte groups
+// phases A / E: match records are staged per lane and stored as whole aligned 32-byte groups
 // (16-byte stores of each lane's own records, scattered over 64 lanes, cost about 4x their
-// bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt)
+// bytes in HBM writes plus L2 fills: measured, profiles/r2_traffic_attribution.txt).  Round 6
+// A/B on one box (profiles/r6_ab_record_groups.txt): 16-byte groups 196.1-200.8 GB/s, 32-byte
+// groups (last record from registers, no ring mirror: 16 waves per CU) 203.0-203.2, HBM traffic
+// per launch 90.4 -> 77.8 GB; 32-byte groups staged whole cost the 16th wave (173 GB/s)
 #ifndef HZ2_RGRP
-#define HZ2_RGRP 2
+#define HZ2_RGRP 4
 #endif
 constexpr uint32_t RGRP = HZ2_RGRP;
 static_assert(RGRP == 2 || RGRP == 4 || RGRP == 8, "RGRP: 2, 4 or 8 records");
+// the last record of a group is stored from registers with the staged ones (it completes
+// the group), so the LDS stage holds RGRP - 1 records per lane (1: on)
+#ifndef HZ2_RLAST
+#define HZ2_RLAST 1
+#endif
+constexpr uint32_t RSTG = RGRP - (HZ2_RLAST ? 1u : 0u);    // staged records per lane
 // bit ring (phases A .. E): RS stream words per lane in LDS, refilled a quad at a time at
 // wave-uniform ticks; a token reads at most 48 bits, so a window advances at most 1.5
 // words per token
@@ -126,7 +135,8 @@ static_assert(RGRP == 2 || RGRP == 4 || RGRP == 8, "RGRP: 2, 4 or 8 records");
 #endif
 constexpr uint32_t RS = HZ2_RS;           // ring words per lane (a multiple of 4)
 #ifndef HZ2_MIRROR
-#define HZ2_MIRROR 1                      // a copy of ring slot 0 after slot RS - 1 (no wrap select)
+#define HZ2_MIRROR 0                      // a copy of ring slot 0 after slot RS - 1 (no wrap select;
+                                          // its 256 bytes of LDS go to the record stage instead)
 #endif
 // phase E literal staging: bytes per lane, stored whole (16: one 16-byte store per 16 literals)
 #ifndef HZ2_OS
@@ -205,7 +215,7 @@ struct alignas(16) Shared {
         uint32_t rec[K][WAVE];        // phases A .. R: recorded token starts (lane-interleaved)
         struct {                      // phase E
           alignas(16) uint8_t ostage[WAVE][OS];     // each lane's current OS bytes of the literal stream
-          uint64_t rstage[WAVE][RGRP];              // each lane's current group of match records
+          uint64_t rstage[WAVE][RSTG];              // each lane's current group of match records
         };
       };
     };

@@ -86,13 +86,17 @@ struct HzProf { int unused; };
 namespace hz {
 
 constexpr int WAVE = 64;
-constexpr int LL_ROOT = 10;
+#ifndef HZ_LL_ROOT
+#define HZ_LL_ROOT 10
+#endif
+constexpr int LL_ROOT = HZ_LL_ROOT;
+static_assert(LL_ROOT == 9 || LL_ROOT == 10, "literal/length root: 9 or 10 bits");
 constexpr int D_ROOT = 8;
 // second-level entries (codes longer than the root).  Sized at or above zlib's exact
 // worst cases (ENOUGH: 286 symbols / root 10 -> 308 extra entries; 30 symbols /
 // root 8 -> at most 3 x 128), so every complete code fits and no slow path exists.
 #ifndef HZ_LL_SUB
-#define HZ_LL_SUB 320
+#define HZ_LL_SUB (HZ_LL_ROOT == 9 ? 352 : 320)     // zlib ENOUGH_LENS - 2^root: 340 / 308
 #endif
 constexpr int LL_SUB = HZ_LL_SUB;
 constexpr int D_SUB = 384;

@@ -3,6 +3,7 @@ iterating the 64 lanes) checked against libz and the oracle: the kernel's exact 
 (long segments, recorded-start sync, repairs, emit, batched match resolve through the match
 ring, fused byte unshuffle) runs on CPU; `-m gpu` tests run the same source on the MI355X."""
 import ctypes
+import hashlib
 import os
 import subprocess
 import zlib
@@ -19,10 +20,14 @@ STATS = ("windows blocks stored tokens matches lanes_valid repairs repair_lanes 
 
 @pytest.fixture(scope="module")
 def emu():
+    # HZ2_EMU_FLAGS="-DHZ2_RGRP=4 ...": the same tests over an experiment build of the kernel
+    flags = os.environ.get("HZ2_EMU_FLAGS", "").split()
+    tag = hashlib.sha1(" ".join(flags).encode()).hexdigest()[:10]
+    lib = EMU if not flags else os.path.join("/tmp", f"libinflate2_emu_{tag}.so")
     hdrs = [os.path.join(ROOT, "hsds_amd", "csrc", h) for h in ("inflate2.h", "inflate2_stream.inc", "inflate_wave.h")]
-    if not os.path.exists(EMU) or os.path.getmtime(EMU) < max(os.path.getmtime(p) for p in [SRC] + hdrs):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", EMU, SRC])
-    L = ctypes.CDLL(EMU)
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(p) for p in [SRC] + hdrs):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread"] + flags + ["-o", lib, SRC])
+    L = ctypes.CDLL(lib)
     L.emu_inflate2.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
     L.emu_inflate2_nw.argtypes = L.emu_inflate2.argtypes + [ctypes.c_int]
