@@ -527,6 +527,18 @@ def run_cfg5_sharded(args, dev, rank, world):
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        if os.environ.get("HSDS_PROFILE_CFG5W") and rank == 0:
+            # host hot spots of the write path (tools/gpu_r6p.sh): two more steps under cProfile
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            pr.disable()
+            print(f"--- cfg5w {name} host profile (2 steps)", file=sys.stderr)
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -1250,7 +1250,6 @@ __global__ void __launch_bounds__(64) zstd_seq_kernel(const uint32_t* __restrict
                                                       uint32_t seg_cap) {
   __shared__ uint32_t sa[hze::SEQ_MAX];
   __shared__ uint16_t sb[hze::SEQ_MAX];
-  __shared__ uint8_t lbuf[hd::SEG + 16];
   uint32_t total = segoffs[nchunks];
   if (total > seg_cap) total = seg_cap;
   const uint32_t l = threadIdx.x;
@@ -1258,39 +1257,29 @@ __global__ void __launch_bounds__(64) zstd_seq_kernel(const uint32_t* __restrict
     uint16_t* const ts = tok + (size_t)s * hd::SEG_TOK;
     hz_gcu32* const gw = HZ_GLOBAL(hz_gcu32*, ts);
     const uint32_t ns = sp[s].nslot[l];
-    const hze::LaneSeq r = hze::lane_seq_count(gw, ns, l);
+    const hze::LaneSeq r = hze::lane_seq_count<16>(gw, ns, l);
     const uint32_t Li = hz::wave_incl_scan_dpp(r.lits), Si = hz::wave_incl_scan_dpp(r.nm);
     const uint32_t L = Li - r.lits, S = Si - r.nm;
     const uint32_t qprev = hz::wave_excl_max(r.hm ? Li - r.run : 0u, (int)l);
     const uint32_t nlit = (uint32_t)__builtin_amdgcn_readlane((int)Li, 63);
     const uint32_t nseq = (uint32_t)__builtin_amdgcn_readlane((int)Si, 63);
-    hze::lane_seq_emit(gw, ns, l, L + r.lead - qprev,
-                       [&](uint32_t k, uint32_t v) { lbuf[L + k] = (uint8_t)v; },
-                       [&](uint32_t j, uint32_t run, uint32_t ml, uint32_t off) {
-                         sa[S + j] = run | (ml << 16);
-                         sb[S + j] = (uint16_t)(off - 1u);
-                       });
+    // the raw literals section (levels below 6): its header after the block header's 3 bytes
+    // (encode_segment writes those last), then every lane's literal bytes at their offsets
+    const bool raw = lsz[s] == 0u;
+    uint8_t h[3] = {0, 0, 0};
+    const uint32_t p0 = 3u + hze::lit_header(nlit, h);
+    uint8_t* const blk = zscr + (size_t)s * hze::ZCAP;
+    if (raw && l < p0 - 3u) blk[3u + l] = l == 0u ? h[0] : l == 1u ? h[1] : h[2];
+    hze::lane_seq_emit<16>(gw, ns, l, L + r.lead - qprev,
+                           [&](uint32_t k, uint32_t v) { if (raw) blk[p0 + L + k] = (uint8_t)v; },
+                           [&](uint32_t j, uint32_t run, uint32_t ml, uint32_t off) {
+                             sa[S + j] = run | (ml << 16);
+                             sb[S + j] = (uint16_t)(off - 1u);
+                           });
     __syncthreads();            // every lane's slot reads are done: the sequences may overwrite them
     uint32_t* const ga = hze::seq_a(ts);
     uint16_t* const gb = hze::seq_b(ts);
     for (uint32_t i = l; i < nseq; i += 64u) { ga[i] = sa[i]; gb[i] = sb[i]; }
-    if (lsz[s] == 0u) {
-      // dwords of the block scratch from byte 0: bytes 0-2 the block header (encode_segment
-      // writes it last), then the literals section header and the literal bytes
-      uint32_t* const out = (uint32_t*)(zscr + (size_t)s * hze::ZCAP);
-      uint8_t h[3] = {0, 0, 0};
-      const uint32_t p0 = 3u + hze::lit_header(nlit, h), end = p0 + nlit;
-      for (uint32_t k = l; 4u * k < end; k += 64u) {
-        uint32_t w = 0;
-HZ_UNROLL
-        for (uint32_t b = 0; b < 4u; b++) {
-          const uint32_t x = 4u * k + b;
-          const uint32_t v = x < 3u ? 0u : x < p0 ? h[x - 3u] : x < end ? lbuf[x - p0] : 0u;
-          w |= v << (8u * b);
-        }
-        out[k] = w;
-      }
-    }
     __syncthreads();            // (the LDS of the next segment)
   }
 }

@@ -555,22 +555,27 @@ HZ_HD uint32_t lit_section(LitShared& sh, const uint16_t* tok, const hd::SegPars
 // w * WAVE + l), forward or backward, loaded 8 dwords at a time: a batch costs one memory
 // latency instead of one per slot (the block writes in between would otherwise keep the
 // compiler from hoisting the loads).
-template <class F>
-HZ_HD void slots_fwd(hz_gcu32* gw, uint32_t ns, uint32_t l, F&& f) {
+// the lane's slots in order, NB dwords (2 NB slots) per batch of loads
+template <uint32_t NB, class F>
+HZ_HD void slots_fwd_n(hz_gcu32* gw, uint32_t ns, uint32_t l, F&& f) {
   const uint32_t nw = (ns + 1u) >> 1;
-  for (uint32_t w0 = 0; w0 < nw; w0 += 8u) {
-    uint32_t wv[8];
+  for (uint32_t w0 = 0; w0 < nw; w0 += NB) {
+    uint32_t wv[NB];
 HZ_UNROLL
-    for (uint32_t i = 0; i < 8u; i++) wv[i] = w0 + i < nw ? gw[(size_t)(w0 + i) * (uint32_t)hd::WAVE + l] : 0u;
-    const uint32_t cnt = nw - w0 < 8u ? nw - w0 : 8u;
+    for (uint32_t i = 0; i < NB; i++) wv[i] = w0 + i < nw ? gw[(size_t)(w0 + i) * (uint32_t)hd::WAVE + l] : 0u;
+    const uint32_t cnt = nw - w0 < NB ? nw - w0 : NB;
     for (uint32_t k = 0; k < cnt; k++) {
       const uint32_t word = wv[0];
 HZ_UNROLL
-      for (uint32_t i = 0; i + 1 < 8u; i++) wv[i] = wv[i + 1];
+      for (uint32_t i = 0; i + 1 < NB; i++) wv[i] = wv[i + 1];
       f(word & 0xffffu);
       if (2u * (w0 + k) + 1u < ns) f(word >> 16);
     }
   }
+}
+template <class F>
+HZ_HD void slots_fwd(hz_gcu32* gw, uint32_t ns, uint32_t l, F&& f) {
+  slots_fwd_n<8>(gw, ns, l, static_cast<F&&>(f));
 }
 template <class F>
 HZ_HD void slots_bwd(hz_gcu32* gw, uint32_t ns, uint32_t l, F&& f) {
@@ -694,7 +699,8 @@ HZ_HD void count_segment(const CodeTabs& ct, const uint16_t* tok, const hd::SegP
 // lines, 64 segments' slots per wave.  zstd_seq_kernel (one wave per segment, each lane on its
 // own parse lane: coalesced rows) turns the slots into a compact sequence array in the same
 // scratch -- a[i] = literal run | match length << 16, b[i] = offset - 1, in segment order --
-// and writes the raw literals section's bytes into the block scratch.
+// and writes the raw literals section's bytes into the block scratch (byte stores: no LDS copy
+// of the literals, so that more waves per CU hide the token loads; 16 dwords per batch).
 constexpr uint32_t SEQ_MAX = (uint32_t)hd::SEG / 3u + 1u;     // a match covers >= 3 input bytes
 static_assert(SEQ_MAX * 6u <= (uint32_t)hd::SEG_TOK * 2u, "the compact sequences fit the segment's token slots");
 HZ_HD uint32_t* seq_a(uint16_t* tok) { return (uint32_t*)tok; }
@@ -713,10 +719,11 @@ HZ_HD uint32_t lit_header(uint32_t n, uint8_t* h) {
 struct LaneSeq {
   uint32_t lits, run, lead, hm, nm;
 };
+template <uint32_t NB = 8>
 HZ_HD LaneSeq lane_seq_count(hz_gcu32* gw, uint32_t ns, uint32_t l) {
   LaneSeq r = {0u, 0u, 0u, 0u, 0u};
   uint32_t want_dist = 0;
-  slots_fwd(gw, ns, l, [&](uint32_t v) {
+  slots_fwd_n<NB>(gw, ns, l, [&](uint32_t v) {
     if (want_dist) {
       if (!r.hm) r.lead = r.run;
       r.hm = 1; r.nm++; r.run = 0; want_dist = 0;
@@ -730,10 +737,10 @@ HZ_HD LaneSeq lane_seq_count(hz_gcu32* gw, uint32_t ns, uint32_t l) {
 }
 // pass 2: lit(k, byte) for the lane's k-th literal, seq(j, run, length, offset) for its j-th
 // match (the first one's run = first, from the scans over the lanes)
-template <class Lit, class Sq>
+template <uint32_t NB = 8, class Lit, class Sq>
 HZ_HD void lane_seq_emit(hz_gcu32* gw, uint32_t ns, uint32_t l, uint32_t first, Lit&& lit, Sq&& sq) {
   uint32_t want_dist = 0, ml = 0, run = 0, k = 0, j = 0;
-  slots_fwd(gw, ns, l, [&](uint32_t v) {
+  slots_fwd_n<NB>(gw, ns, l, [&](uint32_t v) {
     if (want_dist) {
       sq(j, j ? run : first, ml, v + 1u);
       j++; run = 0; want_dist = 0;
