@@ -229,7 +229,7 @@ class SelectionPlan:
         DIRECT is direct_descs built on the device (chunk -> slab at slab_base)."""
         import torch
         from . import _native as nat
-        from .engine import COPY_DESC_DTYPE, _ptr, _stream_handle
+        from .engine import COPY_DESC_DTYPE, _ptr, _stream_handle, to_device_bytes
         rs = list(range(self.world)) if ranks is None else list(ranks)
         ii = np.concatenate([self.by_rank[r] for r in rs]) if rs else np.zeros(0, np.int64)
         n = len(ii)
@@ -250,7 +250,9 @@ class SelectionPlan:
             if len(co) != n:
                 raise ValueError("one chunk offset per owned piece expected")
             parts.append(co)
-        buf = torch.from_numpy(np.concatenate(parts)).to(device)
+        # (page-locked staging, asynchronous: the host does not wait here for the kernels
+        # queued before -- the previous request's decode or encode)
+        buf = to_device_bytes(np.concatenate(parts), device)
         g = nat.PlanGeom()
         g.rank, g.itemsize, g.mode = self.rank, self.itemsize, int(mode)
         cs = _c_strides(self.layout, self.itemsize)

@@ -981,6 +981,7 @@ class ChunkStore:
             release()
 
         finish.abort = abort
+        finish.reads_pending = rfin is not None      # stored objects being decoded (statuses to check)
         return [out[r.chunk_id] for r in reads], finish
 
     def _resident(self, reads, dtype, chunk_dims, filter_ops, fill_value):
@@ -991,8 +992,12 @@ class ChunkStore:
         import torch
         vals, finish = self.get_chunks_deferred(reads, dtype, chunk_dims, filter_ops=filter_ops,
                                                 fill_value=fill_value, chunk_init=True, views=False)
+        # only decoded objects have statuses to wait for: cache hits and fill-value slots are
+        # stream-ordered before the write's copies, so the host goes on without waiting for
+        # the kernels queued before (the previous request's encode)
         try:
-            torch.cuda.current_stream(self.cache.arena.buf.device).synchronize()
+            if finish.reads_pending:
+                torch.cuda.current_stream(self.cache.arena.buf.device).synchronize()
         except BaseException:
             finish.abort()
             raise

@@ -269,15 +269,17 @@ def encode_descs(src_lens, align=256, overhead=16):
     Returns (descs CHUNK_DESC_DTYPE ndarray, src_extent, dst_extent)."""
     n = len(src_lens)
     descs = np.zeros(n, CHUNK_DESC_DTYPE)
-    so = do = 0
-    for i, L in enumerate(src_lens):
-        descs[i]["src_off"] = so
-        descs[i]["src_len"] = L
-        descs[i]["dst_off"] = do
-        descs[i]["dst_len"] = L + overhead
-        so += (L + align - 1) // align * align
-        do += (L + overhead + align - 1) // align * align
-    return descs, so, do
+    if n == 0:
+        return descs, 0, 0
+    L = np.asarray(src_lens, np.int64)
+    sa = (L + align - 1) // align * align
+    da = (L + overhead + align - 1) // align * align
+    so, do = np.cumsum(sa), np.cumsum(da)
+    descs["src_off"] = so - sa
+    descs["src_len"] = L
+    descs["dst_off"] = do - da
+    descs["dst_len"] = L + overhead
+    return descs, int(so[-1]), int(do[-1])
 
 
 def pack_chunks(blobs, dst_lens, align=256):
