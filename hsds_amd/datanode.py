@@ -1126,13 +1126,20 @@ class ChunkStore:
         chunk_dims = tuple(int(c) for c in chunk_dims)
         if len({r.chunk_id for r in reads}) != len(reads):
             raise ValueError("put_pieces takes each chunk once")
-        self._resident(reads, dtype, chunk_dims, filter_ops, fill_value)
-        for r in reads:
-            n = self.cache._lru.get(r.chunk_id)
-            if n is None:
-                raise MemoryError("chunk cache cannot hold the write batch")
-            n.pinned += 1
+        # chunk_init reads without a wait: the stored objects' decodes, the compare and the
+        # copy are stream-ordered, and the one wait of the batch (the dirty flags below)
+        # covers the decode statuses too -- the host builds the write while the device still
+        # runs what was queued before (the previous request's encode)
+        _, rfin = self.get_chunks_deferred(reads, dtype, chunk_dims, filter_ops=filter_ops, fill_value=fill_value,
+                                           chunk_init=True, views=False)
+        pinned = []
         try:
+            for r in reads:
+                n = self.cache._lru.get(r.chunk_id)
+                if n is None:
+                    raise MemoryError("chunk cache cannot hold the write batch")
+                n.pinned += 1
+                pinned.append(r.chunk_id)
             abase = self.cache.arena.buf
             offs = [self.cache._lru[r.chunk_id].off for r in reads]
             dd = make_descs(offs)
@@ -1141,14 +1148,29 @@ class ChunkStore:
                 d_desc = self.reader.eng.compare(d_data, abase, dd, _kind(dtype), differs)
                 self.reader.eng.copy(d_data, abase, d_desc, flags=differs)
             dirty = differs[:len(reads)].cpu().numpy().astype(bool)
-        finally:
-            for r in reads:
-                self.cache.unpin(r.chunk_id)
+        except BaseException:
+            for key in pinned:
+                self.cache.unpin(key)
+            rfin.abort()
+            raise
+        for key in pinned:
+            self.cache.unpin(key)
+        # each chunk's PUT stands alone (one PUT_Chunk per chunk in the reference): a chunk
+        # whose stored object failed to decode leaves the cache (finish) and its 500 is
+        # raised after the other chunks' updates are marked
+        vals = rfin()
+        err = None
         out = []
-        for r, d in zip(reads, dirty):
+        for r, d, v in zip(reads, dirty, vals):
+            if isinstance(v, Exception):
+                err = err or v
+                out.append(False)
+                continue
             if d or write_zero_chunks:
                 self.cache.setDirty(r.chunk_id)
             out.append(bool(d))
+        if err is not None:
+            raise err
         return out
 
     @_locked

@@ -148,3 +148,46 @@ def test_sharded_write_broadcast(dev, oracle_lib):
     want = before.copy()
     want[selection] = 3.25
     assert np.array_equal(_dataset(orc, objs, dims, layout, dt, 0), want)
+
+
+def test_sharded_write_corrupt_stored_object(dev, oracle_lib):
+    """A chunk whose stored object fails to decode (get_chunk's 500 in its PUT_Chunk): the
+    write raises it, that chunk leaves the cache, and every other chunk's update stands
+    (one PUT_Chunk per chunk in the reference: the others are not undone)."""
+    import torch
+    from hsds_amd import crawl
+    from hsds_amd.codec import HTTPInternalServerError
+    from hsds_amd.datanode import ChunkStore
+    from hsds_amd.partition import getS3Key
+    orc = oracle_lib
+    dt = np.dtype("<f4")
+    dims, layout = (192, 256), (64, 64)
+    rng = np.random.default_rng(5)
+    before = np.round(np.cumsum(rng.normal(size=dims), axis=1), 2).astype(dt)
+    grid = [(i, j) for i in range(3) for j in range(4)]
+    stored = _existing(orc, dims, layout, dt, before, grid)
+    bad = "c-" + DSET[2:] + "_1_2"
+    blob = bytearray(stored[getS3Key(bad)])
+    blob[16:] = bytes(len(blob) - 16)                 # header intact, stream zeroed: decode fails
+    stored[getS3Key(bad)] = bytes(blob)
+    selection = (slice(10, 192, 1), slice(20, 256, 1))  # every chunk partly covered: all are read
+    arr = np.full((182, 236), 7.5, dt)
+    plan = crawl.SelectionPlan(DSET, dims, layout, selection, dt, 1)
+    store = ChunkStore(lambda k, o, n: stored.get(k), mem_target=64 << 20, device=dev)
+    w = crawl.ShardedWriter(plan, 0, store)
+    with pytest.raises(HTTPInternalServerError):
+        w.write(arr, filter_ops=_ops(dt, layout))
+    torch.cuda.synchronize()
+    assert bad not in store.cache
+    out = {}
+    store.flush(lambda k, b: out.__setitem__(k, b), filter_ops=_ops(dt, layout))
+    assert getS3Key(bad) not in out and len(out) == len(grid) - 1
+    expect = before.copy()
+    expect[selection] = 7.5
+    cb = int(np.prod(layout)) * dt.itemsize
+    for i, j in grid:
+        cid = "c-" + DSET[2:] + f"_{i}_{j}"
+        if cid == bad:
+            continue
+        got = np.frombuffer(orc.uncompress(out[getS3Key(cid)], "zlib", 1, 4, cb), dt).reshape(layout)
+        assert np.array_equal(got, expect[i * 64:(i + 1) * 64, j * 64:(j + 1) * 64]), cid
