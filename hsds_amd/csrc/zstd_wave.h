@@ -24,6 +24,9 @@
 #define LZ_LANE0_ZW
 #endif
 
+#ifndef ZW_HUF_PAR
+#define ZW_HUF_PAR 1                  // Huffman literal streams on every lane (0: one lane per stream)
+#endif
 #ifndef ZW_PRIO_KB
 #define ZW_PRIO_KB 32                 // wave priority: one level per 32 KiB of the split's input left (0: off)
 #endif
@@ -648,6 +651,175 @@ inline int64_t seq_table_w(Shared& ls, zs::Fse* tab, uint32_t& al, uint32_t mode
   return u;
 }
 
+// ---- the Huffman literal streams on every lane (round 6) ----------------------------
+// A stream's bits are cut into G equal ranges, one per lane (G = 16 per stream for four
+// streams, 64 for one).  Lane j decodes from W bits above its range (any bit position:
+// Huffman codes resynchronise within a few symbols) down to the first symbol boundary at
+// or below its range top (s), then counts the symbols whose boundaries lie in its range
+// down to the first boundary below it (e).  Lane 0 starts at the stream's top, so its
+// chain is the true one; lane j's is true when its s equals lane j - 1's e, and a lane
+// where they differ decodes its range again from there (repair rounds, wave-uniform, at
+// most G).  The counts' prefix sums place every lane's symbols, which it decodes a second
+// time into the literal area.  The stream must end exactly at its first bit and hold the
+// section's count of symbols, as huf_stream checks.
+#ifndef ZW_HUF_WARM
+#define ZW_HUF_WARM 96                // warm-up bits above a lane's range
+#endif
+#if HZ_GPU
+#define ZW_MEM __device__ __forceinline__
+#else
+#define ZW_MEM inline
+#endif
+struct HufRd {                        // a backward reader: four dwords in registers (huf_stream)
+  hz_gcu8* base;
+  uint32_t a;
+  int32_t pos, top;
+  uint32_t W0, W1, W2, W3;
+  ZW_MEM uint32_t dw(int32_t k) const {
+    if (k > 0) return *(hz_gcu32*)(base + 4 * k);
+    if (k < 0) return 0u;
+    return *(hz_gcu32*)base & ~hz::bmask(8u * a);
+  }
+  ZW_MEM void init(int32_t p) {
+    pos = p;
+    top = (p - 1) >> 5;
+    W0 = dw(top); W1 = dw(top - 1); W2 = dw(top - 2); W3 = dw(top - 3);
+  }
+  template <class TT>
+  ZW_MEM uint32_t step(const TT& t, uint32_t hb, uint32_t mask) {
+    const uint64_t win = ((uint64_t)W0 << 32) | W1;
+    const uint32_t rel = (uint32_t)(pos - (int32_t)hb - 32 * (top - 1));
+    const zs::Huf e = t.huf[(uint32_t)(win >> rel) & mask];
+    pos -= e.nb;
+    if (pos <= 32 * top) {
+      W0 = W1; W1 = W2; W2 = W3;
+      W3 = dw(top - 4);
+      top--;
+    }
+    return e.sym;
+  }
+};
+
+// lane `lane`'s stream of the section: its bytes [at, at + n), its symbols go to out[0, cnt)
+struct HufLane {
+  uint32_t at, n, cnt;
+  hz_gu8* out;
+};
+
+// the streams' symbols; returns 0 or -1 (uniform)
+#if HZ_GPU
+__device__ inline int huf_streams_wave(const WTables& t, const zs::In& in, const HufLane& L, uint32_t G) {
+  const uint32_t lane = threadIdx.x, j = lane % G;
+  int bad = (L.n == 0u || L.at + L.n > in.n) ? 1 : 0;
+  const uint32_t last = bad ? 1u : zs::b8(in, L.at + L.n - 1u);
+  bad |= last == 0u ? 1 : 0;
+  HufRd r;
+  r.a = (uint32_t)(((uintptr_t)in.p + L.at) & 3u);
+  r.base = HZ_GLOBAL(hz_gcu8*, in.p + L.at - r.a);
+  const int32_t start = 8 * (int32_t)r.a;
+  const int32_t ptop = bad ? start : 8 * (int32_t)(L.n - 1u) + (int32_t)zs::hib(last) + start;
+  const int64_t span = ptop - start;
+  const int32_t pj = start + (int32_t)(span - span * (int64_t)j / (int64_t)G);
+  const int32_t pj1 = start + (int32_t)(span - span * (int64_t)(j + 1u) / (int64_t)G);
+  const uint32_t hb = t.huf_bits, mask = (1u << hb) - 1u;
+  // pass 1: warm-up, then the range's symbols counted
+  const int32_t b0 = j == 0u ? ptop : (pj + ZW_HUF_WARM < ptop ? pj + ZW_HUF_WARM : ptop);
+  r.init(b0);
+  while (r.pos > pj) (void)r.step(t, hb, mask);
+  int32_t s = r.pos, e;
+  uint32_t n = 0;
+  while (r.pos > pj1) { (void)r.step(t, hb, mask); n++; }
+  e = r.pos;
+  // repair rounds: a lane whose first boundary is not its predecessor's end decodes again
+  for (uint32_t round = 0; round < G; round++) {
+    const int32_t ep = __shfl_up(e, 1, 64);
+    const bool fix = j > 0u && ep != s;
+    if (!__ballot(fix)) break;
+    if (fix) {
+      s = ep;
+      r.init(ep);
+      n = 0;
+      while (r.pos > pj1) { (void)r.step(t, hb, mask); n++; }
+      e = r.pos;
+    }
+  }
+  // placement: prefix sums of the counts inside each group of G lanes
+  uint32_t inc = n;
+  for (uint32_t o = 1; o < G; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (j >= o) inc += v;
+  }
+  const uint32_t total = __shfl(inc, (int)(lane - j + G - 1u), 64);
+  bad |= (total != L.cnt || (j == G - 1u && e != start)) ? 1 : 0;
+  if (__ballot(bad != 0)) return -1;
+  // pass 2: the lane's symbols into place
+  r.init(s);
+  hz_gu8* const o = L.out + (inc - n);
+  for (uint32_t k = 0; k < n; k++) o[k] = (uint8_t)r.step(t, hb, mask);
+  return 0;
+}
+#else
+static inline int huf_streams_wave(const WTables& t, const zs::In& in, const HufLane* L, uint32_t G) {
+  int32_t S[64], E[64], PJ[64], PJ1[64], START[64];
+  uint32_t N[64];
+  HufRd R[64];
+  int bad = 0;
+  const uint32_t hb = t.huf_bits, mask = (1u << hb) - 1u;
+  for (uint32_t lane = 0; lane < 64; lane++) {
+    const uint32_t j = lane % G;
+    int lb = (L[lane].n == 0u || L[lane].at + L[lane].n > in.n) ? 1 : 0;
+    const uint32_t last = lb ? 1u : zs::b8(in, L[lane].at + L[lane].n - 1u);
+    lb |= last == 0u ? 1 : 0;
+    bad |= lb;
+    HufRd& r = R[lane];
+    r.a = (uint32_t)(((uintptr_t)in.p + L[lane].at) & 3u);
+    r.base = in.p + L[lane].at - r.a;
+    const int32_t start = 8 * (int32_t)r.a;
+    const int32_t ptop = lb ? start : 8 * (int32_t)(L[lane].n - 1u) + (int32_t)zs::hib(last) + start;
+    const int64_t span = ptop - start;
+    PJ[lane] = start + (int32_t)(span - span * (int64_t)j / (int64_t)G);
+    PJ1[lane] = start + (int32_t)(span - span * (int64_t)(j + 1u) / (int64_t)G);
+    START[lane] = start;
+    const int32_t b0 = j == 0u ? ptop : (PJ[lane] + ZW_HUF_WARM < ptop ? PJ[lane] + ZW_HUF_WARM : ptop);
+    r.init(b0);
+    while (r.pos > PJ[lane]) (void)r.step(t, hb, mask);
+    S[lane] = r.pos;
+    N[lane] = 0;
+    while (r.pos > PJ1[lane]) { (void)r.step(t, hb, mask); N[lane]++; }
+    E[lane] = r.pos;
+  }
+  for (uint32_t round = 0; round < G; round++) {
+    int32_t EP[64];
+    bool any = false, fix[64];
+    for (uint32_t lane = 0; lane < 64; lane++) EP[lane] = lane ? E[lane - 1] : E[0];
+    for (uint32_t lane = 0; lane < 64; lane++) { fix[lane] = lane % G > 0u && EP[lane] != S[lane]; any |= fix[lane]; }
+    if (!any) break;
+    for (uint32_t lane = 0; lane < 64; lane++) {
+      if (!fix[lane]) continue;
+      HufRd& r = R[lane];
+      S[lane] = EP[lane];
+      r.init(EP[lane]);
+      N[lane] = 0;
+      while (r.pos > PJ1[lane]) { (void)r.step(t, hb, mask); N[lane]++; }
+      E[lane] = r.pos;
+    }
+  }
+  uint32_t X[64];
+  for (uint32_t g0 = 0; g0 < 64; g0 += G) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < G; k++) { X[g0 + k] = acc; acc += N[g0 + k]; }
+    bad |= (acc != L[g0].cnt || E[g0 + G - 1u] != START[g0 + G - 1u]) ? 1 : 0;
+  }
+  if (bad) return -1;
+  for (uint32_t lane = 0; lane < 64; lane++) {
+    HufRd& r = R[lane];
+    r.init(S[lane]);
+    for (uint32_t k = 0; k < N[lane]; k++) L[lane].out[X[lane] + k] = (uint8_t)r.step(t, hb, mask);
+  }
+  return 0;
+}
+#endif
+
 // one compressed block at input [at, at + n); output from op; returns the new op or < 0 (uniform)
 #if HZ_GPU
 __device__
@@ -708,6 +880,49 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     }
     const uint32_t s0 = at + q + (uint32_t)tsz, ssz = csz - (uint32_t)tsz;
     HZ_T(1);
+#if ZW_HUF_PAR
+    {
+      // every lane on a stream: 64 on a single stream, 16 on each of four
+      uint32_t l1 = ssz, l2 = 0, l3 = 0, l4 = 0, seg = rsz, p1 = s0;
+      if (ns != 1) {
+        if (ssz < 6) return zs::E_DATA;
+        l1 = ub8(in, s0) | (ub8(in, s0 + 1) << 8); l2 = ub8(in, s0 + 2) | (ub8(in, s0 + 3) << 8);
+        l3 = ub8(in, s0 + 4) | (ub8(in, s0 + 5) << 8);
+        if (l1 + l2 + l3 + 6 > ssz) return zs::E_DATA;
+        l4 = ssz - 6 - l1 - l2 - l3;
+        seg = (rsz + 3) / 4;
+        if (rsz < 3 * seg) return zs::E_DATA;
+        p1 = s0 + 6;
+      }
+      const uint32_t G = ns == 1 ? 64u : 16u;
+      WAVE_SYNC();
+#if HZ_GPU
+      HufLane hl;
+      {
+        const uint32_t st = threadIdx.x / G;
+        const uint32_t off = st == 0 ? 0u : st == 1 ? l1 : st == 2 ? l1 + l2 : l1 + l2 + l3;
+        hl.at = p1 + off;
+        hl.n = ns == 1 ? ssz : st == 0 ? l1 : st == 1 ? l2 : st == 2 ? l3 : l4;
+        hl.cnt = ns == 1 ? rsz : st == 3 ? rsz - 3 * seg : seg;
+        hl.out = lit + st * seg;
+      }
+      const int herr = huf_streams_wave(t, in, hl, G);
+#else
+      HufLane hl[64];
+      for (uint32_t lane = 0; lane < 64; lane++) {
+        const uint32_t st = lane / G;
+        const uint32_t off = st == 0 ? 0u : st == 1 ? l1 : st == 2 ? l1 + l2 : l1 + l2 + l3;
+        hl[lane].at = p1 + off;
+        hl[lane].n = ns == 1 ? ssz : st == 0 ? l1 : st == 1 ? l2 : st == 2 ? l3 : l4;
+        hl[lane].cnt = ns == 1 ? rsz : st == 3 ? rsz - 3 * seg : seg;
+        hl[lane].out = lit + st * seg;
+      }
+      const int herr = huf_streams_wave(t, in, hl, G);
+#endif
+      WAVE_SYNC();
+      if (herr) return zs::E_DATA;
+    }
+#else
     if (ns == 1) {
       LANE_LOOP { if (lane == 0) ls.u_err = zs::huf_stream(t, in, s0, ssz, lit, rsz); }
     } else {
@@ -732,6 +947,7 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
     }
     WAVE_SYNC();
     if (uni((uint32_t)ls.u_err)) return zs::E_DATA;
+#endif
     q += csz;
   }
   WAVE_SYNC_GLOBAL();         // literals visible to every lane
