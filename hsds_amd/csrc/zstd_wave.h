@@ -24,6 +24,11 @@
 #define LZ_LANE0_ZW
 #endif
 
+#ifndef ZW_WALK4
+#define ZW_WALK4 0                    // FSE walk: four stage dwords read with the table entries
+                                      // (one LDS round trip per sequence; measured slower: bench
+                                      // zstd 63.1 -> 57.0 GB/s, the 4 reads cost more than the wait)
+#endif
 #ifndef ZW_HUF_PAR
 #define ZW_HUF_PAR 1                  // Huffman literal streams on every lane (0: one lane per stream)
 #endif
@@ -1014,14 +1019,29 @@ inline int64_t block(Shared& ls, const zs::In& in, uint32_t at, uint32_t n, hz_g
           sb_stage(ls, b, f < 0 ? 0 : f);
           sb = b.sb;
         }
+#if ZW_WALK4
+        // the four stage dwords below the position are read with the table entries (they
+        // depend on the position only): the sequence's extra and state bits (<= 89) lie in
+        // them, so one LDS round trip per sequence instead of two dependent ones
+        const int32_t xs = vpos - 8 * sb;                            // stage bit (exclusive top)
+        const int32_t jt = (xs - 1) >> 5, j0 = jt - 3 < 0 ? 0 : jt - 3;
+        const uint32_t w0 = ls.t.stage[j0], w1 = ls.t.stage[j0 + 1], w2 = ls.t.stage[j0 + 2], w3 = ls.t.stage[j0 + 3];
+#endif
         const uint32_t eL = fse_word(t.ll, vl), eO = fse_word(t.of, vo), eM = fse_word(t.ml, vm);
         const uint32_t xb = sq_eb(eL) + sq_eb(eO) + sq_eb(eM);
         const uint32_t nL = sq_nb(eL), nM = sq_nb(eM), nO = sq_nb(eO);
         const uint32_t nsb = k + 1u < nseq ? nL + nM + nO : 0u;   // state updates: LL, ML, OF
         int32_t lo = vpos - 8 * sb - (int32_t)(xb + nsb);           // stage bit of the state bits
         lo = lo < 0 ? 0 : lo;                                        // (< 0 only past the stream start)
+#if ZW_WALK4
+        const uint32_t d = (uint32_t)((lo >> 5) - j0);              // 0..3 (3: the bits lie in w3)
+        const uint32_t lw = d == 0u ? w0 : d == 1u ? w1 : d == 2u ? w2 : w3;
+        const uint32_t hw = d == 0u ? w1 : d == 1u ? w2 : d == 2u ? w3 : 0u;
+        const uint32_t fld = ubfe(funnel(hw, lw, (uint32_t)lo & 31u), 0u, nsb);
+#else
         const uint32_t j = (uint32_t)lo >> 5;
         const uint32_t fld = ubfe(funnel(ls.t.stage[j + 1u], ls.t.stage[j], (uint32_t)lo & 31u), 0u, nsb);
+#endif
         ls.t.seq[ns_w][0] = eL; ls.t.seq[ns_w][1] = eO; ls.t.seq[ns_w][2] = eM; ls.t.seq[ns_w][3] = (uint32_t)vpos;
         vl = sq_base(eL) + (fld >> (nM + nO));
         vm = sq_base(eM) + ubfe(fld, nO, nM);
