@@ -288,6 +288,9 @@ struct ParseShared {
 // 122.1 ms at 4 and 6 replicas, so one set stays.  (An XOR bank swizzle of the ring and the
 // prev[] links -- the lanes start 128 bytes apart, one bank -- measured 130 ms: its address
 // arithmetic costs more than the conflicts.)
+#ifndef HD_ADLER_DOT
+#define HD_ADLER_DOT 1                      // the staging's adler sums by byte dot products
+#endif
 #ifndef HD_NREP
 #define HD_NREP 1
 #endif
@@ -305,6 +308,15 @@ HZ_HD uint32_t funnel(uint32_t a, uint32_t b, uint32_t p) {
 #else
   const uint32_t s = (p & 3u) * 8u;
   return s ? (a >> s) | (b << (32u - s)) : a;
+#endif
+}
+// c + the dot product of the four bytes of a and of b (v_dot4_u32_u8)
+HZ_HD uint32_t dot4(uint32_t a, uint32_t b, uint32_t c) {
+#if HZ_GPU
+  return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+  for (uint32_t i = 0; i < 32u; i += 8u) c += ((a >> i) & 255u) * ((b >> i) & 255u);
+  return c;
 #endif
 }
 HZ_HD uint32_t rd32(const ParseShared& sh, uint32_t p) {
@@ -560,6 +572,17 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
     LANE_LOOP {
       const uint32_t nw = (stage_hi - s0 + 3u) / 4u;
       // byte sums of the word at p: S1 += bytes below s1, S2 += their positions * bytes
+#if HD_ADLER_DOT
+      // (byte dot products: sum b and sum (p + k) b of the word's bytes below s1 -- one
+      // 32 x 32 -> 64 multiply per word instead of four 64-bit ones, round 6)
+#define HD_ADLER_WORD(p, v)                                                    \
+      {                                                                        \
+        const uint32_t w_ = (p) + 4u <= s1 ? (v) : (p) >= s1 ? 0u : (v) & hz::bmask(8u * (s1 - (p))); \
+        const uint32_t sb_ = hd::dot4(w_, 0x01010101u, 0u);                   \
+        LV(as1) += sb_;                                                        \
+        LV(as2) += (uint64_t)(p) * sb_ + hd::dot4(w_, 0x03020100u, 0u);       \
+      }
+#else
 #define HD_ADLER_WORD(p, v)                                                    \
       for (uint32_t b = 0; b < 4u; b++) {                                      \
         const uint32_t q = (p) + b;                                            \
@@ -569,6 +592,7 @@ HZ_HD uint32_t parse_stream(ParseShared& sh, const EncJob& job, const Tune& tune
           LV(as2) += (uint64_t)q * byte;                                       \
         }                                                                      \
       }
+#endif
 #if HZ_GPU
       if (pf_ok) {
         // the words were fetched into registers while the previous segment was parsed
