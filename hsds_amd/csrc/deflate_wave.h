@@ -288,6 +288,9 @@ struct ParseShared {
 // 122.1 ms at 4 and 6 replicas, so one set stays.  (An XOR bank swizzle of the ring and the
 // prev[] links -- the lanes start 128 bytes apart, one bank -- measured 130 ms: its address
 // arithmetic costs more than the conflicts.)
+#ifndef HD_WALKB
+#define HD_WALKB 8                          // the emit walk's token dwords per batch of loads
+#endif
 #ifndef HD_ADLER_DOT
 #define HD_ADLER_DOT 1                      // the staging's adler sums by byte dot products
 #endif
@@ -1377,17 +1380,18 @@ HZ_HD uint32_t tok_bits(const EmitShared& sh, uint32_t t, uint32_t dv) {
 // latency per 16 slots instead of one per dependent load.
 template <class F>
 HZ_HD void walk_tokens(hz_gcu8* gtok, int lane, uint32_t ns, F&& f) {
+  constexpr uint32_t NB = HD_WALKB;  // token dwords per batch of loads
   uint32_t mt = 0;                 // a match's first slot waiting for its distance slot
   const uint32_t nd = (ns + 1u) / 2u;
-  for (uint32_t j0 = 0; j0 < nd; j0 += 8u) {
-    uint32_t d[8];
+  for (uint32_t j0 = 0; j0 < nd; j0 += NB) {
+    uint32_t d[NB];
     HZ_UNROLL
-    for (uint32_t u = 0; u < 8u; u++) {
+    for (uint32_t u = 0; u < NB; u++) {
       const uint32_t j = j0 + u;
       d[u] = j < nd ? *(hz_gcu32*)(gtok + (size_t)(j * (uint32_t)WAVE + (uint32_t)lane) * 4u) : 0u;
     }
     HZ_UNROLL
-    for (uint32_t u = 0; u < 16u; u++) {
+    for (uint32_t u = 0; u < 2u * NB; u++) {
       if (2u * j0 + u < ns) {
         const uint32_t v = (u & 1u) ? d[u >> 1] >> 16 : d[u >> 1] & 0xffffu;
         const bool call = mt || !(v & 0x8000u);
