@@ -285,3 +285,49 @@ def test_batch_decode_zstd_goldens_with_oracle(golden2, oracle_lib, torch_dev):
             assert out[o:o + sizes[k]].tobytes() == ref, names[k]
             nz += "zstd" in names[k]
     assert nz >= 40
+
+
+def test_batch_decode_zstd_literal_heavy(torch_dev):
+    """Blosc-zstd frames (the image's libblosc 1.21) of literal-heavy data in ONE batch: the
+    Huffman literal streams decoded on every lane (zstd_wave.h huf_streams_wave) -- skewed
+    and near-uniform bytes, text with noise, one- and four-stream literal sections, levels
+    1 / 5 / 9 -- decode to their input"""
+    import ctypes
+    import os
+    import torch
+    from hsds_amd.engine import ChunkEngine, pack_chunks
+    if not os.path.exists("/opt/conda/lib/libblosc.so.1"):
+        pytest.skip("the image's libblosc is absent")
+    lb = ctypes.CDLL("/opt/conda/lib/libblosc.so.1")
+    lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    rng = np.random.default_rng(62)
+    raws, blobs = [], []
+    for n in (40, 300, 1500, 5000, 40000, 131072, 300000, 1 << 20):
+        for kind in range(3):
+            if kind == 0:
+                a = np.minimum(rng.geometric(0.08, n), 255).astype(np.uint8)
+            elif kind == 1:
+                a = (rng.integers(0, 200, n) + (np.arange(n) % 7)).astype(np.uint8)
+            else:
+                a = np.frombuffer((b"the quick brown fox %d jumps " * (n // 20 + 1))[:n], np.uint8).copy()
+                a[rng.integers(0, n, n // 5)] = rng.integers(0, 256, n // 5).astype(np.uint8)
+            for level in (1, 5, 9):
+                out = np.zeros(a.size + 64, np.uint8)
+                k = lb.blosc_compress_ctx(level, 0, 1, a.size, a.ctypes.data, out.ctypes.data, out.size, b"zstd", 0, 1)
+                assert k > 0
+                raws.append(a)
+                blobs.append(out[:k].tobytes())
+    src, descs, ext = pack_chunks(blobs, [a.size for a in raws])
+    eng = ChunkEngine(0)
+    d_src = torch.from_numpy(src).to(torch_dev)
+    d_dst = torch.zeros(ext, dtype=torch.uint8, device=torch_dev)
+    d_st = torch.full((len(blobs),), 77, dtype=torch.int32, device=torch_dev)
+    eng.decode(d_src, descs, d_dst, d_st, compressor="zstd", shuffle=0, itemsize=1)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    out = d_dst.cpu().numpy()
+    for k, a in enumerate(raws):
+        assert st[k] == 0, (k, a.size, st[k])
+        o = int(descs[k]["dst_off"])
+        assert out[o:o + a.size].tobytes() == a.tobytes(), (k, a.size)

@@ -115,3 +115,40 @@ def test_zstd_bench_corpus(emu, wave):
         got = frame_decode(emu, bytes(np.asarray(b, np.uint8)))
         assert not isinstance(got, int), got
         assert got == np.ascontiguousarray(r).view(np.uint8).tobytes()
+
+
+def test_zstd_wave_literal_streams(emu):
+    """The wave decoder's Huffman literals on every lane (zstd_wave.h huf_streams_wave):
+    libblosc 1.21 zstd frames of literal-heavy data -- skewed random bytes (Huffman codes of
+    many lengths), short and long blocks (one-stream and four-stream literal sections),
+    levels 1-9 -- decode to their input, as the one-lane-per-stream decoder's do"""
+    if not os.path.exists("/opt/conda/lib/libblosc.so.1"):
+        pytest.skip("the image's libblosc is absent")
+    lb = ctypes.CDLL("/opt/conda/lib/libblosc.so.1")
+    lb.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    rng = np.random.default_rng(61)
+    cases = []
+    for n in (40, 300, 1500, 5000, 40000, 131072, 300000):
+        for kind in range(3):
+            if kind == 0:      # geometric bytes: a few very short codes, a long tail of 11-bit ones
+                a = np.minimum(rng.geometric(0.08, n), 255).astype(np.uint8)
+            elif kind == 1:    # near-uniform bytes with a little structure (codes of 7-9 bits)
+                a = (rng.integers(0, 200, n) + (np.arange(n) % 7)).astype(np.uint8)
+            else:              # text-like runs mixed with noise: matches and literals
+                a = np.frombuffer((b"the quick brown fox %d jumps " * (n // 20 + 1))[:n], np.uint8).copy()
+                a[rng.integers(0, n, n // 5)] = rng.integers(0, 256, n // 5).astype(np.uint8)
+            cases.append(a)
+    checked = 0
+    for wave in (False, True):
+        WAVE[0] = wave
+        for a in cases:
+            for level in (1, 5, 9):
+                out = np.zeros(a.size + 64, np.uint8)
+                k = lb.blosc_compress_ctx(level, 0, 1, a.size, a.ctypes.data, out.ctypes.data, out.size, b"zstd", 0, 1)
+                assert k > 0
+                got = frame_decode(emu, out[:k].tobytes())
+                assert not isinstance(got, int), (a.size, level, got)
+                assert got == a.tobytes(), (a.size, level)
+                checked += 1
+    assert checked == 2 * len(cases) * 3
