@@ -328,11 +328,52 @@ __device__ __forceinline__ void raw_copy(const Item& it, int lane) {
   }
 }
 
+// Longest streams first (HZ2_LPT): the batch kernel's waves claim items in the order
+// ord[0..total), the pool's items sorted by compressed length, longest first (a counting
+// sort over 1024 log-linear length classes: 5 bits of exponent, 5 of mantissa), so the
+// last claims are the shortest streams and the waves end closer together.  One workgroup;
+// ties keep no particular order (scheduling only: every item decodes the same either way).
+#ifndef HZ2_LPT
+#define HZ2_LPT 1
+#endif
+__device__ __forceinline__ uint32_t lpt_key(uint32_t len) {
+  const uint32_t ex = 31u - (uint32_t)__builtin_clz(len | 1u);
+  const uint32_t mt = ex >= 5u ? (len >> (ex - 5u)) & 31u : (len << (5u - ex)) & 31u;
+  return 1023u - (ex * 32u + mt);                     // descending length -> ascending key
+}
+__global__ void __launch_bounds__(1024) order_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
+                                                     uint32_t* __restrict__ ord) {
+  __shared__ uint32_t cnt[1024];
+  __shared__ uint32_t sum[1024];
+  const uint32_t total = *pool_ctr, t = threadIdx.x;
+  cnt[t] = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < total; i += 1024u) atomicAdd(&cnt[lpt_key(pool[i].src_len)], 1u);
+  __syncthreads();
+  // inclusive scan of the counts (Hillis-Steele, double-buffered), then each class's start
+  uint32_t v = cnt[t];
+  sum[t] = v;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024u; o <<= 1) {
+    const uint32_t a = t >= o ? sum[t - o] : 0u;
+    __syncthreads();
+    v += a;
+    sum[t] = v;
+    __syncthreads();
+  }
+  cnt[t] = v - cnt[t];                                // exclusive start of class t
+  __syncthreads();
+  for (uint32_t i = t; i < total; i += 1024u) {
+    const uint32_t k = atomicAdd(&cnt[lpt_key(pool[i].src_len)], 1u);
+    ord[k] = i;
+  }
+}
+
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ2_WPE))) inflate2_kernel(const Item* __restrict__ pool, const uint32_t* __restrict__ pool_ctr,
                                                       uint32_t* __restrict__ counter, int32_t* __restrict__ status,
                                                       uint32_t* __restrict__ sizes,
                                                       const uint32_t* __restrict__ kind_counts, hz2::Tune tune,
-                                                      uint8_t* __restrict__ rings) {
+                                                      uint8_t* __restrict__ rings, const uint32_t* __restrict__ ord) {
   __shared__ hz2::Shared sh;
   if (kind_counts[1] == 0) return;   // only LZ / zstd splits in this batch
   const uint32_t total = *pool_ctr;
@@ -354,6 +395,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HZ2_WPE
     if (lane == 0) item = atomicAdd(counter, 1u);
     item = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(item, 0, 64));
     if (item >= total) break;
+    if (ord) item = (uint32_t)__builtin_amdgcn_readfirstlane((int)ord[item]);
     const Item it = pool[item];
     const uint32_t kind = it.kind & 0xff;
     int st;
@@ -1911,12 +1953,14 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   const size_t sz_pool = ((size_t)pool_cap * sizeof(Item) + 255) & ~(size_t)255;
   const size_t sz_meta = ((size_t)nchunks * sizeof(ChunkMeta) + 255) & ~(size_t)255;
   const size_t sz_list = ((size_t)nchunks * 4 + 255) & ~(size_t)255;
-  const size_t need = sz_pool + sz_meta + sz_list + 256;
+  const size_t sz_ord = ((size_t)pool_cap * 4 + 255) & ~(size_t)255;
+  const size_t need = sz_pool + sz_meta + sz_list + sz_ord + 256;
   if (grow((void**)&e->ws, &e->ws_bytes, need)) return HSDS_ERR_DEVICE;
   uint8_t* w = e->ws;
   Item* pool = (Item*)w; w += sz_pool;
   ChunkMeta* meta = (ChunkMeta*)w; w += sz_meta;
   uint32_t* list = (uint32_t*)w; w += sz_list;
+  uint32_t* ord = (uint32_t*)w; w += sz_ord;          // the batch kernel's claim order (HZ2_LPT)
   // [0] inflate item counter, [1] meta list count, [2] inexact size, [3] LZ item counter,
   // [4] LZ items, [5] zlib + raw items, [6] zstd items, [7] zstd item counter, [8] pool fill
   uint32_t* ctr = (uint32_t*)w;
@@ -1952,6 +1996,7 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   hipLaunchKernelGGL(frame_walk_kernel, dim3(nb), dim3(tpb), 0, st, (const uint8_t*)d_src, d_chunks, nchunks,
                      (uint8_t*)d_dst, tmp, pool, pool_cap, ctr + 8, meta, list, ctr + 1, ctr + 4, d_status,
                      compressor, shuffle, itemsize, inexact);
+  if (!pipe && HZ2_LPT) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, pool, ctr + 8, ord);
   hipEventRecord(e->ev0, st);
   if (nw == 4)
     hipLaunchKernelGGL(inflate2w_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, pool, ctr + 8, ctr, d_status,
@@ -1961,7 +2006,7 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
                        ctr + 2, ctr + 4, e->tune, e->rings);
   else
     hipLaunchKernelGGL(inflate2_kernel, dim3((unsigned)grid), dim3(64), 0, st, pool, ctr + 8, ctr, d_status, ctr + 2,
-                       ctr + 4, e->tune, e->rings);
+                       ctr + 4, e->tune, e->rings, HZ2_LPT ? (const uint32_t*)ord : (const uint32_t*)nullptr);
   int64_t lgrid = (int64_t)e->num_cus * e->lz_blocks_per_cu;
   if (lgrid > (nchunks * 64 + lz::GROUP - 1) / lz::GROUP) lgrid = (nchunks * 64 + lz::GROUP - 1) / lz::GROUP;
   if (lgrid < 1) lgrid = 1;
