@@ -162,7 +162,7 @@ class Engine:
     def set_tuning(self, seg_over16=None, warmup_bits=None, rounds=None, waves_per_stream=None):
         """Inflate tuning; a setting left at None keeps the engine's current value
         (hsds_engine_create's defaults: the GPU-swept ones).  waves_per_stream: 0 by batch
-        size, 1, 2 or 4 wavefronts per zlib stream (None: keep)."""
+        size, 1, 2, 4 or 8 wavefronts per zlib stream (None: keep)."""
         keep = 0xFFFFFFFF
         rc = lib().hsds_set_tuning(self.h, keep if seg_over16 is None else seg_over16,
                                    keep if warmup_bits is None else warmup_bits,

@@ -1648,6 +1648,7 @@ struct hsds_engine {
   int inflate_blocks_per_cu;   // occupancy of inflate2_kernel
   int inflate2w_blocks_per_cu; // occupancy of inflate2w_kernel<2> (two wavefronts per workgroup)
   int inflate4w_blocks_per_cu; // occupancy of inflate2w_kernel<4>
+  int inflate8w_blocks_per_cu; // occupancy of inflate2w_kernel<8>
   int inflate_pipe;            // wavefronts per stream: 0 by batch size, else 1, 2 or 4
   int lz_blocks_per_cu;        // occupancy of lz_kernel
   int bshuf_blocks_per_cu;     // occupancy of bshuf_kernel
@@ -1818,17 +1819,20 @@ int hsds_engine_create(int device, hsds_engine** out) {
     if (v >= 1 && v < occ) occ = v;
   }
   e->inflate_blocks_per_cu = occ;
-  int occ2 = 0, occ4 = 0;
+  int occ2 = 0, occ4 = 0, occ8 = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, inflate2w_kernel<2>, 128, 0) != hipSuccess || occ2 < 1)
     occ2 = occ / 2 > 0 ? occ / 2 : 1;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, inflate2w_kernel<4>, 256, 0) != hipSuccess || occ4 < 1)
     occ4 = occ / 4 > 0 ? occ / 4 : 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ8, inflate2w_kernel<8>, 512, 0) != hipSuccess || occ8 < 1)
+    occ8 = occ / 8 > 0 ? occ / 8 : 1;
   e->inflate2w_blocks_per_cu = occ2;
   e->inflate4w_blocks_per_cu = occ4;
+  e->inflate8w_blocks_per_cu = occ8;
   e->inflate_pipe = HZ2_PIPE_DEFAULT;
-  if (const char* ev = getenv("HSDS_INFLATE_PIPE")) {       // 0 (or < 0): by batch size; 1, 2, 4 wavefronts
+  if (const char* ev = getenv("HSDS_INFLATE_PIPE")) {       // 0 (or < 0): by batch size; 1, 2, 4, 8 wavefronts
     const int v = atoi(ev);
-    e->inflate_pipe = v == 1 || v == 2 || v == 4 ? v : 0;
+    e->inflate_pipe = v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
   }
   int olz = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&olz, lz_kernel, 64, 0) != hipSuccess || olz < 1) olz = 8;
@@ -1909,7 +1913,8 @@ int hsds_set_tuning(hsds_engine* e, uint32_t seg_over16, uint32_t warmup_bits, u
   if (!e) return HSDS_ERR_ARG;
   // HSDS_TUNE_KEEP (0xffffffff; -1 for rounds) leaves a setting as it is
   if ((seg_over16 > 16u && seg_over16 != HSDS_TUNE_KEEP) || (warmup_bits > 4096u && warmup_bits != HSDS_TUNE_KEEP) ||
-      (waves_per_stream > 4u && waves_per_stream != HSDS_TUNE_KEEP) || waves_per_stream == 3u || rounds < -1 ||
+      (waves_per_stream != HSDS_TUNE_KEEP && waves_per_stream > 2u && waves_per_stream != 4u && waves_per_stream != 8u) ||
+      rounds < -1 ||
       rounds > 64)
     return HSDS_ERR_ARG;
   if (waves_per_stream != HSDS_TUNE_KEEP) e->inflate_pipe = (int)waves_per_stream;
@@ -1984,7 +1989,8 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
   int nw = e->inflate_pipe;
   if (nw == 0) nw = nchunks * 4 * 4 <= waves1 ? 4 : nchunks * 4 * 2 <= waves1 ? 2 : 1;
   const bool pipe = nw > 1;
-  int64_t grid = nw == 4 ? (int64_t)e->num_cus * e->inflate4w_blocks_per_cu
+  int64_t grid = nw == 8 ? (int64_t)e->num_cus * e->inflate8w_blocks_per_cu
+                 : nw == 4 ? (int64_t)e->num_cus * e->inflate4w_blocks_per_cu
                  : nw == 2 ? (int64_t)e->num_cus * e->inflate2w_blocks_per_cu : waves1;
   if (grid > nchunks * 64) grid = nchunks * 64;
   if (grid < 1) grid = 1;
@@ -1998,7 +2004,10 @@ static int decode_batch_impl(hsds_engine* e, const void* d_src, const hsds_chunk
                      compressor, shuffle, itemsize, inexact);
   if (!pipe && HZ2_LPT) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, pool, ctr + 8, ord);
   hipEventRecord(e->ev0, st);
-  if (nw == 4)
+  if (nw == 8)
+    hipLaunchKernelGGL(inflate2w_kernel<8>, dim3((unsigned)grid), dim3(512), 0, st, pool, ctr + 8, ctr, d_status,
+                       ctr + 2, ctr + 4, e->tune, e->rings);
+  else if (nw == 4)
     hipLaunchKernelGGL(inflate2w_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, pool, ctr + 8, ctr, d_status,
                        ctr + 2, ctr + 4, e->tune, e->rings);
   else if (pipe)

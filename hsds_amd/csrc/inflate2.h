@@ -933,7 +933,7 @@ struct WinState {                // a window's start
   uint32_t est;                  // WK_CONT: expected bits left in the block
   uint32_t prev_block_bits;      // the last Huffman block's size (next block's estimate)
 };
-constexpr int NW_MAX = 4;        // wavefronts per stream in the window pipeline
+constexpr int NW_MAX = 8;        // wavefronts per stream in the window pipeline
 struct Ctl {                     // in LDS, shared by the workgroup's wavefronts
   uint32_t synced;               // the window whose start is in `next`
   uint32_t mdone;                // windows whose output is final

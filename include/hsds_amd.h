@@ -113,7 +113,7 @@ const char* hsds_strerror(int status);
 /* Tuning of the inflate kernel: segment over-provisioning against the previous
  * deflate block in 16ths (0..16), warm-up bits before a segment (0..4096), wavefronts
  * per zlib stream (0: by batch size -- four or two when the batch's streams times that
- * fit in the resident wavefronts --, 1, 2 or 4), repair rounds per window (0..64).  Any setting
+ * fit in the resident wavefronts --, 1, 2, 4 or 8), repair rounds per window (0..64).  Any setting
  * decodes the same bytes; it only moves work between the phases and wavefronts.
  * Defaults are set by hsds_engine_create; HSDS_TUNE_KEEP (rounds: -1) leaves a setting
  * unchanged. */

@@ -11,7 +11,7 @@
 // (dst holds the unshuffled bytes), as the engine does for F2 chunks.
 // dst_off: the stream's output starts dst_off bytes into dst (dst has dst_len + dst_off + 8
 // bytes; the bytes around the output must stay untouched)
-// nwaves == 2 or 4: the window pipeline of inflate2w_kernel -- one thread per emulated
+// nwaves == 2, 4 or 8: the window pipeline of inflate2w_kernel -- one thread per emulated
 // wavefront, sharing a hz2::Ctl and the previous window's wavefront's LDS tables; all must
 // return the same status
 // Tune::spin_max of the emulated pipeline (0: hz2::SPIN_MAX); tests set it tiny to force the
@@ -60,6 +60,7 @@ static int run_pipe(hz2::Shared* sh0, const hz2::Job& job, const hz2::Tune& tune
 
 static int run_stream(hz2::Shared* sh, const hz2::Job& job, const hz2::Tune& tune, uint8_t* ring, hz2::Stats& st,
                       int nwaves) {
+  if (nwaves >= 8) return run_pipe<8>(sh, job, tune, ring, st);
   if (nwaves >= 4) return run_pipe<4>(sh, job, tune, ring, st);
   if (nwaves == 2) return run_pipe<2>(sh, job, tune, ring, st);
   return hz2::inflate_stream<hz2::Stats, 1>(*sh, job, tune, ring, &st);

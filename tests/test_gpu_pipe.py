@@ -1,6 +1,6 @@
 """Every inflate mode on the GPU, bit-exact against the CPU oracle: one wavefront per zlib
-stream (inflate2_kernel, large batches) and two or four wavefronts per stream
-(inflate2w_kernel<2|4>, the window pipeline used when a batch cannot fill the GPU: lone
+stream (inflate2_kernel, large batches) and two, four or eight wavefronts per stream
+(inflate2w_kernel<2|4|8>, the window pipeline used when a batch cannot fill the GPU: lone
 GET_Chunk requests, small batches).  Every batch here is decoded in each mode explicitly (hsds_set_tuning's
 waves_per_stream), with multi-block streams, stored blocks, F2 1 MiB streams and
 corruptions."""
@@ -46,7 +46,7 @@ def _streams(rng):
     return out, [zlib.compress(x, lv) for x, lv in zip(out, (4, 1, 6, 9))] + [c], out + [data]
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4])
+@pytest.mark.parametrize("mode", [1, 2, 4, 8])
 def test_zlib_streams_both_modes(mode, oracle_lib):
     rng = np.random.default_rng(31)
     _, blobs, raws = _streams(rng)
@@ -57,7 +57,7 @@ def test_zlib_streams_both_modes(mode, oracle_lib):
         assert out[o:o + len(r)].tobytes() == r, (mode, k)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4])
+@pytest.mark.parametrize("mode", [1, 2, 4, 8])
 def test_f1_frames_both_modes(mode, oracle_lib):
     orc = oracle_lib
     rng = np.random.default_rng(32)
@@ -70,7 +70,7 @@ def test_f1_frames_both_modes(mode, oracle_lib):
         assert out[o:o + len(c)].tobytes() == c, (mode, k)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4])
+@pytest.mark.parametrize("mode", [1, 2, 4, 8])
 def test_corruptions_both_modes(mode, oracle_lib):
     orc = oracle_lib
     rng = np.random.default_rng(33)

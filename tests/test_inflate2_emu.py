@@ -232,7 +232,7 @@ def test_long_overlapping_matches_and_far_distances(emu):
 
 
 # ---- two and four wavefronts per stream (inflate2w_kernel's window pipeline, one thread each) ----
-@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("nw", [2, 4, 8])
 @pytest.mark.parametrize("level", [0, 1, 4, 9])
 def test_two_wavefronts_match_zlib(emu, level, nw):
     for name, data in corpus().items():
@@ -242,7 +242,7 @@ def test_two_wavefronts_match_zlib(emu, level, nw):
         assert out == data, (name, level)
 
 
-@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("nw", [2, 4, 8])
 def test_two_wavefronts_strategies_and_stored_blocks(emu, nw):
     for strategy in (zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED):
         for name in ("smooth_f32", "text", "random", "runs"):
@@ -266,7 +266,7 @@ def test_two_wavefronts_strategies_and_stored_blocks(emu, nw):
     assert st["stored"] > 0
 
 
-@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("nw", [2, 4, 8])
 def test_two_wavefronts_continuation_windows_and_f1_stream(emu, nw):
     """one block over several windows (the continuation copies the other wavefront's tables),
     and a 256 KiB split of the bench chunk (7 blocks: both wavefronts alternate)"""
@@ -284,7 +284,7 @@ def test_two_wavefronts_continuation_windows_and_f1_stream(emu, nw):
     assert r == 0 and out == data
 
 
-@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("nw", [2, 4, 8])
 @pytest.mark.parametrize("off", [1, 3])
 def test_two_wavefronts_unaligned_output(emu, off, nw):
     data = corpus()["smooth_f32"][:50001]
@@ -292,7 +292,7 @@ def test_two_wavefronts_unaligned_output(emu, off, nw):
     assert r == 0 and out == data
 
 
-@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("nw", [2, 4, 8])
 def test_two_wavefronts_corruptions_fail_like_libz(emu, nw):
     import sys
     sys.path.insert(0, ROOT)
@@ -325,7 +325,7 @@ def test_two_wavefronts_corruptions_fail_like_libz(emu, nw):
     assert run(emu, c, len(data) + 1, nwaves=nw)[0] not in (0, -100)
 
 
-@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("nw", [2, 4, 8])
 def test_pipeline_timeout_redecodes_with_one_wavefront(emu, nw):
     """A window-pipeline wait that gives up (Tune::spin_max; inflate2.h inflate_stream /
     inflate_stream_pipe) is not reported as corrupt data: wavefront 0 decodes the stream

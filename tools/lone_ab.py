@@ -1,5 +1,5 @@
 """Lone-chunk device latency of one library build (HSDS_AMD_LIB, HSDS_AMD_DEV=1): one 1 MiB
-F1 and one F2 chunk of the bench data decoded alone, 1 / 2 / 4 wavefronts per stream, median of
+F1 and one F2 chunk of the bench data decoded alone, 1 / 2 / 4 / 8 wavefronts per stream, median of
 15 HIP-event kernel times.  Prints one JSON line.  (tools/latency.py has the full set.)"""
 import json
 import os
@@ -28,7 +28,7 @@ def main():
         d_src = torch.from_numpy(src).to(dev)
         d_dst = torch.empty(ext, dtype=torch.uint8, device=dev)
         d_st = torch.zeros(1, dtype=torch.int32, device=dev)
-        for w in (1, 2, 4):
+        for w in (1, 2, 4, 8):
             eng.set_tuning(waves_per_stream=w)
             ks = []
             for _ in range(15):
