@@ -159,6 +159,16 @@ static_assert(OS == 4 || OS == 8 || OS == 16, "OS: 4, 8 or 16 bytes");
 #ifndef HZ2_PRIO_ABS
 #define HZ2_PRIO_ABS 40
 #endif
+// M's record loads non-temporal: the records are read once, so their lines go first when L2
+// evicts, and the output lines the far-source gathers read stay longer.  Three boxes (tools/
+// gpu_r6ae.sh, gpu_r6af.sh, gpu_r6ag.sh): F1 +0 / +3 / -0.3 %, HBM traffic -3 % (FETCH 15.4 ->
+// 14.6 GB per 2048 chunks).  The gathers' loads made non-temporal too lost 6-9 %.
+#ifndef HZ2_NTREC
+#define HZ2_NTREC 1
+#endif
+#ifndef HZ2_NTGATH
+#define HZ2_NTGATH 0                      // M's gather loads non-temporal (experiment)
+#endif
 // phase A's warm-up decoded by a loop of its own (1) or inside the segment loop (0)
 #ifndef HZ2_WARM2
 #define HZ2_WARM2 1
