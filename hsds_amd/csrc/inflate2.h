@@ -95,13 +95,18 @@ constexpr uint32_t SCRATCH_BYTES = RING_BYTES + LIT_BYTES;   // per resident wav
 #define HZ2_SPAN 1024
 #endif
 constexpr uint32_t SPAN = HZ2_SPAN;       // resolve batch: output bytes covered by the source map
-constexpr uint32_t MPL = 4;               // resolve: matches per lane per batch
+// (round 6, two boxes, three pairs each, tools/gpu_r6ai.sh: 3 instead of 4 -- 6 fewer live
+// registers in M, 22 VGPRs spilled instead of 24 -- F1 equal, F2 149.1 -> 152.0 GB/s)
+#ifndef HZ2_MPL
+#define HZ2_MPL 3
+#endif
+constexpr uint32_t MPL = HZ2_MPL;         // resolve: matches per lane per batch
 #ifndef HZ2_FILLCAP
 #define HZ2_FILLCAP 16
 #endif
 constexpr uint32_t FILL_CAP = HZ2_FILLCAP;
    // resolve: source-map bytes a lane fills per match (258: all)
-static_assert(MPL == 4, "sel4 selects among four per-lane matches");
+static_assert(MPL >= 2 && MPL <= 4, "sel4 selects among up to four per-lane matches");
 constexpr uint32_t SPL = SPAN / WAVE;     // resolve: span bytes per lane
 static_assert(SPL <= 24, "resolve slots per lane");
 constexpr uint32_t RGP = SPL;              // resolve: byte slots per lane (q = lane + 64 i)
@@ -808,7 +813,7 @@ HZ_HD uint32_t dot4(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // a[u] for a register array and a runtime u < MPL (no dynamic register indexing)
-HZ_HD uint32_t sel4(const uint32_t* a, uint32_t u) { return u == 0u ? a[0] : u == 1u ? a[1] : u == 2u ? a[2] : a[3]; }
+HZ_HD uint32_t sel4(const uint32_t* a, uint32_t u) { return u == 0u ? a[0] : (u == 1u || MPL < 3u) ? a[1] : (u == 2u || MPL < 4u) ? a[MPL < 3u ? 1u : 2u] : a[MPL - 1u]; }
 // a[j] of a lane's K recorded starts (registers) for a runtime j < K: masks OR-ed (a select
 // chain is folded back into an indexed load, which puts the array in scratch)
 template <int N>
